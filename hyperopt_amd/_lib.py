@@ -1,0 +1,102 @@
+"""ctypes binding of the HIP C-ABI library ``libtpe_hip.so`` (include/tpe_hip.h).
+
+The struct mirrors below are numpy dtypes with C alignment; their sizes are
+checked against the library at load time.  The library is REQUIRED: there is
+no CPU fallback anywhere on the product path, and loading fails loudly if the
+library has not been built (``make`` or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"))
+
+# enums (tpe_hip.h)
+GMM1, LGMM1, CAT = 0, 1, 2
+OBS_IDENTITY, OBS_LOG = 0, 1
+F_LOW, F_HIGH, F_QUANT, F_INJECTED = 1, 2, 4, 8
+
+SEG_DTYPE = np.dtype([
+    ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
+    ("transform", "<i4"), ("family", "<i4"), ("floor", "<f8"), ("prior_weight", "<f8"),
+    ("prior_mu", "<f8"), ("prior_sigma", "<f8"), ("low", "<f8"), ("high", "<f8"),
+    ("bounded", "<i4"), ("prior_pos", "<i4"), ("p_accept", "<f8"), ("cmax", "<f8"),
+    ("center", "<f8")], align=True)
+CAT_SEG_DTYPE = np.dtype([
+    ("obs_off", "<i8"), ("p_off", "<i8"), ("n_obs", "<i4"), ("n_cat", "<i4"),
+    ("lf", "<i4"), ("mode", "<i4"), ("prior_weight", "<f8"), ("prior_p_off", "<i8")],
+    align=True)
+JOB_DTYPE = np.dtype([
+    ("family", "<i4"), ("flags", "<i4"), ("below", "<i4"), ("above", "<i4"),
+    ("low", "<f8"), ("high", "<f8"), ("q", "<f8"), ("n_cand", "<i8"), ("cand_base", "<i8"),
+    ("cand_off", "<i8"), ("key", "<u8"), ("lat_off", "<i8"), ("lat_kmin", "<i8"),
+    ("lat_n", "<i8"), ("out_off", "<i8")], align=True)
+BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
+                       ("n_scored", "<i8")], align=True)
+
+
+class TpeHipError(RuntimeError):
+    """A C-ABI call returned an error status."""
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+
+_SIGNATURES = {
+    "tpe_parzen_fit": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_cat_posterior": (_I, [_P, _P, _I, _P, _P, _P, _P]),
+    "tpe_score_partials": (_I64, [_P, _I]),
+    "tpe_score_continuous": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P,
+                                  _P, _I64, _P, _P]),
+    "tpe_lattice_sample": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_lattice_compact": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
+    "tpe_quantized_partials": (_I64, [_P, _I, _I64]),
+    "tpe_score_quantized": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _I64,
+                                 _P, _P, _P]),
+    "tpe_categorical_partials": (_I64, [_P, _I]),
+    "tpe_score_categorical": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P]),
+    "tpe_sample": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "tpe_best_combine": (_I, [_P, _I, _I, _P, _P]),
+    "tpe_last_error": (ctypes.c_char_p, []),
+    "tpe_abi_version": (_I, []),
+    "tpe_struct_sizes": (_I, [_P, _I]),
+}
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the ctypes library; raise if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "hyperopt_amd: HIP library %s is missing; build it with `make` "
+            "(or __graft_entry__.build()). There is no CPU fallback." % LIB_PATH)
+    # torch must be loaded first so this library binds torch's HIP runtime
+    # (same SONAME libamdhip64.so.7) instead of a second copy.
+    import torch  # noqa: F401
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    sizes = (ctypes.c_int32 * 4)()
+    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 4)
+    want = (SEG_DTYPE.itemsize, CAT_SEG_DTYPE.itemsize, JOB_DTYPE.itemsize, BEST_DTYPE.itemsize)
+    if tuple(sizes) != want:
+        raise ImportError("hyperopt_amd: ABI struct size mismatch %s vs %s" % (tuple(sizes), want))
+    _lib = lib
+    return lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = load().tpe_last_error().decode(errors="replace")
+        raise TpeHipError("%s failed (%d): %s" % (what, status, msg))

@@ -1,0 +1,875 @@
+// tpe_score.hip -- candidate sampling, EI scoring and argmax for TPE.
+//
+// Replaces, per label:
+//   GMM1 / LGMM1 sampling          hyperopt/tpe.py:79-106, 229-257
+//   categorical sampling           hyperopt/pyll/stochastic.py:119-158
+//   GMM1_lpdf / LGMM1_lpdf         hyperopt/tpe.py:117-180, 265-307 (+ logsum_rows :260-262)
+//   categorical_lpdf               hyperopt/tpe.py:60-73
+//   broadcast_best (argmax)        hyperopt/tpe.py:649-658
+//
+// Continuous, unquantized labels (the N x M hot loop):
+//   grid = (candidate chunks, labels); a block owns kBS*R candidates held in
+//   registers (R per thread), sampled with Philox from the below mixture (or
+//   read, for injected candidates), and streams each mixture's components
+//   through one LDS tile (float4 {a,b,c,-} / double4 {mu,1/sigma,logcoef,w}),
+//   read back as wave-wide broadcasts.  fp32 terms are evaluated as
+//       t = xc*a + b ;  v = c - t*t ;  sum += 2^v        (one v_exp_f32 / pair)
+//   with the log2 coefficients pre-offset by the mixture's max, so no running
+//   max is needed; a wave whose prior term shows the sum could leave the
+//   normal range (v_prior < -100) takes the exact online log-sum-exp instead.
+//   fp64 (parity mode) always runs the exact online log-sum-exp.
+//   The argmax is fused: per-thread -> wave butterfly -> block -> partials ->
+//   one reduce block per label.  Nothing per-candidate touches HBM unless the
+//   caller asks for the per-candidate outputs.
+//
+// Quantized labels (lattice path): candidate values are k*q, so each distinct
+// value is scored once in fp64 with the reference's erf-pair sum and the
+// argmax keeps the first candidate index of the best value.
+#include <algorithm>
+
+#include "tpe_common.hpp"
+
+namespace tpe {
+
+namespace {
+constexpr int kBS = 256;
+constexpr int kR32 = 8;
+constexpr int kR64 = 4;
+constexpr int kTile32 = 1024;  // float4 components per tile (16 KB)
+constexpr int kTile64 = 512;   // double4 components per tile (16 KB)
+constexpr int kStage = 64;     // below-mixture components staged in LDS for sampling
+constexpr int kLatR = 16;      // lattice sampler: candidates per thread
+constexpr int kLatLds = 4096;  // lattice slots deduplicated in LDS per block
+constexpr uint32_t kMaxAttempts = 256;
+constexpr uint32_t kStreamSample = 0x53414D50u;  // "SAMP"
+constexpr float kFastFloor = -100.0f;            // log2 units below the mixture max
+constexpr float kLn2f = 0.6931471805599453f;
+
+__device__ __forceinline__ tpe_best empty_best() { return tpe_best{0.0, -1, 0.0, 0}; }
+
+// first j with cdf[j] > u  (numpy multinomial / inverse CDF)
+__device__ __forceinline__ int upper_bound(const double* cdf, int n, double u) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+struct Mix {  // sampler view of the below mixture (LDS or global)
+  const double* cdf;
+  const double* mu;
+  const double* sg;
+  int n;
+};
+
+// stage the below mixture for sampling; returns the view (call by all threads)
+__device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, const double* mu,
+                                         const double* sigma, double* s_cdf, double* s_mu,
+                                         double* s_sg) {
+  const int n = S.n_obs + 1;
+  if (n > kStage) return Mix{wcdf + S.comp_off, mu + S.comp_off, sigma + S.comp_off, n};
+  for (int k = threadIdx.x; k < n; k += kBS) {
+    s_cdf[k] = wcdf[S.comp_off + k];
+    s_mu[k] = mu[S.comp_off + k];
+    s_sg[k] = sigma[S.comp_off + k];
+  }
+  __syncthreads();
+  return Mix{s_cdf, s_mu, s_sg, n};
+}
+
+// One draw from the (possibly truncated) below mixture: returns the value in
+// the mixture's own space (x for GMM1, log x for LGMM1).  Same accepted
+// distribution as the reference's rejection loop (component ~ w, then
+// N(mu, sigma), accept low <= y < high).
+__device__ __forceinline__ double draw64(const Mix& M, uint64_t key, int64_t g, bool lo_on,
+                                         bool hi_on, double lo, double hi) {
+  double y = 0.0;
+  for (uint32_t a = 0; a < kMaxAttempts; ++a) {
+    const U4 r = draw_words(key, g, a, kStreamSample);
+    const double u = (double)r.x * 0x1.0p-32 * M.cdf[M.n - 1];
+    const int j = upper_bound(M.cdf, M.n, u);
+    y = M.mu[j] + M.sg[j] * normal_f64(r.y, r.z, r.w);
+    if ((!lo_on || lo <= y) && (!hi_on || y < hi)) return y;
+  }
+  // acceptance below ~1e-77: keep the last draw, clamped into the support
+  if (lo_on && y < lo) y = lo;
+  if (hi_on && !(y < hi)) y = nextafter(hi, -INFINITY);
+  return y;
+}
+
+__device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, bool lo_on,
+                                        bool hi_on, float lo, float hi) {
+  float y = 0.0f;
+  for (uint32_t a = 0; a < kMaxAttempts; ++a) {
+    const U4 r = draw_words(key, g, a, kStreamSample);
+    const double u = (double)r.x * 0x1.0p-32 * M.cdf[M.n - 1];
+    const int j = upper_bound(M.cdf, M.n, u);
+    y = (float)M.mu[j] + (float)M.sg[j] * normal_f32(r.y, r.z);
+    if ((!lo_on || lo <= y) && (!hi_on || y < hi)) return y;
+  }
+  if (lo_on && y < lo) y = lo;
+  if (hi_on && !(y < hi)) y = nextafterf(hi, -INFINITY);
+  return y;
+}
+
+// ---------------------------------------------------------------------------
+// mixture log-density at R candidates, fp32 (log2-domain, offset by cmax)
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void lse32(const float4* __restrict__ coef, const tpe_seg& S,
+                                      const float (&y)[R], float (&out)[R], float4* tile) {
+  const int nc = S.n_obs + 1;
+  const float cen = (float)S.center;
+  float xc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) xc[r] = y[r] - cen;
+  const float4 cp = coef[S.prior_pos];
+  bool ok = true;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float t = fmaf(xc[r], cp.x, cp.y);
+    ok = ok && (fmaf(-t, t, cp.z) >= kFastFloor);
+  }
+  const bool fast = __all(ok);
+  float s[R], m[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    s[r] = 0.0f;
+    m[r] = -INFINITY;
+  }
+  for (int t0 = 0; t0 < nc; t0 += kTile32) {
+    const int mm = min(kTile32, nc - t0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < mm; j += kBS) tile[j] = coef[t0 + j];
+    __syncthreads();
+    if (fast) {
+      float acc[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+#pragma unroll 4
+      for (int k = 0; k < mm; ++k) {
+        const float4 c = tile[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const float t = fmaf(xc[r], c.x, c.y);
+          acc[r] += __builtin_amdgcn_exp2f(fmaf(-t, t, c.z));
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) s[r] += acc[r];
+    } else {
+      for (int k = 0; k < mm; ++k) {
+        const float4 c = tile[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const float t = fmaf(xc[r], c.x, c.y);
+          const float v = fmaf(-t, t, c.z);
+          if (v > m[r]) {
+            s[r] = s[r] * __builtin_amdgcn_exp2f(m[r] - v) + 1.0f;
+            m[r] = v;
+          } else {
+            s[r] += __builtin_amdgcn_exp2f(v - m[r]);
+          }
+        }
+      }
+    }
+  }
+  const float C = (float)S.cmax;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float l2 = __builtin_amdgcn_logf(s[r]);  // log2
+    out[r] = (fast ? (l2 + C) : (m[r] + l2 + C)) * kLn2f;
+  }
+}
+
+// exact online log-sum-exp, fp64 (parity mode)
+template <int R>
+__device__ __forceinline__ void lse64(const double4* __restrict__ coef, const tpe_seg& S,
+                                      const double (&y)[R], double (&out)[R], double4* tile) {
+  const int nc = S.n_obs + 1;
+  double s[R], m[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    s[r] = 0.0;
+    m[r] = -INFINITY;
+  }
+  for (int t0 = 0; t0 < nc; t0 += kTile64) {
+    const int mm = min(kTile64, nc - t0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < mm; j += kBS) tile[j] = coef[t0 + j];
+    __syncthreads();
+    for (int k = 0; k < mm; ++k) {
+      const double4 c = tile[k];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double t = (y[r] - c.x) * c.y;
+        const double v = -0.5 * (t * t) + c.z;
+        if (v > m[r]) {
+          s[r] = s[r] * exp(m[r] - v) + 1.0;
+          m[r] = v;
+        } else {
+          s[r] += exp(v - m[r]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) out[r] = log(s[r]) + m[r];
+}
+
+// ---------------------------------------------------------------------------
+// continuous, unquantized: sample/read + score + argmax
+// ---------------------------------------------------------------------------
+template <bool INJ>
+__global__ __launch_bounds__(kBS) void k_score32(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ wcdf, const float4* __restrict__ coef32,
+    const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
+    double* __restrict__ out_x, tpe_best* __restrict__ partial) {
+  __shared__ float4 tile[kTile32];
+  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ BestT red[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kR32);
+  if (base >= J.n_cand) {
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
+  }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  float x[kR32], y[kR32];
+  if (INJ) {
+#pragma unroll
+    for (int r = 0; r < kR32; ++r) {
+      const int64_t li = base + r * kBS + threadIdx.x;
+      x[r] = li < J.n_cand ? (float)cand[J.cand_off + li] : 1.0f;
+    }
+  } else {
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+#pragma unroll
+    for (int r = 0; r < kR32; ++r) {
+      const int64_t li = base + r * kBS + threadIdx.x;
+      float v = 1.0f;
+      if (li < J.n_cand) {
+        v = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
+        if (lgmm) v = __expf(v);
+      }
+      x[r] = v;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kR32; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li < J.n_cand)
+      y[r] = lgmm ? __logf(x[r]) : x[r];
+    else
+      y[r] = (float)SA.center;  // inactive lanes sit on the prior mean
+  }
+  float lb[kR32], la[kR32];
+  lse32<kR32>(coef32 + SB.comp_off, SB, y, lb, tile);
+  lse32<kR32>(coef32 + SA.comp_off, SA, y, la, tile);
+  BestT b{0.0, -1, 0.0};
+#pragma unroll
+  for (int r = 0; r < kR32; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) continue;
+    double bl = lb[r], al = la[r];
+    if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
+      const double lx = (double)__logf(x[r]);
+      bl -= lx;
+      al -= lx;
+    }
+    const int64_t o = J.out_off + li;
+    if (out_bl) out_bl[o] = bl;
+    if (out_al) out_al[o] = al;
+    if (out_x) out_x[o] = (double)x[r];
+    best_update(b, bl - al, J.cand_base + li, (double)x[r]);
+  }
+  b = block_best<kBS>(b, red);
+  if (threadIdx.x == 0) *P = tpe_best{b.score, b.index, b.value, 0};
+}
+
+template <bool INJ>
+__global__ __launch_bounds__(kBS) void k_score64(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ wcdf, const double4* __restrict__ coef64,
+    const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
+    double* __restrict__ out_x, tpe_best* __restrict__ partial) {
+  __shared__ double4 tile[kTile64];
+  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ BestT red[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kR64);
+  if (base >= J.n_cand) {
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
+  }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  double x[kR64], y[kR64];
+  if (INJ) {
+#pragma unroll
+    for (int r = 0; r < kR64; ++r) {
+      const int64_t li = base + r * kBS + threadIdx.x;
+      x[r] = li < J.n_cand ? cand[J.cand_off + li] : 1.0;
+    }
+  } else {
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+#pragma unroll
+    for (int r = 0; r < kR64; ++r) {
+      const int64_t li = base + r * kBS + threadIdx.x;
+      double v = 1.0;
+      if (li < J.n_cand) {
+        v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+        if (lgmm) v = exp(v);
+      }
+      x[r] = v;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kR64; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    y[r] = li < J.n_cand ? (lgmm ? log(x[r]) : x[r]) : SA.prior_mu;
+  }
+  double lb[kR64], la[kR64];
+  lse64<kR64>(coef64 + SB.comp_off, SB, y, lb, tile);
+  lse64<kR64>(coef64 + SA.comp_off, SA, y, la, tile);
+  BestT b{0.0, -1, 0.0};
+#pragma unroll
+  for (int r = 0; r < kR64; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) continue;
+    double bl = lb[r], al = la[r];
+    if (lgmm) {
+      bl -= y[r];
+      al -= y[r];
+    }
+    const int64_t o = J.out_off + li;
+    if (out_bl) out_bl[o] = bl;
+    if (out_al) out_al[o] = al;
+    if (out_x) out_x[o] = x[r];
+    best_update(b, bl - al, J.cand_base + li, x[r]);
+  }
+  b = block_best<kBS>(b, red);
+  if (threadIdx.x == 0) *P = tpe_best{b.score, b.index, b.value, 0};
+}
+
+// one block per job: combine its partials
+__global__ __launch_bounds__(kBS) void k_reduce(const tpe_job* __restrict__ jobs,
+                                                const tpe_best* __restrict__ partial, int64_t nper,
+                                                tpe_best* __restrict__ best) {
+  __shared__ BestT red[kBS / kWave];
+  BestT b{0.0, -1, 0.0};
+  const tpe_best* P = partial + (int64_t)blockIdx.x * nper;
+  for (int64_t i = threadIdx.x; i < nper; i += kBS) {
+    const tpe_best p = P[i];
+    best_update(b, p.score, p.index, p.value);
+  }
+  b = block_best<kBS>(b, red);
+  if (threadIdx.x == 0) best[blockIdx.x] = tpe_best{b.score, b.index, b.value, jobs[blockIdx.x].n_cand};
+}
+
+// ---------------------------------------------------------------------------
+// quantized labels
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBS) void k_lattice_sample(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
+    int32_t* __restrict__ err) {
+  __shared__ uint32_t lfirst[kLatLds];
+  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
+  if (base >= J.n_cand) return;
+  const tpe_seg SB = segs[J.below];
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  const bool local = J.lat_n <= kLatLds;
+  if (local)
+    for (int s = threadIdx.x; s < J.lat_n; s += kBS) lfirst[s] = 0xFFFFFFFFu;
+  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+  __syncthreads();
+  for (int r = 0; r < kLatR; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) break;
+    double v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+    if (lgmm) v = exp(v);
+    const int64_t slot = (int64_t)rint(v / J.q) - J.lat_kmin;  // np.round(x/q) (tpe.py:106)
+    if (slot < 0 || slot >= J.lat_n) {
+      atomicOr(err, 2);
+      continue;
+    }
+    if (local)
+      atomicMin(&lfirst[slot], (uint32_t)(li - base));
+    else
+      atomicMin(&slot_first[J.lat_off + slot], (unsigned long long)(J.cand_base + li));
+  }
+  if (local) {
+    __syncthreads();
+    for (int s = threadIdx.x; s < J.lat_n; s += kBS) {
+      const uint32_t f = lfirst[s];
+      if (f != 0xFFFFFFFFu)
+        atomicMin(&slot_first[J.lat_off + s], (unsigned long long)(J.cand_base + base + f));
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_lattice_compact(
+    const tpe_job* __restrict__ jobs, const unsigned long long* __restrict__ slot_first,
+    double* __restrict__ vals, int64_t* __restrict__ firsts,
+    unsigned long long* __restrict__ counts) {
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t s = (int64_t)blockIdx.x * kBS + threadIdx.x;
+  if (s >= J.lat_n) return;
+  const unsigned long long f = slot_first[J.lat_off + s];
+  if (f == ~0ull) return;
+  const unsigned long long pos = atomicAdd(&counts[blockIdx.y], 1ull);
+  vals[J.lat_off + pos] = (double)(J.lat_kmin + s) * J.q;  // np.round(x/q) * q
+  firsts[J.lat_off + pos] = (int64_t)f;
+}
+
+// quantized mixture log-mass of one value, one wave, lanes stride components.
+// tpe.py:159-174 (GMM1) and :288-305 (LGMM1): sum_k w_k*cdf(ub) - w_k*cdf(lb),
+// then log(prob) - log(p_accept).
+__device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
+                                        const double* __restrict__ w,
+                                        const double* __restrict__ mu,
+                                        const double* __restrict__ sigma, double x,
+                                        int32_t* err) {
+  const bool lg = J.family == TPE_LGMM1;
+  const double hq = J.q / 2.0;
+  double ub = x + hq, lb = x - hq;
+  if (J.flags & TPE_F_HIGH) ub = fmin(ub, lg ? exp(J.high) : J.high);
+  if (J.flags & TPE_F_LOW) lb = fmax(lb, lg ? exp(J.low) : J.low);
+  double lub = 0.0, llb = 0.0;
+  if (lg) {
+    lb = fmax(0.0, lb);
+    if (ub < 0.0 && lane_id() == 0) atomicOr(err, 1);  // tpe.py:196-197
+    lub = log(ub < kEps ? kEps : ub);
+    llb = log(lb < kEps ? kEps : lb);
+  }
+  const int nc = S.n_obs + 1;
+  double acc = 0.0;
+  for (int k = lane_id(); k < nc; k += kWave) {
+    const double wk = w[S.comp_off + k], m = mu[S.comp_off + k], s = sigma[S.comp_off + k];
+    double cu, cl;
+    if (lg) {
+      cu = lognormal_cdf_logx(lub, m, s);
+      cl = lognormal_cdf_logx(llb, m, s);
+    } else {
+      cu = normal_cdf(ub, m, s);
+      cl = normal_cdf(lb, m, s);
+    }
+    acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+  acc = __shfl(acc, 0, kWave);
+  return log(acc) - log(S.p_accept);
+}
+
+constexpr int kQW = kBS / kWave;  // values per block (one wave each)
+
+__global__ __launch_bounds__(kBS) void k_score_q(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ w, const double* __restrict__ mu,
+    const double* __restrict__ sigma, const double* __restrict__ vals,
+    const int64_t* __restrict__ firsts, const unsigned long long* __restrict__ counts,
+    double* __restrict__ out_bl, double* __restrict__ out_al, tpe_best* __restrict__ partial,
+    int32_t* __restrict__ err) {
+  __shared__ BestT red[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t cnt = counts ? (int64_t)counts[blockIdx.y] : J.n_cand;
+  const int64_t pos = (int64_t)blockIdx.x * kQW + threadIdx.x / kWave;
+  BestT b{0.0, -1, 0.0};
+  if (pos < cnt) {  // wave-uniform
+    const int64_t voff = counts ? J.lat_off : J.cand_off;
+    const double v = vals[voff + pos];
+    const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err);
+    const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err);
+    const int64_t idx = firsts ? firsts[J.lat_off + pos] : J.cand_base + pos;
+    if (lane_id() == 0) {
+      if (out_bl) out_bl[J.out_off + pos] = bl;
+      if (out_al) out_al[J.out_off + pos] = al;
+    }
+    b = BestT{bl - al, idx, v};
+  }
+  b = block_best<kBS>(b, red);
+  if (threadIdx.x == 0)
+    partial[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = tpe_best{b.score, b.index, b.value, 0};
+}
+
+// ---------------------------------------------------------------------------
+// categorical labels
+// ---------------------------------------------------------------------------
+constexpr int kRC = 8;
+template <bool INJ>
+__global__ __launch_bounds__(kBS) void k_score_cat(
+    const tpe_job* __restrict__ jobs, const tpe_cat_seg* __restrict__ csegs,
+    const double* __restrict__ logp, const double* __restrict__ cdf,
+    const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
+    double* __restrict__ out_x, tpe_best* __restrict__ partial) {
+  __shared__ BestT red[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kRC);
+  if (base >= J.n_cand) {
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
+  }
+  const tpe_cat_seg CB = csegs[J.below], CA = csegs[J.above];
+  const int K = CB.n_cat;
+  const double* lb = logp + CB.p_off;
+  const double* la = logp + CA.p_off;
+  const double* cb = cdf + CB.p_off;
+  BestT b{0.0, -1, 0.0};
+#pragma unroll
+  for (int r = 0; r < kRC; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) continue;
+    const int64_t g = J.cand_base + li;
+    int64_t k;
+    if (INJ) {
+      k = (int64_t)cand[J.cand_off + li];
+    } else {
+      const U4 rw = draw_words(J.key, g, 0, kStreamSample);
+      k = upper_bound(cb, K, u01_f64(rw.x, rw.y) * cb[K - 1]);
+    }
+    double bl = NAN, al = NAN;
+    if (k >= 0 && k < K) {
+      bl = lb[k];
+      al = la[k];
+    }
+    const int64_t o = J.out_off + li;
+    if (out_bl) out_bl[o] = bl;
+    if (out_al) out_al[o] = al;
+    if (out_x) out_x[o] = (double)k;
+    best_update(b, bl - al, g, (double)k);
+  }
+  b = block_best<kBS>(b, red);
+  if (threadIdx.x == 0) *P = tpe_best{b.score, b.index, b.value, 0};
+}
+
+// ---------------------------------------------------------------------------
+// sampler only
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBS) void k_sample(const tpe_job* __restrict__ jobs,
+                                                const tpe_seg* __restrict__ segs,
+                                                const double* __restrict__ mu,
+                                                const double* __restrict__ sigma,
+                                                const double* __restrict__ wcdf,
+                                                double* __restrict__ out_x) {
+  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
+  if (base >= J.n_cand) return;
+  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  for (int r = 0; r < kLatR; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) break;
+    double v;
+    if (sizeof(T) == 4) {
+      float f = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
+      v = lgmm ? (double)__expf(f) : (double)f;
+    } else {
+      v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+      if (lgmm) v = exp(v);
+    }
+    if (J.flags & TPE_F_QUANT) v = rint(v / J.q) * J.q;
+    out_x[J.out_off + li] = v;
+  }
+}
+
+__global__ void k_combine(const tpe_best* __restrict__ sets, int n_sets, int n_labels,
+                          tpe_best* __restrict__ out) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= n_labels) return;
+  tpe_best b = sets[l];
+  int64_t n = b.n_scored;
+  for (int s = 1; s < n_sets; ++s) {
+    const tpe_best o = sets[(int64_t)s * n_labels + l];
+    n += o.n_scored;
+    if (better(o.score, o.index, b.score, b.index)) b = o;
+  }
+  b.n_scored = n;
+  out[l] = b;
+}
+
+int64_t max_blocks(const tpe_job* hj, int n, int64_t per_block, int want_quant) {
+  int64_t g = 1;
+  for (int i = 0; i < n; ++i) {
+    const bool q = (hj[i].flags & TPE_F_QUANT) != 0;
+    if (want_quant >= 0 && q != (bool)want_quant) continue;
+    g = std::max(g, (hj[i].n_cand + per_block - 1) / per_block);
+  }
+  return g;
+}
+
+bool check_jobs(const char* fn, const tpe_job* hj, int n) {
+  if (n < 0 || n > 65535) {
+    set_error("%s: n_jobs=%d outside [0, 65535]", fn, n);
+    return false;
+  }
+  if (n > 0 && !hj) {
+    set_error("%s: host_jobs is NULL", fn);
+    return false;
+  }
+  for (int i = 0; i < n; ++i)
+    if (hj[i].n_cand < 0) {
+      set_error("%s: job %d has n_cand < 0", fn, i);
+      return false;
+    }
+  return true;
+}
+}  // namespace
+}  // namespace tpe
+
+using namespace tpe;
+
+extern "C" int64_t tpe_score_partials(const tpe_job* host_jobs, int n_jobs) {
+  // the larger of the fp32 and fp64 grids
+  return (int64_t)n_jobs * max_blocks(host_jobs, n_jobs, kBS * kR64, -1);
+}
+
+extern "C" int tpe_score_continuous(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                    const tpe_seg* segs, const double* w, const double* mu,
+                                    const double* sigma, const double* wcdf,
+                                    const double* coef64, const float* coef32,
+                                    const double* cand, int precision, double* out_bl,
+                                    double* out_al, double* out_x, tpe_best* partial,
+                                    int64_t n_partial, tpe_best* best, void* stream) {
+  (void)w;
+  if (!check_jobs("tpe_score_continuous", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (precision != 32 && precision != 64) {
+    set_error("tpe_score_continuous: precision must be 32 or 64, got %d", precision);
+    return TPE_E_ARG;
+  }
+  bool inj = false;
+  for (int i = 0; i < n_jobs; ++i) {
+    if (host_jobs[i].family == TPE_CAT || (host_jobs[i].flags & TPE_F_QUANT)) {
+      set_error("tpe_score_continuous: job %d is not an unquantized GMM1/LGMM1 job", i);
+      return TPE_E_ARG;
+    }
+    const bool ji = (host_jobs[i].flags & TPE_F_INJECTED) != 0;
+    if (i > 0 && ji != inj) {
+      set_error("tpe_score_continuous: mixed injected / sampled jobs in one call");
+      return TPE_E_ARG;
+    }
+    inj = ji;
+  }
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !partial || !best || (inj && !cand) ||
+      (precision == 32 ? !coef32 : !coef64)) {
+    set_error("tpe_score_continuous: null pointer");
+    return TPE_E_ARG;
+  }
+  const int R = precision == 32 ? kR32 : kR64;
+  const int64_t gx = max_blocks(host_jobs, n_jobs, (int64_t)kBS * R, -1);
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_score_continuous: partial workspace %lld < %lld", (long long)n_partial,
+              (long long)(gx * n_jobs));
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)gx, (unsigned)n_jobs);
+  if (precision == 32) {
+    const float4* c = reinterpret_cast<const float4*>(coef32);
+    if (inj)
+      hipLaunchKernelGGL(k_score32<true>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf, c,
+                         cand, out_bl, out_al, out_x, partial);
+    else
+      hipLaunchKernelGGL(k_score32<false>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
+                         c, cand, out_bl, out_al, out_x, partial);
+  } else {
+    const double4* c = reinterpret_cast<const double4*>(coef64);
+    if (inj)
+      hipLaunchKernelGGL(k_score64<true>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf, c,
+                         cand, out_bl, out_al, out_x, partial);
+    else
+      hipLaunchKernelGGL(k_score64<false>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
+                         c, cand, out_bl, out_al, out_x, partial);
+  }
+  hipLaunchKernelGGL(k_reduce, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
+  return check_launch("tpe_score_continuous");
+}
+
+extern "C" int tpe_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                  const tpe_seg* segs, const double* mu, const double* sigma,
+                                  const double* wcdf, uint64_t* slot_first, int32_t* err,
+                                  void* stream) {
+  if (!check_jobs("tpe_lattice_sample", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !slot_first || !err) {
+    set_error("tpe_lattice_sample: null pointer");
+    return TPE_E_ARG;
+  }
+  int64_t end = 0;
+  for (int i = 0; i < n_jobs; ++i) {
+    const tpe_job& j = host_jobs[i];
+    if (!(j.flags & TPE_F_QUANT) || j.family == TPE_CAT || !(j.q > 0) || j.lat_n <= 0) {
+      set_error("tpe_lattice_sample: job %d is not a quantized job with a lattice", i);
+      return TPE_E_ARG;
+    }
+    end = std::max(end, j.lat_off + j.lat_n);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(slot_first, 0xFF, (size_t)end * sizeof(uint64_t), st) != hipSuccess)
+    return check_launch("tpe_lattice_sample memset");
+  const int64_t gx = max_blocks(host_jobs, n_jobs, (int64_t)kBS * kLatR, -1);
+  hipLaunchKernelGGL(k_lattice_sample, dim3((unsigned)gx, (unsigned)n_jobs), dim3(kBS), 0, st,
+                     jobs, segs, mu, sigma, wcdf, (unsigned long long*)slot_first, err);
+  return check_launch("tpe_lattice_sample");
+}
+
+extern "C" int tpe_lattice_compact(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                   const uint64_t* slot_first, double* vals, int64_t* firsts,
+                                   int64_t* counts, void* stream) {
+  if (!check_jobs("tpe_lattice_compact", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !slot_first || !vals || !firsts || !counts) {
+    set_error("tpe_lattice_compact: null pointer");
+    return TPE_E_ARG;
+  }
+  int64_t maxn = 1;
+  for (int i = 0; i < n_jobs; ++i) maxn = std::max(maxn, host_jobs[i].lat_n);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(counts, 0, (size_t)n_jobs * sizeof(int64_t), st) != hipSuccess)
+    return check_launch("tpe_lattice_compact memset");
+  hipLaunchKernelGGL(k_lattice_compact, dim3((unsigned)((maxn + kBS - 1) / kBS), (unsigned)n_jobs),
+                     dim3(kBS), 0, st, jobs, (const unsigned long long*)slot_first, vals, firsts,
+                     (unsigned long long*)counts);
+  return check_launch("tpe_lattice_compact");
+}
+
+extern "C" int64_t tpe_quantized_partials(const tpe_job* host_jobs, int n_jobs, int64_t max_vals) {
+  (void)host_jobs;
+  return (int64_t)n_jobs * std::max((int64_t)1, (max_vals + kQW - 1) / kQW);
+}
+
+extern "C" int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                   const tpe_seg* segs, const double* w, const double* mu,
+                                   const double* sigma, const double* vals,
+                                   const int64_t* firsts, const int64_t* counts, int64_t max_vals,
+                                   double* out_bl, double* out_al, tpe_best* partial,
+                                   int64_t n_partial, tpe_best* best, int32_t* err,
+                                   void* stream) {
+  if (!check_jobs("tpe_score_quantized", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !w || !mu || !sigma || !vals || !partial || !best || !err ||
+      ((firsts == nullptr) != (counts == nullptr))) {
+    set_error("tpe_score_quantized: null pointer (firsts and counts go together)");
+    return TPE_E_ARG;
+  }
+  for (int i = 0; i < n_jobs; ++i)
+    if (!(host_jobs[i].flags & TPE_F_QUANT) || !(host_jobs[i].q > 0) ||
+        host_jobs[i].family == TPE_CAT) {
+      set_error("tpe_score_quantized: job %d is not quantized", i);
+      return TPE_E_ARG;
+    }
+  const int64_t gx = std::max((int64_t)1, (max_vals + kQW - 1) / kQW);
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_score_quantized: partial workspace too small");
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_score_q, dim3((unsigned)gx, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
+                     segs, w, mu, sigma, vals, firsts, (const unsigned long long*)counts, out_bl,
+                     out_al, partial, err);
+  hipLaunchKernelGGL(k_reduce, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
+  return check_launch("tpe_score_quantized");
+}
+
+extern "C" int64_t tpe_categorical_partials(const tpe_job* host_jobs, int n_jobs) {
+  return (int64_t)n_jobs * max_blocks(host_jobs, n_jobs, kBS * kRC, -1);
+}
+
+extern "C" int tpe_score_categorical(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                     const tpe_cat_seg* csegs, const double* logp_pool,
+                                     const double* cdf_pool, const double* cand,
+                                     double* out_bl, double* out_al, double* out_x,
+                                     tpe_best* partial, int64_t n_partial, tpe_best* best,
+                                     void* stream) {
+  if (!check_jobs("tpe_score_categorical", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  bool inj = false;
+  for (int i = 0; i < n_jobs; ++i) {
+    if (host_jobs[i].family != TPE_CAT) {
+      set_error("tpe_score_categorical: job %d is not categorical", i);
+      return TPE_E_ARG;
+    }
+    const bool ji = (host_jobs[i].flags & TPE_F_INJECTED) != 0;
+    if (i > 0 && ji != inj) {
+      set_error("tpe_score_categorical: mixed injected / sampled jobs in one call");
+      return TPE_E_ARG;
+    }
+    inj = ji;
+  }
+  if (!jobs || !csegs || !logp_pool || !cdf_pool || !partial || !best || (inj && !cand)) {
+    set_error("tpe_score_categorical: null pointer");
+    return TPE_E_ARG;
+  }
+  const int64_t gx = max_blocks(host_jobs, n_jobs, (int64_t)kBS * kRC, -1);
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_score_categorical: partial workspace too small");
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)gx, (unsigned)n_jobs);
+  if (inj)
+    hipLaunchKernelGGL(k_score_cat<true>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool,
+                       cdf_pool, cand, out_bl, out_al, out_x, partial);
+  else
+    hipLaunchKernelGGL(k_score_cat<false>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool,
+                       cdf_pool, cand, out_bl, out_al, out_x, partial);
+  hipLaunchKernelGGL(k_reduce, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
+  return check_launch("tpe_score_categorical");
+}
+
+extern "C" int tpe_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                          const tpe_seg* segs, const double* mu, const double* sigma,
+                          const double* wcdf, int precision, double* out_x, void* stream) {
+  if (!check_jobs("tpe_sample", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !out_x || (precision != 32 && precision != 64)) {
+    set_error("tpe_sample: bad arguments");
+    return TPE_E_ARG;
+  }
+  for (int i = 0; i < n_jobs; ++i)
+    if (host_jobs[i].family == TPE_CAT) {
+      set_error("tpe_sample: categorical jobs are sampled by tpe_score_categorical");
+      return TPE_E_ARG;
+    }
+  const int64_t gx = max_blocks(host_jobs, n_jobs, (int64_t)kBS * kLatR, -1);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)gx, (unsigned)n_jobs);
+  if (precision == 32)
+    hipLaunchKernelGGL(k_sample<float>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf, out_x);
+  else
+    hipLaunchKernelGGL(k_sample<double>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
+                       out_x);
+  return check_launch("tpe_sample");
+}
+
+extern "C" int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* out,
+                                void* stream) {
+  if (n_sets <= 0 || n_labels < 0 || (n_labels > 0 && (!sets || !out))) {
+    set_error("tpe_best_combine: bad arguments");
+    return TPE_E_ARG;
+  }
+  if (n_labels == 0) return TPE_OK;
+  hipLaunchKernelGGL(k_combine, dim3((n_labels + kBS - 1) / kBS), dim3(kBS), 0,
+                     (hipStream_t)stream, sets, n_sets, n_labels, out);
+  return check_launch("tpe_best_combine");
+}

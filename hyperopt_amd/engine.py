@@ -1,0 +1,446 @@
+"""GPU engine for one level of TPE labels: Parzen fit, sampling, scoring, argmax.
+
+This is the product path behind ``hyperopt_amd.tpe.suggest``.  One call to
+``Engine.run`` takes every label that is active at one level of the search
+space (all labels, for a flat space) and runs, on the current torch stream:
+
+    tpe_parzen_fit        adaptive_parzen_normal for every below/above set
+    tpe_cat_posterior     randint / categorical pseudocount posteriors
+    tpe_score_continuous  unquantized labels: sample + GMM1/LGMM1_lpdf + argmax
+    tpe_lattice_*         quantized labels: sample -> distinct values -> score
+    tpe_score_categorical categorical labels: sample + lookup + argmax
+
+with one host->device upload of the packed inputs and one device->host copy of
+the per-label winners.  Reference: hyperopt/tpe.py:661-757 (build_posterior),
+:837-964 (suggest).  There is no CPU fallback: every numeric step above is a
+HIP kernel from libtpe_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib as L
+
+EPS = 1e-12  # tpe.py:32
+DEFAULT_LF = 25  # tpe.py:36
+LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense fallback
+_ALIGN = 256
+
+CONTINUOUS = ("uniform", "quniform", "loguniform", "qloguniform",
+              "normal", "qnormal", "lognormal", "qlognormal")
+CATEGORICAL = ("randint", "categorical")
+
+
+@dataclass
+class LabelWork:
+    """One label's inputs for one suggest level."""
+    label: str
+    kind: str                 # prior distribution name (hp node name)
+    args: tuple               # prior arguments, positional
+    obs_below: np.ndarray     # below-set observations, tid order (tpe.py:641)
+    obs_above: np.ndarray     # above-set observations, tid order (tpe.py:644)
+    n_cand: int = 24          # candidates scored on this device
+    key: int = 0              # Philox key (seed mixed with the label)
+    cand_base: int = 0        # global index of this device's first candidate
+    cand: Optional[np.ndarray] = None  # injected candidates (values / category ids)
+
+
+@dataclass
+class LabelResult:
+    label: str
+    index: int                # global candidate index of the winner (-1: none)
+    value: float              # winning candidate value (category id for categorical)
+    score: float              # below_llik - above_llik at the winner
+    n_scored: int
+    below_llik: Optional[np.ndarray] = None
+    above_llik: Optional[np.ndarray] = None
+    cand: Optional[np.ndarray] = None
+    extra: dict = field(default_factory=dict)
+
+
+def posterior_params(kind, args):
+    """Prior -> posterior construction parameters (tpe.py:484-572)."""
+    if kind in ("uniform", "quniform", "loguniform", "qloguniform"):
+        low, high = float(args[0]), float(args[1])
+        q = float(args[2]) if kind.startswith("q") else None
+        fam = L.LGMM1 if "log" in kind else L.GMM1
+        floor = -math.inf
+        if kind == "qloguniform":
+            floor = max(EPS, math.exp(low))  # tpe.py:527-532
+        return dict(family=fam, transform=L.OBS_LOG if fam == L.LGMM1 else L.OBS_IDENTITY,
+                    floor=floor, prior_mu=0.5 * (high + low), prior_sigma=1.0 * (high - low),
+                    low=low, high=high, q=q, bounded=True)
+    if kind in ("normal", "qnormal", "lognormal", "qlognormal"):
+        mu, sigma = float(args[0]), float(args[1])
+        q = float(args[2]) if kind.startswith("q") else None
+        fam = L.LGMM1 if "log" in kind else L.GMM1
+        floor = EPS if kind == "qlognormal" else -math.inf  # tpe.py:567
+        return dict(family=fam, transform=L.OBS_LOG if fam == L.LGMM1 else L.OBS_IDENTITY,
+                    floor=floor, prior_mu=mu, prior_sigma=sigma, low=0.0, high=0.0, q=q,
+                    bounded=False)
+    raise ValueError("not a continuous prior: %r" % (kind,))
+
+
+def categorical_params(kind, args):
+    """(K, offset, mode, prior p) for randint / categorical (tpe.py:578-615)."""
+    if kind == "randint":
+        if len(args) >= 2 and args[1] is not None:
+            low, high = int(args[0]), int(args[1])
+            return high - low, low, 0, None
+        return int(args[0]), 0, 0, None
+    if kind == "categorical":
+        p = np.asarray(args[0], dtype=np.float64)
+        if p.ndim == 2:
+            p = p[0]
+        return p.size, 0, 1, p
+    raise ValueError("not a categorical prior: %r" % (kind,))
+
+
+def _align(n):
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class _Pack:
+    """Packs host arrays into one buffer for a single host->device copy."""
+
+    def __init__(self):
+        self.parts = []
+        self.size = 0
+
+    def add(self, arr):
+        arr = np.ascontiguousarray(arr)
+        off = _align(self.size)
+        self.parts.append((off, arr))
+        self.size = off + max(arr.nbytes, 1)
+        return off
+
+
+class Engine:
+    """Owns the device workspace; one instance per device (kept by tpe.py)."""
+
+    def __init__(self, device=None):
+        import torch
+        self.torch = torch
+        self.lib = L.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        self._bufs = {}
+        self._pinned = None
+
+    # -- memory --------------------------------------------------------------
+    def _buf(self, name, nbytes):
+        t = self._bufs.get(name)
+        nbytes = max(int(nbytes), 16)
+        if t is None or t.numel() < nbytes:
+            t = self.torch.empty(_align(int(nbytes * 1.25)), dtype=self.torch.uint8,
+                                 device=self.device)
+            self._bufs[name] = t
+        return t.data_ptr()
+
+    def _upload(self, pack, stream):
+        torch = self.torch
+        if self._pinned is None or self._pinned.numel() < pack.size:
+            self._pinned = torch.empty(_align(int(pack.size * 1.25) + 1), dtype=torch.uint8,
+                                       pin_memory=True)
+        host = self._pinned.numpy()
+        for off, arr in pack.parts:
+            host[off:off + arr.nbytes] = arr.reshape(-1).view(np.uint8)
+        dev = self._buf("stage", pack.size)
+        dst = self._bufs["stage"]
+        with torch.cuda.stream(stream):
+            dst[:pack.size].copy_(self._pinned[:pack.size], non_blocking=True)
+        return dev
+
+    # -- main entry ----------------------------------------------------------
+    def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
+            outputs=False, stream=None) -> List[LabelResult]:
+        torch = self.torch
+        lib = self.lib
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        cont, quant, cat = [], [], []
+        for i, w in enumerate(works):
+            if w.kind in CONTINUOUS:
+                (quant if w.kind.startswith("q") else cont).append(i)
+            elif w.kind in CATEGORICAL:
+                cat.append(i)
+            else:
+                raise ValueError("unsupported prior %r for label %r" % (w.kind, w.label))
+
+        pack = _Pack()
+        # ---- continuous / quantized segments --------------------------------
+        fit_ids = cont + quant
+        segs = np.zeros(2 * len(fit_ids), L.SEG_DTYPE)
+        obs_parts, params = [], {}
+        obs_off = comp_off = max_obs = 0
+        for si, i in enumerate(fit_ids):
+            w = works[i]
+            P = posterior_params(w.kind, w.args)
+            params[i] = P
+            for half, obs in enumerate((w.obs_below, w.obs_above)):
+                obs = np.asarray(obs, dtype=np.float64).reshape(-1)
+                s = segs[2 * si + half]
+                s["obs_off"], s["comp_off"], s["n_obs"] = obs_off, comp_off, obs.size
+                s["lf"], s["transform"], s["family"] = lf, P["transform"], P["family"]
+                s["floor"], s["prior_weight"] = P["floor"], prior_weight
+                s["prior_mu"], s["prior_sigma"] = P["prior_mu"], P["prior_sigma"]
+                s["low"], s["high"], s["bounded"] = P["low"], P["high"], int(P["bounded"])
+                obs_parts.append(obs)
+                obs_off += obs.size
+                comp_off += obs.size + 1
+                max_obs = max(max_obs, obs.size)
+        n_comp = comp_off
+        obs_pool = np.concatenate(obs_parts) if obs_parts else np.zeros(1)
+
+        # ---- categorical segments ------------------------------------------
+        csegs = np.zeros(2 * len(cat), L.CAT_SEG_DTYPE)
+        cobs_parts, p_init = [], []
+        cobs_off = p_off = 0
+        cat_meta = {}
+        for ci, i in enumerate(cat):
+            w = works[i]
+            K, offset, mode, prior_p = categorical_params(w.kind, w.args)
+            cat_meta[i] = (K, offset)
+            prior_off = -1
+            if mode == 1:
+                prior_off = p_off
+                p_init.append(prior_p)
+                p_off += K
+            for half, obs in enumerate((w.obs_below, w.obs_above)):
+                obs = np.asarray(obs).reshape(-1).astype(np.int64) - offset
+                c = csegs[2 * ci + half]
+                c["obs_off"], c["p_off"], c["n_obs"], c["n_cat"] = cobs_off, p_off, obs.size, K
+                c["lf"], c["mode"], c["prior_weight"], c["prior_p_off"] = lf, mode, prior_weight, \
+                    max(prior_off, 0)
+                cobs_parts.append(obs)
+                p_init.append(np.zeros(K))
+                cobs_off += obs.size
+                p_off += K
+        cobs_pool = np.concatenate(cobs_parts) if cobs_parts else np.zeros(1, np.int64)
+        p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
+
+        # ---- jobs, ordered so every kernel call takes a contiguous slice -----------
+        inj = lambda i: works[i].cand is not None  # noqa: E731
+        lat_ranges = {}
+        fallback = []
+        for i in quant:
+            if not inj(i):
+                kmin, kmax = _lattice_range(works[i], params[i])
+                if kmax - kmin + 1 > LATTICE_CAP:
+                    fallback.append(i)
+                else:
+                    lat_ranges[i] = (kmin, kmax - kmin + 1)
+        groups = [
+            ("cont", [i for i in cont if inj(i)]),
+            ("cont", [i for i in cont if not inj(i)]),
+            ("lat", [i for i in quant if i in lat_ranges]),
+            ("qfb", fallback),
+            ("qinj", [i for i in quant if inj(i)]),
+            ("cat", [i for i in cat if inj(i)]),
+            ("cat", [i for i in cat if not inj(i)]),
+        ]
+        order = [i for _, ids in groups for i in ids]
+        jobs = np.zeros(len(order), L.JOB_DTYPE)
+        cand_parts, cand_off, out_off, lat_off, qfb_off = [], 0, 0, 0, 0
+        seg_of = {i: si for si, i in enumerate(fit_ids)}
+        cseg_of = {i: ci for ci, i in enumerate(cat)}
+        for pos, i in enumerate(order):
+            w, j = works[i], jobs[pos]
+            j["key"] = np.uint64(int(w.key) & 0xFFFFFFFFFFFFFFFF)
+            j["cand_base"] = w.cand_base
+            n = int(np.asarray(w.cand).size) if inj(i) else int(w.n_cand)
+            j["n_cand"] = n
+            j["out_off"] = out_off
+            out_off += n
+            if inj(i):
+                # categorical candidates are category indices (0..K-1), as the
+                # reference's randint_via_categorical samples them (tpe.py:590)
+                c = np.asarray(w.cand, dtype=np.float64).reshape(-1)
+                j["cand_off"] = cand_off
+                cand_parts.append(c)
+                cand_off += c.size
+                j["flags"] |= L.F_INJECTED
+            if i in cat_meta:
+                j["family"] = L.CAT
+                j["below"], j["above"] = 2 * cseg_of[i], 2 * cseg_of[i] + 1
+                continue
+            P = params[i]
+            j["family"] = P["family"]
+            j["below"], j["above"] = 2 * seg_of[i], 2 * seg_of[i] + 1
+            if P["bounded"]:
+                j["flags"] |= L.F_LOW | L.F_HIGH
+                j["low"], j["high"] = P["low"], P["high"]
+            if P["q"] is not None:
+                j["flags"] |= L.F_QUANT
+                j["q"] = P["q"]
+                if i in lat_ranges:
+                    j["lat_off"], j["lat_kmin"], j["lat_n"] = lat_off, *lat_ranges[i]
+                    lat_off += lat_ranges[i][1]
+                elif i in fallback:
+                    j["cand_off"] = qfb_off
+                    qfb_off += n
+        cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
+        # the dense fallback first materialises its draws: a job copy whose
+        # out_off points into the scratch candidate buffer
+        fb_slice = _slice_of(groups, 3)
+        fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
+        fb_jobs["out_off"] = fb_jobs["cand_off"]
+
+        # ---- upload -------------------------------------------------------------
+        o_segs = pack.add(segs) if segs.size else None
+        o_obs = pack.add(obs_pool)
+        o_csegs = pack.add(csegs) if csegs.size else None
+        o_cobs = pack.add(cobs_pool)
+        o_p = pack.add(p_pool)
+        o_jobs = pack.add(jobs) if jobs.size else None
+        o_fb = pack.add(fb_jobs) if fb_jobs.size else None
+        o_cand = pack.add(cand_pool)
+        base = self._upload(pack, stream)
+        d_segs = base + o_segs if o_segs is not None else None
+        d_csegs = base + o_csegs if o_csegs is not None else None
+        d_cand = base + o_cand
+        JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
+
+        n_jobs = len(order)
+        d_best = self._buf("best", n_jobs * BS)
+        d_err = self._buf("err", 16)
+        err_t = self._bufs["err"]
+        with torch.cuda.stream(stream):
+            err_t[:16].zero_()
+        d_bl = d_al = d_x = None
+        if outputs:
+            d_bl = self._buf("out_bl", 8 * max(out_off, 1))
+            d_al = self._buf("out_al", 8 * max(out_off, 1))
+            d_x = self._buf("out_x", 8 * max(out_off, 1))
+
+        # ---- posterior fit ------------------------------------------------------
+        d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
+        if fit_ids:
+            d_w = self._buf("w", 8 * n_comp)
+            d_mu = self._buf("mu", 8 * n_comp)
+            d_sig = self._buf("sigma", 8 * n_comp)
+            d_cdf = self._buf("wcdf", 8 * n_comp)
+            d_c64 = self._buf("coef64", 32 * n_comp)
+            d_c32 = self._buf("coef32", 16 * n_comp)
+            d_xf = self._buf("xf", 8 * max(obs_pool.size, 1))
+            L.check(lib.tpe_parzen_fit(base + o_obs, d_xf, d_segs, len(segs), max_obs, d_w, d_mu,
+                                       d_sig, d_cdf, d_c64, d_c32, sp), "tpe_parzen_fit")
+        if cat:
+            d_logp = self._buf("cat_logp", 8 * p_pool.size)
+            d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
+            L.check(lib.tpe_cat_posterior(base + o_cobs, d_csegs, len(csegs), base + o_p, d_logp,
+                                          d_ccdf, sp), "tpe_cat_posterior")
+
+        # ---- scoring, one call per group ----------------------------------------
+        for g, (kind, ids) in enumerate(groups):
+            if not ids:
+                continue
+            a, b = _slice_of(groups, g)
+            hj = jobs[a:b]
+            hjp = hj.ctypes.data_as(ctypes.c_void_p)
+            dj = base + o_jobs + a * JS
+            db = d_best + a * BS
+            nj = b - a
+            if kind == "cont":
+                npart = lib.tpe_score_partials(hjp, nj)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                L.check(lib.tpe_score_continuous(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
+                                                 d_c64, d_c32, d_cand, precision, d_bl, d_al, d_x,
+                                                 d_part, npart, db, sp), "tpe_score_continuous")
+            elif kind == "lat":
+                d_slot = self._buf("lat_slot", 8 * lat_off)
+                d_vals = self._buf("lat_vals", 8 * lat_off)
+                d_first = self._buf("lat_first", 8 * lat_off)
+                d_cnt = self._buf("lat_cnt", 8 * nj)
+                L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_slot,
+                                               d_err, sp), "tpe_lattice_sample")
+                L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt, sp),
+                        "tpe_lattice_compact")
+                max_vals = int(hj["lat_n"].max())
+                npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_vals,
+                                                d_first, d_cnt, max_vals, None, None, d_part,
+                                                npart, db, d_err, sp), "tpe_score_quantized")
+            elif kind in ("qfb", "qinj"):
+                vals = d_cand
+                if kind == "qfb":
+                    vals = self._buf("q_cand", 8 * max(qfb_off, 1))
+                    L.check(lib.tpe_sample(base + o_fb, fb_jobs.ctypes.data_as(ctypes.c_void_p),
+                                           nj, d_segs, d_mu, d_sig, d_cdf, 64, vals, sp),
+                            "tpe_sample")
+                max_vals = int(hj["n_cand"].max())
+                npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, vals, None,
+                                                None, max_vals, d_bl, d_al, d_part, npart, db,
+                                                d_err, sp), "tpe_score_quantized")
+            else:
+                npart = lib.tpe_categorical_partials(hjp, nj)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf, d_cand,
+                                                  d_bl, d_al, d_x, d_part, npart, db, sp),
+                        "tpe_score_categorical")
+
+        # ---- results (one device->host copy; syncs the stream) --------------------
+        with torch.cuda.stream(stream):
+            best_h = self._bufs["best"][:n_jobs * BS].to("cpu").numpy().view(L.BEST_DTYPE)
+            err = int(err_t[:4].to("cpu").view(torch.int32).item())
+            outs = None
+            if outputs:
+                outs = [self._bufs[k][:8 * max(out_off, 1)].to("cpu").numpy().view(np.float64)
+                        for k in ("out_bl", "out_al", "out_x")]
+        if err & 1:
+            raise ValueError("negative arg to lognormal_cdf")  # tpe.py:196-197
+        if err & 2:
+            raise L.TpeHipError("lattice slot out of range (internal error)")
+        results = [None] * len(works)
+        for pos, i in enumerate(order):
+            b = best_h[pos]
+            w = works[i]
+            r = LabelResult(w.label, int(b["index"]), float(b["value"]), float(b["score"]),
+                            int(b["n_scored"]))
+            if outputs:
+                o, n = int(jobs[pos]["out_off"]), int(jobs[pos]["n_cand"])
+                r.below_llik = outs[0][o:o + n].copy()
+                r.above_llik = outs[1][o:o + n].copy()
+                r.cand = outs[2][o:o + n].copy()
+            results[i] = r
+        return results
+
+
+def _slice_of(groups, g):
+    a = sum(len(ids) for _, ids in groups[:g])
+    return a, a + len(groups[g][1])
+
+
+def _lattice_range(w: LabelWork, P):
+    """Inclusive lattice index range [kmin, kmax] covering every possible draw.
+
+    Bounded: draws lie in [low, high) (log space for LGMM1).  Unbounded: every
+    component has sigma <= prior_sigma (tpe.py:454-459) and a Box-Muller normal
+    from 53-bit uniforms satisfies |z| < 8.6, so mean +- 9 sigma_prior bounds
+    every draw.
+    """
+    q = P["q"]
+    if P["bounded"]:
+        lo, hi = P["low"], P["high"]
+    else:
+        obs = np.asarray(w.obs_below, dtype=np.float64)
+        if P["transform"] == L.OBS_LOG:
+            obs = np.log(np.maximum(obs, P["floor"])) if obs.size else obs
+        pts = np.concatenate([obs, [P["prior_mu"]]])
+        lo = float(pts.min()) - 9.0 * P["prior_sigma"]
+        hi = float(pts.max()) + 9.0 * P["prior_sigma"]
+    if P["family"] == L.LGMM1:
+        lo, hi = math.exp(min(lo, 700.0)), math.exp(min(hi, 700.0))
+    kmin = int(math.floor(lo / q)) - 1
+    kmax = int(math.ceil(hi / q)) + 1
+    return kmin, kmax

@@ -1,0 +1,211 @@
+/*
+ * tpe_hip.h -- C ABI of the MI355X TPE suggest engine (libtpe_hip.so).
+ *
+ * The reference (hyperopt 0.2.4, /root/reference) is pure Python/numpy and
+ * has no FFI of its own; its hot path is the per-label posterior evaluation
+ * that `tpe.suggest` drives through `pyll.rec_eval` (hyperopt/tpe.py:942).
+ * Each entry point below replaces one group of the numpy expressions on that
+ * path and is what a binding of that path (ctypes / cffi / pybind) would
+ * call.  The Python host layer `hyperopt_amd/_lib.py` binds these with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - every pointer is a caller-owned DEVICE pointer unless marked "host";
+ *   - `stream` is a hipStream_t passed as void* (0 = legacy default stream);
+ *   - every call is asynchronous on `stream`, captures into a hipGraph,
+ *     performs no allocation and no host synchronisation;
+ *   - return value: 0 on success, a negative TPE_E* code otherwise; the text
+ *     of the last error on the calling thread is tpe_last_error();
+ *   - scores/log-densities are float64 on the ABI; `precision` (32 or 64)
+ *     selects the arithmetic of the continuous scoring kernel only.
+ */
+#ifndef TPE_HIP_H
+#define TPE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TPE_ABI_VERSION 1
+
+enum {
+  TPE_OK = 0,
+  TPE_E_ARG = -1,        /* bad argument (null pointer, bad size/kind)      */
+  TPE_E_LAUNCH = -2,     /* HIP launch / runtime error                      */
+  TPE_E_UNSUPPORTED = -3 /* configuration outside what the kernels support  */
+};
+
+/* mixture families (hyperopt/tpe.py:79, 229; categorical tpe.py:60-73) */
+enum { TPE_GMM1 = 0, TPE_LGMM1 = 1, TPE_CAT = 2 };
+
+/* observation transform applied before the Parzen fit (tpe.py:506-572) */
+enum { TPE_OBS_IDENTITY = 0, TPE_OBS_LOG = 1 };
+
+/* job flags */
+enum {
+  TPE_F_LOW = 1,        /* lower bound present (tpe.py:93, 166)              */
+  TPE_F_HIGH = 2,       /* upper bound present                               */
+  TPE_F_QUANT = 4,      /* quantized (q is not None)                         */
+  TPE_F_INJECTED = 8    /* candidates read from `cand` instead of sampled    */
+};
+
+/*
+ * One Parzen-fit segment: the below- or above-set observations of one label.
+ * Replaces `adaptive_parzen_normal` (tpe.py:399-467) and the observation
+ * transforms of the ap_*_sampler functions (tpe.py:484-572).  Inputs are set
+ * by the host; the kernel fills the outputs.  The fitted mixture has
+ * n_obs + 1 components written at [comp_off, comp_off + n_obs + 1), sorted
+ * by mean, exactly as the reference returns them.
+ */
+typedef struct tpe_seg {
+  /* inputs */
+  int64_t obs_off;      /* first observation in the obs pool                */
+  int64_t comp_off;     /* first output component in the mixture pool       */
+  int32_t n_obs;        /* observations in this segment (tid order)         */
+  int32_t lf;           /* linear forgetting (tpe.py:380-392); 0 = off      */
+  int32_t transform;    /* TPE_OBS_*                                         */
+  int32_t family;       /* TPE_GMM1 / TPE_LGMM1 (coefficient layout)         */
+  double floor;         /* log transform: log(max(obs, floor))              */
+  double prior_weight, prior_mu, prior_sigma;
+  double low, high;     /* truncation for p_accept (tpe.py:145-150)         */
+  int32_t bounded;      /* 1 if low/high given                              */
+  /* outputs */
+  int32_t prior_pos;    /* index of the prior component in the sorted mix   */
+  double p_accept;      /* sum w*(Phi(high)-Phi(low)), 1 if unbounded        */
+  double cmax;          /* max_k log2-coefficient (fp32 scoring offset)      */
+  double center;        /* fp32 scoring origin (float-rounded prior_mu)      */
+} tpe_seg;
+
+/*
+ * One categorical segment (randint / pchoice / choice posterior,
+ * tpe.py:578-615 with pyll/base.py:1053-1060).  counts are accumulated in
+ * observation order, so they are bit-identical to np.bincount.
+ */
+typedef struct tpe_cat_seg {
+  int64_t obs_off;      /* int64 observations (already offset-free)         */
+  int64_t p_off;        /* first output probability                          */
+  int32_t n_obs;
+  int32_t n_cat;        /* K                                                 */
+  int32_t lf;
+  int32_t mode;         /* 0 randint: counts+pw ; 1 categorical: counts+K*pw*p */
+  double prior_weight;
+  int64_t prior_p_off;  /* mode 1: prior probabilities p in the p pool       */
+} tpe_cat_seg;
+
+/*
+ * One label's scoring job.  For continuous labels below/above index two
+ * tpe_seg entries; for categorical labels two tpe_cat_seg entries.
+ * Candidates are either sampled in registers from the BELOW posterior with
+ * Philox4x32-10 keyed by (key, global candidate index) -- so results do not
+ * depend on how candidates are sharded over GPUs -- or injected (TPE_F_INJECTED).
+ */
+typedef struct tpe_job {
+  int32_t family;       /* TPE_GMM1 / TPE_LGMM1 / TPE_CAT                    */
+  int32_t flags;        /* TPE_F_*                                           */
+  int32_t below, above; /* segment indices                                   */
+  double low, high, q;  /* GMM1: x-space bounds; LGMM1: log-space bounds    */
+  int64_t n_cand;       /* candidates scored by this call                   */
+  int64_t cand_base;    /* global index of the first one (multi-GPU shard)  */
+  int64_t cand_off;     /* TPE_F_INJECTED: first candidate in `cand`         */
+  uint64_t key;         /* Philox key (seed mixed with label id)            */
+  int64_t lat_off;      /* quantized: first lattice slot in the slot pool   */
+  int64_t lat_kmin;     /* quantized: lattice index of slot 0               */
+  int64_t lat_n;        /* quantized: number of slots                       */
+  int64_t out_off;      /* optional per-candidate outputs: first element    */
+} tpe_job;
+
+/* best candidate of one label: np.argmax semantics (first max, NaN wins) */
+typedef struct tpe_best {
+  double score;         /* below_llik - above_llik of the winner            */
+  int64_t index;        /* global candidate index of the winner (-1: none)  */
+  double value;         /* candidate value (category index for TPE_CAT)     */
+  int64_t n_scored;     /* candidates entered into the argmax               */
+} tpe_best;
+
+/* ---- Parzen posterior (adaptive_parzen_normal, tpe.py:399-467) ---------- */
+/* obs: fp64 pool; xf: fp64 scratch (same size as obs);
+ * w/mu/sigma: fp64 mixture pool (sorted components);
+ * wcdf: fp64 cumulative weights (sampler); coef64: 4 doubles / component;
+ * coef32: 4 floats / component.  max_obs = max n_obs over segs. */
+int tpe_parzen_fit(const double* obs, double* xf, tpe_seg* segs, int n_seg, int max_obs,
+                   double* w, double* mu, double* sigma, double* wcdf,
+                   double* coef64, float* coef32, void* stream);
+
+/* ---- categorical posterior (tpe.py:578-615) ------------------------------ */
+/* p_pool: probabilities (mode 1 also reads the prior p from it at
+ * prior_p_off); logp_pool / cdf_pool: log p and cumulative p at p_off. */
+int tpe_cat_posterior(const int64_t* obs, const tpe_cat_seg* segs, int n_seg,
+                      double* p_pool, double* logp_pool, double* cdf_pool, void* stream);
+
+/* ---- continuous candidates: sample (or read) + score + argmax ------------
+ * Replaces GMM1/LGMM1 sampling (tpe.py:79-106, 229-257), GMM1_lpdf /
+ * LGMM1_lpdf (tpe.py:117-180, 265-307) and broadcast_best (tpe.py:649-658)
+ * for UNQUANTIZED labels.  partial: workspace of tpe_best, capacity
+ * n_partial (query with tpe_score_partials()).  out_bl/out_al (nullable):
+ * per-candidate log-likelihoods at job.out_off; out_x (nullable): the
+ * candidates themselves.  best: one tpe_best per job. */
+int64_t tpe_score_partials(const tpe_job* host_jobs, int n_jobs);
+int tpe_score_continuous(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                         const tpe_seg* segs, const double* w, const double* mu,
+                         const double* sigma, const double* wcdf, const double* coef64,
+                         const float* coef32, const double* cand, int precision,
+                         double* out_bl, double* out_al, double* out_x,
+                         tpe_best* partial, int64_t n_partial, tpe_best* best,
+                         void* stream);
+
+/* ---- quantized labels: lattice path ---------------------------------------
+ * Candidates of a quantized label take values k*q (np.round(x/q)*q,
+ * tpe.py:106, 256); equal values have equal scores, so every distinct value
+ * is scored once (fp64, the reference's erf-pair sum) and the argmax keeps the
+ * first candidate index of the best value -- identical to np.argmax over all
+ * candidates.  slot_first: uint64 pool of lattice slots (all jobs);
+ * vals/firsts/scores: compacted present values (capacity n_cap per job at
+ * job.lat_off); counts: int64 per job. */
+int tpe_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                       const tpe_seg* segs, const double* mu, const double* sigma,
+                       const double* wcdf, uint64_t* slot_first, int32_t* err,
+                       void* stream);
+int tpe_lattice_compact(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                        const uint64_t* slot_first, double* vals, int64_t* firsts,
+                        int64_t* counts, void* stream);
+/* scores values (lattice values, or injected candidates when firsts==NULL
+ * and counts==NULL: then job.n_cand values at job.cand_off of `vals`).
+ * err: int32 flag set to 1 on a negative lognormal_cdf argument
+ * (tpe.py:196-197). */
+int64_t tpe_quantized_partials(const tpe_job* host_jobs, int n_jobs, int64_t max_vals);
+int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                        const tpe_seg* segs, const double* w, const double* mu,
+                        const double* sigma, const double* vals, const int64_t* firsts,
+                        const int64_t* counts, int64_t max_vals, double* out_bl,
+                        double* out_al, tpe_best* partial, int64_t n_partial,
+                        tpe_best* best, int32_t* err, void* stream);
+
+/* ---- categorical labels: sample (or read) + score + argmax ---------------- */
+int64_t tpe_categorical_partials(const tpe_job* host_jobs, int n_jobs);
+int tpe_score_categorical(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                          const tpe_cat_seg* csegs, const double* logp_pool,
+                          const double* cdf_pool, const double* cand, double* out_bl, double* out_al,
+                          double* out_x, tpe_best* partial, int64_t n_partial,
+                          tpe_best* best, void* stream);
+
+/* ---- sampler only (KS tests, debugging): n_cand draws of job.below ------- */
+int tpe_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+               const tpe_seg* segs, const double* mu, const double* sigma,
+               const double* wcdf, int precision, double* out_x, void* stream);
+
+/* ---- argmax combine: n_sets tpe_best arrays of n_labels each (e.g. one per
+ * rank after an all-gather) -> n_labels winners, same tie rules. ------------ */
+int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* out,
+                     void* stream);
+
+const char* tpe_last_error(void);
+int tpe_abi_version(void);
+/* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best) to out[0..n) */
+int tpe_struct_sizes(int32_t* out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TPE_HIP_H */

@@ -1,0 +1,131 @@
+"""HIP path vs the reference's own vectors (tests/golden) and vs the oracle.
+
+Every test here runs the product kernels (libtpe_hip.so) on the GPU through
+the C ABI; the oracle / golden vectors are only the checker.
+Tolerances (north_star): fp64 rtol 1e-6, fp32 rtol 1e-4 (atol 1e-4 for
+log-densities near 0); argmax indices and categorical results bit-exact.
+"""
+import numpy as np
+import pytest
+
+from oracle import tpe_oracle as O
+from tests.golden_io import E2E_CASES, load
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from hyperopt_amd.engine import Engine
+    return Engine()
+
+
+def _works_from_fixture(case):
+    from hyperopt_amd.engine import LabelWork
+    arrays, meta = load("e2e_" + case)
+    works, golden = [], []
+    for lab, lm in sorted(meta["labels"].items()):
+        if lm["n"] == 0:
+            continue
+        spec = meta["specs"][lab]
+        below, above = O.ap_split_trials(arrays["obs_idxs/" + lab], arrays["obs_vals/" + lab],
+                                         arrays["hist_tids"], arrays["hist_losses"],
+                                         meta["gamma"])
+        works.append(LabelWork(label=lab, kind=spec["kind"], args=tuple(spec["args"]),
+                               obs_below=below, obs_above=above, cand=arrays["cand/" + lab]))
+        golden.append((arrays["bl/" + lab], arrays["al/" + lab], lm["best"]))
+    return works, golden, meta
+
+
+@pytest.mark.parametrize("case", E2E_CASES)
+def test_golden_fp64(engine, case):
+    works, golden, meta = _works_from_fixture(case)
+    res = engine.run(works, prior_weight=meta["prior_weight"], precision=64, outputs=True)
+    for w, r, (bl, al, best) in zip(works, res, golden):
+        np.testing.assert_allclose(r.below_llik, bl, rtol=1e-6, atol=0, equal_nan=True,
+                                   err_msg="%s/%s below" % (case, w.label))
+        np.testing.assert_allclose(r.above_llik, al, rtol=1e-6, atol=0, equal_nan=True,
+                                   err_msg="%s/%s above" % (case, w.label))
+        assert r.index == best, (case, w.label, r.index, best)
+        assert r.value == float(w.cand[best])
+        assert r.n_scored == len(w.cand)
+
+
+@pytest.mark.parametrize("case", E2E_CASES)
+def test_golden_fp32(engine, case):
+    works, golden, meta = _works_from_fixture(case)
+    res = engine.run(works, prior_weight=meta["prior_weight"], precision=32, outputs=True)
+    for w, r, (bl, al, best) in zip(works, res, golden):
+        np.testing.assert_allclose(r.below_llik, bl, rtol=1e-4, atol=1e-4, equal_nan=True,
+                                   err_msg="%s/%s below" % (case, w.label))
+        np.testing.assert_allclose(r.above_llik, al, rtol=1e-4, atol=1e-4, equal_nan=True,
+                                   err_msg="%s/%s above" % (case, w.label))
+        score = bl - al
+        if w.kind in ("randint", "categorical") or w.kind.startswith("q"):
+            assert r.index == best  # fp64 paths: exact
+        else:
+            # fp32 may pick a different candidate only within fp32 error of the max
+            assert score[r.index] >= np.nanmax(score) - 1e-4 * max(1.0, abs(np.nanmax(score)))
+
+
+def _mixture_case(rng, kind, args, n_obs_b, n_obs_a, n_cand):
+    from hyperopt_amd.engine import LabelWork
+    fam, pmu, psig, tf, low, high, q = O.posterior_spec(kind, args)
+    if kind in ("uniform", "quniform"):
+        draw = lambda n: rng.uniform(args[0], args[1], n)  # noqa: E731
+    elif kind in ("loguniform", "qloguniform"):
+        draw = lambda n: np.exp(rng.uniform(args[0], args[1], n))  # noqa: E731
+    elif kind in ("normal", "qnormal"):
+        draw = lambda n: rng.normal(args[0], args[1], n)  # noqa: E731
+    else:
+        draw = lambda n: np.exp(rng.normal(args[0], args[1], n))  # noqa: E731
+    obs_b, obs_a, cand = draw(n_obs_b), draw(n_obs_a), draw(n_cand)
+    if q is not None:
+        obs_b, obs_a, cand = (np.round(v / q) * q for v in (obs_b, obs_a, cand))
+    return LabelWork(label=kind, kind=kind, args=args, obs_below=obs_b, obs_above=obs_a,
+                     cand=cand)
+
+
+KINDS = [("uniform", (-5.0, 5.0)), ("loguniform", (-5.0, 0.0)), ("normal", (0.0, 2.0)),
+         ("lognormal", (0.0, 1.0)), ("quniform", (0.0, 100.0, 1.0)),
+         ("qloguniform", (0.0, 4.0, 1.0)), ("qnormal", (0.0, 10.0, 2.0)),
+         ("qlognormal", (0.0, 1.0, 0.5))]
+
+
+@pytest.mark.parametrize("kind,args", KINDS)
+@pytest.mark.parametrize("n_above", [0, 1, 2, 30, 3000])
+def test_oracle_random_mixtures(engine, kind, args, n_above):
+    """Bigger / edge histories than the goldens: HIP fp64 vs the oracle."""
+    rng = np.random.RandomState(hash((kind, n_above)) % (2 ** 31))
+    w = _mixture_case(rng, kind, args, min(n_above, 25), n_above, 2048)
+    r64, = engine.run([w], precision=64, outputs=True)
+    with np.errstate(all="ignore"):
+        ref = O.continuous_label_scores(kind, args, w.obs_below, w.obs_above, w.cand)
+    np.testing.assert_allclose(r64.below_llik, ref["below_llik"], rtol=1e-6, equal_nan=True)
+    np.testing.assert_allclose(r64.above_llik, ref["above_llik"], rtol=1e-6, equal_nan=True)
+    assert r64.index == ref["best"]
+    r32, = engine.run([w], precision=32, outputs=True)
+    np.testing.assert_allclose(r32.below_llik, ref["below_llik"], rtol=1e-4, atol=1e-4,
+                               equal_nan=True)
+    np.testing.assert_allclose(r32.above_llik, ref["above_llik"], rtol=1e-4, atol=1e-4,
+                               equal_nan=True)
+
+
+def test_argmax_ties_and_far_tails(engine):
+    """Duplicate candidates (exact score ties -> first index) and far-tail
+    candidates (fp32 exact-LSE fallback path)."""
+    from hyperopt_amd.engine import LabelWork
+    rng = np.random.RandomState(7)
+    obs_b = rng.uniform(-5, 5, 25)
+    obs_a = rng.uniform(-5, 5, 4000)
+    base = rng.uniform(-5, 5, 300)
+    cand = np.concatenate([base, base[::-1], [-1e3, 1e3, 60.0, -60.0]])
+    w = LabelWork("x", "uniform", (-5.0, 5.0), obs_b, obs_a, cand=cand)
+    with np.errstate(all="ignore"):
+        ref = O.continuous_label_scores("uniform", (-5.0, 5.0), obs_b, obs_a, cand)
+    r64, = engine.run([w], precision=64, outputs=True)
+    assert r64.index == ref["best"]
+    np.testing.assert_allclose(r64.above_llik, ref["above_llik"], rtol=1e-6)
+    r32, = engine.run([w], precision=32, outputs=True)
+    np.testing.assert_allclose(r32.above_llik, ref["above_llik"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(r32.below_llik, ref["below_llik"], rtol=1e-4, atol=1e-4)
