@@ -1,0 +1,238 @@
+#!/usr/bin/env python
+"""Benchmark: EI candidates scored/sec for one TPE suggest step on config C3.
+
+Workload (BASELINE.json configs[2]): a 50-dim mixed space
+(10 x uniform(-5,5), 10 x loguniform(-5,0), 10 x quniform(0,100,1),
+10 x normal(0,2), 10 x choice(8)), a 10k-trial history drawn from the prior
+(seed 0) with N(0,1) losses (seed 1), and 2^22 EI candidates per label per
+GPU.  One step = one full suggest level on the device path: the below/above
+split of the resident columnar history, the Parzen fit of all 100 mixtures,
+sampling 50 x 2^22 candidates from the below posteriors, scoring each under
+both posteriors, and the per-label argmax (plus the cross-GPU max-loc combine
+when N > 1).  Scaling is weak: every rank scores 2^22 candidates per label
+(its own global index range), the job total grows with N.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+T_HIST = 10_000
+N_CAND = 1 << 22
+FP32_PEAK_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
+FLOPS_PER_PAIR = 9  # unquantized GMM1/LGMM1 pair
+
+
+def c3_space():
+    kinds = []
+    for i in range(10):
+        kinds += [("u%d" % i, "uniform", (-5.0, 5.0)), ("lu%d" % i, "loguniform", (-5.0, 0.0)),
+                  ("qu%d" % i, "quniform", (0.0, 100.0, 1.0)), ("n%d" % i, "normal", (0.0, 2.0)),
+                  ("c%d" % i, "randint", (8,))]
+    return kinds
+
+
+def c3_history(space, T=T_HIST):
+    """Prior draws (seed 0) and N(0,1) losses (seed 1): SURVEY.md §8(d) C3."""
+    rng = np.random.RandomState(0)
+    vals = {}
+    for lab, kind, a in space:
+        if kind == "uniform":
+            v = rng.uniform(a[0], a[1], T)
+        elif kind == "loguniform":
+            v = np.exp(rng.uniform(a[0], a[1], T))
+        elif kind == "quniform":
+            v = np.round(rng.uniform(a[0], a[1], T) / a[2]) * a[2]
+        elif kind == "normal":
+            v = rng.normal(a[0], a[1], T)
+        else:
+            v = rng.randint(0, a[0], T).astype(np.float64)
+        vals[lab] = v
+    losses = np.random.RandomState(1).normal(size=T)
+    return vals, losses
+
+
+def split(vals, losses, gamma=0.25):
+    """ap_split_trials for every label at once (tpe.py:623-646), columnar."""
+    T = losses.size
+    n_below = min(int(math.ceil(gamma * math.sqrt(T))), 25)
+    order = np.argsort(losses, kind="stable")
+    isb = np.zeros(T, bool)
+    isb[order[:n_below]] = True
+    return {lab: (v[isb], v[~isb]) for lab, v in vals.items()}
+
+
+def label_key(seed, step, lab):
+    h = 1469598103934665603
+    for ch in ("%d/%d/%s" % (seed, step, lab)).encode():
+        h = ((h ^ ch) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def make_works(space, splits, step, n_cand, cand_base):
+    from hyperopt_amd.engine import LabelWork
+    return [LabelWork(label=lab, kind=kind, args=a, obs_below=splits[lab][0],
+                      obs_above=splits[lab][1], n_cand=n_cand, key=label_key(0, step, lab),
+                      cand_base=cand_base) for lab, kind, a in space]
+
+
+def cpu_baseline(space, vals, losses, seconds_hint=True):
+    """The oracle (numpy restatement of tpe.suggest's per-label pipeline) on a
+    bounded sample: one label of each kind, 2048 candidates each, same 10k
+    history.  Test infrastructure only -- never on the product path."""
+    from oracle import tpe_oracle as O
+    sp = split(vals, losses)
+    picks = [s for s in space if s[0] in ("u0", "lu0", "qu0", "n0", "c0")]
+    n = 8192
+    rng = np.random.RandomState(5)
+    t0 = time.perf_counter()
+    for lab, kind, a in picks:
+        below, above = sp[lab]
+        if kind == "randint":
+            pb = O.randint_posterior(below, 1.0, a[0])
+            cand = rng.choice(a[0], size=n, p=pb)
+            O.categorical_label_scores(kind, a, below, above, cand)
+            continue
+        fam, pmu, psig, tf, low, high, q = O.posterior_spec(kind, a)
+        post_b = O.adaptive_parzen_normal(tf(below), 1.0, pmu, psig)
+        samp = O.gmm1_sample if fam == "GMM1" else O.lgmm1_sample
+        cand = samp(*post_b, low=low, high=high, q=q, rng=rng, size=n)
+        with np.errstate(all="ignore"):
+            O.continuous_label_scores(kind, a, below, above, cand)
+    dt = time.perf_counter() - t0
+    return {"value": len(picks) * n / dt, "unit": "EI candidates/s", "cores": 1, "kind": "port",
+            "sample": "oracle/tpe_oracle.py numpy pipeline (fit+sample+score+argmax), 5 labels "
+                      "(uniform, loguniform, quniform, normal, choice8) x %d candidates, 10k-trial "
+                      "history, %.2f s on %s" % (n, dt, platform.processor() or platform.machine())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--precision", type=int, default=32)
+    ap.add_argument("--n-cand", type=int, default=N_CAND)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd import dist as hdist
+
+    space = c3_space()
+    vals, losses = c3_history(space)
+    eng = Engine()
+    n_cand = args.n_cand
+    cand_base = rank * n_cand
+
+    def step(k, timers=None):
+        sp = split(vals, losses)
+        works = make_works(space, sp, k, n_cand, cand_base)
+        res = eng.run(works, precision=args.precision, timers=timers)
+        if world > 1:
+            hdist.allreduce_best(res)
+        return works, res
+
+    for k in range(args.warmup):
+        step(k)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    timers = {}
+    step_times = []
+    barrier()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        t0 = time.perf_counter()
+        works, res = step(args.warmup + k, timers)
+        step_times.append(time.perf_counter() - t0)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # dominant kernel: unquantized continuous scoring (k_score32 + its reduce)
+    cont = [w for w in works if w.kind in ("uniform", "loguniform", "normal", "lognormal")]
+    pairs = sum(n_cand * (w.obs_below.size + 1 + w.obs_above.size + 1) for w in cont)
+    flops = pairs * FLOPS_PER_PAIR
+    cont_ms = [e0.elapsed_time(e1) for e0, e1 in timers.get("cont", [])]
+    avg_ms = float(np.mean(cont_ms)) if cont_ms else float("nan")
+    achieved = flops / (avg_ms * 1e-3) / 1e12
+    group_ms = {k: round(float(np.mean([a.elapsed_time(b) for a, b in v])), 4)
+                for k, v in timers.items()}
+
+    total_cand = len(space) * n_cand * world * args.steps
+    value = total_cand / elapsed
+    traffic = None
+    tfile = os.path.join(HERE, "profiles", "traffic_k_score32.json")
+    if os.path.exists(tfile):
+        try:
+            traffic = json.load(open(tfile)).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    line = {
+        "metric": "EI candidates scored/sec (50-dim, 10k trials)",
+        "value": value,
+        "unit": "EI candidates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "suggest_p50_ms": float(np.median(step_times)) * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if args.precision == 32 else "f64",
+        "data": "synthetic: prior draws (seed 0), N(0,1) losses (seed 1), Philox candidates",
+        "config": {"workload": "C3: 50-dim mixed (10x uniform/loguniform/quniform/normal/"
+                               "choice8), 10k-trial history, 2^%d EI candidates per label per GPU"
+                               % int(round(math.log2(n_cand))),
+                   "labels": len(space), "history": T_HIST, "candidates_per_label": n_cand,
+                   "parallelism": "candidate-sharded x%d, RCCL max-loc combine" % world},
+        "roofline": {"bound": "valu", "kernel": "k_score32 (tpe_score_continuous)",
+                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
+                     "algorithmic_flops_per_launch": flops, "avg_launch_ms": avg_ms,
+                     "flops_per_pair": FLOPS_PER_PAIR},
+        "group_ms": group_ms,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(space, vals, losses)
+    elif rank == 0:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

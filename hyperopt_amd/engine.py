@@ -159,8 +159,21 @@ class Engine:
 
     # -- main entry ----------------------------------------------------------
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
-            outputs=False, stream=None) -> List[LabelResult]:
+            outputs=False, stream=None, timers=None) -> List[LabelResult]:
+        """Run one level.  ``timers`` (optional dict) collects HIP event pairs
+        per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``."""
         torch = self.torch
+
+        def tick():
+            if timers is None:
+                return None
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            return e
+
+        def tock(name, e0):
+            if timers is not None:
+                timers.setdefault(name, []).append((e0, tick()))
         lib = self.lib
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
@@ -330,13 +343,17 @@ class Engine:
             d_c64 = self._buf("coef64", 32 * n_comp)
             d_c32 = self._buf("coef32", 16 * n_comp)
             d_xf = self._buf("xf", 8 * max(obs_pool.size, 1))
+            e0 = tick()
             L.check(lib.tpe_parzen_fit(base + o_obs, d_xf, d_segs, len(segs), max_obs, d_w, d_mu,
                                        d_sig, d_cdf, d_c64, d_c32, sp), "tpe_parzen_fit")
+            tock("fit", e0)
         if cat:
             d_logp = self._buf("cat_logp", 8 * p_pool.size)
             d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
+            e0 = tick()
             L.check(lib.tpe_cat_posterior(base + o_cobs, d_csegs, len(csegs), base + o_p, d_logp,
                                           d_ccdf, sp), "tpe_cat_posterior")
+            tock("cat_fit", e0)
 
         # ---- scoring, one call per group ----------------------------------------
         for g, (kind, ids) in enumerate(groups):
@@ -348,6 +365,7 @@ class Engine:
             dj = base + o_jobs + a * JS
             db = d_best + a * BS
             nj = b - a
+            e0 = tick()
             if kind == "cont":
                 npart = lib.tpe_score_partials(hjp, nj)
                 d_part = self._buf("partial", 32 * max(npart, 1))
@@ -388,6 +406,7 @@ class Engine:
                 L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf, d_cand,
                                                   d_bl, d_al, d_x, d_part, npart, db, sp),
                         "tpe_score_categorical")
+            tock(kind, e0)
 
         # ---- results (one device->host copy; syncs the stream) --------------------
         with torch.cuda.stream(stream):
