@@ -159,9 +159,13 @@ class Engine:
 
     # -- main entry ----------------------------------------------------------
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
-            outputs=False, stream=None, timers=None) -> List[LabelResult]:
+            outputs=False, stream=None, timers=None, sample_only=False) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
-        per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``."""
+        per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``.
+        ``sample_only``: fit, then only draw the candidates of the continuous
+        labels (tpe_sample) into ``LabelResult.cand`` -- the sampler test hook."""
+        if sample_only:
+            outputs = True
         torch = self.torch
 
         def tick():
@@ -358,6 +362,14 @@ class Engine:
         # ---- scoring, one call per group ----------------------------------------
         for g, (kind, ids) in enumerate(groups):
             if not ids:
+                continue
+            if sample_only:
+                if kind in ("cont", "lat", "qfb"):
+                    a, b = _slice_of(groups, g)
+                    hj = jobs[a:b]
+                    L.check(lib.tpe_sample(base + o_jobs + a * L.JOB_DTYPE.itemsize,
+                                           hj.ctypes.data_as(ctypes.c_void_p), b - a, d_segs,
+                                           d_mu, d_sig, d_cdf, precision, d_x, sp), "tpe_sample")
                 continue
             a, b = _slice_of(groups, g)
             hj = jobs[a:b]

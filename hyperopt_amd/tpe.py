@@ -1,0 +1,212 @@
+"""Tree-of-Parzen-Estimators suggest on MI355X: drop-in for hyperopt.tpe.suggest.
+
+    fmin(fn, space, algo=hyperopt_amd.tpe.suggest, ...)
+    algo = functools.partial(tpe.suggest, n_EI_candidates=2**20, gamma=0.25)
+
+Same signature, defaults, startup rule, history rules and returned document
+as the reference (hyperopt/tpe.py:837-964):
+  * per-tid best loss, ``from_tid`` aliasing, None -> +inf (tpe.py:874-896);
+  * fewer than ``n_startup_jobs`` distinct tids -> rand.suggest (tpe.py:909-911);
+  * the below set is the best min(ceil(gamma*sqrt(T)), 25) tids (tpe.py:637);
+  * every live label gets ``n_EI_candidates`` candidates drawn from its below
+    posterior, scored by l(x)/g(x), and the argmax is kept (tpe.py:649-658);
+  * one document for ``new_ids[0]`` with ``randint(low, high)`` offsets
+    re-applied (tpe.py:945-964).
+Differences (documented in DESIGN.md): candidates come from counter-based
+Philox streams (the reference's RandomState streams cannot be reproduced),
+ties in sorts are stable, and the numeric work runs on the GPU through
+``hyperopt_amd.engine`` -- there is no CPU fallback.
+
+Extra keyword arguments: ``linear_forgetting`` (25), ``precision`` (None =
+auto: float64 when n_EI_candidates x history is small, float32 otherwise;
+or 32 / 64; env HYPEROPT_AMD_PRECISION).  Under torch.distributed each rank
+scores its share of the candidates and the winners are combined with an
+all-gather + device max-loc (hyperopt_amd/dist.py).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import time
+
+import numpy as np
+
+from . import dist as hdist
+from . import rand
+from .engine import DEFAULT_LF, Engine, LabelWork
+
+logger = logging.getLogger(__name__)
+
+EPS = 1e-12
+_default_prior_weight = 1.0
+_default_n_EI_candidates = 24
+_default_gamma = 0.25
+_default_n_startup_jobs = 20
+_default_linear_forgetting = DEFAULT_LF
+
+_engines = {}
+
+
+def engine():
+    """The Engine of the current device (created on first use)."""
+    import torch
+    dev = torch.cuda.current_device()
+    eng = _engines.get(dev)
+    if eng is None:
+        eng = _engines[dev] = Engine(torch.device("cuda", dev))
+    return eng
+
+
+def label_key(seed, label):
+    """64-bit Philox key for (suggest seed, label): FNV-1a then a splitmix finaliser."""
+    h = 0xCBF29CE484222325
+    for ch in ("%d:%s" % (int(seed), label)).encode():
+        h = ((h ^ ch) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    h ^= h >> 30
+    h = (h * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    h ^= h >> 27
+    h = (h * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return h ^ (h >> 31)
+
+
+class History(object):
+    """The history tpe.suggest conditions on, one row per distinct tid."""
+
+    def __init__(self, tids, losses, obs_tids, vals, active):
+        self.tids = tids          # (T,) loss tids, sorted
+        self.losses = losses      # (T,) float64, +inf for unfinished/failed
+        self.obs_tids = obs_tids  # (T,) the tid each row's observations are filed under
+        self.vals = vals          # (T, L) float64
+        self.active = active      # (T, L) bool
+
+
+def collect_history(trials, labels):
+    """Best document per tid, sorted by tid (tpe.py:874-896), as columns."""
+    best_loss, best_doc = {}, {}
+    for doc in trials.trials:
+        tid = doc["misc"].get("from_tid", doc["tid"])
+        loss = doc["result"].get("loss")
+        loss = float("inf") if loss is None else float(loss)
+        prev = best_loss.get(tid)
+        if prev is None or loss <= prev:
+            best_loss[tid] = loss
+            best_doc[tid] = doc
+    tids = sorted(best_doc)
+    docs = [best_doc[t] for t in tids]
+    losses = np.array([best_loss[t] for t in tids], dtype=np.float64)
+    obs_tids = np.array([d["misc"]["tid"] for d in docs], dtype=np.int64)
+    L = len(labels)
+    col = trials.columnar(labels) if hasattr(trials, "columnar") else None
+    if col is not None and all(id(d) in col.row_of for d in docs):
+        rows = np.fromiter((col.row_of[id(d)] for d in docs), dtype=np.int64, count=len(docs))
+        vals, active = col.vals[rows], col.active[rows]
+    else:
+        index = {lab: j for j, lab in enumerate(labels)}
+        vals = np.full((len(docs), L), np.nan)
+        active = np.zeros((len(docs), L), bool)
+        for r, d in enumerate(docs):
+            for lab, vv in d["misc"]["vals"].items():
+                j = index.get(lab)
+                if j is not None and len(vv):
+                    vals[r, j] = float(vv[0])
+                    active[r, j] = True
+    return History(np.asarray(tids, dtype=np.int64), losses, obs_tids, vals, active)
+
+
+def split_masks(hist, gamma, gamma_cap=DEFAULT_LF):
+    """Row masks of the below / above sets (ap_split_trials, tpe.py:623-646).
+
+    Membership is decided on loss tids, observations are matched on the tid
+    they are filed under -- the reference's behaviour for from_tid documents.
+    """
+    T = hist.losses.size
+    n_below = min(int(np.ceil(gamma * np.sqrt(T))), gamma_cap)
+    order = np.argsort(hist.losses, kind="stable")
+    below_tids = hist.tids[order[:n_below]]
+    above_tids = hist.tids[order[n_below:]]
+    return np.isin(hist.obs_tids, below_tids), np.isin(hist.obs_tids, above_tids)
+
+
+def _precision(precision, n_ei, T):
+    if precision is None:
+        env = os.environ.get("HYPEROPT_AMD_PRECISION", "")
+        if env:
+            precision = int(env)
+        else:
+            precision = 64 if n_ei * max(T, 1) <= (1 << 24) else 32
+    if precision not in (32, 64):
+        raise ValueError("precision must be 32 or 64", precision)
+    return precision
+
+
+def _decode(spec, value):
+    """Engine value -> (value used by switches, value stored in the trial)."""
+    if spec.kind == "randint":
+        k = int(round(value))
+        offset = int(spec.args[0]) if spec.args[1] is not None else 0
+        return k, k + offset  # tpe.py:945-948
+    if spec.kind == "categorical":
+        k = int(round(value))
+        return k, k
+    return float(value), float(value)
+
+
+def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
+            n_startup_jobs=_default_n_startup_jobs, n_EI_candidates=_default_n_EI_candidates,
+            gamma=_default_gamma, verbose=True, linear_forgetting=_default_linear_forgetting,
+            precision=None):
+    """TPE suggest: one new trial document for new_ids[0] (tpe.py:837-964)."""
+    t0 = time.time()
+    labels = list(domain.params)
+    hist = collect_history(trials, labels)
+    if verbose:
+        if hist.tids.size:
+            logger.info("TPE using %i/%i trials with best loss %f" % (
+                hist.tids.size, len(trials), np.nanmin(hist.losses)))
+        else:
+            logger.info("TPE using 0 trials")
+    if hist.tids.size < n_startup_jobs:
+        return rand.suggest(new_ids, domain, trials, seed)
+
+    first_new_id = new_ids[0]
+    isb, isa = split_masks(hist, gamma)
+    prec = _precision(precision, n_EI_candidates, hist.tids.size)
+    rank, ws = hdist.world()
+    start, count = hdist.shard(max(int(n_EI_candidates), 0), rank, ws)
+    col = {lab: j for j, lab in enumerate(labels)}
+
+    walk, stored = {}, {}
+    live = []
+    if n_EI_candidates > 0:
+        eng = engine()
+        while True:
+            live = domain.reachable(walk)
+            level = [lab for lab in live if lab not in walk]
+            if not level:
+                break
+            works = []
+            for lab in level:
+                spec = domain.specs[lab]
+                j = col[lab]
+                act = hist.active[:, j]
+                v = hist.vals[:, j]
+                works.append(LabelWork(label=lab, kind=spec.kind, args=spec.args,
+                                       obs_below=v[act & isb], obs_above=v[act & isa],
+                                       n_cand=count, key=label_key(seed, lab), cand_base=start))
+            res = eng.run(works, prior_weight=prior_weight, lf=linear_forgetting,
+                          precision=prec)
+            if ws > 1:
+                hdist.allreduce_best(res)
+            for lab, r in zip(level, res):
+                walk[lab], stored[lab] = _decode(domain.specs[lab], r.value)
+    live = set(live)
+    misc = {"tid": first_new_id, "cmd": domain.cmd, "workdir": domain.workdir,
+            "idxs": {lab: ([first_new_id] if lab in live else []) for lab in labels},
+            "vals": {lab: ([stored[lab]] if lab in live else []) for lab in labels}}
+    if verbose:
+        logger.info("tpe.suggest took %f seconds" % (time.time() - t0))
+    return trials.new_trial_docs([first_new_id], [None], [domain.new_result()], [misc])
+
+
+_ = math

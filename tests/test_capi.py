@@ -1,0 +1,63 @@
+"""The C-ABI library loads without a GPU and exports every entry point that
+include/tpe_hip.h declares; argument errors are reported, never crash."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from hyperopt_amd import _lib as L
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                      "tpe_hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+(tpe_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_symbols_exported():
+    lib = L.load()
+    names = declared_functions()
+    assert len(names) >= 15, names
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(L._SIGNATURES), set(names) ^ set(L._SIGNATURES)
+
+
+def test_struct_sizes_and_abi():
+    lib = L.load()
+    assert lib.tpe_abi_version() == 1
+    sizes = (ctypes.c_int32 * 4)()
+    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 4) == 4
+    assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
+                            L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize)
+
+
+def test_argument_errors_are_reported():
+    lib = L.load()
+    jobs = np.zeros(1, L.JOB_DTYPE)
+    jobs["n_cand"] = -5
+    hp_ = jobs.ctypes.data_as(ctypes.c_void_p)
+    rc = lib.tpe_score_continuous(None, hp_, 1, None, None, None, None, None, None, None, None,
+                                  32, None, None, None, None, 0, None, None)
+    assert rc == -1
+    assert b"n_cand" in lib.tpe_last_error()
+    jobs["n_cand"] = 10
+    jobs["flags"] = L.F_QUANT
+    rc = lib.tpe_score_continuous(None, hp_, 1, None, None, None, None, None, None, None, None,
+                                  32, None, None, None, None, 0, None, None)
+    assert rc == -1 and b"not an unquantized" in lib.tpe_last_error()
+    rc = lib.tpe_score_continuous(None, hp_, 0, None, None, None, None, None, None, None, None,
+                                  48, None, None, None, None, 0, None, None)
+    assert rc == 0  # nothing to do
+    assert lib.tpe_parzen_fit(None, None, None, 0, 0, None, None, None, None, None, None,
+                              None) == 0
+    assert lib.tpe_parzen_fit(None, None, None, -1, 0, None, None, None, None, None, None,
+                              None) == -1
+    assert lib.tpe_best_combine(None, 0, 1, None, None) == -1
+    with pytest.raises(L.TpeHipError):
+        L.check(-1, "probe")

@@ -1,0 +1,245 @@
+"""Host-side drop-in API (no GPU): hp, Domain, Trials, fmin with rand.suggest,
+and the columnar history / split that feeds the GPU engine, pinned against the
+oracle on the reference's own histories (tests/golden)."""
+import numpy as np
+import pytest
+
+from hyperopt_amd import (STATUS_FAIL, STATUS_OK, AllTrialsFailed, Domain, DuplicateLabel,
+                          InvalidTrial, Trials, fmin, hp, pyll, rand, space_eval,
+                          trials_from_docs)
+from hyperopt_amd import tpe
+from hyperopt_amd.fmin import generate_trials_to_calculate
+from hyperopt_amd.pyll import scope
+from oracle import tpe_oracle as O
+from tests.golden import spaces
+from tests.golden_io import E2E_CASES, load
+
+
+def test_hp_validation():
+    with pytest.raises(TypeError):
+        hp.uniform(3, 0, 1)
+    with pytest.raises(ValueError):
+        hp.uniform("x", 2, 1)
+    hp.uniform("x", 0, -1)  # reference quirk: a falsy bound skips the check
+    with pytest.raises(DuplicateLabel):
+        Domain(lambda x: 0, {"a": hp.uniform("x", 0, 1), "b": hp.normal("x", 0, 1)})
+
+
+def test_param_specs():
+    d = Domain(lambda x: 0, spaces.many_dists(hp))
+    kinds = {k: s.kind for k, s in d.specs.items()}
+    assert kinds["a"] == "randint" and kinds["k"] == "categorical" and kinds["f"] == "qloguniform"
+    assert d.specs["bb"].args == (12, 25)
+    assert d.specs["b"].args == (10, None)
+    np.testing.assert_allclose(d.specs["k"].args[0], [0.1, 0.3, 0.6])
+    d2 = Domain(lambda x: 0, {"x": hp.uniform("x", low=-1, high=2)})
+    assert d2.specs["x"].args == (-1, 2)
+
+
+def test_reachable_nested():
+    d = Domain(lambda x: 0, spaces.nested(hp))
+    assert d.reachable({}) == ["root"]
+    assert set(d.reachable({"root": 1})) == {"root", "tree_depth", "tree_split"}
+    assert set(d.reachable({"root": 1, "tree_split": 1})) == {"root", "tree_depth", "tree_split",
+                                                                "ent_w", "ent_s"}
+    assert set(d.reachable({"root": 2})) == {"root", "nn_units", "nn_drop"}
+
+
+def test_rand_suggest_docs_and_space_eval():
+    sp = spaces.nested(hp)
+    d = Domain(lambda x: 0, sp)
+    t = Trials()
+    docs = rand.suggest([0, 1, 2], d, t, 5)
+    assert [doc["tid"] for doc in docs] == [0, 1, 2]
+    for doc in docs:
+        t.assert_valid_trial(doc)
+        vals = doc["misc"]["vals"]
+        live = set(d.reachable({k: v[0] for k, v in vals.items() if v}))
+        assert {k for k, v in vals.items() if v} == live
+        cfg = {k: v[0] for k, v in vals.items() if v}
+        out = space_eval(sp, cfg)
+        assert out["kind"] in ("lin", "tree", "nn")
+
+
+def test_fmin_rand_quadratic():
+    trials = Trials()
+    best = fmin(lambda x: (x - 1) ** 2, hp.uniform("x", -5, 5), algo=rand.suggest,
+                max_evals=200, trials=trials, rstate=np.random.RandomState(0),
+                show_progressbar=False)
+    assert len(trials) == 200 and abs(best["x"] - 1) < 0.3
+    assert trials.argmin == best
+    assert trials.best_trial["result"]["loss"] == min(trials.losses())
+
+
+def test_fmin_options():
+    # points_to_evaluate, early stop, loss threshold, return_argmin=False
+    trials = generate_trials_to_calculate([{"x": 0.5}, {"x": 1.5}])
+    fmin(lambda x: (x - 1) ** 2, hp.uniform("x", -5, 5), algo=rand.suggest, max_evals=5,
+         trials=trials, rstate=np.random.RandomState(1), show_progressbar=False)
+    # like the reference, points are evaluated on top of max_evals (fmin.py:459-465)
+    assert len(trials) == 7 and trials.trials[0]["misc"]["vals"]["x"] == [0.5]
+
+    def stop_after(trials, count=0):
+        return count + 1 >= 3, [count + 1]
+
+    t2 = Trials()
+    fmin(lambda x: x, hp.uniform("x", 0, 1), algo=rand.suggest, max_evals=100, trials=t2,
+         early_stop_fn=stop_after, rstate=np.random.RandomState(2), show_progressbar=False)
+    assert len(t2) == 3
+    t3 = Trials()
+    fmin(lambda x: x, hp.uniform("x", 0, 1), algo=rand.suggest, max_evals=1000, trials=t3,
+         loss_threshold=0.5, rstate=np.random.RandomState(3), show_progressbar=False)
+    assert len(t3) < 1000 and min(t3.losses()) < 0.5
+    out = fmin(lambda p: p[1] ** 2 if p[0] == "b" else 1.0,
+               hp.choice("c", [("a", 1.0), ("b", hp.uniform("y", -1, 1))]), algo=rand.suggest,
+               max_evals=30, rstate=np.random.RandomState(4), return_argmin=False,
+               show_progressbar=False)
+    assert out[0] in ("a", "b")
+
+
+def test_fmin_failures():
+    def fn(x):
+        return {"status": STATUS_FAIL}
+
+    t = Trials()
+    with pytest.raises(AllTrialsFailed):  # space_eval(trials.argmin), as fmin.py:546-549
+        fmin(fn, hp.uniform("x", 0, 1), algo=rand.suggest, max_evals=5, trials=t,
+             rstate=np.random.RandomState(0), show_progressbar=False, return_argmin=False)
+    assert len(t) == 5
+    with pytest.raises(AllTrialsFailed):
+        t.best_trial
+
+    def boom(x):
+        raise RuntimeError("x")
+
+    t2 = Trials()
+    fmin(boom, hp.uniform("x", 0, 1), algo=rand.suggest, max_evals=3, trials=t2,
+         catch_eval_exceptions=True, rstate=np.random.RandomState(0), show_progressbar=False,
+         return_argmin=False)
+    assert len(t2) == 0 and len(t2._dynamic_trials) == 3
+    with pytest.raises(RuntimeError):
+        fmin(boom, hp.uniform("x", 0, 1), algo=rand.suggest, max_evals=3,
+             rstate=np.random.RandomState(0), show_progressbar=False)
+
+
+def test_trials_semantics():
+    t = Trials()
+    with pytest.raises(InvalidTrial):
+        t.insert_trial_doc({"tid": 0})
+    ids = t.new_trial_ids(3)
+    assert ids == [0, 1, 2]
+    docs = t.new_trial_docs(ids, [None] * 3, [{"status": "new"}] * 3,
+                            [{"tid": i, "cmd": None, "idxs": {"x": [i]}, "vals": {"x": [i * 0.1]}}
+                             for i in ids])
+    t.insert_trial_docs(docs)
+    assert len(t) == 0  # not refreshed yet
+    t.refresh()
+    assert len(t) == 3 and t.count_by_state_synced(0) == 3
+    t._dynamic_trials[1]["state"] = 3  # error jobs disappear on refresh
+    t.refresh()
+    assert t.tids == [0, 2]
+    t2 = trials_from_docs([dict(d) for d in t.trials])
+    assert t2.tids == [0, 2]
+    assert t.idxs_vals[1]["x"] == [0.0, 0.2]
+
+
+def test_columnar_cache_incremental():
+    trials = Trials()
+    sp = spaces.nested(hp)
+    fmin(lambda p: 0.0, sp, algo=rand.suggest, max_evals=20, trials=trials,
+         rstate=np.random.RandomState(0), show_progressbar=False)
+    d = Domain(lambda x: 0, sp)
+    labels = list(d.params)
+    c1 = trials.columnar(labels)
+    assert c1.rows == 20
+    fmin(lambda p: 0.0, sp, algo=rand.suggest, max_evals=35, trials=trials,
+         rstate=np.random.RandomState(1), show_progressbar=False)
+    c2 = trials.columnar(labels)
+    assert c2 is c1 and c2.rows == 35
+    for r, doc in enumerate(trials._dynamic_trials):
+        for j, lab in enumerate(labels):
+            v = doc["misc"]["vals"][lab]
+            assert c2.active[r, j] == bool(v)
+            if v:
+                assert c2.vals[r, j] == v[0]
+
+
+def _trials_from_fixture(arrays, meta):
+    tids = arrays["hist_tids"]
+    losses = arrays["hist_losses"]
+    labels = sorted(meta["specs"])
+    docs = []
+    for tid, loss in zip(tids, losses):
+        idxs, vals = {}, {}
+        for lab in labels:
+            oi = arrays["obs_idxs/" + lab]
+            pos = np.nonzero(oi == tid)[0]
+            idxs[lab] = [int(tid)] if pos.size else []
+            vals[lab] = [float(arrays["obs_vals/" + lab][pos[0]])] if pos.size else []
+        result = {"status": STATUS_OK, "loss": float(loss)} if np.isfinite(loss) else \
+            {"status": STATUS_FAIL}
+        docs.append({"state": 2, "tid": int(tid), "spec": None, "result": result,
+                     "misc": {"tid": int(tid), "cmd": None, "workdir": None, "idxs": idxs,
+                              "vals": vals},
+                     "exp_key": None, "owner": None, "version": 0, "book_time": None,
+                     "refresh_time": None})
+    return trials_from_docs(docs), labels
+
+
+@pytest.mark.parametrize("case", E2E_CASES)
+def test_history_split_matches_reference(case):
+    """collect_history + split_masks == ap_split_trials on the reference's histories."""
+    arrays, meta = load("e2e_" + case)
+    trials, labels = _trials_from_fixture(arrays, meta)
+    hist = tpe.collect_history(trials, labels)
+    np.testing.assert_array_equal(hist.tids, arrays["hist_tids"])
+    np.testing.assert_array_equal(hist.losses, arrays["hist_losses"])
+    isb, isa = tpe.split_masks(hist, meta["gamma"])
+    for j, lab in enumerate(labels):
+        act = hist.active[:, j]
+        below, above = O.ap_split_trials(arrays["obs_idxs/" + lab], arrays["obs_vals/" + lab],
+                                         arrays["hist_tids"], arrays["hist_losses"], meta["gamma"])
+        np.testing.assert_array_equal(hist.vals[act & isb, j], below)
+        np.testing.assert_array_equal(hist.vals[act & isa, j], above)
+
+
+def test_history_from_tid_and_duplicates():
+    """Per-tid best loss with from_tid aliasing (tpe.py:876-896)."""
+    t = Trials()
+    mk = lambda tid, loss, x, src=None: {  # noqa: E731
+        "state": 2, "tid": tid, "spec": None,
+        "result": {"status": "ok", "loss": loss} if loss is not None else {"status": "new"},
+        "misc": dict({"tid": tid, "cmd": None, "idxs": {"x": [tid]}, "vals": {"x": [x]}},
+                     **({"from_tid": src} if src is not None else {})),
+        "exp_key": None, "owner": None, "version": 0, "book_time": None, "refresh_time": None}
+    t.insert_trial_docs([mk(0, 3.0, 0.1), mk(1, None, 0.2), mk(2, 1.0, 0.3, src=0),
+                         mk(3, 2.0, 0.4)])
+    t.refresh()
+    h = tpe.collect_history(t, ["x"])
+    assert list(h.tids) == [0, 1, 3]
+    assert list(h.losses) == [1.0, np.inf, 2.0]
+    assert list(h.obs_tids) == [2, 1, 3]
+
+
+def test_label_key_and_precision():
+    assert tpe.label_key(1, "x") == tpe.label_key(1, "x")
+    assert tpe.label_key(1, "x") != tpe.label_key(2, "x")
+    assert tpe.label_key(1, "x") != tpe.label_key(1, "y")
+    assert tpe._precision(None, 24, 100) == 64
+    assert tpe._precision(None, 1 << 22, 10_000) == 32
+    with pytest.raises(ValueError):
+        tpe._precision(16, 1, 1)
+
+
+def test_pyll_graph_ops():
+    x = hp.uniform("x", 0, 1)
+    e = pyll.as_apply({"a": (x + 1) * 2, "b": [x, -x], "c": scope.exp(x) ** 2})
+    memo = {n: 0.5 for n in pyll.dfs(e) if n.name == "hyperopt_param"}
+    out = pyll.rec_eval(e, memo=memo)
+    assert out["a"] == 3.0 and out["b"] == (0.5, -0.5)
+    assert np.isclose(out["c"], np.exp(1.0))
+    sw = scope.switch(hp.randint("i", 2), 10, scope.Raise(ValueError, "not taken"))
+    memo = {n: 0 for n in pyll.dfs(sw) if n.name == "hyperopt_param"}
+    assert pyll.rec_eval(sw, memo=memo) == 10
+    s = pyll.sample(hp.normal("n", 0, 1), np.random.RandomState(0))
+    assert np.isfinite(s)
