@@ -25,7 +25,7 @@ SEG_DTYPE = np.dtype([
     ("transform", "<i4"), ("family", "<i4"), ("floor", "<f8"), ("prior_weight", "<f8"),
     ("prior_mu", "<f8"), ("prior_sigma", "<f8"), ("low", "<f8"), ("high", "<f8"),
     ("bounded", "<i4"), ("prior_pos", "<i4"), ("p_accept", "<f8"), ("cmax", "<f8"),
-    ("center", "<f8")], align=True)
+    ("center", "<f8"), ("lglob", "<f8"), ("n_wide", "<i4"), ("pad", "<i4")], align=True)
 CAT_SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("p_off", "<i8"), ("n_obs", "<i4"), ("n_cat", "<i4"),
     ("lf", "<i4"), ("mode", "<i4"), ("prior_weight", "<f8"), ("prior_p_off", "<i8")],
@@ -34,7 +34,8 @@ JOB_DTYPE = np.dtype([
     ("family", "<i4"), ("flags", "<i4"), ("below", "<i4"), ("above", "<i4"),
     ("low", "<f8"), ("high", "<f8"), ("q", "<f8"), ("n_cand", "<i8"), ("cand_base", "<i8"),
     ("cand_off", "<i8"), ("key", "<u8"), ("lat_off", "<i8"), ("lat_kmin", "<i8"),
-    ("lat_n", "<i8"), ("out_off", "<i8")], align=True)
+    ("lat_n", "<i8"), ("out_off", "<i8"), ("bin_lo", "<f8"), ("bin_hi", "<f8"),
+    ("sort_off", "<i8"), ("cnt_off", "<i8")], align=True)
 BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
                        ("n_scored", "<i8")], align=True)
 
@@ -48,7 +49,11 @@ _I = ctypes.c_int
 _I64 = ctypes.c_int64
 
 _SIGNATURES = {
-    "tpe_parzen_fit": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_parzen_fit": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_sort_layout": (_I64, [_I64, _P]),
+    "tpe_sort_candidates": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_score_sorted": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
+                              _P]),
     "tpe_cat_posterior": (_I, [_P, _P, _I, _P, _P, _P, _P]),
     "tpe_score_partials": (_I64, [_P, _I]),
     "tpe_score_continuous": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P,

@@ -103,7 +103,11 @@ __global__ __launch_bounds__(kFitBS) void k_fit_finalize(tpe_seg* __restrict__ s
                                                          double* __restrict__ sigma,
                                                          double* __restrict__ wcdf,
                                                          double* __restrict__ coef64,
-                                                         float* __restrict__ coef32) {
+                                                         float* __restrict__ coef32,
+                                                         float* __restrict__ coef32n,
+                                                         float* __restrict__ wide32,
+                                                         float* __restrict__ pm,
+                                                         float* __restrict__ sm) {
   __shared__ double redd[kFitBS / kWave];
   tpe_seg* S = segs + blockIdx.x;
   const int n = S->n_obs, nc = n + 1, pos = S->prior_pos;
@@ -216,6 +220,103 @@ __global__ __launch_bounds__(kFitBS) void k_fit_finalize(tpe_seg* __restrict__ s
   const double base = chunk_tot[threadIdx.x];
   if (base != 0.0)
     for (int k = k0; k < k1; ++k) wcdf[off + k] += base;
+
+  // 7) pruning data for the sorted fp32 path.  In log2 units relative to
+  //    cmax, every candidate y of the support has log2(sum) >= v_prior(y) >=
+  //    lglob (bounded: the prior term at the farther end of [low, high];
+  //    unbounded: at 6 prior sigmas -- blocks beyond fall back to all
+  //    components).  Component k's term is below 2^(lglob - 40), i.e.
+  //    negligible at fp32 resolution even summed over 1e4 terms, once
+  //    |y - mu_k| > r_k = sqrt(c_k - lglob + 40) / a_k.  Wide components (the
+  //    prior and sigma >= prior_sigma/4) are always evaluated from a compact
+  //    list; narrow ones through a [k_lo, k_hi] window found with the prefix
+  //    max of mu + r (pm) and the suffix min of mu - r (sm).
+  const double ap = coef64[4 * (off + pos) + 1] * sq;
+  const double cp = coef64[4 * (off + pos) + 2] * kLog2e - cmax;
+  double lglob;
+  if (S->bounded) {
+    const double dl = S->low - S->prior_mu, dh = S->high - S->prior_mu;
+    lglob = cp - ap * ap * fmax(dl * dl, dh * dh);
+  } else {
+    lglob = cp - ap * ap * 36.0 * ps * ps;
+  }
+  const double thr = lglob - 40.0;
+  for (int k = threadIdx.x; k < nc; k += kFitBS) {
+    const float4 f = reinterpret_cast<const float4*>(coef32)[off + k];
+    const bool wide = (k == pos) || (sigma[off + k] >= 0.25 * ps);
+    float4 g = f;
+    if (wide) g.z = -INFINITY;
+    reinterpret_cast<float4*>(coef32n)[off + k] = g;
+    const double m = mu[off + k];
+    if (wide) {
+      pm[off + k] = -INFINITY;
+      sm[off + k] = INFINITY;
+    } else {
+      const double r = sqrt(fmax(f.z - thr, 0.0)) / (double)f.x * 1.001 + 1e-6 * fabs(m) + 1e-30;
+      pm[off + k] = (float)(m + r);
+      sm[off + k] = (float)(m - r);
+    }
+  }
+  __syncthreads();
+  __shared__ float chunk_f[kFitBS];
+  __shared__ int chunk_n[kFitBS];
+  // prefix max (pm), chunked
+  float run_max = -INFINITY;
+  int n_wide_local = 0;
+  for (int k = k0; k < k1; ++k) {
+    run_max = fmaxf(run_max, pm[off + k]);
+    pm[off + k] = run_max;
+    n_wide_local += (k == pos) || (sigma[off + k] >= 0.25 * ps);
+  }
+  chunk_f[threadIdx.x] = run_max;
+  chunk_n[threadIdx.x] = n_wide_local;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float acc = -INFINITY;
+    int nacc = 0;
+    for (int t = 0; t < kFitBS; ++t) {
+      const float c = chunk_f[t];
+      chunk_f[t] = acc;
+      acc = fmaxf(acc, c);
+      const int cn = chunk_n[t];
+      chunk_n[t] = nacc;
+      nacc += cn;
+    }
+    S->lglob = lglob;
+    S->n_wide = nacc;
+  }
+  __syncthreads();
+  {
+    const float before = chunk_f[threadIdx.x];
+    for (int k = k0; k < k1; ++k) pm[off + k] = fmaxf(pm[off + k], before);
+    int wpos = chunk_n[threadIdx.x];
+    for (int k = k0; k < k1; ++k)
+      if ((k == pos) || (sigma[off + k] >= 0.25 * ps))
+        reinterpret_cast<float4*>(wide32)[off + (wpos++)] =
+            reinterpret_cast<const float4*>(coef32)[off + k];
+  }
+  __syncthreads();
+  // suffix min (sm), chunked
+  float run_min = INFINITY;
+  for (int k = k1 - 1; k >= k0; --k) {
+    run_min = fminf(run_min, sm[off + k]);
+    sm[off + k] = run_min;
+  }
+  chunk_f[threadIdx.x] = run_min;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float acc = INFINITY;
+    for (int t = kFitBS - 1; t >= 0; --t) {
+      const float c = chunk_f[t];
+      chunk_f[t] = acc;
+      acc = fminf(acc, c);
+    }
+  }
+  __syncthreads();
+  {
+    const float after = chunk_f[threadIdx.x];
+    for (int k = k0; k < k1; ++k) sm[off + k] = fminf(sm[off + k], after);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -352,13 +453,15 @@ using namespace tpe;
 
 extern "C" int tpe_parzen_fit(const double* obs, double* xf, tpe_seg* segs, int n_seg,
                               int max_obs, double* w, double* mu, double* sigma, double* wcdf,
-                              double* coef64, float* coef32, void* stream) {
+                              double* coef64, float* coef32, float* coef32n, float* wide32,
+                              float* pm, float* sm, void* stream) {
   if (n_seg < 0 || max_obs < 0) {
     set_error("tpe_parzen_fit: n_seg=%d max_obs=%d", n_seg, max_obs);
     return TPE_E_ARG;
   }
   if (n_seg == 0) return TPE_OK;
-  if (!segs || !w || !mu || !sigma || !wcdf || !coef64 || !coef32 || (max_obs > 0 && (!obs || !xf))) {
+  if (!segs || !w || !mu || !sigma || !wcdf || !coef64 || !coef32 || !coef32n || !wide32 ||
+      !pm || !sm || (max_obs > 0 && (!obs || !xf))) {
     set_error("tpe_parzen_fit: null pointer");
     return TPE_E_ARG;
   }
@@ -373,7 +476,7 @@ extern "C" int tpe_parzen_fit(const double* obs, double* xf, tpe_seg* segs, int 
   }
   hipLaunchKernelGGL(k_fit_rank, dim3(gx, n_seg), dim3(kFitBS), 0, st, xf, segs, w, mu);
   hipLaunchKernelGGL(k_fit_finalize, dim3(n_seg), dim3(kFitBS), 0, st, segs, w, mu, sigma, wcdf,
-                     coef64, coef32);
+                     coef64, coef32, coef32n, wide32, pm, sm);
   return check_launch("tpe_parzen_fit");
 }
 

@@ -118,33 +118,41 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
 // mixture log-density at R candidates, fp32 (log2-domain, offset by cmax)
 // ---------------------------------------------------------------------------
 template <int R>
-__device__ __forceinline__ void lse32(const float4* __restrict__ coef, const tpe_seg& S,
-                                      const float (&y)[R], float (&out)[R], float4* tile) {
-  const int nc = S.n_obs + 1;
+struct Lse32 {
+  float xc[R], s[R], m[R];
+  bool fast;
+};
+
+// centre the candidates and decide the wave's mode: the fast path (fixed
+// offset, one v_exp_f32 per pair) is exact whenever the prior component's
+// term keeps the sum in the normal fp32 range for every lane of the wave
+template <int R>
+__device__ __forceinline__ void lse32_begin(Lse32<R>& L, const float4* __restrict__ coef,
+                                            const tpe_seg& S, const float (&y)[R]) {
   const float cen = (float)S.center;
-  float xc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) xc[r] = y[r] - cen;
   const float4 cp = coef[S.prior_pos];
   bool ok = true;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const float t = fmaf(xc[r], cp.x, cp.y);
+    L.xc[r] = y[r] - cen;
+    const float t = fmaf(L.xc[r], cp.x, cp.y);
     ok = ok && (fmaf(-t, t, cp.z) >= kFastFloor);
+    L.s[r] = 0.0f;
+    L.m[r] = -INFINITY;
   }
-  const bool fast = __all(ok);
-  float s[R], m[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    s[r] = 0.0f;
-    m[r] = -INFINITY;
-  }
-  for (int t0 = 0; t0 < nc; t0 += kTile32) {
-    const int mm = min(kTile32, nc - t0);
+  L.fast = __all(ok);
+}
+
+// accumulate components [k0, k1) of `coef` (block-uniform bounds; syncs)
+template <int R>
+__device__ __forceinline__ void lse32_accum(Lse32<R>& L, const float4* __restrict__ coef, int k0,
+                                            int k1, float4* tile) {
+  for (int t0 = k0; t0 < k1; t0 += kTile32) {
+    const int mm = min(kTile32, k1 - t0);
     __syncthreads();
     for (int j = threadIdx.x; j < mm; j += kBS) tile[j] = coef[t0 + j];
     __syncthreads();
-    if (fast) {
+    if (L.fast) {
       float acc[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[r] = 0.0f;
@@ -153,35 +161,48 @@ __device__ __forceinline__ void lse32(const float4* __restrict__ coef, const tpe
         const float4 c = tile[k];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const float t = fmaf(xc[r], c.x, c.y);
+          const float t = fmaf(L.xc[r], c.x, c.y);
           acc[r] += __builtin_amdgcn_exp2f(fmaf(-t, t, c.z));
         }
       }
 #pragma unroll
-      for (int r = 0; r < R; ++r) s[r] += acc[r];
+      for (int r = 0; r < R; ++r) L.s[r] += acc[r];
     } else {
       for (int k = 0; k < mm; ++k) {
         const float4 c = tile[k];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const float t = fmaf(xc[r], c.x, c.y);
+          const float t = fmaf(L.xc[r], c.x, c.y);
           const float v = fmaf(-t, t, c.z);
-          if (v > m[r]) {
-            s[r] = s[r] * __builtin_amdgcn_exp2f(m[r] - v) + 1.0f;
-            m[r] = v;
-          } else {
-            s[r] += __builtin_amdgcn_exp2f(v - m[r]);
+          if (v > L.m[r]) {
+            L.s[r] = L.s[r] * __builtin_amdgcn_exp2f(L.m[r] - v) + 1.0f;
+            L.m[r] = v;
+          } else if (c.z > -INFINITY) {  // masked (wide) components add nothing
+            L.s[r] += __builtin_amdgcn_exp2f(v - L.m[r]);
           }
         }
       }
     }
   }
+}
+
+template <int R>
+__device__ __forceinline__ void lse32_end(const Lse32<R>& L, const tpe_seg& S, float (&out)[R]) {
   const float C = (float)S.cmax;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const float l2 = __builtin_amdgcn_logf(s[r]);  // log2
-    out[r] = (fast ? (l2 + C) : (m[r] + l2 + C)) * kLn2f;
+    const float l2 = __builtin_amdgcn_logf(L.s[r]);  // log2
+    out[r] = (L.fast ? (l2 + C) : (L.m[r] + l2 + C)) * kLn2f;
   }
+}
+
+template <int R>
+__device__ __forceinline__ void lse32(const float4* __restrict__ coef, const tpe_seg& S,
+                                      const float (&y)[R], float (&out)[R], float4* tile) {
+  Lse32<R> L;
+  lse32_begin(L, coef, S, y);
+  lse32_accum(L, coef, 0, S.n_obs + 1, tile);
+  lse32_end(L, S, out);
 }
 
 // exact online log-sum-exp, fp64 (parity mode)
@@ -375,6 +396,236 @@ __global__ __launch_bounds__(kBS) void k_reduce(const tpe_job* __restrict__ jobs
   }
   b = block_best<kBS>(b, red);
   if (threadIdx.x == 0) best[blockIdx.x] = tpe_best{b.score, b.index, b.value, jobs[blockIdx.x].n_cand};
+}
+
+// ---------------------------------------------------------------------------
+// continuous, unquantized, sorted + pruned (fp32)
+// ---------------------------------------------------------------------------
+constexpr int kNB = 1024;                // value bins per label
+constexpr int kSortR = 32;               // candidates per thread in count / scatter
+constexpr int kSortPer = kBS * kSortR;   // candidates per count / scatter block
+
+__device__ __forceinline__ int bin_of(float y, float lo, float scale) {
+  float t = (y - lo) * scale;
+  t = fminf(fmaxf(t, 0.0f), (float)(kNB - 1));  // NaN -> 0
+  return (int)t;
+}
+
+// the candidate exactly as k_score32<false> draws it
+__device__ __forceinline__ float cand32(const Mix& M, const tpe_job& J, int64_t li, bool lgmm,
+                                        bool lo_on, bool hi_on) {
+  float v = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
+  return lgmm ? __expf(v) : v;
+}
+
+__global__ __launch_bounds__(kBS) void k_sort_count(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ wcdf, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[kNB];
+  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t base = (int64_t)blockIdx.x * kSortPer;
+  if (base >= J.n_cand) return;
+  for (int i = threadIdx.x; i < kNB; i += kBS) h[i] = 0u;
+  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+  __syncthreads();
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  const float lo = (float)J.bin_lo, scale = (float)(kNB / (J.bin_hi - J.bin_lo));
+  for (int r = 0; r < kSortR; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) break;
+    const float x = cand32(M, J, li, lgmm, lo_on, hi_on);
+    atomicAdd(&h[bin_of(lgmm ? __logf(x) : x, lo, scale)], 1u);
+  }
+  __syncthreads();
+  uint32_t* row = counts + J.cnt_off + (int64_t)blockIdx.x * kNB;
+  for (int i = threadIdx.x; i < kNB; i += kBS) row[i] = h[i];
+}
+
+// counts[block][bin] -> exclusive offsets in (bin, block) order, in place
+__global__ __launch_bounds__(kNB) void k_sort_scan(const tpe_job* __restrict__ jobs,
+                                                   uint32_t* __restrict__ counts) {
+  __shared__ uint32_t tot[kNB];
+  const tpe_job J = jobs[blockIdx.x];
+  const int64_t nblk = (J.n_cand + kSortPer - 1) / kSortPer;
+  uint32_t* C = counts + J.cnt_off;
+  const int bin = threadIdx.x;
+  uint32_t t = 0;
+  for (int64_t b = 0; b < nblk; ++b) t += C[b * kNB + bin];
+  tot[bin] = t;
+  __syncthreads();
+  if (bin == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < kNB; ++i) {
+      const uint32_t c = tot[i];
+      tot[i] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  uint32_t run = tot[bin];
+  for (int64_t b = 0; b < nblk; ++b) {
+    const uint32_t c = C[b * kNB + bin];
+    C[b * kNB + bin] = run;
+    run += c;
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_sort_scatter(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ wcdf, const uint32_t* __restrict__ offsets,
+    float* __restrict__ sorted_x, uint32_t* __restrict__ sorted_i) {
+  __shared__ uint32_t cur[kNB];
+  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t base = (int64_t)blockIdx.x * kSortPer;
+  if (base >= J.n_cand) return;
+  const uint32_t* row = offsets + J.cnt_off + (int64_t)blockIdx.x * kNB;
+  for (int i = threadIdx.x; i < kNB; i += kBS) cur[i] = row[i];
+  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+  __syncthreads();
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  const float lo = (float)J.bin_lo, scale = (float)(kNB / (J.bin_hi - J.bin_lo));
+  for (int r = 0; r < kSortR; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) break;
+    const float x = cand32(M, J, li, lgmm, lo_on, hi_on);
+    const uint32_t pos = atomicAdd(&cur[bin_of(lgmm ? __logf(x) : x, lo, scale)], 1u);
+    sorted_x[J.sort_off + pos] = x;
+    sorted_i[J.sort_off + pos] = (uint32_t)li;
+  }
+}
+
+// first k with a[k] > v (a non-decreasing)
+__device__ __forceinline__ int first_greater(const float* a, int n, float v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] > v) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kBS) void k_score_sorted(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const float4* __restrict__ coef32, const float4* __restrict__ coef32n,
+    const float4* __restrict__ wide32, const float* __restrict__ pm,
+    const float* __restrict__ sm, const float* __restrict__ sorted_x,
+    const uint32_t* __restrict__ sorted_i, tpe_best* __restrict__ partial,
+    unsigned long long* __restrict__ pairs) {
+  __shared__ float4 tile[kTile32];
+  __shared__ BestT red[kBS / kWave];
+  __shared__ float fred[3][kBS / kWave];
+  __shared__ int win[2];
+  const tpe_job J = jobs[blockIdx.y];
+  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kR32);
+  if (base >= J.n_cand) {
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
+  }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const bool lgmm = J.family == TPE_LGMM1;
+  float x[kR32], y[kR32];
+  uint32_t li[kR32];
+  float ymin = INFINITY, ymax = -INFINITY, vmin = INFINITY;
+  const float4 cp = coef32[SA.comp_off + SA.prior_pos];
+  const float cen = (float)SA.center;
+  int nvalid = 0;
+#pragma unroll
+  for (int r = 0; r < kR32; ++r) {
+    const int64_t p = base + r * kBS + threadIdx.x;
+    if (p < J.n_cand) {
+      x[r] = sorted_x[J.sort_off + p];
+      li[r] = sorted_i[J.sort_off + p];
+      y[r] = lgmm ? __logf(x[r]) : x[r];
+      ymin = fminf(ymin, y[r]);
+      ymax = fmaxf(ymax, y[r]);
+      const float t = fmaf(y[r] - cen, cp.x, cp.y);
+      vmin = fminf(vmin, fmaf(-t, t, cp.z));
+      ++nvalid;
+    } else {
+      x[r] = 1.0f;
+      li[r] = 0;
+      y[r] = cen;
+    }
+  }
+  // block reductions: y range and the smallest prior term
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    ymin = fminf(ymin, __shfl_xor(ymin, off, kWave));
+    ymax = fmaxf(ymax, __shfl_xor(ymax, off, kWave));
+    vmin = fminf(vmin, __shfl_xor(vmin, off, kWave));
+  }
+  const int wid = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+    fred[0][wid] = ymin;
+    fred[1][wid] = ymax;
+    fred[2][wid] = vmin;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = fred[0][0], b = fred[1][0], c = fred[2][0];
+    for (int k = 1; k < kBS / kWave; ++k) {
+      a = fminf(a, fred[0][k]);
+      b = fmaxf(b, fred[1][k]);
+      c = fminf(c, fred[2][k]);
+    }
+    const int nc = SA.n_obs + 1;
+    if (c >= (float)SA.lglob) {
+      const float* PM = pm + SA.comp_off;
+      const float* SMn = sm + SA.comp_off;
+      win[0] = first_greater(PM, nc, a);           // first k with mu+r > ymin
+      win[1] = first_greater(SMn, nc, b) - 1;      // last k with mu-r < ymax... (sm < b)
+    } else {
+      win[0] = -1;  // far-out block: every component, unmasked
+      win[1] = nc - 1;
+    }
+  }
+  __syncthreads();
+  const int k_lo = win[0], k_hi = win[1];
+
+  float lb[kR32], la[kR32];
+  lse32<kR32>(coef32 + SB.comp_off, SB, y, lb, tile);
+  Lse32<kR32> L;
+  lse32_begin(L, coef32 + SA.comp_off, SA, y);
+  int64_t evaluated;
+  if (k_lo < 0) {
+    lse32_accum(L, coef32 + SA.comp_off, 0, SA.n_obs + 1, tile);
+    evaluated = SA.n_obs + 1;
+  } else {
+    if (k_hi >= k_lo) lse32_accum(L, coef32n + SA.comp_off, k_lo, k_hi + 1, tile);
+    lse32_accum(L, wide32 + SA.comp_off, 0, SA.n_wide, tile);
+    evaluated = (k_hi >= k_lo ? k_hi - k_lo + 1 : 0) + SA.n_wide;
+  }
+  lse32_end(L, SA, la);
+
+  BestT b{0.0, -1, 0.0};
+#pragma unroll
+  for (int r = 0; r < kR32; ++r) {
+    const int64_t p = base + r * kBS + threadIdx.x;
+    if (p >= J.n_cand) continue;
+    double bl = lb[r], al = la[r];
+    if (lgmm) {
+      const double lx = (double)__logf(x[r]);
+      bl -= lx;
+      al -= lx;
+    }
+    best_update(b, bl - al, J.cand_base + (int64_t)li[r], (double)x[r]);
+  }
+  b = block_best<kBS>(b, red);
+  if (threadIdx.x == 0) {
+    *P = tpe_best{b.score, b.index, b.value, 0};
+    if (pairs) {
+      const int64_t n = min((int64_t)(kBS * kR32), J.n_cand - base);
+      atomicAdd(pairs, (unsigned long long)(n * (evaluated + SB.n_obs + 1)));
+    }
+  }
+  (void)nvalid;
 }
 
 // ---------------------------------------------------------------------------
@@ -872,4 +1123,73 @@ extern "C" int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, 
   hipLaunchKernelGGL(k_combine, dim3((n_labels + kBS - 1) / kBS), dim3(kBS), 0,
                      (hipStream_t)stream, sets, n_sets, n_labels, out);
   return check_launch("tpe_best_combine");
+}
+
+extern "C" int64_t tpe_sort_layout(int64_t n_cand, int64_t* sorted_slots) {
+  if (sorted_slots) *sorted_slots = n_cand;
+  return ((n_cand + kSortPer - 1) / kSortPer) * (int64_t)kNB;
+}
+
+static bool check_sorted_jobs(const char* fn, const tpe_job* host_jobs, int n_jobs) {
+  if (!check_jobs(fn, host_jobs, n_jobs)) return false;
+  for (int i = 0; i < n_jobs; ++i) {
+    const tpe_job& j = host_jobs[i];
+    if (j.family == TPE_CAT || (j.flags & (TPE_F_QUANT | TPE_F_INJECTED))) {
+      set_error("%s: job %d is not a sampled unquantized GMM1/LGMM1 job", fn, i);
+      return false;
+    }
+    if (!(j.bin_hi > j.bin_lo) || j.n_cand > 0xFFFFFFFFll) {
+      set_error("%s: job %d has an empty bin range or > 2^32 candidates", fn, i);
+      return false;
+    }
+  }
+  return true;
+}
+
+extern "C" int tpe_sort_candidates(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                   const tpe_seg* segs, const double* mu, const double* sigma,
+                                   const double* wcdf, uint32_t* counts, float* sorted_x,
+                                   uint32_t* sorted_i, void* stream) {
+  if (!check_sorted_jobs("tpe_sort_candidates", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !counts || !sorted_x || !sorted_i) {
+    set_error("tpe_sort_candidates: null pointer");
+    return TPE_E_ARG;
+  }
+  const int64_t gs = max_blocks(host_jobs, n_jobs, (int64_t)kSortPer, -1);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_sort_count, dim3((unsigned)gs, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
+                     segs, mu, sigma, wcdf, counts);
+  hipLaunchKernelGGL(k_sort_scan, dim3(n_jobs), dim3(kNB), 0, st, jobs, counts);
+  hipLaunchKernelGGL(k_sort_scatter, dim3((unsigned)gs, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
+                     segs, mu, sigma, wcdf, counts, sorted_x, sorted_i);
+  return check_launch("tpe_sort_candidates");
+}
+
+extern "C" int tpe_score_sorted(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                const tpe_seg* segs, const float* coef32, const float* coef32n,
+                                const float* wide32, const float* pm, const float* sm,
+                                const float* sorted_x, const uint32_t* sorted_i,
+                                tpe_best* partial, int64_t n_partial, tpe_best* best,
+                                uint64_t* pairs, void* stream) {
+  if (!check_sorted_jobs("tpe_score_sorted", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !coef32 || !coef32n || !wide32 || !pm || !sm || !sorted_x ||
+      !sorted_i || !partial || !best) {
+    set_error("tpe_score_sorted: null pointer");
+    return TPE_E_ARG;
+  }
+  const int64_t gx = max_blocks(host_jobs, n_jobs, (int64_t)kBS * kR32, -1);
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_score_sorted: partial workspace too small");
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_score_sorted, dim3((unsigned)gx, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
+                     segs, reinterpret_cast<const float4*>(coef32),
+                     reinterpret_cast<const float4*>(coef32n),
+                     reinterpret_cast<const float4*>(wide32), pm, sm, sorted_x, sorted_i, partial,
+                     (unsigned long long*)pairs);
+  hipLaunchKernelGGL(k_reduce, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
+  return check_launch("tpe_score_sorted");
 }

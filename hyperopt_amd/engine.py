@@ -159,11 +159,14 @@ class Engine:
 
     # -- main entry ----------------------------------------------------------
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
-            outputs=False, stream=None, timers=None, sample_only=False) -> List[LabelResult]:
+            outputs=False, stream=None, timers=None, sample_only=False,
+            pruned=True) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``.
         ``sample_only``: fit, then only draw the candidates of the continuous
-        labels (tpe_sample) into ``LabelResult.cand`` -- the sampler test hook."""
+        labels (tpe_sample) into ``LabelResult.cand`` -- the sampler test hook.
+        ``pruned``: sampled unquantized labels at precision 32 take the sorted,
+        component-pruned kernel (tpe_score_sorted); False = dense k_score32."""
         if sample_only:
             outputs = True
         torch = self.torch
@@ -254,9 +257,11 @@ class Engine:
                     fallback.append(i)
                 else:
                     lat_ranges[i] = (kmin, kmax - kmin + 1)
+        use_sorted = pruned and precision == 32 and not outputs and not sample_only
         groups = [
             ("cont", [i for i in cont if inj(i)]),
-            ("cont", [i for i in cont if not inj(i)]),
+            ("cont", [i for i in cont if not inj(i) and not use_sorted]),
+            ("sorted", [i for i in cont if not inj(i) and use_sorted]),
             ("lat", [i for i in quant if i in lat_ranges]),
             ("qfb", fallback),
             ("qinj", [i for i in quant if inj(i)]),
@@ -266,6 +271,7 @@ class Engine:
         order = [i for _, ids in groups for i in ids]
         jobs = np.zeros(len(order), L.JOB_DTYPE)
         cand_parts, cand_off, out_off, lat_off, qfb_off = [], 0, 0, 0, 0
+        sort_off = cnt_off = 0
         seg_of = {i: si for si, i in enumerate(fit_ids)}
         cseg_of = {i: ci for ci, i in enumerate(cat)}
         for pos, i in enumerate(order):
@@ -303,10 +309,16 @@ class Engine:
                 elif i in fallback:
                     j["cand_off"] = qfb_off
                     qfb_off += n
+            elif use_sorted and not inj(i):
+                j["bin_lo"], j["bin_hi"] = _support(w, P)
+                j["sort_off"], j["cnt_off"] = sort_off, cnt_off
+                slots = ctypes.c_int64(0)
+                cnt_off += lib.tpe_sort_layout(n, ctypes.byref(slots))
+                sort_off += slots.value
         cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
         # the dense fallback first materialises its draws: a job copy whose
         # out_off points into the scratch candidate buffer
-        fb_slice = _slice_of(groups, 3)
+        fb_slice = _slice_of(groups, 4)
         fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
         fb_jobs["out_off"] = fb_jobs["cand_off"]
 
@@ -346,10 +358,15 @@ class Engine:
             d_cdf = self._buf("wcdf", 8 * n_comp)
             d_c64 = self._buf("coef64", 32 * n_comp)
             d_c32 = self._buf("coef32", 16 * n_comp)
+            d_c32n = self._buf("coef32n", 16 * n_comp)
+            d_w32 = self._buf("wide32", 16 * n_comp)
+            d_pm = self._buf("pm", 4 * n_comp)
+            d_sm = self._buf("sm", 4 * n_comp)
             d_xf = self._buf("xf", 8 * max(obs_pool.size, 1))
             e0 = tick()
             L.check(lib.tpe_parzen_fit(base + o_obs, d_xf, d_segs, len(segs), max_obs, d_w, d_mu,
-                                       d_sig, d_cdf, d_c64, d_c32, sp), "tpe_parzen_fit")
+                                       d_sig, d_cdf, d_c64, d_c32, d_c32n, d_w32, d_pm, d_sm, sp),
+                    "tpe_parzen_fit")
             tock("fit", e0)
         if cat:
             d_logp = self._buf("cat_logp", 8 * p_pool.size)
@@ -384,6 +401,22 @@ class Engine:
                 L.check(lib.tpe_score_continuous(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
                                                  d_c64, d_c32, d_cand, precision, d_bl, d_al, d_x,
                                                  d_part, npart, db, sp), "tpe_score_continuous")
+            elif kind == "sorted":
+                npart = lib.tpe_score_partials(hjp, nj) * 2
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_cnt = self._buf("sort_cnt", 4 * max(cnt_off, 1))
+                d_sx = self._buf("sort_x", 4 * max(sort_off, 1))
+                d_si = self._buf("sort_i", 4 * max(sort_off, 1))
+                d_pairs = self._buf("pairs", 16)
+                with torch.cuda.stream(stream):
+                    self._bufs["pairs"][:8].zero_()
+                L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
+                                                d_sx, d_si, sp), "tpe_sort_candidates")
+                tock("sort", e0)
+                e0 = tick()
+                L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,
+                                             d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
+                        "tpe_score_sorted")
             elif kind == "lat":
                 d_slot = self._buf("lat_slot", 8 * lat_off)
                 d_vals = self._buf("lat_vals", 8 * lat_off)
@@ -424,6 +457,9 @@ class Engine:
         with torch.cuda.stream(stream):
             best_h = self._bufs["best"][:n_jobs * BS].to("cpu").numpy().view(L.BEST_DTYPE)
             err = int(err_t[:4].to("cpu").view(torch.int32).item())
+            self.last_pairs = None
+            if any(k == "sorted" and ids for k, ids in groups):
+                self.last_pairs = int(self._bufs["pairs"][:8].to("cpu").view(torch.int64).item())
             outs = None
             if outputs:
                 outs = [self._bufs[k][:8 * max(out_off, 1)].to("cpu").numpy().view(np.float64)
@@ -450,6 +486,18 @@ class Engine:
 def _slice_of(groups, g):
     a = sum(len(ids) for _, ids in groups[:g])
     return a, a + len(groups[g][1])
+
+
+def _support(w: LabelWork, P):
+    """Coordinate range (x for GMM1, log x for LGMM1) every candidate lies in:
+    [low, high] when bounded, else the below means +- 9 prior sigmas."""
+    if P["bounded"]:
+        return P["low"], P["high"]
+    obs = np.asarray(w.obs_below, dtype=np.float64)
+    if P["transform"] == L.OBS_LOG and obs.size:
+        obs = np.log(np.maximum(obs, P["floor"]))
+    pts = np.concatenate([obs[np.isfinite(obs)], [P["prior_mu"]]])
+    return float(pts.min()) - 9.0 * P["prior_sigma"], float(pts.max()) + 9.0 * P["prior_sigma"]
 
 
 def _lattice_range(w: LabelWork, P):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 1
+#define TPE_ABI_VERSION 2
 
 enum {
   TPE_OK = 0,
@@ -76,6 +76,9 @@ typedef struct tpe_seg {
   double p_accept;      /* sum w*(Phi(high)-Phi(low)), 1 if unbounded        */
   double cmax;          /* max_k log2-coefficient (fp32 scoring offset)      */
   double center;        /* fp32 scoring origin (float-rounded prior_mu)      */
+  double lglob;         /* lower bound of log2(sum)-cmax over the support    */
+  int32_t n_wide;       /* wide components (prior + sigma >= sigma_p/4)      */
+  int32_t pad;
 } tpe_seg;
 
 /*
@@ -114,6 +117,9 @@ typedef struct tpe_job {
   int64_t lat_kmin;     /* quantized: lattice index of slot 0               */
   int64_t lat_n;        /* quantized: number of slots                       */
   int64_t out_off;      /* optional per-candidate outputs: first element    */
+  double bin_lo, bin_hi;/* sorted path: candidate coordinate range to bin    */
+  int64_t sort_off;     /* sorted path: first slot in the sorted pool        */
+  int64_t cnt_off;      /* sorted path: first element of the count matrix    */
 } tpe_job;
 
 /* best candidate of one label: np.argmax semantics (first max, NaN wins) */
@@ -129,9 +135,14 @@ typedef struct tpe_best {
  * w/mu/sigma: fp64 mixture pool (sorted components);
  * wcdf: fp64 cumulative weights (sampler); coef64: 4 doubles / component;
  * coef32: 4 floats / component.  max_obs = max n_obs over segs. */
+/* Pruning data for the sorted scoring path (per component, float):
+ * coef32n = coef32 with wide components masked (c = -inf), wide32 = the
+ * wide components' coefficients compacted at comp_off, pm / sm = prefix max
+ * of (mu + reach) / suffix min of (mu - reach) over narrow components. */
 int tpe_parzen_fit(const double* obs, double* xf, tpe_seg* segs, int n_seg, int max_obs,
                    double* w, double* mu, double* sigma, double* wcdf,
-                   double* coef64, float* coef32, void* stream);
+                   double* coef64, float* coef32, float* coef32n, float* wide32,
+                   float* pm, float* sm, void* stream);
 
 /* ---- categorical posterior (tpe.py:578-615) ------------------------------ */
 /* p_pool: probabilities (mode 1 also reads the prior p from it at
@@ -154,6 +165,32 @@ int tpe_score_continuous(const tpe_job* jobs, const tpe_job* host_jobs, int n_jo
                          double* out_bl, double* out_al, double* out_x,
                          tpe_best* partial, int64_t n_partial, tpe_best* best,
                          void* stream);
+
+/* ---- continuous candidates, sorted + pruned (fp32 throughput path) -------
+ * Same results as tpe_score_continuous(precision=32) on sampled candidates
+ * (same Philox draws, same winner up to fp32 rounding), but candidates are
+ * first bucketed by value (count -> scan -> scatter, deterministic, no
+ * global atomics) so each scoring block spans a narrow interval and only
+ * components within reach -- those whose term can exceed 2^-40 of the
+ * mixture sum -- plus the wide components are evaluated.
+ * tpe_sort_layout: count-matrix elements and sorted-pool slots one job of
+ * n_cand candidates needs.  pairs (nullable): u64 counter of evaluated
+ * (candidate, component) pairs. */
+int64_t tpe_sort_layout(int64_t n_cand, int64_t* sorted_slots);
+/* draw the candidates (same Philox streams as tpe_score_continuous) and
+ * bucket them by value into sorted_x / sorted_i (candidate value, local
+ * index) at job.sort_off; counts: job.cnt_off workspace */
+int tpe_sort_candidates(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                        const tpe_seg* segs, const double* mu, const double* sigma,
+                        const double* wcdf, uint32_t* counts, float* sorted_x,
+                        uint32_t* sorted_i, void* stream);
+/* score the bucketed candidates with component pruning + fused argmax */
+int tpe_score_sorted(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                     const tpe_seg* segs, const float* coef32, const float* coef32n,
+                     const float* wide32, const float* pm, const float* sm,
+                     const float* sorted_x, const uint32_t* sorted_i,
+                     tpe_best* partial, int64_t n_partial, tpe_best* best,
+                     uint64_t* pairs, void* stream);
 
 /* ---- quantized labels: lattice path ---------------------------------------
  * Candidates of a quantized label take values k*q (np.round(x/q)*q,

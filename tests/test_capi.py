@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == 1
+    assert lib.tpe_abi_version() == 2
     sizes = (ctypes.c_int32 * 4)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 4) == 4
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -54,10 +54,13 @@ def test_argument_errors_are_reported():
     rc = lib.tpe_score_continuous(None, hp_, 0, None, None, None, None, None, None, None, None,
                                   48, None, None, None, None, 0, None, None)
     assert rc == 0  # nothing to do
-    assert lib.tpe_parzen_fit(None, None, None, 0, 0, None, None, None, None, None, None,
-                              None) == 0
-    assert lib.tpe_parzen_fit(None, None, None, -1, 0, None, None, None, None, None, None,
-                              None) == -1
+    nul = [None] * 11
+    assert lib.tpe_parzen_fit(None, None, None, 0, 0, *nul) == 0
+    assert lib.tpe_parzen_fit(None, None, None, -1, 0, *nul) == -1
+    jobs["flags"] = 0
+    jobs["bin_lo"] = jobs["bin_hi"] = 1.0
+    rc = lib.tpe_score_sorted(None, hp_, 1, *([None] * 9), 0, None, None, None)
+    assert rc == -1 and b"empty bin range" in lib.tpe_last_error()
     assert lib.tpe_best_combine(None, 0, 1, None, None) == -1
     with pytest.raises(L.TpeHipError):
         L.check(-1, "probe")

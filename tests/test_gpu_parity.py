@@ -129,3 +129,39 @@ def test_argmax_ties_and_far_tails(engine):
     r32, = engine.run([w], precision=32, outputs=True)
     np.testing.assert_allclose(r32.above_llik, ref["above_llik"], rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(r32.below_llik, ref["below_llik"], rtol=1e-4, atol=1e-4)
+
+
+SORT_KINDS = [("uniform", (-5.0, 5.0), lambda r, n: r.uniform(-5, 5, n)),
+              ("loguniform", (-5.0, 0.0), lambda r, n: np.exp(r.uniform(-5, 0, n))),
+              ("normal", (0.0, 2.0), lambda r, n: r.normal(0, 2, n)),
+              ("lognormal", (0.0, 1.0), lambda r, n: np.exp(r.normal(0, 1, n)))]
+
+
+@pytest.mark.parametrize("kind,args,gen", SORT_KINDS)
+@pytest.mark.parametrize("n_hist", [3, 40, 2000, 10000])
+def test_sorted_pruned_matches_dense(engine, kind, args, gen, n_hist):
+    """The sorted + component-pruned fp32 path picks the dense path's winner
+    (same Philox candidates) -- or, on a near tie, one whose exact fp64 score
+    is within fp32 rounding of it."""
+    from hyperopt_amd.engine import LabelWork
+    rng = np.random.RandomState(n_hist)
+    obs = gen(rng, n_hist)
+    losses = rng.normal(size=n_hist)
+    below, above = O.ap_split_trials(np.arange(n_hist), obs, np.arange(n_hist), losses, 0.25)
+    w = LabelWork(kind, kind, args, below, above, n_cand=1 << 18, key=987654321 + n_hist)
+    dense, = engine.run([w], precision=32, pruned=False)
+    pruned, = engine.run([w], precision=32, pruned=True)
+    pairs = engine.last_pairs
+    assert pruned.n_scored == dense.n_scored == 1 << 18
+    if pruned.index == dense.index:
+        assert pruned.value == dense.value
+    else:
+        w2 = LabelWork(kind, kind, args, below, above,
+                       cand=np.array([dense.value, pruned.value]))
+        r, = engine.run([w2], precision=64, outputs=True)
+        s = r.below_llik - r.above_llik
+        assert abs(s[0] - s[1]) <= 1e-4 * max(1.0, abs(s[0])), (s, dense, pruned)
+    dense_pairs = (1 << 18) * (below.size + above.size + 2)
+    assert 0 < pairs <= dense_pairs
+    if n_hist >= 2000:
+        assert pairs < 0.5 * dense_pairs  # pruning is effective on real histories
