@@ -377,7 +377,7 @@ __device__ double np_pairwise_sum(const double* a, int64_t n) {
 }
 
 constexpr int kCatBS = 256;
-constexpr int kCatTile = 2048;
+constexpr int kCatTile = 1024;
 
 __global__ __launch_bounds__(kCatBS) void k_cat_posterior(const int64_t* __restrict__ obs,
                                                           const tpe_cat_seg* __restrict__ segs,
@@ -385,20 +385,38 @@ __global__ __launch_bounds__(kCatBS) void k_cat_posterior(const int64_t* __restr
                                                           double* __restrict__ logp,
                                                           double* __restrict__ cdf) {
   __shared__ int64_t tile[kCatTile];
+  __shared__ double tw[kCatTile];
   const tpe_cat_seg& S = segs[blockIdx.x];
   const int n = S.n_obs, K = S.n_cat;
-  // per-category weighted counts, accumulated in observation order (bincount)
+  // linear-forgetting ramp constants, once (np.linspace(1/N, 1, N-LF), tpe.py:380-392)
+  const bool ramp = S.lf > 0 && S.lf < n;
+  const int64_t num = n - S.lf;
+  const double start = 1.0 / (double)n;
+  const double step = (ramp && num > 1) ? (1.0 - start) / (double)(num - 1) : 0.0;
+  // per-category weighted counts, accumulated in observation order (bincount):
+  // the tile's weights are computed by all threads, then each category's
+  // thread walks the tile sequentially
   for (int k0 = 0; k0 < K; k0 += kCatBS) {
     const int k = k0 + threadIdx.x;
     double cnt = 0.0;
     for (int t0 = 0; t0 < n; t0 += kCatTile) {
       const int m = min(kCatTile, n - t0);
       __syncthreads();
-      for (int j = threadIdx.x; j < m; j += kCatBS) tile[j] = obs[S.obs_off + t0 + j];
+      for (int j = threadIdx.x; j < m; j += kCatBS) {
+        const int64_t i = t0 + j;
+        tile[j] = obs[S.obs_off + i];
+        double wt = 1.0;
+        if (ramp && i < num) {
+          if (num == 1) wt = start;
+          else if (i == num - 1) wt = 1.0;
+          else wt = __dadd_rn(__dmul_rn((double)i, step), start);
+        }
+        tw[j] = wt;
+      }
       __syncthreads();
       if (k < K)
         for (int j = 0; j < m; ++j)
-          if (tile[j] == k) cnt += lf_weight(t0 + j, n, S.lf);
+          if (tile[j] == k) cnt += tw[j];
     }
     if (k < K) {
       double pseudo;
