@@ -120,6 +120,34 @@ def cpu_baseline(space, vals, losses, seconds_hint=True):
                       "history, %.2f s on %s" % (n, dt, platform.processor() or platform.machine())}
 
 
+def readme_suggest_p50():
+    """Config C1 (BASELINE configs[0]): the README space, fmin(max_evals=100,
+    n_EI_candidates=24, rstate=RandomState(3)) through the drop-in API; p50 of
+    the wall time of TPE suggest calls 21-100 (calls 1-20 are the random
+    startup)."""
+    from hyperopt_amd import Trials, fmin, hp, tpe
+    times = []
+
+    def timed(new_ids, domain, trials, seed):
+        t0 = time.perf_counter()
+        out = tpe.suggest(new_ids, domain, trials, seed, verbose=False)
+        times.append(time.perf_counter() - t0)
+        return out
+
+    space = hp.choice("a", [("case 1", 1 + hp.lognormal("c1", 0, 1)),
+                            ("case 2", hp.uniform("c2", -10, 10))])
+
+    def objective(args):
+        case, val = args
+        return val if case == "case 1" else val ** 2
+
+    fmin(objective, space, algo=timed, max_evals=100, trials=Trials(),
+         rstate=np.random.RandomState(3), show_progressbar=False)
+    t = np.array(times[20:]) * 1e3
+    return {"p50_ms": float(np.median(t)), "p90_ms": float(np.percentile(t, 90)),
+            "calls": int(t.size), "config": "README space, max_evals=100, n_EI=24"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,6 +261,8 @@ def main():
                      "dense_equivalent_tflops": effective},
         "group_ms": group_ms,
     }
+    if rank == 0 and world == 1:
+        line["readme_suggest"] = readme_suggest_p50()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(space, vals, losses)
     elif rank == 0:

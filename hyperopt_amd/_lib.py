@@ -51,7 +51,7 @@ _I64 = ctypes.c_int64
 _SIGNATURES = {
     "tpe_parzen_fit": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_sort_layout": (_I64, [_I64, _P]),
-    "tpe_sort_candidates": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_sort_candidates": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_sorted": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
                               _P]),
     "tpe_cat_posterior": (_I, [_P, _P, _I, _P, _P, _P, _P]),

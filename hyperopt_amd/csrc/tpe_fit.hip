@@ -414,9 +414,12 @@ __global__ __launch_bounds__(kCatBS) void k_cat_posterior(const int64_t* __restr
         tw[j] = wt;
       }
       __syncthreads();
-      if (k < K)
-        for (int j = 0; j < m; ++j)
-          if (tile[j] == k) cnt += tw[j];
+      if (k < K) {
+        // adding +0.0 leaves cnt unchanged, so the branchless form is the
+        // same sequential sum as np.bincount's
+#pragma unroll 8
+        for (int j = 0; j < m; ++j) cnt += (tile[j] == k) ? tw[j] : 0.0;
+      }
     }
     if (k < K) {
       double pseudo;

@@ -414,9 +414,9 @@ __global__ __launch_bounds__(kBS) void k_reduce(const tpe_job* __restrict__ jobs
 // ---------------------------------------------------------------------------
 // continuous, unquantized, sorted + pruned (fp32)
 // ---------------------------------------------------------------------------
-constexpr int kNB = 1024;                // value bins per label
-constexpr int kSortR = 32;               // candidates per thread in count / scatter
-constexpr int kSortPer = kBS * kSortR;   // candidates per count / scatter block
+constexpr int kNB = 512;                 // value bins per label
+constexpr int kSortR = 16;               // candidates per thread in count / scatter
+constexpr int kSortPer = kBS * kSortR;   // candidates per count / scatter block (4096)
 
 __device__ __forceinline__ int bin_of(float y, float lo, float scale) {
   float t = (y - lo) * scale;
@@ -431,10 +431,12 @@ __device__ __forceinline__ float cand32(const Mix& M, const tpe_job& J, int64_t 
   return lgmm ? __expf(v) : v;
 }
 
+// K1: draw every candidate once (kept in `gen`, generation order, coalesced)
+// and count them per (block, value bin)
 __global__ __launch_bounds__(kBS) void k_sort_count(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
-    const double* __restrict__ wcdf, uint32_t* __restrict__ counts) {
+    const double* __restrict__ wcdf, uint32_t* __restrict__ counts, float* __restrict__ gen) {
   __shared__ uint32_t h[kNB];
   __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
   const tpe_job J = jobs[blockIdx.y];
@@ -450,20 +452,23 @@ __global__ __launch_bounds__(kBS) void k_sort_count(
     const int64_t li = base + r * kBS + threadIdx.x;
     if (li >= J.n_cand) break;
     const float x = cand32(M, J, li, lgmm, lo_on, hi_on);
+    gen[J.sort_off + li] = x;
     atomicAdd(&h[bin_of(lgmm ? __logf(x) : x, lo, scale)], 1u);
   }
   __syncthreads();
-  uint32_t* row = counts + J.cnt_off + (int64_t)blockIdx.x * kNB;
+  uint32_t* row = counts + 2 * J.cnt_off + (int64_t)blockIdx.x * kNB;
   for (int i = threadIdx.x; i < kNB; i += kBS) row[i] = h[i];
 }
 
-// counts[block][bin] -> exclusive offsets in (bin, block) order, in place
+// K2: per job, global start of every (block, bin) run in (bin, block) order;
+// counts keep their values (row b at 2*cnt_off), offsets go to the second half
 __global__ __launch_bounds__(kNB) void k_sort_scan(const tpe_job* __restrict__ jobs,
                                                    uint32_t* __restrict__ counts) {
   __shared__ uint32_t tot[kNB];
   const tpe_job J = jobs[blockIdx.x];
   const int64_t nblk = (J.n_cand + kSortPer - 1) / kSortPer;
-  uint32_t* C = counts + J.cnt_off;
+  const uint32_t* C = counts + 2 * J.cnt_off;
+  uint32_t* O = counts + 2 * J.cnt_off + nblk * kNB;
   const int bin = threadIdx.x;
   uint32_t t = 0;
   for (int64_t b = 0; b < nblk; ++b) t += C[b * kNB + bin];
@@ -480,36 +485,67 @@ __global__ __launch_bounds__(kNB) void k_sort_scan(const tpe_job* __restrict__ j
   __syncthreads();
   uint32_t run = tot[bin];
   for (int64_t b = 0; b < nblk; ++b) {
-    const uint32_t c = C[b * kNB + bin];
-    C[b * kNB + bin] = run;
-    run += c;
+    O[b * kNB + bin] = run;
+    run += C[b * kNB + bin];
   }
 }
 
-__global__ __launch_bounds__(kBS) void k_sort_scatter(
-    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
-    const double* __restrict__ mu, const double* __restrict__ sigma,
-    const double* __restrict__ wcdf, const uint32_t* __restrict__ offsets,
-    float* __restrict__ sorted_x, uint32_t* __restrict__ sorted_i) {
-  __shared__ uint32_t cur[kNB];
-  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+// K3: bucket the block's candidates in LDS by bin, then write each bin's run
+// contiguously to its global slot range (coalesced runs instead of scattered
+// 4-byte stores)
+__global__ __launch_bounds__(kBS) void k_sort_scatter(const tpe_job* __restrict__ jobs,
+                                                      const uint32_t* __restrict__ counts,
+                                                      const float* __restrict__ gen,
+                                                      float* __restrict__ sorted_x,
+                                                      uint32_t* __restrict__ sorted_i) {
+  __shared__ uint32_t lstart[kNB], cur[kNB], goff[kNB];
+  __shared__ float sx[kSortPer];
+  __shared__ uint32_t si[kSortPer];
+  __shared__ uint16_t sb[kSortPer];
+  __shared__ uint32_t part[kBS];
   const tpe_job J = jobs[blockIdx.y];
   const int64_t base = (int64_t)blockIdx.x * kSortPer;
   if (base >= J.n_cand) return;
-  const uint32_t* row = offsets + J.cnt_off + (int64_t)blockIdx.x * kNB;
-  for (int i = threadIdx.x; i < kNB; i += kBS) cur[i] = row[i];
-  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+  const int64_t nblk = (J.n_cand + kSortPer - 1) / kSortPer;
+  const uint32_t* C = counts + 2 * J.cnt_off + (int64_t)blockIdx.x * kNB;
+  const uint32_t* O = counts + 2 * J.cnt_off + nblk * kNB + (int64_t)blockIdx.x * kNB;
+  // local exclusive scan of this block's bin counts (kNB = 2 * kBS)
+  const uint32_t c0 = C[2 * threadIdx.x], c1 = C[2 * threadIdx.x + 1];
+  part[threadIdx.x] = c0 + c1;
+  goff[2 * threadIdx.x] = O[2 * threadIdx.x];
+  goff[2 * threadIdx.x + 1] = O[2 * threadIdx.x + 1];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int t = 0; t < kBS; ++t) {
+      const uint32_t c = part[t];
+      part[t] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  lstart[2 * threadIdx.x] = cur[2 * threadIdx.x] = part[threadIdx.x];
+  lstart[2 * threadIdx.x + 1] = cur[2 * threadIdx.x + 1] = part[threadIdx.x] + c0;
   __syncthreads();
   const bool lgmm = J.family == TPE_LGMM1;
-  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
   const float lo = (float)J.bin_lo, scale = (float)(kNB / (J.bin_hi - J.bin_lo));
+  const int n = (int)min((int64_t)kSortPer, J.n_cand - base);
   for (int r = 0; r < kSortR; ++r) {
-    const int64_t li = base + r * kBS + threadIdx.x;
-    if (li >= J.n_cand) break;
-    const float x = cand32(M, J, li, lgmm, lo_on, hi_on);
-    const uint32_t pos = atomicAdd(&cur[bin_of(lgmm ? __logf(x) : x, lo, scale)], 1u);
-    sorted_x[J.sort_off + pos] = x;
-    sorted_i[J.sort_off + pos] = (uint32_t)li;
+    const int e = r * kBS + threadIdx.x;
+    if (e >= n) break;
+    const float x = gen[J.sort_off + base + e];
+    const int b = bin_of(lgmm ? __logf(x) : x, lo, scale);
+    const uint32_t lp = atomicAdd(&cur[b], 1u);
+    sx[lp] = x;
+    si[lp] = (uint32_t)(base + e);
+    sb[lp] = (uint16_t)b;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += kBS) {
+    const int b = sb[e];
+    const uint32_t g = goff[b] + (uint32_t)(e - lstart[b]);
+    sorted_x[J.sort_off + g] = sx[e];
+    sorted_i[J.sort_off + g] = si[e];
   }
 }
 
@@ -1139,6 +1175,7 @@ extern "C" int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, 
 }
 
 extern "C" int64_t tpe_sort_layout(int64_t n_cand, int64_t* sorted_slots) {
+  // count matrix (blocks x bins) twice: counts, then run offsets
   if (sorted_slots) *sorted_slots = n_cand;
   return ((n_cand + kSortPer - 1) / kSortPer) * (int64_t)kNB;
 }
@@ -1161,21 +1198,21 @@ static bool check_sorted_jobs(const char* fn, const tpe_job* host_jobs, int n_jo
 
 extern "C" int tpe_sort_candidates(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                                    const tpe_seg* segs, const double* mu, const double* sigma,
-                                   const double* wcdf, uint32_t* counts, float* sorted_x,
-                                   uint32_t* sorted_i, void* stream) {
+                                   const double* wcdf, uint32_t* counts, float* gen,
+                                   float* sorted_x, uint32_t* sorted_i, void* stream) {
   if (!check_sorted_jobs("tpe_sort_candidates", host_jobs, n_jobs)) return TPE_E_ARG;
   if (n_jobs == 0) return TPE_OK;
-  if (!jobs || !segs || !mu || !sigma || !wcdf || !counts || !sorted_x || !sorted_i) {
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !counts || !gen || !sorted_x || !sorted_i) {
     set_error("tpe_sort_candidates: null pointer");
     return TPE_E_ARG;
   }
   const int64_t gs = max_blocks(host_jobs, n_jobs, (int64_t)kSortPer, -1);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_sort_count, dim3((unsigned)gs, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
-                     segs, mu, sigma, wcdf, counts);
+                     segs, mu, sigma, wcdf, counts, gen);
   hipLaunchKernelGGL(k_sort_scan, dim3(n_jobs), dim3(kNB), 0, st, jobs, counts);
   hipLaunchKernelGGL(k_sort_scatter, dim3((unsigned)gs, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
-                     segs, mu, sigma, wcdf, counts, sorted_x, sorted_i);
+                     counts, gen, sorted_x, sorted_i);
   return check_launch("tpe_sort_candidates");
 }
 

@@ -404,14 +404,15 @@ class Engine:
             elif kind == "sorted":
                 npart = lib.tpe_score_partials(hjp, nj) * 2
                 d_part = self._buf("partial", 32 * max(npart, 1))
-                d_cnt = self._buf("sort_cnt", 4 * max(cnt_off, 1))
+                d_cnt = self._buf("sort_cnt", 8 * max(cnt_off, 1))
+                d_gen = self._buf("sort_gen", 4 * max(sort_off, 1))
                 d_sx = self._buf("sort_x", 4 * max(sort_off, 1))
                 d_si = self._buf("sort_i", 4 * max(sort_off, 1))
                 d_pairs = self._buf("pairs", 16)
                 with torch.cuda.stream(stream):
                     self._bufs["pairs"][:8].zero_()
                 L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
-                                                d_sx, d_si, sp), "tpe_sort_candidates")
+                                                d_gen, d_sx, d_si, sp), "tpe_sort_candidates")
                 tock("sort", e0)
                 e0 = tick()
                 L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,

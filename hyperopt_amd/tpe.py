@@ -209,4 +209,86 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
     return trials.new_trial_docs([first_new_id], [None], [domain.new_result()], [misc])
 
 
+class SuggestRequest(object):
+    """One study's suggest call for ``suggest_many``."""
+
+    def __init__(self, new_ids, domain, trials, seed, **kwargs):
+        self.new_ids, self.domain, self.trials, self.seed = new_ids, domain, trials, seed
+        self.kwargs = kwargs
+
+
+def suggest_many(requests, shard_studies=False):
+    """Batched suggest over many independent studies.
+
+    Every study runs tpe.suggest's exact logic, but the labels of all studies
+    that are live at the same conditional depth are scored in ONE engine launch
+    (one fit launch, one scoring launch per label kind).  Studies differ in
+    history, space and options; each keeps its own Philox keys.  With
+    ``shard_studies`` under torch.distributed, rank r serves studies r::world
+    (no collective on the data path) and returns None for the others.
+    Returns one list of trial documents per request.
+    """
+    rank, ws = hdist.world()
+    out = [None] * len(requests)
+    states = []
+    for qi, rq in enumerate(requests):
+        if shard_studies and ws > 1 and qi % ws != rank:
+            continue
+        kw = dict(prior_weight=_default_prior_weight, n_startup_jobs=_default_n_startup_jobs,
+                  n_EI_candidates=_default_n_EI_candidates, gamma=_default_gamma,
+                  linear_forgetting=_default_linear_forgetting, precision=None)
+        kw.update({k: v for k, v in rq.kwargs.items() if k != "verbose"})
+        labels = list(rq.domain.params)
+        hist = collect_history(rq.trials, labels)
+        if hist.tids.size < kw["n_startup_jobs"]:
+            out[qi] = rand.suggest(rq.new_ids, rq.domain, rq.trials, rq.seed)
+            continue
+        isb, isa = split_masks(hist, kw["gamma"])
+        n_ei = max(int(kw["n_EI_candidates"]), 0)
+        start, count = (0, n_ei) if (shard_studies or ws == 1) else hdist.shard(n_ei, rank, ws)
+        states.append(dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist, isb=isb, isa=isa,
+                           col={lab: j for j, lab in enumerate(labels)}, walk={}, stored={},
+                           live=[], start=start, count=count, done=n_ei == 0,
+                           prec=_precision(kw["precision"], n_ei, hist.tids.size)))
+    eng = engine() if states else None
+    while True:
+        batches = {}  # (prior_weight, lf, precision) -> [(state, label, work)]
+        for st in states:
+            if st["done"]:
+                continue
+            live = st["rq"].domain.reachable(st["walk"])
+            st["live"] = live
+            level = [lab for lab in live if lab not in st["walk"]]
+            if not level:
+                st["done"] = True
+                continue
+            key = (st["kw"]["prior_weight"], st["kw"]["linear_forgetting"], st["prec"])
+            for lab in level:
+                spec = st["rq"].domain.specs[lab]
+                j = st["col"][lab]
+                act, v = st["hist"].active[:, j], st["hist"].vals[:, j]
+                w = LabelWork(label=lab, kind=spec.kind, args=spec.args,
+                              obs_below=v[act & st["isb"]], obs_above=v[act & st["isa"]],
+                              n_cand=st["count"], key=label_key(st["rq"].seed, lab),
+                              cand_base=st["start"])
+                batches.setdefault(key, []).append((st, lab, w))
+        if not batches:
+            break
+        for (pw, lf, prec), items in batches.items():
+            res = eng.run([w for _, _, w in items], prior_weight=pw, lf=lf, precision=prec)
+            if ws > 1 and not shard_studies:
+                hdist.allreduce_best(res)
+            for (st, lab, _), r in zip(items, res):
+                st["walk"][lab], st["stored"][lab] = _decode(st["rq"].domain.specs[lab], r.value)
+    for st in states:
+        rq, live = st["rq"], set(st["live"])
+        tid = rq.new_ids[0]
+        misc = {"tid": tid, "cmd": rq.domain.cmd, "workdir": rq.domain.workdir,
+                "idxs": {lab: ([tid] if lab in live else []) for lab in st["labels"]},
+                "vals": {lab: ([st["stored"][lab]] if lab in live else [])
+                         for lab in st["labels"]}}
+        out[st["qi"]] = rq.trials.new_trial_docs([tid], [None], [rq.domain.new_result()], [misc])
+    return out
+
+
 _ = math

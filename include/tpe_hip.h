@@ -177,13 +177,14 @@ int tpe_score_continuous(const tpe_job* jobs, const tpe_job* host_jobs, int n_jo
  * n_cand candidates needs.  pairs (nullable): u64 counter of evaluated
  * (candidate, component) pairs. */
 int64_t tpe_sort_layout(int64_t n_cand, int64_t* sorted_slots);
-/* draw the candidates (same Philox streams as tpe_score_continuous) and
- * bucket them by value into sorted_x / sorted_i (candidate value, local
- * index) at job.sort_off; counts: job.cnt_off workspace */
+/* draw the candidates (same Philox streams as tpe_score_continuous) into
+ * gen (generation order) and bucket them by value into sorted_x / sorted_i
+ * (candidate value, local index); gen/sorted at job.sort_off, counts: a
+ * workspace of 2 x tpe_sort_layout() elements per job at 2 * job.cnt_off */
 int tpe_sort_candidates(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                         const tpe_seg* segs, const double* mu, const double* sigma,
-                        const double* wcdf, uint32_t* counts, float* sorted_x,
-                        uint32_t* sorted_i, void* stream);
+                        const double* wcdf, uint32_t* counts, float* gen,
+                        float* sorted_x, uint32_t* sorted_i, void* stream);
 /* score the bucketed candidates with component pruning + fused argmax */
 int tpe_score_sorted(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                      const tpe_seg* segs, const float* coef32, const float* coef32n,

@@ -198,3 +198,22 @@ def test_large_candidate_count_fp32_and_fp64_agree():
     d64 = tpe.suggest([2000], dom, trials, 99, n_EI_candidates=1 << 20, precision=64)[0]
     for k in ("x", "y"):
         assert abs(d32["misc"]["vals"][k][0] - d64["misc"]["vals"][k][0]) < 0.05
+
+
+def test_suggest_many_matches_single_calls():
+    """Batched multi-study suggest (C4 shape, scaled down) == per-study suggest."""
+    reqs = []
+    for s in range(6):
+        space = spaces.many_dists(hp) if s % 2 else spaces.nested(hp)
+        dom = Domain(passthrough, space)
+        trials = Trials()
+        fmin(lambda p: float(hash(str(p)) % 101) / 101.0, space, algo=rand.suggest,
+             max_evals=30 + 5 * s, trials=trials, rstate=np.random.RandomState(s),
+             show_progressbar=False)
+        reqs.append(tpe.SuggestRequest([len(trials)], dom, trials, 1000 + s,
+                                       n_EI_candidates=256))
+    batched = tpe.suggest_many(reqs)
+    for rq, docs in zip(reqs, batched):
+        single = tpe.suggest(rq.new_ids, rq.domain, rq.trials, rq.seed, n_EI_candidates=256)
+        assert docs[0]["misc"]["vals"] == single[0]["misc"]["vals"]
+        assert docs[0]["misc"]["idxs"] == single[0]["misc"]["idxs"]
