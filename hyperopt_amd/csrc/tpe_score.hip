@@ -145,6 +145,53 @@ __device__ __forceinline__ void lse32_begin(Lse32<R>& L, const float4* __restric
   L.fast = __all(ok);
 }
 
+// accumulate the mm components staged in `tile` (block-uniform mm)
+template <int R>
+__device__ __forceinline__ void lse32_tile(Lse32<R>& L, const float4* tile, int mm) {
+  if (L.fast) {
+    // packed fp32: two candidates per v_pk_fma_f32 (the microbenchmark in
+    // tools/valu_microbench.hip: 15.8 vs 18.9 cycles per 64 pairs)
+    static_assert(R % 2 == 0, "R must be even");
+    f32x2 xc2[R / 2], acc[R / 2];
+#pragma unroll
+    for (int p = 0; p < R / 2; ++p) {
+      xc2[p] = f32x2{L.xc[2 * p], L.xc[2 * p + 1]};
+      acc[p] = f32x2{0.0f, 0.0f};
+    }
+#pragma unroll 4
+    for (int k = 0; k < mm; ++k) {
+      const float4 c = tile[k];
+      const f32x2 a2 = f32x2{c.x, c.x}, b2 = f32x2{c.y, c.y}, c2 = f32x2{c.z, c.z};
+#pragma unroll
+      for (int p = 0; p < R / 2; ++p) {
+        const f32x2 t = __builtin_elementwise_fma(xc2[p], a2, b2);
+        const f32x2 v = __builtin_elementwise_fma(-t, t, c2);
+        acc[p] += f32x2{__builtin_amdgcn_exp2f(v.x), __builtin_amdgcn_exp2f(v.y)};
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < R / 2; ++p) {
+      L.s[2 * p] += acc[p].x;
+      L.s[2 * p + 1] += acc[p].y;
+    }
+  } else {
+    for (int k = 0; k < mm; ++k) {
+      const float4 c = tile[k];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float t = fmaf(L.xc[r], c.x, c.y);
+        const float v = fmaf(-t, t, c.z);
+        if (v > L.m[r]) {
+          L.s[r] = L.s[r] * __builtin_amdgcn_exp2f(L.m[r] - v) + 1.0f;
+          L.m[r] = v;
+        } else if (c.z > -INFINITY) {  // masked (wide) components add nothing
+          L.s[r] += __builtin_amdgcn_exp2f(v - L.m[r]);
+        }
+      }
+    }
+  }
+}
+
 // accumulate components [k0, k1) of `coef` (block-uniform bounds; syncs)
 template <int R>
 __device__ __forceinline__ void lse32_accum(Lse32<R>& L, const float4* __restrict__ coef, int k0,
@@ -154,49 +201,72 @@ __device__ __forceinline__ void lse32_accum(Lse32<R>& L, const float4* __restric
     __syncthreads();
     for (int j = threadIdx.x; j < mm; j += kBS) tile[j] = coef[t0 + j];
     __syncthreads();
-    if (L.fast) {
-      // packed fp32: two candidates per v_pk_fma_f32 (the microbenchmark in
-      // tools/valu_microbench.hip: 15.8 vs 18.9 cycles per 64 pairs)
-      static_assert(R % 2 == 0, "R must be even");
-      f32x2 xc2[R / 2], acc[R / 2];
-#pragma unroll
-      for (int p = 0; p < R / 2; ++p) {
-        xc2[p] = f32x2{L.xc[2 * p], L.xc[2 * p + 1]};
-        acc[p] = f32x2{0.0f, 0.0f};
-      }
-#pragma unroll 4
-      for (int k = 0; k < mm; ++k) {
-        const float4 c = tile[k];
-        const f32x2 a2 = f32x2{c.x, c.x}, b2 = f32x2{c.y, c.y}, c2 = f32x2{c.z, c.z};
-#pragma unroll
-        for (int p = 0; p < R / 2; ++p) {
-          const f32x2 t = __builtin_elementwise_fma(xc2[p], a2, b2);
-          const f32x2 v = __builtin_elementwise_fma(-t, t, c2);
-          acc[p] += f32x2{__builtin_amdgcn_exp2f(v.x), __builtin_amdgcn_exp2f(v.y)};
-        }
-      }
-#pragma unroll
-      for (int p = 0; p < R / 2; ++p) {
-        L.s[2 * p] += acc[p].x;
-        L.s[2 * p + 1] += acc[p].y;
-      }
-    } else {
-      for (int k = 0; k < mm; ++k) {
-        const float4 c = tile[k];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const float t = fmaf(L.xc[r], c.x, c.y);
-          const float v = fmaf(-t, t, c.z);
-          if (v > L.m[r]) {
-            L.s[r] = L.s[r] * __builtin_amdgcn_exp2f(L.m[r] - v) + 1.0f;
-            L.m[r] = v;
-          } else if (c.z > -INFINITY) {  // masked (wide) components add nothing
-            L.s[r] += __builtin_amdgcn_exp2f(v - L.m[r]);
-          }
-        }
-      }
-    }
+    lse32_tile(L, tile, mm);
   }
+}
+
+// largest / smallest term of component c over centred candidates [xlo, xhi]
+// (t = xc*a + b is increasing in xc, v = c - t^2)
+__device__ __forceinline__ float term_max(const float4 c, float xlo, float xhi) {
+  const float tl = fmaf(xlo, c.x, c.y), th = fmaf(xhi, c.x, c.y);
+  const float t2 = (tl <= 0.0f && th >= 0.0f) ? 0.0f : fminf(tl * tl, th * th);
+  return c.z - t2;
+}
+__device__ __forceinline__ float term_min(const float4 c, float xlo, float xhi) {
+  const float tl = fmaf(xlo, c.x, c.y), th = fmaf(xhi, c.x, c.y);
+  return c.z - fmaxf(tl * tl, th * th);
+}
+
+// like lse32_accum, but only components whose largest term over the block's
+// candidates reaches `thr` are staged (compacted, in index order) and summed.
+// Returns the number of components summed (block-uniform).
+template <int R>
+__device__ __forceinline__ int lse32_accum_pruned(Lse32<R>& L, const float4* __restrict__ coef,
+                                                  int k0, int k1, float4* tile, int* cnt,
+                                                  float xlo, float xhi, float thr) {
+  constexpr int kQ = kTile32 / kBS, kW = kBS / kWave;
+  const int wid = threadIdx.x / kWave;
+  const unsigned lane = lane_id();
+  const uint64_t below_me = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int used = 0;
+  for (int t0 = k0; t0 < k1; t0 += kTile32) {
+    const int mm = min(kTile32, k1 - t0);
+    float4 c[kQ];
+    bool keep[kQ];
+    uint64_t bal[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const int j = q * kBS + threadIdx.x;
+      keep[q] = false;
+      if (j < mm) {
+        c[q] = coef[t0 + j];
+        keep[q] = term_max(c[q], xlo, xhi) >= thr;
+      }
+      bal[q] = __ballot(keep[q]);
+    }
+    __syncthreads();  // previous tile consumed, cnt free
+    if (lane == 0)
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) cnt[q * kW + wid] = __popcll(bal[q]);
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      int mine = 0;
+#pragma unroll
+      for (int w = 0; w < kW; ++w) {
+        const int n = cnt[q * kW + w];
+        if (w < wid) mine += n;
+        tot += n;
+      }
+      if (keep[q]) tile[pre + mine + __popcll(bal[q] & below_me)] = c[q];
+      pre = tot;
+    }
+    __syncthreads();
+    lse32_tile(L, tile, tot);
+    used += tot;
+  }
+  return used;
 }
 
 template <int R>
@@ -570,6 +640,9 @@ __global__ __launch_bounds__(kBS) void k_score_sorted(
   __shared__ BestT red[kBS / kWave];
   __shared__ float fred[3][kBS / kWave];
   __shared__ int win[2];
+  __shared__ float yr[2];
+  __shared__ int cnt[kTile32 / kWave];
+  __shared__ float lred[2][kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t base = (int64_t)blockIdx.x * (kBS * kR32);
@@ -625,6 +698,8 @@ __global__ __launch_bounds__(kBS) void k_score_sorted(
       c = fminf(c, fred[2][k]);
     }
     const int nc = SA.n_obs + 1;
+    yr[0] = a;
+    yr[1] = b;
     if (c >= (float)SA.lglob) {
       const float* PM = pm + SA.comp_off;
       const float* SMn = sm + SA.comp_off;
@@ -647,9 +722,51 @@ __global__ __launch_bounds__(kBS) void k_score_sorted(
     lse32_accum(L, coef32 + SA.comp_off, 0, SA.n_obs + 1, tile);
     evaluated = SA.n_obs + 1;
   } else {
-    if (k_hi >= k_lo) lse32_accum(L, coef32n + SA.comp_off, k_lo, k_hi + 1, tile);
+    // Block threshold.  Every candidate of the block has log2(sum) >= Lb =
+    // log2(sum_k 2^min_block(v_k)) over the window + wide components.  A
+    // component whose largest term over the block is below Lb - margin adds
+    // less than 2^-margin of the sum; with margin = log2(n) + 20 all dropped
+    // components together change the sum by < 2^-20 (relative).  Components
+    // outside the window were already below 2^(lglob - 40) (tpe_fit.hip).
+    const float xlo = yr[0] - cen, xhi = yr[1] - cen;
+    float m = -INFINITY, sacc = 0.0f;
+    auto add = [&](const float4 cc) {
+      const float v = term_min(cc, xlo, xhi);
+      if (v > m) {
+        sacc = sacc * __builtin_amdgcn_exp2f(m - v) + 1.0f;
+        m = v;
+      } else if (v > -INFINITY) {
+        sacc += __builtin_amdgcn_exp2f(v - m);
+      }
+    };
+    for (int k = k_lo + (int)threadIdx.x; k <= k_hi; k += kBS) add(coef32n[SA.comp_off + k]);
+    for (int k = threadIdx.x; k < SA.n_wide; k += kBS) add(wide32[SA.comp_off + k]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float mo = __shfl_xor(m, off, kWave), so = __shfl_xor(sacc, off, kWave);
+      const float mn = fmaxf(m, mo);
+      sacc = (mn == -INFINITY) ? 0.0f
+                               : sacc * __builtin_amdgcn_exp2f(m - mn) + so * __builtin_amdgcn_exp2f(mo - mn);
+      m = mn;
+    }
+    if (lane_id() == 0) {
+      lred[0][wid] = m;
+      lred[1][wid] = sacc;
+    }
+    __syncthreads();
+    float mb = -INFINITY;
+    for (int w = 0; w < kBS / kWave; ++w) mb = fmaxf(mb, lred[0][w]);
+    float sb = 0.0f;
+    for (int w = 0; w < kBS / kWave; ++w)
+      if (lred[0][w] > -INFINITY) sb += lred[1][w] * __builtin_amdgcn_exp2f(lred[0][w] - mb);
+    const float margin = __builtin_amdgcn_logf((float)(SA.n_obs + 1)) + 20.0f;
+    const float thr = (mb > -INFINITY) ? mb + __builtin_amdgcn_logf(sb) - margin : -INFINITY;
+    evaluated = 0;
+    if (k_hi >= k_lo)
+      evaluated = lse32_accum_pruned(L, coef32n + SA.comp_off, k_lo, k_hi + 1, tile, cnt, xlo,
+                                     xhi, thr);
     lse32_accum(L, wide32 + SA.comp_off, 0, SA.n_wide, tile);
-    evaluated = (k_hi >= k_lo ? k_hi - k_lo + 1 : 0) + SA.n_wide;
+    evaluated += SA.n_wide;
   }
   lse32_end(L, SA, la);
 
