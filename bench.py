@@ -211,6 +211,7 @@ def main():
     # dominant kernel: unquantized continuous scoring of the 30 continuous labels
     cont = [w for w in works if w.kind in ("uniform", "loguniform", "normal", "lognormal")]
     dense_pairs = sum(n_cand * (w.obs_below.size + 1 + w.obs_above.size + 1) for w in cont)
+    exec_cand = n_cand * len(cont)  # sorted value + index read once per candidate
     group = "cont" if args.dense else "sorted"
     kname = "k_score32 (tpe_score_continuous)" if args.dense else \
         "k_score_sorted (tpe_score_sorted)"
@@ -225,13 +226,16 @@ def main():
 
     total_cand = len(space) * n_cand * world * args.steps
     value = total_cand / elapsed
-    traffic = None
-    tfile = os.path.join(HERE, "profiles", "traffic_k_score32.json")
+    # per-launch HBM bytes / VALU busy of the dominant kernel, from the PMC
+    # passes of tools/profile_round.sh (tools/make_traffic.py)
+    traffic, prof = None, {}
+    tfile = os.path.join(HERE, "profiles", "traffic.json")
     if os.path.exists(tfile):
-        try:
-            traffic = json.load(open(tfile)).get("bytes_per_launch")
-        except Exception:
-            traffic = None
+        prof = json.load(open(tfile))
+        if prof.get("kernel") in kname:
+            traffic = prof.get("bytes_per_launch")
+        else:
+            prof = {}
     line = {
         "metric": "EI candidates scored/sec (50-dim, 10k trials)",
         "value": value,
@@ -258,7 +262,10 @@ def main():
                      "flops_per_pair": FLOPS_PER_PAIR,
                      "evaluated_pairs_per_launch": exec_pairs,
                      "dense_pairs_per_launch": dense_pairs,
-                     "dense_equivalent_tflops": effective},
+                     "dense_equivalent_tflops": effective,
+                     "algorithmic_bytes_per_launch": 8 * exec_cand,
+                     "valu_busy": prof.get("valu_busy"),
+                     "traffic_source": prof.get("source")},
         "group_ms": group_ms,
     }
     if rank == 0 and world == 1:

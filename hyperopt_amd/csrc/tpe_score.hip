@@ -532,31 +532,71 @@ __global__ __launch_bounds__(kBS) void k_sort_count(
 
 // K2: per job, global start of every (block, bin) run in (bin, block) order;
 // counts keep their values (row b at 2*cnt_off), offsets go to the second half
+// K2: exclusive offsets of every (block, bin) run in bin-major order.  The
+// count matrix is cut into chunks of kScanChunk blocks: column sums per chunk
+// (K2a), one scan over (bin, chunk) per job (K2b), offsets per chunk (K2c).
+constexpr int kScanChunk = 32;
+
+__device__ __forceinline__ int64_t sort_nblk(const tpe_job& J) {
+  return (J.n_cand + kSortPer - 1) / kSortPer;
+}
+
+__global__ __launch_bounds__(kNB) void k_sort_colsum(const tpe_job* __restrict__ jobs,
+                                                     uint32_t* __restrict__ counts) {
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t nblk = sort_nblk(J);
+  const int64_t b0 = (int64_t)blockIdx.x * kScanChunk;
+  if (b0 >= nblk) return;
+  const int64_t b1 = min(nblk, b0 + kScanChunk);
+  const uint32_t* C = counts + 2 * J.cnt_off;
+  uint32_t* S = counts + 2 * J.cnt_off + 2 * nblk * kNB;
+  uint32_t t = 0;
+#pragma unroll 8
+  for (int64_t b = b0; b < b1; ++b) t += C[b * kNB + threadIdx.x];
+  S[blockIdx.x * kNB + threadIdx.x] = t;
+}
+
 __global__ __launch_bounds__(kNB) void k_sort_scan(const tpe_job* __restrict__ jobs,
                                                    uint32_t* __restrict__ counts) {
   __shared__ uint32_t tot[kNB];
   const tpe_job J = jobs[blockIdx.x];
-  const int64_t nblk = (J.n_cand + kSortPer - 1) / kSortPer;
-  const uint32_t* C = counts + 2 * J.cnt_off;
-  uint32_t* O = counts + 2 * J.cnt_off + nblk * kNB;
+  const int64_t nblk = sort_nblk(J);
+  const int nch = (int)((nblk + kScanChunk - 1) / kScanChunk);
+  uint32_t* S = counts + 2 * J.cnt_off + 2 * nblk * kNB;
   const int bin = threadIdx.x;
   uint32_t t = 0;
-  for (int64_t b = 0; b < nblk; ++b) t += C[b * kNB + bin];
+  for (int c = 0; c < nch; ++c) t += S[c * kNB + bin];
   tot[bin] = t;
   __syncthreads();
-  if (bin == 0) {
-    uint32_t acc = 0;
-    for (int i = 0; i < kNB; ++i) {
-      const uint32_t c = tot[i];
-      tot[i] = acc;
-      acc += c;
-    }
+  // inclusive Hillis-Steele scan over bins
+  for (int d = 1; d < kNB; d <<= 1) {
+    const uint32_t v = bin >= d ? tot[bin - d] : 0u;
+    __syncthreads();
+    tot[bin] += v;
+    __syncthreads();
   }
-  __syncthreads();
-  uint32_t run = tot[bin];
-  for (int64_t b = 0; b < nblk; ++b) {
-    O[b * kNB + bin] = run;
-    run += C[b * kNB + bin];
+  uint32_t run = tot[bin] - t;  // exclusive
+  for (int c = 0; c < nch; ++c) {
+    const uint32_t v = S[c * kNB + bin];
+    S[c * kNB + bin] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(kNB) void k_sort_offsets(const tpe_job* __restrict__ jobs,
+                                                      uint32_t* __restrict__ counts) {
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t nblk = sort_nblk(J);
+  const int64_t b0 = (int64_t)blockIdx.x * kScanChunk;
+  if (b0 >= nblk) return;
+  const int64_t b1 = min(nblk, b0 + kScanChunk);
+  const uint32_t* C = counts + 2 * J.cnt_off;
+  uint32_t* O = counts + 2 * J.cnt_off + nblk * kNB;
+  const uint32_t* S = counts + 2 * J.cnt_off + 2 * nblk * kNB;
+  uint32_t run = S[blockIdx.x * kNB + threadIdx.x];
+  for (int64_t b = b0; b < b1; ++b) {
+    O[b * kNB + threadIdx.x] = run;
+    run += C[b * kNB + threadIdx.x];
   }
 }
 
@@ -818,8 +858,14 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   for (int r = 0; r < kLatR; ++r) {
     const int64_t li = base + r * kBS + threadIdx.x;
     if (li >= J.n_cand) break;
-    double v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
-    if (lgmm) v = exp(v);
+    double v;
+    if (J.flags & TPE_F_DRAW32) {
+      const float f = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
+      v = lgmm ? (double)__expf(f) : (double)f;
+    } else {
+      v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+      if (lgmm) v = exp(v);
+    }
     const int64_t slot = (int64_t)rint(v / J.q) - J.lat_kmin;  // np.round(x/q) (tpe.py:106)
     if (slot < 0 || slot >= J.lat_n) {
       atomicOr(err, 2);
@@ -1292,9 +1338,12 @@ extern "C" int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, 
 }
 
 extern "C" int64_t tpe_sort_layout(int64_t n_cand, int64_t* sorted_slots) {
-  // count matrix (blocks x bins) twice: counts, then run offsets
+  // u32 words used = 2 x the returned value: the count matrix (blocks x
+  // bins), the run offsets (same shape), then per-chunk column sums
   if (sorted_slots) *sorted_slots = n_cand;
-  return ((n_cand + kSortPer - 1) / kSortPer) * (int64_t)kNB;
+  const int64_t nblk = (n_cand + kSortPer - 1) / kSortPer;
+  const int64_t nch = (nblk + kScanChunk - 1) / kScanChunk;
+  return nblk * (int64_t)kNB + (nch * (int64_t)kNB + 1) / 2;
 }
 
 static bool check_sorted_jobs(const char* fn, const tpe_job* host_jobs, int n_jobs) {
@@ -1327,7 +1376,12 @@ extern "C" int tpe_sort_candidates(const tpe_job* jobs, const tpe_job* host_jobs
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_sort_count, dim3((unsigned)gs, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
                      segs, mu, sigma, wcdf, counts, gen);
+  const int64_t gch = (gs + kScanChunk - 1) / kScanChunk;
+  hipLaunchKernelGGL(k_sort_colsum, dim3((unsigned)gch, (unsigned)n_jobs), dim3(kNB), 0, st, jobs,
+                     counts);
   hipLaunchKernelGGL(k_sort_scan, dim3(n_jobs), dim3(kNB), 0, st, jobs, counts);
+  hipLaunchKernelGGL(k_sort_offsets, dim3((unsigned)gch, (unsigned)n_jobs), dim3(kNB), 0, st, jobs,
+                     counts);
   hipLaunchKernelGGL(k_sort_scatter, dim3((unsigned)gs, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
                      counts, gen, sorted_x, sorted_i);
   return check_launch("tpe_sort_candidates");

@@ -28,6 +28,7 @@ from . import _lib as L
 
 EPS = 1e-12  # tpe.py:32
 DEFAULT_LF = 25  # tpe.py:36
+DRAW32_MAX_SLOT = 1 << 12  # fp32 lattice draws only while |k| <= 2^12
 LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense fallback
 _ALIGN = 256
 
@@ -305,6 +306,9 @@ class Engine:
                 j["q"] = P["q"]
                 if i in lat_ranges:
                     j["lat_off"], j["lat_kmin"], j["lat_n"] = lat_off, *lat_ranges[i]
+                    kmin, nk = lat_ranges[i]
+                    if precision == 32 and max(abs(kmin), abs(kmin + nk - 1)) <= DRAW32_MAX_SLOT:
+                        j["flags"] |= L.F_DRAW32
                     lat_off += lat_ranges[i][1]
                 elif i in fallback:
                     j["cand_off"] = qfb_off

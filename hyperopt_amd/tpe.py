@@ -122,10 +122,31 @@ def split_masks(hist, gamma, gamma_cap=DEFAULT_LF):
     """
     T = hist.losses.size
     n_below = min(int(np.ceil(gamma * np.sqrt(T))), gamma_cap)
-    order = np.argsort(hist.losses, kind="stable")
-    below_tids = hist.tids[order[:n_below]]
-    above_tids = hist.tids[order[n_below:]]
-    return np.isin(hist.obs_tids, below_tids), np.isin(hist.obs_tids, above_tids)
+    below_rows = _smallest_rows(hist.losses, n_below)
+    if hist.obs_tids.size == T and np.array_equal(hist.obs_tids, hist.tids):
+        isb = np.zeros(T, bool)  # no from_tid aliasing: rows are the tids
+        isb[below_rows] = True
+        return isb, ~isb
+    below = np.zeros(T, bool)
+    below[below_rows] = True
+    return np.isin(hist.obs_tids, hist.tids[below]), np.isin(hist.obs_tids, hist.tids[~below])
+
+
+def _smallest_rows(losses, n):
+    """Rows of argsort(losses, kind="stable")[:n] (as a set), in O(T) for small n:
+    everything strictly below the n-th smallest loss, then the earliest rows
+    equal to it."""
+    T = losses.size
+    if n <= 0:
+        return np.zeros(0, np.int64)
+    if n >= T:
+        return np.arange(T)
+    v = np.partition(losses, n - 1)[n - 1]
+    if np.isnan(v):
+        return np.argsort(losses, kind="stable")[:n]
+    lt = np.flatnonzero(losses < v)
+    eq = np.flatnonzero(losses == v)[:n - lt.size]
+    return np.concatenate([lt, eq])
 
 
 def _precision(precision, n_ei, T):

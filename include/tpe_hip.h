@@ -48,7 +48,10 @@ enum {
   TPE_F_LOW = 1,        /* lower bound present (tpe.py:93, 166)              */
   TPE_F_HIGH = 2,       /* upper bound present                               */
   TPE_F_QUANT = 4,      /* quantized (q is not None)                         */
-  TPE_F_INJECTED = 8    /* candidates read from `cand` instead of sampled    */
+  TPE_F_INJECTED = 8,   /* candidates read from `cand` instead of sampled    */
+  TPE_F_DRAW32 = 16     /* sampled quantized job: draw in fp32 (set only when
+                           every lattice index |k| <= 2^12, so fp32 resolves a
+                           slot to < 2^-11 of q)                              */
 };
 
 /*

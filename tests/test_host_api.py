@@ -243,3 +243,18 @@ def test_pyll_graph_ops():
     assert pyll.rec_eval(sw, memo=memo) == 10
     s = pyll.sample(hp.normal("n", 0, 1), np.random.RandomState(0))
     assert np.isfinite(s)
+
+
+def test_smallest_rows_matches_stable_argsort():
+    """split_masks' O(T) below-set selection == argsort(kind="stable")[:n] as a set
+    (ties, inf and NaN losses included; tpe.py:637-640)."""
+    from hyperopt_amd.tpe import _smallest_rows
+    rng = np.random.RandomState(0)
+    for trial in range(2000):
+        T, n = rng.randint(1, 120), rng.randint(0, 30)
+        if trial % 2:
+            losses = rng.choice([0.0, 1.0, 2.0, np.inf, np.nan, -1.0], size=T)
+        else:
+            losses = rng.normal(size=T)
+        want = set(np.argsort(losses, kind="stable")[:n].tolist())
+        assert set(_smallest_rows(losses, n).tolist()) == want, (losses, n)

@@ -1,0 +1,36 @@
+"""profiles/<tag>_counters.json (tools/rocpd_summary.py) -> profiles/traffic.json,
+the per-launch HBM traffic and VALU busy figures bench.py reports for its
+dominant kernel.
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE counts half the
+bytes of coalesced streaming reads (MI355X_MICROARCH.md, HBM / rocprofv3
+section), so it is doubled; WRITE_SIZE is taken as is.  GRBM_GUI_ACTIVE is
+summed over the 8 XCDs; VALU busy = SQ_ACTIVE_INST_VALU * 4 / 1024 SIMDs /
+(GRBM_GUI_ACTIVE / 8).
+
+    python tools/make_traffic.py profiles/r01_v6_counters.json k_score_sorted
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(src, kernel):
+    c = json.load(open(src))[kernel]
+    fetch = 2.0 * c["FETCH_SIZE"] * 1024.0
+    write = c["WRITE_SIZE"] * 1024.0
+    out = {"kernel": kernel, "bytes_per_launch": fetch + write, "fetch_bytes": fetch,
+           "write_bytes": write, "source": os.path.relpath(src, HERE),
+           "correction": "FETCH_SIZE x2 (gfx950 half-count), KiB -> B"}
+    if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        out["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4.0 / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0)
+    if "SQ_INSTS_VALU" in c:
+        out["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
+    json.dump(out, open(os.path.join(HERE, "profiles", "traffic.json"), "w"), indent=1)
+    print(out)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
