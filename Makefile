@@ -2,14 +2,14 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := hyperopt_amd/csrc
-SRCS := $(CSRC)/tpe_fit.hip $(CSRC)/tpe_score.hip $(CSRC)/tpe_util.hip
+SRCS := $(CSRC)/tpe_fit.hip $(CSRC)/tpe_score.hip $(CSRC)/tpe_table.hip $(CSRC)/tpe_util.hip
 OBJS := $(SRCS:.hip=.o)
 LIB := hyperopt_amd/libtpe_hip.so
 FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function
 
 all: $(LIB)
 
-$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/tpe_common.hpp include/tpe_hip.h
+$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/tpe_common.hpp $(CSRC)/tpe_sample.hpp include/tpe_hip.h
 	$(HIPCC) $(FLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)

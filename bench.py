@@ -157,7 +157,9 @@ def main():
     ap.add_argument("--n-cand", type=int, default=N_CAND)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense", action="store_true",
-                    help="score with the dense fp32 kernel instead of the sorted/pruned one")
+                    help="score with the dense fp32 kernel (same as --scorer dense)")
+    ap.add_argument("--scorer", default="auto", choices=("auto", "dense", "sorted", "table"),
+                    help="fp32 kernel for the unquantized labels (engine.Engine.run)")
     args = ap.parse_args()
 
     import torch
@@ -171,6 +173,7 @@ def main():
     from hyperopt_amd.engine import Engine
     from hyperopt_amd import dist as hdist
 
+    scorer = "dense" if args.dense else args.scorer
     space = c3_space()
     vals, losses = c3_history(space)
     eng = Engine()
@@ -180,7 +183,7 @@ def main():
     def step(k, timers=None):
         sp = split(vals, losses)
         works = make_works(space, sp, k, n_cand, cand_base)
-        res = eng.run(works, precision=args.precision, timers=timers, pruned=not args.dense)
+        res = eng.run(works, precision=args.precision, timers=timers, scorer=scorer)
         if world > 1:
             hdist.allreduce_best(res)
         return works, res

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32 = 1, 2, 4, 8, 16
+ABI_VERSION = 3
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -35,7 +36,12 @@ JOB_DTYPE = np.dtype([
     ("low", "<f8"), ("high", "<f8"), ("q", "<f8"), ("n_cand", "<i8"), ("cand_base", "<i8"),
     ("cand_off", "<i8"), ("key", "<u8"), ("lat_off", "<i8"), ("lat_kmin", "<i8"),
     ("lat_n", "<i8"), ("out_off", "<i8"), ("bin_lo", "<f8"), ("bin_hi", "<f8"),
-    ("sort_off", "<i8"), ("cnt_off", "<i8")], align=True)
+    ("sort_off", "<i8"), ("cnt_off", "<i8"), ("tbl_off", "<i8"), ("tbl_cap", "<i8")],
+    align=True)
+TABLE_DTYPE = np.dtype([
+    ("lo", "<f8"), ("hi", "<f8"), ("h_below", "<f8"), ("h_above", "<f8"), ("origin", "<f8"),
+    ("h", "<f8"), ("inv_h", "<f4"), ("inv_w", "<f4"), ("nb", "<i4"), ("n_wide_below", "<i4"),
+    ("n_wide_above", "<i4"), ("pad", "<i4")], align=True)
 BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
                        ("n_scored", "<i8")], align=True)
 
@@ -55,6 +61,10 @@ _SIGNATURES = {
     "tpe_score_sorted": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
                               _P]),
     "tpe_cat_posterior": (_I, [_P, _P, _I, _P, _P, _P, _P]),
+    "tpe_table_partials": (_I64, [_P, _I]),
+    "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_score_table": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
+                             _P, _P, _P]),
     "tpe_score_partials": (_I64, [_P, _I]),
     "tpe_score_continuous": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P,
                                   _P, _I64, _P, _P]),
@@ -92,9 +102,13 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    sizes = (ctypes.c_int32 * 4)()
-    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 4)
-    want = (SEG_DTYPE.itemsize, CAT_SEG_DTYPE.itemsize, JOB_DTYPE.itemsize, BEST_DTYPE.itemsize)
+    sizes = (ctypes.c_int32 * 5)()
+    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 5)
+    want = (SEG_DTYPE.itemsize, CAT_SEG_DTYPE.itemsize, JOB_DTYPE.itemsize, BEST_DTYPE.itemsize,
+            TABLE_DTYPE.itemsize)
+    if lib.tpe_abi_version() != ABI_VERSION:
+        raise ImportError("hyperopt_amd: libtpe_hip.so ABI %d, expected %d (rebuild with make)"
+                          % (lib.tpe_abi_version(), ABI_VERSION))
     if tuple(sizes) != want:
         raise ImportError("hyperopt_amd: ABI struct size mismatch %s vs %s" % (tuple(sizes), want))
     _lib = lib

@@ -1,0 +1,622 @@
+// tpe_table.hip -- cell-table scoring of unquantized continuous labels.
+//
+// Computes the same per-candidate quantities as GMM1_lpdf / LGMM1_lpdf
+// (hyperopt/tpe.py:117-180, 265-307, logsum_rows :260-262) and the argmax of
+// broadcast_best (tpe.py:649-658), for candidates sampled from the below
+// posterior (tpe.py:79-106, 229-257) -- but without a component loop per
+// candidate.
+//
+// Expansion.  In the scoring coordinate y (x for GMM1, log x for LGMM1) a
+// mixture's density is S(y) = sum_j exp(l_j(y)),
+//     l_j(y) = lc_j - 0.5 ((y - mu_j) inv_j)^2        (coef64: {mu, inv, lc, w}).
+// The candidate range is cut into nb cells of half-width h.  Around a cell
+// centre y0, with u = (y - y0)/h in [-1, 1],
+//     l_j(y0 + h u) = l_j(y0) + A_j u + B_j u^2,
+//     A_j = -h (y0 - mu_j) inv_j^2,   B_j = -0.5 h^2 inv_j^2,
+// and exp(A u + B u^2) = sum_n c_n u^n with c_0 = 1, c_1 = A,
+// (n+1) c_{n+1} = A c_n + 2B c_{n-1}.  So on the cell
+//     S(y) = exp(m) * sum_{n<kP} P_n u^n,  P_n = sum_j exp(l_j(y0) - m) c_n^(j),
+// a degree-11 polynomial per cell and mixture: the per-candidate work is two
+// Horner evaluations and two logs, independent of the number of components.
+//
+// Error.  Every term is positive, so the relative error of S is at most the
+// worst relative error of one component's truncated series.  By the Cauchy
+// estimate on |u| = 8, for |u| <= 1 that is
+//     exp(9|A| + 65|B|) * 8^-11 / 7  <=  5.5e-9   when 9|A| + 65|B| <= 5.8.
+// Components whose largest term on the cell is below exp(-25)/M of the
+// cell's smallest lower bound on S are left out (together < 1.4e-11 of S).
+// The plan step chooses h so that every component that can be included in
+// any cell satisfies the bound; if the cell budget (job.tbl_cap) forces a
+// larger h, failing cells are flagged and their candidates take the exact
+// fp32 log-sum-exp over all components.  Candidates outside the grid
+// (injected values, rounding at the edges) take the exact path too.
+//
+// Layout.  One tpe_table per job plus 32 floats per cell:
+//     [0,12) below P_n   [12,24) above P_n   [24] m_below  [25] m_above
+//     [26] y0            [27] flags (bit 0 below, bit 1 above failed)
+// 128 B = one cache line per cell, gathered once per candidate.
+#include <algorithm>
+
+#include "tpe_common.hpp"
+#include "tpe_sample.hpp"
+
+namespace tpe {
+namespace {
+constexpr int kP = 12;               // expansion terms per cell and mixture
+constexpr int kCellF = 32;           // floats per cell
+constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
+constexpr double kTauExtra = 25.0;   // exclusion margin (nats) on top of log(M)
+constexpr double kDrawZ = 5.8;       // |z| of an fp32 Box-Muller draw is < 5.77
+constexpr float kULim = 1.05f;       // |u| accepted by the scorer (fp32 cell-centre rounding)
+constexpr int kTR = 8;               // candidates per thread in the scorer
+constexpr int kBuildBlocks = 512;    // build blocks per job (grid-stride over cells)
+constexpr float kLn2T = 0.6931471805599453f;
+
+__device__ __forceinline__ double4 ld4(const double* coef64, int64_t k) {
+  return reinterpret_cast<const double4*>(coef64)[k];
+}
+
+// s = h*inv such that 9 s (z + s) + 32.5 s^2 <= kRhoLim (|y0-mu| inv <= z + s)
+__device__ __forceinline__ double admissible_s(double z) {
+  return (-9.0 * z + sqrt(81.0 * z * z + 166.0 * kRhoLim)) / 83.0;
+}
+
+// inclusive block scans over threadIdx order (256 threads); `sh` holds one
+// entry per wave.  Every thread gets its own inclusive result.
+__device__ __forceinline__ double block_scan_max(double v, double* sh) {
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const double o = __shfl_up(v, off, kWave);
+    if (lane >= off) v = fmax(v, o);
+  }
+  __syncthreads();
+  if (lane == kWave - 1) sh[wid] = v;
+  __syncthreads();
+  for (int w = 0; w < wid; ++w) v = fmax(v, sh[w]);
+  return v;
+}
+__device__ __forceinline__ int block_scan_sum(int v, int* sh) {
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int o = __shfl_up(v, off, kWave);
+    if (lane >= off) v += o;
+  }
+  __syncthreads();
+  if (lane == kWave - 1) sh[wid] = v;
+  __syncthreads();
+  for (int w = 0; w < wid; ++w) v += sh[w];
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// plan: coordinate range, admissible half-width, reach windows, wide list.
+// grid (2, n_jobs): blockIdx.x = 0 below mixture, 1 above mixture.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBS) void k_table_reach(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ coef64, double* __restrict__ reach_hi,
+    double* __restrict__ reach_lo, int32_t* __restrict__ wide_idx, tpe_table* __restrict__ tables) {
+  __shared__ double red[kBS / kWave];
+  __shared__ int red_n[kBS / kWave];
+  __shared__ double scan_d[kBS / kWave];
+  __shared__ int scan_n[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  const tpe_seg SB = segs[J.below];
+  const tpe_seg S = segs[blockIdx.x ? J.above : J.below];
+  tpe_table* Tb = tables + blockIdx.y;
+
+  // 1) range of the scoring coordinate: where the below sampler can put a
+  //    candidate (mu +- 5.8 sigma per component), clipped to the bounds
+  double a = INFINITY, b = -INFINITY;
+  for (int k = threadIdx.x; k < SB.n_obs + 1; k += kBS) {
+    const double m = mu[SB.comp_off + k], s = sigma[SB.comp_off + k];
+    a = fmin(a, m - kDrawZ * s);
+    b = fmax(b, m + kDrawZ * s);
+  }
+  a = -block_max<kBS, double>(-a, red);
+  b = block_max<kBS, double>(b, red);
+  if (J.flags & TPE_F_INJECTED) {
+    a = fmax(a, J.bin_lo);
+    b = fmin(b, J.bin_hi);
+  }
+  if (J.flags & TPE_F_LOW) a = fmax(a, J.low);
+  if (J.flags & TPE_F_HIGH) b = fmin(b, J.high);
+  if (!(isfinite(a) && isfinite(b) && b >= a)) {
+    // empty or degenerate: one cell at a finite point, candidates off it are exact
+    const double c = isfinite(a) ? a : (isfinite(b) ? b : SB.prior_mu);
+    a = b = c;
+  }
+
+  // 2) global lower bound of log S over [a, b]: the prior component's smallest term
+  const int nc = S.n_obs + 1;
+  const int64_t off = S.comp_off;
+  const int pos = S.prior_pos;
+  const double ps = S.prior_sigma;
+  const double4 cp = ld4(coef64, off + pos);
+  const double far = fmax(fabs(a - cp.x), fabs(b - cp.x)) * cp.y;
+  const double T = cp.z - 0.5 * far * far - (log((double)nc) + kTauExtra);
+
+  // 3) per component: largest normalised distance at which it can matter,
+  //    admissible half-width and reach interval [mu - r, mu + r]; wide
+  //    components (the prior, sigma >= prior_sigma/4) are listed apart.
+  //    Coalesced 256-element tiles: prefix max of mu + r and the wide list
+  //    front to back, suffix min of mu - r back to front.
+  const int tid = threadIdx.x;
+  double hmin = INFINITY, carry_hi = -INFINITY;
+  int carry_n = 0;
+  for (int t0 = 0; t0 < nc; t0 += kBS) {
+    const int k = t0 + tid;
+    double hr = -INFINITY;
+    int wide = 0;
+    if (k < nc) {
+      const double4 c = ld4(coef64, off + k);
+      const double d = c.z - T;
+      const double z = d > 0.0 ? sqrt(2.0 * d) : 0.0;
+      if (d > 0.0) hmin = fmin(hmin, admissible_s(z) / c.y);
+      wide = (k == pos) || (sigma[off + k] >= 0.25 * ps);
+      if (!wide) hr = c.x + z / c.y * (1.0 + 1e-9) + 1e-12 * fabs(c.x);
+    }
+    hr = fmax(block_scan_max(hr, scan_d), carry_hi);
+    const int incl = block_scan_sum(wide, scan_n) + carry_n;
+    if (k < nc) {
+      reach_hi[off + k] = hr;
+      if (wide) wide_idx[off + incl - 1] = k;
+    }
+    carry_hi = block_max<kBS, double>(hr, red);  // the tile's last (largest) prefix
+    carry_n = block_max<kBS, int>(incl, red_n);
+  }
+  hmin = -block_max<kBS, double>(-hmin, red);
+  double carry_lo = INFINITY;
+  for (int t1 = nc - 1; t1 >= 0; t1 -= kBS) {
+    const int k = t1 - tid;
+    double lr = INFINITY;
+    if (k >= 0) {
+      const double4 c = ld4(coef64, off + k);
+      const double d = c.z - T;
+      const double z = d > 0.0 ? sqrt(2.0 * d) : 0.0;
+      const bool wide = (k == pos) || (sigma[off + k] >= 0.25 * ps);
+      if (!wide) lr = c.x - z / c.y * (1.0 + 1e-9) - 1e-12 * fabs(c.x);
+    }
+    lr = fmin(-block_scan_max(-lr, scan_d), carry_lo);
+    if (k >= 0) reach_lo[off + k] = lr;
+    carry_lo = -block_max<kBS, double>(-lr, red);
+  }
+  if (tid == 0) {
+    if (blockIdx.x == 0) {
+      Tb->lo = a;
+      Tb->hi = b;
+      Tb->h_below = hmin;
+      Tb->n_wide_below = carry_n;
+    } else {
+      Tb->h_above = hmin;
+      Tb->n_wide_above = carry_n;
+    }
+  }
+}
+
+// cell geometry from the plan (identical in every thread that asks)
+struct Grid {
+  double origin, h;
+  int nb;
+};
+
+__device__ __forceinline__ Grid grid_of(const tpe_table& Tb, int64_t cap) {
+  const double span = Tb.hi - Tb.lo;
+  double hn = fmin(Tb.h_below, Tb.h_above);
+  if (!(hn > 0.0) || !isfinite(hn)) hn = fmax(span, 1.0);
+  Grid g;
+  if (!(span > 0.0)) {
+    g.nb = 1;
+    g.h = hn;
+    g.origin = Tb.lo - hn;
+    return g;
+  }
+  double n = ceil(span / (2.0 * hn));
+  if (!(n <= (double)cap)) n = (double)cap;
+  g.nb = (int)fmax(1.0, n);
+  g.h = span / (2.0 * g.nb);
+  g.origin = Tb.lo;
+  return g;
+}
+
+// first k with a[k] >= v / last k with a[k] <= v  (a non-decreasing)
+__device__ __forceinline__ int first_ge(const double* a, int n, double v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] >= v) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+__device__ __forceinline__ int last_le(const double* a, int n, double v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] > v) hi = mid; else lo = mid + 1;
+  }
+  return lo - 1;
+}
+
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// one wave builds one mixture's expansion on one cell; returns the failed flag
+__device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __restrict__ sigma,
+                                          const double* __restrict__ coef64,
+                                          const double* __restrict__ reach_hi,
+                                          const double* __restrict__ reach_lo,
+                                          const int32_t* __restrict__ wide_idx, int n_wide,
+                                          double y0, double h, float* out_p, float* out_m) {
+  const int nc = S.n_obs + 1;
+  const int64_t off = S.comp_off;
+  const int pos = S.prior_pos;
+  const double wide_sig = 0.25 * S.prior_sigma;
+  const double a = y0 - h, b = y0 + h;
+  const int k_lo = first_ge(reach_hi + off, nc, a);
+  const int k_hi = last_le(reach_lo + off, nc, b);
+  const int nwin = max(0, k_hi - k_lo + 1);
+  const int items = nwin + n_wide;
+  const int lane = lane_id();
+  auto comp = [&](int it, bool& skip) -> int {
+    if (it < nwin) {
+      const int k = k_lo + it;
+      skip = (k == pos) || (sigma[off + k] >= wide_sig);  // wide: taken from the list
+      return k;
+    }
+    skip = false;
+    return wide_idx[off + (it - nwin)];
+  };
+  // pass 1: value at the centre (scale) and a lower bound of log S on the cell
+  double m0 = -INFINITY, lb = -INFINITY;
+  for (int it = lane; it < items; it += kWave) {
+    bool skip;
+    const int k = comp(it, skip);
+    if (skip) continue;
+    const double4 c = ld4(coef64, off + k);
+    const double zc = (y0 - c.x) * c.y;
+    const double zf = fmax(fabs(a - c.x), fabs(b - c.x)) * c.y;
+    m0 = fmax(m0, c.z - 0.5 * zc * zc);
+    lb = fmax(lb, c.z - 0.5 * zf * zf);
+  }
+  m0 = wave_max_d(m0);
+  lb = wave_max_d(lb);
+  const double thr = lb - (log((double)nc) + kTauExtra);
+  // pass 2: moments.  The exponent is formed in fp64, the series in fp32
+  // (each lane sums <= items/64 positive terms, then a 64-lane butterfly)
+  float P[kP];
+#pragma unroll
+  for (int n = 0; n < kP; ++n) P[n] = 0.0f;
+  bool bad = false;
+  for (int it = lane; it < items; it += kWave) {
+    bool skip;
+    const int k = comp(it, skip);
+    if (skip) continue;
+    const double4 c = ld4(coef64, off + k);
+    const double dn = (c.x < a) ? (a - c.x) : ((c.x > b) ? (c.x - b) : 0.0);
+    const double zn = dn * c.y;
+    if (c.z - 0.5 * zn * zn < thr) continue;
+    const double dy = y0 - c.x;
+    const double hi2 = h * c.y * c.y;
+    const double A = -dy * hi2;
+    const double B = -0.5 * h * hi2;
+    bad = bad || (9.0 * fabs(A) + 65.0 * fabs(B) > kRhoLim);
+    const double zc = dy * c.y;
+    const float e = __expf((float)(c.z - 0.5 * zc * zc - m0));
+    const float Af = (float)A, B2 = (float)(2.0 * B);
+    float cm = 0.0f, cc = e;  // e * c_n
+    P[0] += e;
+#pragma unroll
+    for (int n = 0; n + 1 < kP; ++n) {
+      const float cn = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
+      P[n + 1] += cn;
+      cm = cc;
+      cc = cn;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < kP; ++n) P[n] = wave_sum_f(P[n]);
+  bad = __any(bad);
+  if (lane < kP) {
+    float v = P[0];
+#pragma unroll
+    for (int n = 1; n < kP; ++n)
+      if (lane == n) v = P[n];
+    out_p[lane] = v;
+  }
+  if (lane == 0) *out_m = (float)m0;
+  return bad;
+}
+
+__global__ __launch_bounds__(kBS) void k_table_build(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ sigma, const double* __restrict__ coef64,
+    const double* __restrict__ reach_hi, const double* __restrict__ reach_lo,
+    const int32_t* __restrict__ wide_idx, tpe_table* __restrict__ tables,
+    float* __restrict__ cells, unsigned long long* __restrict__ stats) {
+  const tpe_job J = jobs[blockIdx.y];
+  const tpe_table Tb = tables[blockIdx.y];
+  const Grid g = grid_of(Tb, J.tbl_cap);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    tpe_table* W = tables + blockIdx.y;
+    W->origin = g.origin;
+    W->h = g.h;
+    W->inv_h = (float)(1.0 / g.h);
+    W->inv_w = (float)(0.5 / g.h);
+    W->nb = g.nb;
+  }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const int wid = threadIdx.x / kWave;
+  for (int64_t c = (int64_t)blockIdx.x * (kBS / kWave) + wid; c < g.nb;
+       c += (int64_t)gridDim.x * (kBS / kWave)) {
+    const double y0 = (double)(float)(g.origin + (double)(2 * c + 1) * g.h);
+    float* out = cells + (J.tbl_off + c) * kCellF;
+    const bool bb = build_mix(SB, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below,
+                              y0, g.h, out, out + 24);
+    const bool ba = build_mix(SA, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above,
+                              y0, g.h, out + kP, out + 25);
+    if (lane_id() == 0) {
+      const int flags = (bb ? 1 : 0) | (ba ? 2 : 0);
+      out[26] = (float)y0;
+      out[27] = __int_as_float(flags);
+      if (flags && stats) atomicAdd(stats + 1, 1ull);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// scoring
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float horner12(const float4 p0, const float4 p1, const float4 p2,
+                                          float u) {
+  float r = p2.w;
+  r = fmaf(r, u, p2.z);
+  r = fmaf(r, u, p2.y);
+  r = fmaf(r, u, p2.x);
+  r = fmaf(r, u, p1.w);
+  r = fmaf(r, u, p1.z);
+  r = fmaf(r, u, p1.y);
+  r = fmaf(r, u, p1.x);
+  r = fmaf(r, u, p0.w);
+  r = fmaf(r, u, p0.z);
+  r = fmaf(r, u, p0.y);
+  r = fmaf(r, u, p0.x);
+  return r;
+}
+
+// exact fp32 log-sum-exp over every component (natural log), the dense
+// kernel's arithmetic: t = xc*a + b, v = c - t^2 in log2 units offset by cmax
+__device__ float lse_exact32(const float4* __restrict__ coef, const tpe_seg& S, float y) {
+  const float xc = y - (float)S.center;
+  float m = -INFINITY, s = 0.0f;
+#pragma unroll 8
+  for (int k = 0; k < S.n_obs + 1; ++k) {
+    const float4 c = coef[k];
+    const float t = fmaf(xc, c.x, c.y);
+    const float v = fmaf(-t, t, c.z);
+    if (v > m) {
+      s = s * __builtin_amdgcn_exp2f(m - v) + 1.0f;
+      m = v;
+    } else {
+      s += __builtin_amdgcn_exp2f(v - m);
+    }
+  }
+  return (m + __builtin_amdgcn_logf(s) + (float)S.cmax) * kLn2T;
+}
+
+template <bool INJ>
+__global__ __launch_bounds__(kBS) void k_score_table(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ wcdf, const float4* __restrict__ coef32,
+    const tpe_table* __restrict__ tables, const float* __restrict__ cells,
+    const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
+    double* __restrict__ out_x, tpe_best* __restrict__ partial,
+    unsigned long long* __restrict__ stats) {
+  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ BestT red[kBS / kWave];
+  __shared__ int nred[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kTR);
+  if (base >= J.n_cand) {
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
+  }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const tpe_table Tb = tables[blockIdx.y];
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  float x[kTR];
+  if (INJ) {
+#pragma unroll
+    for (int r = 0; r < kTR; ++r) {
+      const int64_t li = base + r * kBS + threadIdx.x;
+      x[r] = li < J.n_cand ? (float)cand[J.cand_off + li] : 1.0f;
+    }
+  } else {
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+#pragma unroll
+    for (int r = 0; r < kTR; ++r) {
+      const int64_t li = base + r * kBS + threadIdx.x;
+      float v = 1.0f;
+      if (li < J.n_cand) {
+        v = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
+        if (lgmm) v = __expf(v);
+      }
+      x[r] = v;
+    }
+  }
+  const float g0 = (float)Tb.origin, inv_w = Tb.inv_w, inv_h = Tb.inv_h;
+  const int nb = Tb.nb;
+  const float4* C4 = reinterpret_cast<const float4*>(cells) + J.tbl_off * (kCellF / 4);
+  BestT best{0.0, -1, 0.0};
+  int n_exact = 0;
+#pragma unroll 2
+  for (int r = 0; r < kTR; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) continue;
+    const float y = lgmm ? __logf(x[r]) : x[r];
+    const float t = (y - g0) * inv_w;
+    int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
+    c = min(c, nb - 1);
+    const float4* q = C4 + (int64_t)c * (kCellF / 4);
+    const float4 q6 = q[6];
+    const float u = (y - q6.z) * inv_h;
+    float lb, la;
+    bool ok = (__float_as_int(q6.w) == 0) && (fabsf(u) <= kULim);
+    if (ok) {
+      const float pb = horner12(q[0], q[1], q[2], u);
+      const float pa = horner12(q[3], q[4], q[5], u);
+      ok = (pb > 0.0f) && (pa > 0.0f);
+      lb = q6.x + __builtin_amdgcn_logf(pb) * kLn2T;
+      la = q6.y + __builtin_amdgcn_logf(pa) * kLn2T;
+    }
+    if (!ok) {
+      lb = lse_exact32(coef32 + SB.comp_off, SB, y);
+      la = lse_exact32(coef32 + SA.comp_off, SA, y);
+      ++n_exact;
+    }
+    double bl = lb, al = la;
+    if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
+      bl -= (double)y;
+      al -= (double)y;
+    }
+    const int64_t o = J.out_off + li;
+    if (out_bl) out_bl[o] = bl;
+    if (out_al) out_al[o] = al;
+    if (out_x) out_x[o] = (double)x[r];
+    best_update(best, bl - al, J.cand_base + li, (double)x[r]);
+  }
+  best = block_best<kBS>(best, red);
+  if (stats) {
+    const int ne = block_sum<kBS, int>(n_exact, nred);
+    if (threadIdx.x == 0 && ne) atomicAdd(stats, (unsigned long long)ne);
+  }
+  if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
+}
+
+__global__ __launch_bounds__(kBS) void k_reduce_t(const tpe_job* __restrict__ jobs,
+                                                  const tpe_best* __restrict__ partial,
+                                                  int64_t nper, tpe_best* __restrict__ best) {
+  __shared__ BestT red[kBS / kWave];
+  BestT b{0.0, -1, 0.0};
+  const tpe_best* P = partial + (int64_t)blockIdx.x * nper;
+  for (int64_t i = threadIdx.x; i < nper; i += kBS) {
+    const tpe_best p = P[i];
+    best_update(b, p.score, p.index, p.value);
+  }
+  b = block_best<kBS>(b, red);
+  if (threadIdx.x == 0)
+    best[blockIdx.x] = tpe_best{b.score, b.index, b.value, jobs[blockIdx.x].n_cand};
+}
+
+bool check_table_jobs(const char* fn, const tpe_job* hj, int n, bool* inj) {
+  if (n < 0 || n > 65535 || (n > 0 && !hj)) {
+    set_error("%s: bad job list (n_jobs=%d)", fn, n);
+    return false;
+  }
+  for (int i = 0; i < n; ++i) {
+    const tpe_job& j = hj[i];
+    if (j.family == TPE_CAT || (j.flags & TPE_F_QUANT) || j.n_cand < 0) {
+      set_error("%s: job %d is not an unquantized GMM1/LGMM1 job", fn, i);
+      return false;
+    }
+    if (j.tbl_cap < 1 || j.tbl_off < 0) {
+      set_error("%s: job %d has no cell table (tbl_cap=%lld)", fn, i, (long long)j.tbl_cap);
+      return false;
+    }
+    const bool ji = (j.flags & TPE_F_INJECTED) != 0;
+    if (i > 0 && ji != *inj) {
+      set_error("%s: mixed injected / sampled jobs in one call", fn);
+      return false;
+    }
+    *inj = ji;
+  }
+  return true;
+}
+}  // namespace
+}  // namespace tpe
+
+using namespace tpe;
+
+extern "C" int tpe_table_build(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                               const tpe_seg* segs, const double* mu, const double* sigma,
+                               const double* coef64, double* reach_hi, double* reach_lo,
+                               int32_t* wide_idx, tpe_table* tables, float* cells,
+                               uint64_t* stats, void* stream) {
+  bool inj = false;
+  if (!check_table_jobs("tpe_table_build", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !mu || !sigma || !coef64 || !reach_hi || !reach_lo || !wide_idx ||
+      !tables || !cells) {
+    set_error("tpe_table_build: null pointer");
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_table_reach, dim3(2, n_jobs), dim3(kBS), 0, st, jobs, segs, mu, sigma,
+                     coef64, reach_hi, reach_lo, wide_idx, tables);
+  hipLaunchKernelGGL(k_table_build, dim3(kBuildBlocks, n_jobs), dim3(kBS), 0, st, jobs, segs,
+                     sigma, coef64, reach_hi, reach_lo, wide_idx, tables, cells,
+                     (unsigned long long*)stats);
+  return check_launch("tpe_table_build");
+}
+
+extern "C" int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                               const tpe_seg* segs, const double* mu, const double* sigma,
+                               const double* wcdf, const float* coef32, const tpe_table* tables,
+                               const float* cells, const double* cand, double* out_bl,
+                               double* out_al, double* out_x, tpe_best* partial,
+                               int64_t n_partial, tpe_best* best, uint64_t* stats,
+                               void* stream) {
+  bool inj = false;
+  if (!check_table_jobs("tpe_score_table", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !coef32 || !tables || !cells || !partial ||
+      !best || (inj && !cand)) {
+    set_error("tpe_score_table: null pointer");
+    return TPE_E_ARG;
+  }
+  int64_t gx = 1;
+  for (int i = 0; i < n_jobs; ++i)
+    gx = std::max(gx, (host_jobs[i].n_cand + kBS * kTR - 1) / (kBS * kTR));
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_score_table: partial workspace %lld < %lld", (long long)n_partial,
+              (long long)(gx * n_jobs));
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)gx, (unsigned)n_jobs);
+  const float4* c = reinterpret_cast<const float4*>(coef32);
+  unsigned long long* s = (unsigned long long*)stats;
+  if (inj)
+    hipLaunchKernelGGL(k_score_table<true>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
+                       c, tables, cells, cand, out_bl, out_al, out_x, partial, s);
+  else
+    hipLaunchKernelGGL(k_score_table<false>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
+                       c, tables, cells, cand, out_bl, out_al, out_x, partial, s);
+  hipLaunchKernelGGL(k_reduce_t, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
+  return check_launch("tpe_score_table");
+}
+
+extern "C" int64_t tpe_table_partials(const tpe_job* host_jobs, int n_jobs) {
+  int64_t gx = 1;
+  for (int i = 0; i < n_jobs; ++i)
+    gx = std::max(gx, (host_jobs[i].n_cand + kBS * kTR - 1) / (kBS * kTR));
+  return gx * n_jobs;
+}

@@ -6,6 +6,8 @@ space (all labels, for a flat space) and runs, on the current torch stream:
 
     tpe_parzen_fit        adaptive_parzen_normal for every below/above set
     tpe_cat_posterior     randint / categorical pseudocount posteriors
+    tpe_table_build       fp32: per-cell Taylor expansions of both mixtures
+    tpe_score_table       fp32: sample + cell lookup + 2 polynomials + argmax
     tpe_score_continuous  unquantized labels: sample + GMM1/LGMM1_lpdf + argmax
     tpe_lattice_*         quantized labels: sample -> distinct values -> score
     tpe_score_categorical categorical labels: sample + lookup + argmax
@@ -30,6 +32,10 @@ EPS = 1e-12  # tpe.py:32
 DEFAULT_LF = 25  # tpe.py:36
 DRAW32_MAX_SLOT = 1 << 12  # fp32 lattice draws only while |k| <= 2^12
 LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense fallback
+TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
+TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
+SORTED_MIN_CAND = 1 << 12  # auto scorer: sorted/pruned path from this many (below: dense)
+SCORERS = ("auto", "dense", "sorted", "table")
 _ALIGN = 256
 
 CONTINUOUS = ("uniform", "quniform", "loguniform", "qloguniform",
@@ -161,15 +167,25 @@ class Engine:
     # -- main entry ----------------------------------------------------------
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
             outputs=False, stream=None, timers=None, sample_only=False,
-            pruned=True) -> List[LabelResult]:
+            pruned=True, scorer=None) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``.
         ``sample_only``: fit, then only draw the candidates of the continuous
         labels (tpe_sample) into ``LabelResult.cand`` -- the sampler test hook.
-        ``pruned``: sampled unquantized labels at precision 32 take the sorted,
-        component-pruned kernel (tpe_score_sorted); False = dense k_score32."""
+        ``scorer`` picks the fp32 kernel for unquantized labels: "dense"
+        (k_score32, every component), "sorted" (bucketed candidates +
+        component pruning; sampled labels without per-candidate outputs),
+        "table" (per-cell expansions, tpe_table_build + tpe_score_table) or
+        "auto" (table from TABLE_MIN_CAND candidates, sorted from
+        SORTED_MIN_CAND, dense below; injected candidates dense).
+        ``pruned=False`` is the old spelling of scorer="dense".  fp64 always
+        runs the exact dense kernel."""
         if sample_only:
             outputs = True
+        if scorer is None:
+            scorer = "auto" if pruned else "dense"
+        if scorer not in SCORERS:
+            raise ValueError("scorer must be one of %s, got %r" % (SCORERS, scorer))
         torch = self.torch
 
         def tick():
@@ -258,11 +274,28 @@ class Engine:
                     fallback.append(i)
                 else:
                     lat_ranges[i] = (kmin, kmax - kmin + 1)
-        use_sorted = pruned and precision == 32 and not outputs and not sample_only
+        def cont_mode(i):
+            if precision != 32 or sample_only:
+                return "cont"
+            n = int(np.asarray(works[i].cand).size) if inj(i) else int(works[i].n_cand)
+            mode = scorer
+            if mode == "auto":
+                mode = "cont"
+                if not inj(i):
+                    if n >= TABLE_MIN_CAND:
+                        mode = "table"
+                    elif n >= SORTED_MIN_CAND and not outputs:
+                        mode = "sorted"
+            if mode == "sorted" and (inj(i) or outputs):
+                mode = "cont"
+            return "cont" if mode == "dense" else mode
+        modes = {i: cont_mode(i) for i in cont}
         groups = [
-            ("cont", [i for i in cont if inj(i)]),
-            ("cont", [i for i in cont if not inj(i) and not use_sorted]),
-            ("sorted", [i for i in cont if not inj(i) and use_sorted]),
+            ("cont", [i for i in cont if inj(i) and modes[i] == "cont"]),
+            ("cont", [i for i in cont if not inj(i) and modes[i] == "cont"]),
+            ("sorted", [i for i in cont if modes[i] == "sorted"]),
+            ("table", [i for i in cont if inj(i) and modes[i] == "table"]),
+            ("table", [i for i in cont if not inj(i) and modes[i] == "table"]),
             ("lat", [i for i in quant if i in lat_ranges]),
             ("qfb", fallback),
             ("qinj", [i for i in quant if inj(i)]),
@@ -272,7 +305,7 @@ class Engine:
         order = [i for _, ids in groups for i in ids]
         jobs = np.zeros(len(order), L.JOB_DTYPE)
         cand_parts, cand_off, out_off, lat_off, qfb_off = [], 0, 0, 0, 0
-        sort_off = cnt_off = 0
+        sort_off = cnt_off = tbl_off = 0
         seg_of = {i: si for si, i in enumerate(fit_ids)}
         cseg_of = {i: ci for ci, i in enumerate(cat)}
         for pos, i in enumerate(order):
@@ -313,7 +346,12 @@ class Engine:
                 elif i in fallback:
                     j["cand_off"] = qfb_off
                     qfb_off += n
-            elif use_sorted and not inj(i):
+            elif modes[i] == "table":
+                j["tbl_off"], j["tbl_cap"] = tbl_off, TABLE_CAP
+                tbl_off += TABLE_CAP
+                if inj(i):
+                    j["bin_lo"], j["bin_hi"] = _injected_range(w, P)
+            elif modes[i] == "sorted":
                 j["bin_lo"], j["bin_hi"] = _support(w, P)
                 j["sort_off"], j["cnt_off"] = sort_off, cnt_off
                 slots = ctypes.c_int64(0)
@@ -322,7 +360,7 @@ class Engine:
         cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
         # the dense fallback first materialises its draws: a job copy whose
         # out_off points into the scratch candidate buffer
-        fb_slice = _slice_of(groups, 4)
+        fb_slice = _slice_of(groups, [k for k, _ in groups].index("qfb"))
         fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
         fb_jobs["out_off"] = fb_jobs["cand_off"]
 
@@ -381,6 +419,7 @@ class Engine:
             tock("cat_fit", e0)
 
         # ---- scoring, one call per group ----------------------------------------
+        table_calls = []
         for g, (kind, ids) in enumerate(groups):
             if not ids:
                 continue
@@ -422,6 +461,28 @@ class Engine:
                 L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,
                                              d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
                         "tpe_score_sorted")
+            elif kind == "table":
+                npart = lib.tpe_table_partials(hjp, nj)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
+                d_cells = self._buf("cells", 128 * int(hj["tbl_off"].max() + TABLE_CAP
+                                                       - hj["tbl_off"].min()))
+                d_cells -= 128 * int(hj["tbl_off"].min())
+                d_rh = self._buf("reach_hi", 8 * n_comp)
+                d_rl = self._buf("reach_lo", 8 * n_comp)
+                d_wide = self._buf("wide_idx", 4 * n_comp)
+                d_stats = self._buf("tstats", 16)
+                with torch.cuda.stream(stream):
+                    self._bufs["tstats"][:16].zero_()
+                L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64, d_rh, d_rl,
+                                            d_wide, d_tab, d_cells, d_stats, sp),
+                        "tpe_table_build")
+                tock("table_build", e0)
+                e0 = tick()
+                L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32, d_tab,
+                                            d_cells, d_cand, d_bl, d_al, d_x, d_part, npart, db,
+                                            d_stats, sp), "tpe_score_table")
+                table_calls.append(nj)
             elif kind == "lat":
                 d_slot = self._buf("lat_slot", 8 * lat_off)
                 d_vals = self._buf("lat_vals", 8 * lat_off)
@@ -465,6 +526,10 @@ class Engine:
             self.last_pairs = None
             if any(k == "sorted" and ids for k, ids in groups):
                 self.last_pairs = int(self._bufs["pairs"][:8].to("cpu").view(torch.int64).item())
+            self.last_table_stats = None
+            if table_calls:
+                st = self._bufs["tstats"][:16].to("cpu").view(torch.int64).tolist()
+                self.last_table_stats = {"exact_candidates": st[0], "failed_cells": st[1]}
             outs = None
             if outputs:
                 outs = [self._bufs[k][:8 * max(out_off, 1)].to("cpu").numpy().view(np.float64)
@@ -503,6 +568,19 @@ def _support(w: LabelWork, P):
         obs = np.log(np.maximum(obs, P["floor"]))
     pts = np.concatenate([obs[np.isfinite(obs)], [P["prior_mu"]]])
     return float(pts.min()) - 9.0 * P["prior_sigma"], float(pts.max()) + 9.0 * P["prior_sigma"]
+
+
+def _injected_range(w: LabelWork, P):
+    """Scoring-coordinate range of injected candidates (finite ones; the table
+    grid covers it, anything outside is scored exactly)."""
+    c = np.asarray(w.cand, dtype=np.float64).reshape(-1)
+    if P["family"] == L.LGMM1:
+        with np.errstate(all="ignore"):
+            c = np.log(c.astype(np.float32)).astype(np.float64)
+    c = c[np.isfinite(c)]
+    if c.size == 0:
+        return P["prior_mu"], P["prior_mu"]
+    return float(c.min()), float(c.max())
 
 
 def _lattice_range(w: LabelWork, P):

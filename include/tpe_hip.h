@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 2
+#define TPE_ABI_VERSION 3
 
 enum {
   TPE_OK = 0,
@@ -123,6 +123,8 @@ typedef struct tpe_job {
   double bin_lo, bin_hi;/* sorted path: candidate coordinate range to bin    */
   int64_t sort_off;     /* sorted path: first slot in the sorted pool        */
   int64_t cnt_off;      /* sorted path: first element of the count matrix    */
+  int64_t tbl_off;      /* table path: first cell of this job's cell table   */
+  int64_t tbl_cap;      /* table path: cells allocated at tbl_off            */
 } tpe_job;
 
 /* best candidate of one label: np.argmax semantics (first max, NaN wins) */
@@ -196,6 +198,50 @@ int tpe_score_sorted(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                      tpe_best* partial, int64_t n_partial, tpe_best* best,
                      uint64_t* pairs, void* stream);
 
+/* ---- continuous candidates, cell-table path (fp32 throughput path) -------
+ * Same quantity as tpe_score_continuous(precision=32): per candidate the log
+ * densities of both mixtures (GMM1_lpdf / LGMM1_lpdf, tpe.py:117-180,
+ * 265-307) and the fused argmax (broadcast_best, tpe.py:649-658).  The
+ * candidate coordinate range is cut into nb cells of half-width h; on every
+ * cell each mixture sum_j exp(l_j(y)) is expanded around the cell centre
+ * y0 as exp(m) * sum_{n<12} P_n u^n, u = (y - y0)/h, built in fp64 from
+ * every component that can reach 2^-36 of the sum on that cell
+ * (tpe_table_build).  Each component's factor exp(A u + B u^2) is expanded
+ * only where 9|A| + 65|B| <= 5.8, which bounds the truncation error of the
+ * whole sum by 6e-9 relative (Cauchy estimate).  A
+ * candidate whose cell fails the bound, or that lies outside the grid, is
+ * scored by the exact fp32 log-sum-exp over all components instead.
+ * tables: one tpe_table per job (device); cells: float pool, 32 floats per
+ * cell at 32 * (job.tbl_off + c); reach_hi / reach_lo: fp64 per-component
+ * workspace (size of the mixture pool); wide_idx: int32, same size.
+ * stats (nullable, 2 x u64): [0] candidates scored by the exact fallback,
+ * [1] cells that failed the bound. */
+typedef struct tpe_table {
+  double lo, hi;        /* candidate coordinate range (x, or log x for LGMM1) */
+  double h_below, h_above; /* largest admissible half-width per mixture       */
+  double origin;        /* left edge of cell 0 (cell c is centred at         */
+                        /* origin + (2c+1) h)                                */
+  double h;             /* cell half-width used                              */
+  float inv_h, inv_w;   /* 1/h and 1/(2h)                                    */
+  int32_t nb;           /* cells used (<= job.tbl_cap)                       */
+  int32_t n_wide_below, n_wide_above;
+  int32_t pad;
+} tpe_table;
+
+/* partial-workspace entries tpe_score_table needs */
+int64_t tpe_table_partials(const tpe_job* host_jobs, int n_jobs);
+int tpe_table_build(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                    const tpe_seg* segs, const double* mu, const double* sigma,
+                    const double* coef64, double* reach_hi, double* reach_lo,
+                    int32_t* wide_idx, tpe_table* tables, float* cells, uint64_t* stats,
+                    void* stream);
+int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                    const tpe_seg* segs, const double* mu, const double* sigma,
+                    const double* wcdf, const float* coef32, const tpe_table* tables,
+                    const float* cells, const double* cand, double* out_bl, double* out_al,
+                    double* out_x, tpe_best* partial, int64_t n_partial, tpe_best* best,
+                    uint64_t* stats, void* stream);
+
 /* ---- quantized labels: lattice path ---------------------------------------
  * Candidates of a quantized label take values k*q (np.round(x/q)*q,
  * tpe.py:106, 256); equal values have equal scores, so every distinct value
@@ -243,7 +289,7 @@ int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* o
 
 const char* tpe_last_error(void);
 int tpe_abi_version(void);
-/* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best) to out[0..n) */
+/* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table) to out[0..n) */
 int tpe_struct_sizes(int32_t* out, int n);
 
 #ifdef __cplusplus

@@ -30,11 +30,11 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == 2
-    sizes = (ctypes.c_int32 * 4)()
-    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 4) == 4
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 3
+    sizes = (ctypes.c_int32 * 5)()
+    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 5) == 5
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
-                            L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize)
+                            L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize, L.TABLE_DTYPE.itemsize)
 
 
 def test_argument_errors_are_reported():
@@ -61,6 +61,14 @@ def test_argument_errors_are_reported():
     jobs["bin_lo"] = jobs["bin_hi"] = 1.0
     rc = lib.tpe_score_sorted(None, hp_, 1, *([None] * 9), 0, None, None, None)
     assert rc == -1 and b"empty bin range" in lib.tpe_last_error()
+    rc = lib.tpe_score_table(None, hp_, 1, *([None] * 12), 0, None, None, None)
+    assert rc == -1 and b"no cell table" in lib.tpe_last_error()
+    jobs["tbl_cap"] = 64
+    rc = lib.tpe_table_build(None, hp_, 1, *([None] * 11))
+    assert rc == -1 and b"null pointer" in lib.tpe_last_error()
+    jobs["flags"] = L.F_QUANT
+    rc = lib.tpe_table_build(None, hp_, 1, *([None] * 11))
+    assert rc == -1 and b"not an unquantized" in lib.tpe_last_error()
     assert lib.tpe_best_combine(None, 0, 1, None, None) == -1
     with pytest.raises(L.TpeHipError):
         L.check(-1, "probe")

@@ -1,0 +1,143 @@
+"""Cell-table scorer (tpe_table_build + tpe_score_table) vs the oracle.
+
+The table path expands each mixture per cell; its
+per-candidate log-densities must match GMM1_lpdf / LGMM1_lpdf (tpe.py:117-180,
+265-307) within the fp32 tolerance of north_star (rtol 1e-4, atol 1e-4 for
+log-densities near 0), on the reference's own injected candidates (goldens),
+on injected candidates of random histories, and on its own sampled
+candidates.  The argmax must be the dense fp32 kernel's winner or a
+candidate whose exact fp64 score ties it within fp32 rounding.
+"""
+import numpy as np
+import pytest
+
+from oracle import tpe_oracle as O
+from tests.golden_io import E2E_CASES
+from tests.test_gpu_parity import _mixture_case, _works_from_fixture
+
+pytestmark = pytest.mark.gpu
+
+RTOL = ATOL = 1e-4
+
+CONT = [("uniform", (-5.0, 5.0)), ("loguniform", (-5.0, 0.0)), ("normal", (0.0, 2.0)),
+        ("lognormal", (0.0, 1.0))]
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from hyperopt_amd.engine import Engine
+    return Engine()
+
+
+def _oracle(w, cand=None):
+    cand = w.cand if cand is None else cand
+    with np.errstate(all="ignore"):
+        return O.continuous_label_scores(w.kind, w.args, w.obs_below, w.obs_above, cand)
+
+
+@pytest.mark.parametrize("case", E2E_CASES)
+def test_golden_table(engine, case):
+    works, golden, meta = _works_from_fixture(case)
+    res = engine.run(works, prior_weight=meta["prior_weight"], precision=32, outputs=True,
+                     scorer="table")
+    for w, r, (bl, al, best) in zip(works, res, golden):
+        np.testing.assert_allclose(r.below_llik, bl, rtol=RTOL, atol=ATOL, equal_nan=True,
+                                   err_msg="%s/%s below" % (case, w.label))
+        np.testing.assert_allclose(r.above_llik, al, rtol=RTOL, atol=ATOL, equal_nan=True,
+                                   err_msg="%s/%s above" % (case, w.label))
+        score = bl - al
+        if w.kind in ("randint", "categorical") or w.kind.startswith("q"):
+            assert r.index == best
+        else:
+            assert score[r.index] >= np.nanmax(score) - 1e-4 * max(1.0, abs(np.nanmax(score)))
+
+
+@pytest.mark.parametrize("kind,args", CONT)
+@pytest.mark.parametrize("n_above", [0, 1, 2, 30, 3000, 10000])
+def test_table_injected_vs_oracle(engine, kind, args, n_above):
+    rng = np.random.RandomState(1000 + n_above)
+    w = _mixture_case(rng, kind, args, min(n_above, 25), n_above, 4096)
+    r, = engine.run([w], precision=32, outputs=True, scorer="table")
+    ref = _oracle(w)
+    np.testing.assert_allclose(r.below_llik, ref["below_llik"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(r.above_llik, ref["above_llik"], rtol=RTOL, atol=ATOL)
+    s = ref["below_llik"] - ref["above_llik"]
+    assert s[r.index] >= np.nanmax(s) - 1e-4 * max(1.0, abs(np.nanmax(s)))
+    st = engine.last_table_stats
+    assert st["failed_cells"] == 0, st
+    # every injected candidate inside the sampler's range is on the table
+    assert st["exact_candidates"] <= 0.01 * w.cand.size, st
+
+
+def test_table_far_tails_and_ties(engine):
+    """Off-grid candidates (+-1e3, +-60) take the exact path; duplicates tie
+    to the first index."""
+    from hyperopt_amd.engine import LabelWork
+    rng = np.random.RandomState(7)
+    obs_b = rng.uniform(-5, 5, 25)
+    obs_a = rng.uniform(-5, 5, 4000)
+    base = rng.uniform(-5, 5, 300)
+    cand = np.concatenate([base, base[::-1], [-1e3, 1e3, 60.0, -60.0]])
+    w = LabelWork("x", "uniform", (-5.0, 5.0), obs_b, obs_a, cand=cand)
+    ref = _oracle(w)
+    r, = engine.run([w], precision=32, outputs=True, scorer="table")
+    np.testing.assert_allclose(r.above_llik, ref["above_llik"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(r.below_llik, ref["below_llik"], rtol=RTOL, atol=ATOL)
+    assert engine.last_table_stats["exact_candidates"] >= 4
+    s = ref["below_llik"] - ref["above_llik"]
+    assert s[r.index] >= np.nanmax(s) - 1e-4 * max(1.0, abs(np.nanmax(s)))
+
+
+@pytest.mark.parametrize("kind,args", CONT)
+def test_table_small_budget_falls_back_exactly(engine, kind, args, monkeypatch):
+    """A cell budget far below what the error bound needs: failing cells are
+    flagged and their candidates scored exactly -- same results."""
+    import hyperopt_amd.engine as E
+    monkeypatch.setattr(E, "TABLE_CAP", 8)
+    rng = np.random.RandomState(3)
+    w = _mixture_case(rng, kind, args, 25, 5000, 2048)
+    r, = engine.run([w], precision=32, outputs=True, scorer="table")
+    ref = _oracle(w)
+    np.testing.assert_allclose(r.below_llik, ref["below_llik"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(r.above_llik, ref["above_llik"], rtol=RTOL, atol=ATOL)
+    assert engine.last_table_stats["failed_cells"] > 0
+
+
+@pytest.mark.parametrize("kind,args", CONT)
+@pytest.mark.parametrize("n_hist", [3, 40, 2000, 10000])
+def test_table_sampled_vs_oracle_and_dense(engine, kind, args, n_hist):
+    """Own Philox candidates: per-candidate log-densities vs the oracle at the
+    drawn values, and the winner vs the dense fp32 kernel's."""
+    from hyperopt_amd.engine import LabelWork
+    rng = np.random.RandomState(n_hist + 17)
+    gen = _mixture_case(rng, kind, args, 1, n_hist, 1)
+    obs = gen.obs_above
+    losses = rng.normal(size=n_hist)
+    below, above = O.ap_split_trials(np.arange(n_hist), obs, np.arange(n_hist), losses, 0.25)
+    n = 1 << 16
+    w = LabelWork(kind, kind, args, below, above, n_cand=n, key=424242 + n_hist)
+    tab, = engine.run([w], precision=32, outputs=True, scorer="table")
+    st = engine.last_table_stats
+    assert st["failed_cells"] == 0 and st["exact_candidates"] == 0, st
+    dense, = engine.run([w], precision=32, outputs=True, scorer="dense")
+    np.testing.assert_array_equal(tab.cand, dense.cand)  # same Philox draws
+    pick = np.random.RandomState(0).choice(n, 3000, replace=False)
+    ref = _oracle(w, cand=tab.cand[pick])
+    np.testing.assert_allclose(tab.below_llik[pick], ref["below_llik"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(tab.above_llik[pick], ref["above_llik"], rtol=RTOL, atol=ATOL)
+    assert tab.n_scored == n
+    if tab.index != dense.index:
+        w2 = LabelWork(kind, kind, args, below, above, cand=np.array([dense.value, tab.value]))
+        r, = engine.run([w2], precision=64, outputs=True)
+        s = r.below_llik - r.above_llik
+        assert abs(s[0] - s[1]) <= 1e-4 * max(1.0, abs(s[0])), (s, dense, tab)
+
+
+def test_auto_scorer_uses_table_for_large_n(engine):
+    from hyperopt_amd.engine import LabelWork, TABLE_MIN_CAND
+    rng = np.random.RandomState(5)
+    w = LabelWork("x", "uniform", (-5.0, 5.0), rng.uniform(-5, 5, 25), rng.uniform(-5, 5, 5000),
+                  n_cand=TABLE_MIN_CAND, key=99)
+    timers = {}
+    engine.run([w], precision=32, timers=timers)
+    assert "table" in timers and "table_build" in timers
