@@ -35,8 +35,10 @@ struct U4 {
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    // 64-bit products: one v_mad_u64_u32 per multiply gives both halves
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -64,12 +66,13 @@ __device__ __forceinline__ double normal_f64(uint32_t a, uint32_t b, uint32_t c)
   const double u2 = (double)c * 0x1.0p-32;
   return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
 }
-__device__ __forceinline__ float normal_f32(uint32_t a, uint32_t b) {
+// both Box-Muller normals of one (a, b) pair
+__device__ __forceinline__ void normal_pair_f32(uint32_t a, uint32_t b, float& z0, float& z1) {
   const float u1 = 1.0f - u01_f32(a);  // (0, 1]
   const float u2 = (float)(b >> 8) * 0x1.0p-24f;
-  // v_log_f32 is log2; v_cos_f32 takes revolutions
   const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-  return r * __builtin_amdgcn_cosf(u2);
+  z0 = r * __builtin_amdgcn_cosf(u2);
+  z1 = r * __builtin_amdgcn_sinf(u2);
 }
 
 // ---------------------------------------------------------------------------

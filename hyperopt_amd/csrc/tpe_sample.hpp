@@ -70,19 +70,107 @@ __device__ __forceinline__ double draw64(const Mix& M, uint64_t key, int64_t g, 
   return y;
 }
 
+// fp32 draws come in pairs: attempt `a` of candidates 2m and 2m+1 is ONE
+// Philox call at counter (m, a): word x picks 2m's component, word w picks
+// 2m+1's, and (y, z) give the Box-Muller pair (cos -> 2m, sin -> 2m+1).
+// Candidate g's value therefore depends on g alone, whichever kernel draws it.
+__device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
+  const double u = (double)word * 0x1.0p-32 * M.cdf[M.n - 1];
+  return upper_bound(M.cdf, M.n, u);
+}
+
+__device__ __forceinline__ void attempt32_pair(const Mix& M, uint64_t key, int64_t m, uint32_t a,
+                                               float& y0, float& y1) {
+  const U4 r = draw_words(key, m, a, kStreamSample);
+  const int j0 = comp_of(M, r.x), j1 = comp_of(M, r.w);
+  float z0, z1;
+  normal_pair_f32(r.y, r.z, z0, z1);
+  y0 = (float)M.mu[j0] + (float)M.sg[j0] * z0;
+  y1 = (float)M.mu[j1] + (float)M.sg[j1] * z1;
+}
+
+// attempt `a` of candidate `g` alone (same value as attempt32_pair's half)
+__device__ __forceinline__ float attempt32(const Mix& M, uint64_t key, int64_t g, uint32_t a) {
+  const U4 r = draw_words(key, g >> 1, a, kStreamSample);
+  const int j = comp_of(M, (g & 1) ? r.w : r.x);
+  const float u1 = 1.0f - u01_f32(r.y);
+  const float u2 = (float)(r.z >> 8) * 0x1.0p-24f;
+  const float rr = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+  const float z = rr * ((g & 1) ? __builtin_amdgcn_sinf(u2) : __builtin_amdgcn_cosf(u2));
+  return (float)M.mu[j] + (float)M.sg[j] * z;
+}
+
+__device__ __forceinline__ bool accept32(float y, bool lo_on, bool hi_on, float lo, float hi) {
+  return (!lo_on || lo <= y) && (!hi_on || y < hi);
+}
+
+// after kMaxAttempts rejections (acceptance below ~1e-77): clamp into the support
+__device__ __forceinline__ float clamp32(float y, bool lo_on, bool hi_on, float lo, float hi) {
+  if (lo_on && y < lo) y = lo;
+  if (hi_on && !(y < hi)) y = nextafterf(hi, -INFINITY);
+  return y;
+}
+
 __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, bool lo_on,
                                         bool hi_on, float lo, float hi) {
   float y = 0.0f;
   for (uint32_t a = 0; a < kMaxAttempts; ++a) {
-    const U4 r = draw_words(key, g, a, kStreamSample);
-    const double u = (double)r.x * 0x1.0p-32 * M.cdf[M.n - 1];
-    const int j = upper_bound(M.cdf, M.n, u);
-    y = (float)M.mu[j] + (float)M.sg[j] * normal_f32(r.y, r.z);
-    if ((!lo_on || lo <= y) && (!hi_on || y < hi)) return y;
+    y = attempt32(M, key, g, a);
+    if (accept32(y, lo_on, hi_on, lo, hi)) return y;
   }
-  if (lo_on && y < lo) y = lo;
-  if (hi_on && !(y < hi)) y = nextafterf(hi, -INFINITY);
-  return y;
+  return clamp32(y, lo_on, hi_on, lo, hi);
+}
+
+// R consecutive candidates g0 .. g0+R-1 per thread (g0 even), n of them
+// valid, each exactly as draw32 draws it.  Every lane walks its own queue of
+// candidate pairs: one Philox call per attempt serves both candidates of a
+// pair, and a rejection costs that lane one more step instead of stalling the
+// whole wave for a full draw.  Results go through `stage` (R*kBS floats of
+// LDS; each thread reads back only its own slots).
+template <int R>
+__device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t g0, int n,
+                                             bool lo_on, bool hi_on, float lo, float hi,
+                                             bool lgmm, float* stage, float (&x)[R]) {
+  static_assert(R % 2 == 0, "pairs");
+  const int tid = threadIdx.x;
+  int p = 0;
+  uint32_t att = 0;
+  bool d0 = false, d1 = false;
+  while (true) {
+    const bool act = p < R / 2 && 2 * p < n;
+    if (!__any(act)) break;
+    if (act) {
+      float y0, y1;
+      attempt32_pair(M, key, (g0 >> 1) + p, att, y0, y1);
+      const bool last = att + 1 >= kMaxAttempts;
+      const bool has1 = 2 * p + 1 < n;
+      if (!d0) {
+        const bool ok = accept32(y0, lo_on, hi_on, lo, hi);
+        if (ok || last) {
+          if (!ok) y0 = clamp32(y0, lo_on, hi_on, lo, hi);
+          stage[(2 * p) * kBS + tid] = lgmm ? __expf(y0) : y0;
+          d0 = true;
+        }
+      }
+      if (has1 && !d1) {
+        const bool ok = accept32(y1, lo_on, hi_on, lo, hi);
+        if (ok || last) {
+          if (!ok) y1 = clamp32(y1, lo_on, hi_on, lo, hi);
+          stage[(2 * p + 1) * kBS + tid] = lgmm ? __expf(y1) : y1;
+          d1 = true;
+        }
+      }
+      if (d0 && (d1 || !has1)) {
+        ++p;
+        att = 0;
+        d0 = d1 = false;
+      } else {
+        ++att;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) x[k] = (k < n) ? stage[k * kBS + tid] : 1.0f;
 }
 
 }  // namespace

@@ -49,6 +49,7 @@ constexpr double kTauExtra = 25.0;   // exclusion margin (nats) on top of log(M)
 constexpr double kDrawZ = 5.8;       // |z| of an fp32 Box-Muller draw is < 5.77
 constexpr float kULim = 1.05f;       // |u| accepted by the scorer (fp32 cell-centre rounding)
 constexpr int kTR = 8;               // candidates per thread in the scorer
+constexpr int kRowF4 = 9;            // LDS row stride (float4) of the gather transpose
 constexpr int kBuildBlocks = 512;    // build blocks per job (grid-stride over cells)
 constexpr float kLn2T = 0.6931471805599453f;
 
@@ -401,7 +402,7 @@ __device__ __forceinline__ float horner12(const float4 p0, const float4 p1, cons
 
 // exact fp32 log-sum-exp over every component (natural log), the dense
 // kernel's arithmetic: t = xc*a + b, v = c - t^2 in log2 units offset by cmax
-__device__ float lse_exact32(const float4* __restrict__ coef, const tpe_seg& S, float y) {
+__device__ __forceinline__ float lse_exact32(const float4* __restrict__ coef, const tpe_seg& S, float y) {
   const float xc = y - (float)S.center;
   float m = -INFINITY, s = 0.0f;
 #pragma unroll 8
@@ -429,8 +430,12 @@ __global__ __launch_bounds__(kBS) void k_score_table(
     double* __restrict__ out_x, tpe_best* __restrict__ partial,
     unsigned long long* __restrict__ stats) {
   __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  // per wave: 64 rows of kRowF4 float4 (the lane's cell, transposed in from
+  // its 8-lane group); also the sampler's staging buffer before scoring
+  __shared__ float4 s_rows[(kBS / kWave) * kWave * kRowF4];
   __shared__ BestT red[kBS / kWave];
   __shared__ int nred[kBS / kWave];
+  static_assert(sizeof(s_rows) >= kTR * kBS * sizeof(float), "staging alias");
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t base = (int64_t)blockIdx.x * (kBS * kTR);
@@ -442,56 +447,29 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   const tpe_table Tb = tables[blockIdx.y];
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  // each thread owns kTR consecutive candidates (pairs share a Philox call)
+  const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
   float x[kTR];
   if (INJ) {
 #pragma unroll
-    for (int r = 0; r < kTR; ++r) {
-      const int64_t li = base + r * kBS + threadIdx.x;
-      x[r] = li < J.n_cand ? (float)cand[J.cand_off + li] : 1.0f;
-    }
+    for (int r = 0; r < kTR; ++r) x[r] = t0 + r < J.n_cand ? (float)cand[J.cand_off + t0 + r] : 1.0f;
   } else {
     const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
-#pragma unroll
-    for (int r = 0; r < kTR; ++r) {
-      const int64_t li = base + r * kBS + threadIdx.x;
-      float v = 1.0f;
-      if (li < J.n_cand) {
-        v = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
-        if (lgmm) v = __expf(v);
-      }
-      x[r] = v;
-    }
+    const int nv = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
+    draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
+                      (float)J.high, lgmm, reinterpret_cast<float*>(s_rows), x);
+    __syncthreads();  // every wave has read its staged draws back
   }
   const float g0 = (float)Tb.origin, inv_w = Tb.inv_w, inv_h = Tb.inv_h;
   const int nb = Tb.nb;
   const float4* C4 = reinterpret_cast<const float4*>(cells) + J.tbl_off * (kCellF / 4);
+  const int lane = lane_id(), gi = lane & 7, gbase = lane & ~7;
+  float4* rows = s_rows + (threadIdx.x / kWave) * (kWave * kRowF4);
   BestT best{0.0, -1, 0.0};
   int n_exact = 0;
-#pragma unroll 2
-  for (int r = 0; r < kTR; ++r) {
-    const int64_t li = base + r * kBS + threadIdx.x;
-    if (li >= J.n_cand) continue;
-    const float y = lgmm ? __logf(x[r]) : x[r];
-    const float t = (y - g0) * inv_w;
-    int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
-    c = min(c, nb - 1);
-    const float4* q = C4 + (int64_t)c * (kCellF / 4);
-    const float4 q6 = q[6];
-    const float u = (y - q6.z) * inv_h;
-    float lb, la;
-    bool ok = (__float_as_int(q6.w) == 0) && (fabsf(u) <= kULim);
-    if (ok) {
-      const float pb = horner12(q[0], q[1], q[2], u);
-      const float pa = horner12(q[3], q[4], q[5], u);
-      ok = (pb > 0.0f) && (pa > 0.0f);
-      lb = q6.x + __builtin_amdgcn_logf(pb) * kLn2T;
-      la = q6.y + __builtin_amdgcn_logf(pa) * kLn2T;
-    }
-    if (!ok) {
-      lb = lse_exact32(coef32 + SB.comp_off, SB, y);
-      la = lse_exact32(coef32 + SA.comp_off, SA, y);
-      ++n_exact;
-    }
+  uint32_t exact_mask = 0;
+  // outputs + argmax of one scored candidate
+  auto finish = [&](float lb, float la, float y, float xv, int64_t li) {
     double bl = lb, al = la;
     if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
       bl -= (double)y;
@@ -500,8 +478,68 @@ __global__ __launch_bounds__(kBS) void k_score_table(
     const int64_t o = J.out_off + li;
     if (out_bl) out_bl[o] = bl;
     if (out_al) out_al[o] = al;
-    if (out_x) out_x[o] = (double)x[r];
-    best_update(best, bl - al, J.cand_base + li, (double)x[r]);
+    if (out_x) out_x[o] = (double)xv;
+    best_update(best, bl - al, J.cand_base + li, (double)xv);
+  };
+#pragma unroll
+  for (int r = 0; r < kTR; ++r) {
+    const int64_t li = t0 + r;
+    const float y = lgmm ? __logf(x[r]) : x[r];
+    const float t = (y - g0) * inv_w;
+    int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
+    c = min(c, nb - 1);
+    // Cooperative gather: lane gi of each 8-lane group fetches 16-B chunk gi
+    // of every group member's cell, so one wave-instruction touches 8 cache
+    // lines instead of 64; rows are then transposed through LDS (row stride
+    // 144 B: conflict-free for these writes and for the row reads below).
+    // (chunk 7 is the cell's unused tail: loading and storing it keeps the
+    // code branch-free and v[] in registers)
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int cj = __shfl(c, gbase | j, kWave);
+      v[j] = C4[(int64_t)cj * (kCellF / 4) + gi];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rows[(gbase + j) * kRowF4 + gi] = v[j];
+    __builtin_amdgcn_wave_barrier();
+    const float4* q = rows + lane * kRowF4;
+    const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6];
+    __builtin_amdgcn_wave_barrier();
+    if (li >= J.n_cand) continue;
+    const float u = (y - q6.z) * inv_h;
+    float lb, la;
+    bool ok = (__float_as_int(q6.w) == 0) && (fabsf(u) <= kULim);
+    if (ok) {
+      const float pb = horner12(q0, q1, q2, u);
+      const float pa = horner12(q3, q4, q5, u);
+      ok = (pb > 0.0f) && (pa > 0.0f);
+      lb = q6.x + __builtin_amdgcn_logf(pb) * kLn2T;
+      la = q6.y + __builtin_amdgcn_logf(pa) * kLn2T;
+    }
+    if (!ok) {  // off the table: scored exactly after the loop
+      exact_mask |= 1u << r;
+      continue;
+    }
+    finish(lb, la, y, x[r], li);
+  }
+  // exact fp32 log-sum-exp for the (rare) candidates the table does not cover;
+  // their values wait in the lane's own LDS row
+  if (__any(exact_mask != 0)) {
+    float* stash = reinterpret_cast<float*>(rows + lane * kRowF4);
+#pragma unroll
+    for (int r = 0; r < kTR; ++r)
+      if (exact_mask & (1u << r)) stash[r] = x[r];
+    __builtin_amdgcn_wave_barrier();
+    while (exact_mask) {
+      const int r = __builtin_ctz(exact_mask);
+      exact_mask &= exact_mask - 1;
+      const float xv = stash[r];
+      const float y = lgmm ? __logf(xv) : xv;
+      finish(lse_exact32(coef32 + SB.comp_off, SB, y), lse_exact32(coef32 + SA.comp_off, SA, y),
+             y, xv, t0 + r);
+      ++n_exact;
+    }
   }
   best = block_best<kBS>(best, red);
   if (stats) {

@@ -149,8 +149,8 @@ def test_sorted_pruned_matches_dense(engine, kind, args, gen, n_hist):
     losses = rng.normal(size=n_hist)
     below, above = O.ap_split_trials(np.arange(n_hist), obs, np.arange(n_hist), losses, 0.25)
     w = LabelWork(kind, kind, args, below, above, n_cand=1 << 18, key=987654321 + n_hist)
-    dense, = engine.run([w], precision=32, pruned=False)
-    pruned, = engine.run([w], precision=32, pruned=True)
+    dense, = engine.run([w], precision=32, scorer="dense")
+    pruned, = engine.run([w], precision=32, scorer="sorted")
     pairs = engine.last_pairs
     assert pruned.n_scored == dense.n_scored == 1 << 18
     if pruned.index == dense.index:

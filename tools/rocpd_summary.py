@@ -56,7 +56,8 @@ def main(src, dst):
     for s in stats[:14]:
         print("%-28s %5d calls  avg %9.1f us  %5.1f%%" % (s["kernel"], s["calls"], s["avg_us"],
                                                           s["pct"]))
-    for k in ("k_score_sorted", "k_sort_count", "k_sort_scatter", "k_lattice_sample"):
+    for s in stats[:6]:
+        k = s["kernel"]
         if k in out:
             print(k, {a: "%.4g" % b for a, b in out[k].items()})
 
