@@ -60,7 +60,7 @@ _SIGNATURES = {
     "tpe_sort_candidates": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_sorted": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
                               _P]),
-    "tpe_cat_posterior": (_I, [_P, _P, _I, _P, _P, _P, _P]),
+    "tpe_cat_posterior": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "tpe_table_partials": (_I64, [_P, _I]),
     "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_table": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,

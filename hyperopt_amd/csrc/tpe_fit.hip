@@ -15,6 +15,7 @@
 // #{j : x_j < x_i or (x_j == x_i and j < i)}, counted over LDS tiles; the
 // prior is inserted at searchsorted(x, prior_mu, 'left') (tpe.py:427), or by
 // the len==1 rule of tpe.py:414-421.
+#include <algorithm>
 #include <stdarg.h>
 #include <stdio.h>
 
@@ -377,72 +378,79 @@ __device__ double np_pairwise_sum(const double* a, int64_t n) {
 }
 
 constexpr int kCatBS = 256;
-constexpr int kCatTile = 1024;
+constexpr int kCatWaves = kCatBS / kWave;
 
-__global__ __launch_bounds__(kCatBS) void k_cat_posterior(const int64_t* __restrict__ obs,
-                                                          const tpe_cat_seg* __restrict__ segs,
-                                                          double* __restrict__ p,
-                                                          double* __restrict__ logp,
-                                                          double* __restrict__ cdf) {
-  __shared__ int64_t tile[kCatTile];
-  __shared__ double tw[kCatTile];
-  const tpe_cat_seg& S = segs[blockIdx.x];
-  const int n = S.n_obs, K = S.n_cat;
-  // linear-forgetting ramp constants, once (np.linspace(1/N, 1, N-LF), tpe.py:380-392)
+// Weighted counts, one wave per (segment, category): the wave scans the
+// observations 64 at a time, ballots the matches, and adds their LF weights
+// in observation order -- exactly np.bincount's sequential sum
+// (pyll/base.py:1053-1060), but the dependent fp64 chain is only as long as
+// the category's own count.
+__global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict__ obs,
+                                                       const tpe_cat_seg* __restrict__ segs,
+                                                       double* __restrict__ p) {
+  const tpe_cat_seg& S = segs[blockIdx.y];
+  const int k = blockIdx.x * kCatWaves + threadIdx.x / kWave;
+  if (k >= S.n_cat) return;  // wave-uniform
+  const int n = S.n_obs, lane = lane_id();
+  // linear-forgetting ramp (np.linspace(1/N, 1, N-LF), tpe.py:380-392)
   const bool ramp = S.lf > 0 && S.lf < n;
   const int64_t num = n - S.lf;
   const double start = 1.0 / (double)n;
   const double step = (ramp && num > 1) ? (1.0 - start) / (double)(num - 1) : 0.0;
-  // per-category weighted counts, accumulated in observation order (bincount):
-  // the tile's weights are computed by all threads, then each category's
-  // thread walks the tile sequentially
-  for (int k0 = 0; k0 < K; k0 += kCatBS) {
-    const int k = k0 + threadIdx.x;
-    double cnt = 0.0;
-    for (int t0 = 0; t0 < n; t0 += kCatTile) {
-      const int m = min(kCatTile, n - t0);
-      __syncthreads();
-      for (int j = threadIdx.x; j < m; j += kCatBS) {
-        const int64_t i = t0 + j;
-        tile[j] = obs[S.obs_off + i];
+  double cnt = 0.0;
+  constexpr int kDepth = 8;  // tiles of 64 observations loaded per step
+  for (int t0 = 0; t0 < n; t0 += kDepth * kWave) {
+    int64_t cur[kDepth];
+#pragma unroll
+    for (int b = 0; b < kDepth; ++b) {
+      const int i = t0 + b * kWave + lane;
+      cur[b] = i < n ? obs[S.obs_off + i] : -1;
+    }
+#pragma unroll
+    for (int b = 0; b < kDepth; ++b) {
+      uint64_t m = __ballot(cur[b] == (int64_t)k);
+      while (m) {  // wave-uniform, in observation order
+        const int64_t i = t0 + b * kWave + __builtin_ctzll(m);
+        m &= m - 1;
         double wt = 1.0;
         if (ramp && i < num) {
           if (num == 1) wt = start;
           else if (i == num - 1) wt = 1.0;
           else wt = __dadd_rn(__dmul_rn((double)i, step), start);
         }
-        tw[j] = wt;
+        cnt = __dadd_rn(cnt, wt);
       }
-      __syncthreads();
-      if (k < K) {
-        // adding +0.0 leaves cnt unchanged, so the branchless form is the
-        // same sequential sum as np.bincount's
-#pragma unroll 8
-        for (int j = 0; j < m; ++j) cnt += (tile[j] == k) ? tw[j] : 0.0;
-      }
-    }
-    if (k < K) {
-      double pseudo;
-      if (S.mode == 0) {
-        pseudo = cnt + S.prior_weight;  // tpe.py:589
-      } else {
-        const double pk = p[S.prior_p_off + k];
-        pseudo = cnt + (double)K * (S.prior_weight * pk);  // tpe.py:603
-      }
-      p[S.p_off + k] = pseudo;
     }
   }
-  __syncthreads();
+  if (lane == 0) {
+    double pseudo;
+    if (S.mode == 0) {
+      pseudo = cnt + S.prior_weight;  // tpe.py:589
+    } else {
+      const double pk = p[S.prior_p_off + k];
+      pseudo = cnt + (double)S.n_cat * (S.prior_weight * pk);  // tpe.py:603
+    }
+    p[S.p_off + k] = pseudo;
+  }
+}
+
+// normalise (numpy pairwise sum), log p (categorical_lpdf, tpe.py:60-73) and
+// the cumulative p of the inverse-CDF sampler; one block per segment
+__global__ __launch_bounds__(kCatBS) void k_cat_finalize(const tpe_cat_seg* __restrict__ segs,
+                                                         double* __restrict__ p,
+                                                         double* __restrict__ logp,
+                                                         double* __restrict__ cdf) {
+  const tpe_cat_seg& S = segs[blockIdx.x];
+  const int K = S.n_cat;
   __shared__ double total;
   if (threadIdx.x == 0) total = np_pairwise_sum(p + S.p_off, K);
   __syncthreads();
   for (int k = threadIdx.x; k < K; k += kCatBS) {
     const double pk = p[S.p_off + k] / total;
     p[S.p_off + k] = pk;
-    logp[S.p_off + k] = log(pk);  // categorical_lpdf (tpe.py:60-73)
+    logp[S.p_off + k] = log(pk);
   }
   __syncthreads();
-  // cumulative probabilities for the inverse-CDF sampler (chunked scan)
   __shared__ double chunk_tot[kCatBS];
   const int per = (K + kCatBS - 1) / kCatBS;
   const int k0 = threadIdx.x * per, k1 = min(K, k0 + per);
@@ -502,14 +510,21 @@ extern "C" int tpe_parzen_fit(const double* obs, double* xf, tpe_seg* segs, int 
 }
 
 extern "C" int tpe_cat_posterior(const int64_t* obs, const tpe_cat_seg* segs, int n_seg,
-                                 double* p_pool, double* logp_pool, double* cdf_pool,
-                                 void* stream) {
+                                 int max_cat, double* p_pool, double* logp_pool,
+                                 double* cdf_pool, void* stream) {
   if (n_seg < 0 || (n_seg > 0 && (!segs || !p_pool || !logp_pool || !cdf_pool))) {
     set_error("tpe_cat_posterior: bad arguments");
     return TPE_E_ARG;
   }
   if (n_seg == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_cat_posterior, dim3(n_seg), dim3(kCatBS), 0, (hipStream_t)stream, obs,
-                     segs, p_pool, logp_pool, cdf_pool);
+  if (n_seg > 65535 || max_cat < 0) {
+    set_error("tpe_cat_posterior: n_seg=%d max_cat=%d", n_seg, max_cat);
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int gx = (std::max(max_cat, 1) + kCatWaves - 1) / kCatWaves;
+  hipLaunchKernelGGL(k_cat_counts, dim3(gx, n_seg), dim3(kCatBS), 0, st, obs, segs, p_pool);
+  hipLaunchKernelGGL(k_cat_finalize, dim3(n_seg), dim3(kCatBS), 0, st, segs, p_pool, logp_pool,
+                     cdf_pool);
   return check_launch("tpe_cat_posterior");
 }

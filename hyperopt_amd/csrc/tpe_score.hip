@@ -772,6 +772,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     int32_t* __restrict__ err) {
   __shared__ uint32_t lfirst[kLatLds];
   __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ float s_stage[kLatR * kBS];
   const tpe_job J = jobs[blockIdx.y];
   const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
   if (base >= J.n_cand) return;
@@ -783,26 +784,35 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     for (int s = threadIdx.x; s < J.lat_n; s += kBS) lfirst[s] = 0xFFFFFFFFu;
   const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
   __syncthreads();
-  for (int r = 0; r < kLatR; ++r) {
-    const int64_t li = base + r * kBS + threadIdx.x;
-    if (li >= J.n_cand) break;
-    double v;
-    if (J.flags & TPE_F_DRAW32) {
-      const float f = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
-      v = lgmm ? (double)__expf(f) : (double)f;
-    } else {
-      v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
-      if (lgmm) v = exp(v);
-    }
+  auto mark = [&](double v, int64_t li) {
     const int64_t slot = (int64_t)rint(v / J.q) - J.lat_kmin;  // np.round(x/q) (tpe.py:106)
     if (slot < 0 || slot >= J.lat_n) {
       atomicOr(err, 2);
-      continue;
+      return;
     }
     if (local)
       atomicMin(&lfirst[slot], (uint32_t)(li - base));
     else
       atomicMin(&slot_first[J.lat_off + slot], (unsigned long long)(J.cand_base + li));
+  };
+  if (J.flags & TPE_F_DRAW32) {
+    // kLatR consecutive candidates per thread, pair-shared Philox draws
+    const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
+    const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
+    float x[kLatR];
+    draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
+                        (float)J.high, lgmm, s_stage, x);
+#pragma unroll
+    for (int r = 0; r < kLatR; ++r)
+      if (r < nv) mark((double)x[r], t0 + r);
+  } else {
+    for (int r = 0; r < kLatR; ++r) {
+      const int64_t li = base + r * kBS + threadIdx.x;
+      if (li >= J.n_cand) break;
+      double v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+      if (lgmm) v = exp(v);
+      mark(v, li);
+    }
   }
   if (local) {
     __syncthreads();

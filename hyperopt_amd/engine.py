@@ -414,8 +414,9 @@ class Engine:
             d_logp = self._buf("cat_logp", 8 * p_pool.size)
             d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
             e0 = tick()
-            L.check(lib.tpe_cat_posterior(base + o_cobs, d_csegs, len(csegs), base + o_p, d_logp,
-                                          d_ccdf, sp), "tpe_cat_posterior")
+            L.check(lib.tpe_cat_posterior(base + o_cobs, d_csegs, len(csegs),
+                                          int(csegs["n_cat"].max()), base + o_p, d_logp, d_ccdf,
+                                          sp), "tpe_cat_posterior")
             tock("cat_fit", e0)
 
         # ---- scoring, one call per group ----------------------------------------

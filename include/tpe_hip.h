@@ -151,8 +151,9 @@ int tpe_parzen_fit(const double* obs, double* xf, tpe_seg* segs, int n_seg, int 
 
 /* ---- categorical posterior (tpe.py:578-615) ------------------------------ */
 /* p_pool: probabilities (mode 1 also reads the prior p from it at
- * prior_p_off); logp_pool / cdf_pool: log p and cumulative p at p_off. */
-int tpe_cat_posterior(const int64_t* obs, const tpe_cat_seg* segs, int n_seg,
+ * prior_p_off); logp_pool / cdf_pool: log p and cumulative p at p_off.
+ * max_cat: the largest n_cat over segs (host value, sizes the grid). */
+int tpe_cat_posterior(const int64_t* obs, const tpe_cat_seg* segs, int n_seg, int max_cat,
                       double* p_pool, double* logp_pool, double* cdf_pool, void* stream);
 
 /* ---- continuous candidates: sample (or read) + score + argmax ------------

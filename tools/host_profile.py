@@ -1,15 +1,16 @@
-"""Host-side profile of bench.py's step (cProfile + wall split)."""
+"""Host-side profile of bench.py's step (wall split + cProfile of Engine.run)."""
 import cProfile
+import os
 import pstats
 import sys
 import time
 
-sys.path.insert(0, ".")
-import numpy as np
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
-import bench
-from hyperopt_amd.engine import Engine
+import bench  # noqa: E402
+from hyperopt_amd.engine import Engine  # noqa: E402
 
 space = bench.c3_space()
 vals, losses = bench.c3_history(space)
@@ -25,9 +26,19 @@ for k in range(5):
     w = bench.make_works(space, sp, k, 1 << 22, 0)
 t2 = time.perf_counter()
 print("split %.3f ms  make_works %.3f ms" % ((t1 - t0) / 5e-3, (t2 - t1) / 5e-3))
+# launch-side cost: run with tiny candidate counts (GPU time negligible)
+for n in (1 << 22, 1 << 10):
+    ws = [bench.make_works(space, sp, k, n, 0) for k in range(5)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for w in ws:
+        eng.run(w)
+    t1 = time.perf_counter()
+    print("run n=%d: %.3f ms/step" % (n, (t1 - t0) / 5e-3))
 pr = cProfile.Profile()
+ws = [bench.make_works(space, sp, k, 1 << 10, 0) for k in range(5)]
 pr.enable()
-for k in range(5):
-    eng.run(bench.make_works(space, sp, k, 1 << 22, 0))
+for w in ws:
+    eng.run(w)
 pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
