@@ -2,10 +2,13 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := hyperopt_amd/csrc
-SRCS := $(CSRC)/tpe_fit.hip $(CSRC)/tpe_score.hip $(CSRC)/tpe_table.hip $(CSRC)/tpe_util.hip
+SRCS := $(CSRC)/tpe_fit.hip $(CSRC)/tpe_parzen.hip $(CSRC)/tpe_score.hip $(CSRC)/tpe_table.hip $(CSRC)/tpe_util.hip
 OBJS := $(SRCS:.hip=.o)
 LIB := hyperopt_amd/libtpe_hip.so
-FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function
+# -ffp-contract=off: no implicit FMA fusion, so expressions written to
+# follow numpy's operation order (linspace ramps, normal_cdf, erf-pair sums)
+# round exactly as numpy does; hot loops spell their FMAs out (fmaf).
+FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -ffp-contract=off
 
 all: $(LIB)
 

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32 = 1, 2, 4, 8, 16
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -55,7 +55,9 @@ _I = ctypes.c_int
 _I64 = ctypes.c_int64
 
 _SIGNATURES = {
-    "tpe_parzen_fit": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_fit_scratch_bytes": (_I64, [_I, _I, _I64]),
+    "tpe_parzen_fit": (_I, [_P, _P, _P, _I, _I, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                            _P]),
     "tpe_sort_layout": (_I64, [_I64, _P]),
     "tpe_sort_candidates": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_sorted": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,

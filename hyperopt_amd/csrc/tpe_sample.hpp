@@ -85,8 +85,8 @@ __device__ __forceinline__ void attempt32_pair(const Mix& M, uint64_t key, int64
   const int j0 = comp_of(M, r.x), j1 = comp_of(M, r.w);
   float z0, z1;
   normal_pair_f32(r.y, r.z, z0, z1);
-  y0 = (float)M.mu[j0] + (float)M.sg[j0] * z0;
-  y1 = (float)M.mu[j1] + (float)M.sg[j1] * z1;
+  y0 = fmaf((float)M.sg[j0], z0, (float)M.mu[j0]);
+  y1 = fmaf((float)M.sg[j1], z1, (float)M.mu[j1]);
 }
 
 // attempt `a` of candidate `g` alone (same value as attempt32_pair's half)
@@ -97,7 +97,7 @@ __device__ __forceinline__ float attempt32(const Mix& M, uint64_t key, int64_t g
   const float u2 = (float)(r.z >> 8) * 0x1.0p-24f;
   const float rr = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
   const float z = rr * ((g & 1) ? __builtin_amdgcn_sinf(u2) : __builtin_amdgcn_cosf(u2));
-  return (float)M.mu[j] + (float)M.sg[j] * z;
+  return fmaf((float)M.sg[j], z, (float)M.mu[j]);
 }
 
 __device__ __forceinline__ bool accept32(float y, bool lo_on, bool hi_on, float lo, float hi) {

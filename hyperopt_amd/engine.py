@@ -167,7 +167,7 @@ class Engine:
     # -- main entry ----------------------------------------------------------
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
             outputs=False, stream=None, timers=None, sample_only=False,
-            pruned=True, scorer=None) -> List[LabelResult]:
+            pruned=True, scorer=None, posteriors=False) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``.
         ``sample_only``: fit, then only draw the candidates of the continuous
@@ -179,7 +179,10 @@ class Engine:
         "auto" (table from TABLE_MIN_CAND candidates, sorted from
         SORTED_MIN_CAND, dense below; injected candidates dense).
         ``pruned=False`` is the old spelling of scorer="dense".  fp64 always
-        runs the exact dense kernel."""
+        runs the exact dense kernel.  ``posteriors``: fit only, and return the
+        fitted mixtures in ``LabelResult.extra`` ("below" / "above" as
+        (w, mu, sigma) sorted by mu, "p_accept"; categorical: "p_below" /
+        "p_above") -- the parity hook for adaptive_parzen_normal."""
         if sample_only:
             outputs = True
         if scorer is None:
@@ -404,20 +407,34 @@ class Engine:
             d_w32 = self._buf("wide32", 16 * n_comp)
             d_pm = self._buf("pm", 4 * n_comp)
             d_sm = self._buf("sm", 4 * n_comp)
-            d_xf = self._buf("xf", 8 * max(obs_pool.size, 1))
+            n_obs_total = int(obs_pool.size)
+            d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
+                                                                       n_obs_total))
+            prune = any(k == "sorted" and ids for k, ids in groups)
+            if not prune:
+                d_c32n = d_w32 = d_pm = d_sm = None
             e0 = tick()
-            L.check(lib.tpe_parzen_fit(base + o_obs, d_xf, d_segs, len(segs), max_obs, d_w, d_mu,
-                                       d_sig, d_cdf, d_c64, d_c32, d_c32n, d_w32, d_pm, d_sm, sp),
-                    "tpe_parzen_fit")
+            L.check(lib.tpe_parzen_fit(base + o_obs, d_fs, d_segs, len(segs), max_obs,
+                                       n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
+                                       d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
             tock("fit", e0)
         if cat:
             d_logp = self._buf("cat_logp", 8 * p_pool.size)
             d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
             e0 = tick()
+            d_p = self._buf("cat_p", 8 * p_pool.size)
+            with torch.cuda.stream(stream):
+                pt = self._bufs["cat_p"]
+                st = self._bufs["stage"]
+                pt[:8 * p_pool.size].copy_(st[o_p:o_p + 8 * p_pool.size])
             L.check(lib.tpe_cat_posterior(base + o_cobs, d_csegs, len(csegs),
-                                          int(csegs["n_cat"].max()), base + o_p, d_logp, d_ccdf,
-                                          sp), "tpe_cat_posterior")
+                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, sp),
+                    "tpe_cat_posterior")
             tock("cat_fit", e0)
+
+        if posteriors:
+            return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
+                                         d_segs, stream)
 
         # ---- scoring, one call per group ----------------------------------------
         table_calls = []
@@ -551,6 +568,41 @@ class Engine:
                 r.above_llik = outs[1][o:o + n].copy()
                 r.cand = outs[2][o:o + n].copy()
             results[i] = r
+        return results
+
+
+    def _read_posteriors(self, works, fit_ids, cat, segs, csegs, n_comp, n_p, d_segs, stream):
+        torch = self.torch
+        with torch.cuda.stream(stream):
+            host = {}
+            if fit_ids:
+                for k in ("w", "mu", "sigma"):
+                    host[k] = self._bufs[k][:8 * n_comp].to("cpu").numpy().view(np.float64)
+                seg_t = self._bufs["stage"]
+                # the fit writes prior_pos / p_accept back into the staged segment table
+                raw = torch.empty(segs.nbytes, dtype=torch.uint8)
+                off = d_segs - seg_t.data_ptr()
+                raw.copy_(seg_t[off:off + segs.nbytes])
+                dsegs = raw.numpy().view(L.SEG_DTYPE)
+            if cat:
+                host["p"] = self._bufs["cat_p"][:8 * n_p].to("cpu").numpy().view(np.float64)
+        results = [LabelResult(w.label, -1, 0.0, 0.0, 0) for w in works]
+        for si, i in enumerate(fit_ids):
+            post = {}
+            for half, name in enumerate(("below", "above")):
+                sg = segs[2 * si + half]
+                a, n = int(sg["comp_off"]), int(sg["n_obs"]) + 1
+                post[name] = tuple(host[k][a:a + n].copy() for k in ("w", "mu", "sigma"))
+            post["p_accept"] = (float(dsegs[2 * si]["p_accept"]),
+                                float(dsegs[2 * si + 1]["p_accept"]))
+            results[i].extra = post
+        for ci, i in enumerate(cat):
+            post = {}
+            for half, name in enumerate(("p_below", "p_above")):
+                c = csegs[2 * ci + half]
+                a, n = int(c["p_off"]), int(c["n_cat"])
+                post[name] = host["p"][a:a + n].copy()
+            results[i].extra = post
         return results
 
 

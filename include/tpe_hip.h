@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 3
+#define TPE_ABI_VERSION 4
 
 enum {
   TPE_OK = 0,
@@ -136,18 +136,21 @@ typedef struct tpe_best {
 } tpe_best;
 
 /* ---- Parzen posterior (adaptive_parzen_normal, tpe.py:399-467) ---------- */
-/* obs: fp64 pool; xf: fp64 scratch (same size as obs);
+/* obs: fp64 pool (n_obs_total); scratch: device workspace of
+ * tpe_fit_scratch_bytes(n_seg, max_obs, n_obs_total) bytes;
  * w/mu/sigma: fp64 mixture pool (sorted components);
  * wcdf: fp64 cumulative weights (sampler); coef64: 4 doubles / component;
- * coef32: 4 floats / component.  max_obs = max n_obs over segs. */
-/* Pruning data for the sorted scoring path (per component, float):
- * coef32n = coef32 with wide components masked (c = -inf), wide32 = the
- * wide components' coefficients compacted at comp_off, pm / sm = prefix max
- * of (mu + reach) / suffix min of (mu - reach) over narrow components. */
-int tpe_parzen_fit(const double* obs, double* xf, tpe_seg* segs, int n_seg, int max_obs,
-                   double* w, double* mu, double* sigma, double* wcdf,
-                   double* coef64, float* coef32, float* coef32n, float* wide32,
-                   float* pm, float* sm, void* stream);
+ * coef32: 4 floats / component.  max_obs = max n_obs over segs.
+ * Pruning data for the sorted scoring path (per component, float; all four
+ * NULL to skip): coef32n = coef32 with wide components masked (c = -inf),
+ * wide32 = the wide components' coefficients compacted at comp_off, pm / sm
+ * = prefix max of (mu + reach) / suffix min of (mu - reach) over narrow
+ * components. */
+int64_t tpe_fit_scratch_bytes(int n_seg, int max_obs, int64_t n_obs_total);
+int tpe_parzen_fit(const double* obs, void* scratch, tpe_seg* segs, int n_seg, int max_obs,
+                   int64_t n_obs_total, double* w, double* mu, double* sigma, double* wcdf,
+                   double* coef64, float* coef32, float* coef32n, float* wide32, float* pm,
+                   float* sm, void* stream);
 
 /* ---- categorical posterior (tpe.py:578-615) ------------------------------ */
 /* p_pool: probabilities (mode 1 also reads the prior p from it at

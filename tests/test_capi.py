@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 3
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 4
     sizes = (ctypes.c_int32 * 5)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 5) == 5
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -55,8 +55,11 @@ def test_argument_errors_are_reported():
                                   48, None, None, None, None, 0, None, None)
     assert rc == 0  # nothing to do
     nul = [None] * 11
-    assert lib.tpe_parzen_fit(None, None, None, 0, 0, *nul) == 0
-    assert lib.tpe_parzen_fit(None, None, None, -1, 0, *nul) == -1
+    assert lib.tpe_parzen_fit(None, None, None, 0, 0, 0, *nul) == 0
+    assert lib.tpe_parzen_fit(None, None, None, -1, 0, 0, *nul) == -1
+    assert lib.tpe_parzen_fit(None, None, None, 1, 0, 0, *nul) == -1  # null pointers
+    assert lib.tpe_fit_scratch_bytes(2, 100, 150) > 150 * 20
+    assert lib.tpe_fit_scratch_bytes(-1, 0, 0) == -1
     jobs["flags"] = 0
     jobs["bin_lo"] = jobs["bin_hi"] = 1.0
     rc = lib.tpe_score_sorted(None, hp_, 1, *([None] * 9), 0, None, None, None)
