@@ -35,6 +35,8 @@ T_HIST = 10_000
 N_CAND = 1 << 22
 FP32_PEAK_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 FLOPS_PER_PAIR = 9  # unquantized GMM1/LGMM1 pair
+OPS_PER_TABLE_CAND = 105  # cell-table scorer, per candidate
+DIRECT_PAIR_CEILING = 9.81e12  # pairs/s of the exp-bound direct loop (profiles/r01_valu_microbench.txt)
 
 
 def c3_space():
@@ -74,6 +76,31 @@ def split(vals, losses, gamma=0.25):
     isb = np.zeros(T, bool)
     isb[order[:n_below]] = True
     return {lab: (v[isb], v[~isb]) for lab, v in vals.items()}
+
+
+def c3_matrix(space, vals):
+    """The history as a (T, labels) matrix in space order (all labels active)."""
+    return np.stack([vals[lab] for lab, _, _ in space], axis=1)
+
+
+def below_rows(losses, gamma=0.25):
+    """Rows of the n_below best losses, ascending (ap_split_trials, tpe.py:623-646)."""
+    from hyperopt_amd.tpe import _smallest_rows
+    T = losses.size
+    n_below = min(int(math.ceil(gamma * math.sqrt(T))), 25)
+    return np.sort(_smallest_rows(losses, n_below))
+
+
+def history_works(space, mat, hist, rows_b, step, n_cand, cand_base):
+    """LabelWork list for the device-resident history: only the (small) below
+    sets are read on the host; the above sets are gathered on the GPU."""
+    from hyperopt_amd.engine import LabelWork
+    below = mat[rows_b]
+    n_b = hist.active_host[rows_b].sum(0)
+    return [LabelWork(label=lab, kind=kind, args=a, obs_below=below[:, j], obs_above=None,
+                      n_cand=n_cand, key=label_key(0, step, lab), cand_base=cand_base, col=j,
+                      n_above=int(hist.n_active[j] - n_b[j]))
+            for j, (lab, kind, a) in enumerate(space)]
 
 
 def label_key(seed, step, lab):
@@ -156,6 +183,9 @@ def main():
     ap.add_argument("--precision", type=int, default=32)
     ap.add_argument("--n-cand", type=int, default=N_CAND)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--upload-history", action="store_true",
+                    help="pack and upload the observation lists every step instead of gathering "
+                         "them from the HBM-resident history")
     ap.add_argument("--dense", action="store_true",
                     help="score with the dense fp32 kernel (same as --scorer dense)")
     ap.add_argument("--scorer", default="auto", choices=("auto", "dense", "sorted", "table"),
@@ -170,7 +200,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.engine import DeviceHistory, Engine
     from hyperopt_amd import dist as hdist
 
     scorer = "dense" if args.dense else args.scorer
@@ -179,11 +209,23 @@ def main():
     eng = Engine()
     n_cand = args.n_cand
     cand_base = rank * n_cand
+    # the history is resident in HBM before timing starts (appended once, as
+    # trials would be); each step uploads only the below-row flags
+    mat = c3_matrix(space, vals)
+    hist = DeviceHistory(eng, len(space), cap=T_HIST)
+    hist.append(mat)
 
     def step(k, timers=None):
-        sp = split(vals, losses)
-        works = make_works(space, sp, k, n_cand, cand_base)
-        res = eng.run(works, precision=args.precision, timers=timers, scorer=scorer)
+        if args.upload_history:
+            works = make_works(space, split(vals, losses), k, n_cand, cand_base)
+            res = eng.run(works, precision=args.precision, timers=timers, scorer=scorer)
+        else:
+            rb = below_rows(losses)
+            isb = np.zeros(T_HIST, np.uint8)
+            isb[rb] = 1
+            works = history_works(space, mat, hist, rb, k, n_cand, cand_base)
+            res = eng.run(works, precision=args.precision, timers=timers, scorer=scorer,
+                          history=hist, is_below=isb)
         if world > 1:
             hdist.allreduce_best(res)
         return works, res
@@ -213,17 +255,27 @@ def main():
 
     # dominant kernel: unquantized continuous scoring of the 30 continuous labels
     cont = [w for w in works if w.kind in ("uniform", "loguniform", "normal", "lognormal")]
-    dense_pairs = sum(n_cand * (w.obs_below.size + 1 + w.obs_above.size + 1) for w in cont)
-    exec_cand = n_cand * len(cont)  # sorted value + index read once per candidate
-    group = "cont" if args.dense else "sorted"
-    kname = "k_score32 (tpe_score_continuous)" if args.dense else \
-        "k_score_sorted (tpe_score_sorted)"
+    dense_pairs = sum(n_cand * (w.obs_below.size + 1 + (w.n_above if w.obs_above is None
+                                                        else w.obs_above.size) + 1)
+                      for w in cont)
+    n_cont = n_cand * len(cont)
+    group = {"dense": "cont", "sorted": "sorted"}.get(scorer, "table")
+    kname = {"cont": "k_score32 (tpe_score_continuous)",
+             "sorted": "k_score_sorted (tpe_score_sorted)",
+             "table": "k_score_table (tpe_score_table)"}[group]
     kms = [e0.elapsed_time(e1) for e0, e1 in timers.get(group, [])]
     avg_ms = float(np.mean(kms)) if kms else float("nan")
-    exec_pairs = dense_pairs if args.dense else (eng.last_pairs or dense_pairs)
-    flops = exec_pairs * FLOPS_PER_PAIR
-    achieved = flops / (avg_ms * 1e-3) / 1e12
-    effective = dense_pairs * FLOPS_PER_PAIR / (avg_ms * 1e-3) / 1e12
+    sec = avg_ms * 1e-3
+    if group == "table":
+        # algorithmic operations per candidate of the
+        # cell-table scorer (sample + cell lookup + two degree-11 polynomials)
+        ops = OPS_PER_TABLE_CAND * n_cont
+        work = {"ops_per_candidate": OPS_PER_TABLE_CAND, "candidates_per_launch": n_cont}
+    else:
+        exec_pairs = dense_pairs if group == "cont" else (eng.last_pairs or dense_pairs)
+        ops = exec_pairs * FLOPS_PER_PAIR
+        work = {"flops_per_pair": FLOPS_PER_PAIR, "evaluated_pairs_per_launch": exec_pairs}
+    achieved = ops / sec / 1e12
     group_ms = {k: round(float(np.mean([a.elapsed_time(b) for a, b in v])), 4)
                 for k, v in timers.items()}
 
@@ -235,10 +287,22 @@ def main():
     tfile = os.path.join(HERE, "profiles", "traffic.json")
     if os.path.exists(tfile):
         prof = json.load(open(tfile))
-        if prof.get("kernel") in kname:
+        if prof.get("kernel") and prof["kernel"] in kname:
             traffic = prof.get("bytes_per_launch")
         else:
             prof = {}
+    roofline = {"bound": "valu", "kernel": kname, "achieved": achieved,
+                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
+                "algorithmic_ops_per_launch": ops, "avg_launch_ms": avg_ms,
+                "dense_pairs_per_launch": dense_pairs,
+                "dense_equivalent_pairs_per_s": dense_pairs / sec,
+                "direct_pair_ceiling_per_s": DIRECT_PAIR_CEILING,
+                "valu_busy": prof.get("valu_busy"), "traffic_source": prof.get("source")}
+    roofline.update(work)
+    if group == "table":
+        roofline["l2_gather_bytes_per_launch"] = 128 * n_cont
+        roofline["build_ms"] = group_ms.get("table_build")
     line = {
         "metric": "EI candidates scored/sec (50-dim, 10k trials)",
         "value": value,
@@ -258,17 +322,7 @@ def main():
                                % int(round(math.log2(n_cand))),
                    "labels": len(space), "history": T_HIST, "candidates_per_label": n_cand,
                    "parallelism": "candidate-sharded x%d, RCCL max-loc combine" % world},
-        "roofline": {"bound": "valu", "kernel": kname,
-                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
-                     "algorithmic_flops_per_launch": flops, "avg_launch_ms": avg_ms,
-                     "flops_per_pair": FLOPS_PER_PAIR,
-                     "evaluated_pairs_per_launch": exec_pairs,
-                     "dense_pairs_per_launch": dense_pairs,
-                     "dense_equivalent_tflops": effective,
-                     "algorithmic_bytes_per_launch": 8 * exec_cand,
-                     "valu_busy": prof.get("valu_busy"),
-                     "traffic_source": prof.get("source")},
+        "roofline": roofline,
         "group_ms": group_ms,
     }
     if rank == 0 and world == 1:

@@ -42,6 +42,9 @@ TABLE_DTYPE = np.dtype([
     ("lo", "<f8"), ("hi", "<f8"), ("h_below", "<f8"), ("h_above", "<f8"), ("origin", "<f8"),
     ("h", "<f8"), ("inv_h", "<f4"), ("inv_w", "<f4"), ("nb", "<i4"), ("n_wide_below", "<i4"),
     ("n_wide_above", "<i4"), ("pad", "<i4")], align=True)
+GATHER_DTYPE = np.dtype([
+    ("col", "<i4"), ("below", "<i4"), ("dst_off", "<i8"), ("offset", "<i8"), ("count", "<i8"),
+    ("to_int", "<i4"), ("pad", "<i4")], align=True)
 BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
                        ("n_scored", "<i8")], align=True)
 
@@ -63,6 +66,7 @@ _SIGNATURES = {
     "tpe_score_sorted": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
                               _P]),
     "tpe_cat_posterior": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
+    "tpe_gather_obs": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _P, _P, _P, _P]),
     "tpe_table_partials": (_I64, [_P, _I]),
     "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_table": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
@@ -104,10 +108,10 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    sizes = (ctypes.c_int32 * 5)()
-    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 5)
+    sizes = (ctypes.c_int32 * 6)()
+    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 6)
     want = (SEG_DTYPE.itemsize, CAT_SEG_DTYPE.itemsize, JOB_DTYPE.itemsize, BEST_DTYPE.itemsize,
-            TABLE_DTYPE.itemsize)
+            TABLE_DTYPE.itemsize, GATHER_DTYPE.itemsize)
     if lib.tpe_abi_version() != ABI_VERSION:
         raise ImportError("hyperopt_amd: libtpe_hip.so ABI %d, expected %d (rebuild with make)"
                           % (lib.tpe_abi_version(), ABI_VERSION))

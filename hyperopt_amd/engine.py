@@ -20,6 +20,7 @@ HIP kernel from libtpe_hip.so.
 from __future__ import annotations
 
 import ctypes
+import functools
 import math
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -55,6 +56,11 @@ class LabelWork:
     key: int = 0              # Philox key (seed mixed with the label)
     cand_base: int = 0        # global index of this device's first candidate
     cand: Optional[np.ndarray] = None  # injected candidates (values / category ids)
+    # history mode (Engine.run(history=...)): the observation lists are
+    # gathered on the device from column `col`; obs_below is still given on
+    # the host (it is small) and obs_above is None with its size in n_above
+    col: Optional[int] = None
+    n_above: int = 0
 
 
 @dataclass
@@ -93,6 +99,18 @@ def posterior_params(kind, args):
     raise ValueError("not a continuous prior: %r" % (kind,))
 
 
+@functools.lru_cache(maxsize=4096)
+def _posterior_params_cached(kind, args):
+    return posterior_params(kind, args)
+
+
+def _params(kind, args):
+    try:
+        return _posterior_params_cached(kind, tuple(args))
+    except TypeError:  # unhashable args
+        return posterior_params(kind, args)
+
+
 def categorical_params(kind, args):
     """(K, offset, mode, prior p) for randint / categorical (tpe.py:578-615)."""
     if kind == "randint":
@@ -125,6 +143,63 @@ class _Pack:
         self.parts.append((off, arr))
         self.size = off + max(arr.nbytes, 1)
         return off
+
+
+class DeviceHistory:
+    """A trials x labels history resident in HBM, appended in place.
+
+    ``vals[j, r]`` / ``active[j, r]`` (label-major, leading dimension ``ld``)
+    hold label j's value in history row r -- the columnar form of the
+    reference's per-suggest ``miscs_to_idxs_vals`` (base.py:200-214).  The host
+    keeps the active mask and per-label active counts so segment sizes are
+    known without a device round trip.
+    """
+
+    def __init__(self, engine, n_labels, cap=1024):
+        self.torch = engine.torch
+        self.device = engine.device
+        self.n_labels = int(n_labels)
+        self.rows = 0
+        self.cap = 0
+        self.vals = self.active = None
+        self.active_host = np.zeros((0, self.n_labels), bool)
+        self.n_active = np.zeros(self.n_labels, np.int64)
+        self._grow(max(int(cap), 16))
+
+    @property
+    def ld(self):
+        return self.cap
+
+    def _grow(self, cap):
+        t = self.torch
+        v = t.zeros((self.n_labels, cap), dtype=t.float64, device=self.device)
+        a = t.zeros((self.n_labels, cap), dtype=t.uint8, device=self.device)
+        if self.rows:
+            v[:, :self.rows].copy_(self.vals[:, :self.rows])
+            a[:, :self.rows].copy_(self.active[:, :self.rows])
+        ah = np.zeros((cap, self.n_labels), bool)
+        ah[:self.rows] = self.active_host[:self.rows]
+        self.vals, self.active, self.active_host, self.cap = v, a, ah, cap
+
+    def append(self, vals, active=None):
+        """Append rows: vals (k, n_labels) float, active (k, n_labels) bool
+        (default: finite values)."""
+        vals = np.asarray(vals, dtype=np.float64).reshape(-1, self.n_labels)
+        active = np.isfinite(vals) if active is None else \
+            np.asarray(active, dtype=bool).reshape(vals.shape)
+        k = vals.shape[0]
+        if k == 0:
+            return
+        if self.rows + k > self.cap:
+            self._grow(max(2 * self.cap, self.rows + k))
+        r0, t = self.rows, self.torch
+        src_v = t.from_numpy(np.ascontiguousarray(np.where(active, vals, 0.0).T))
+        src_a = t.from_numpy(np.ascontiguousarray(active.T.astype(np.uint8)))
+        self.vals[:, r0:r0 + k].copy_(src_v.to(self.device))
+        self.active[:, r0:r0 + k].copy_(src_a.to(self.device))
+        self.active_host[r0:r0 + k] = active
+        self.n_active += active.sum(0)
+        self.rows += k
 
 
 class Engine:
@@ -167,7 +242,8 @@ class Engine:
     # -- main entry ----------------------------------------------------------
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
             outputs=False, stream=None, timers=None, sample_only=False,
-            pruned=True, scorer=None, posteriors=False) -> List[LabelResult]:
+            pruned=True, scorer=None, posteriors=False, history=None, rows=None,
+            is_below=None) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``.
         ``sample_only``: fit, then only draw the candidates of the continuous
@@ -182,7 +258,11 @@ class Engine:
         runs the exact dense kernel.  ``posteriors``: fit only, and return the
         fitted mixtures in ``LabelResult.extra`` ("below" / "above" as
         (w, mu, sigma) sorted by mu, "p_accept"; categorical: "p_below" /
-        "p_above") -- the parity hook for adaptive_parzen_normal."""
+        "p_above") -- the parity hook for adaptive_parzen_normal.
+        ``history`` (DeviceHistory) + ``is_below`` (uint8 per position of
+        ``rows``, or of the history rows when ``rows`` is None): every work
+        names its label column (``col``) and the observation lists are
+        gathered on the device (tpe_gather_obs) instead of being uploaded."""
         if sample_only:
             outputs = True
         if scorer is None:
@@ -215,29 +295,46 @@ class Engine:
                 raise ValueError("unsupported prior %r for label %r" % (w.kind, w.label))
 
         pack = _Pack()
+        hist_mode = history is not None
+        gathers = []  # history mode: (col, below, dst_off, offset, count, to_int)
         # ---- continuous / quantized segments --------------------------------
         fit_ids = cont + quant
-        segs = np.zeros(2 * len(fit_ids), L.SEG_DTYPE)
-        obs_parts, params = [], {}
-        obs_off = comp_off = max_obs = 0
-        for si, i in enumerate(fit_ids):
-            w = works[i]
-            P = posterior_params(w.kind, w.args)
-            params[i] = P
-            for half, obs in enumerate((w.obs_below, w.obs_above)):
-                obs = np.asarray(obs, dtype=np.float64).reshape(-1)
-                s = segs[2 * si + half]
-                s["obs_off"], s["comp_off"], s["n_obs"] = obs_off, comp_off, obs.size
-                s["lf"], s["transform"], s["family"] = lf, P["transform"], P["family"]
-                s["floor"], s["prior_weight"] = P["floor"], prior_weight
-                s["prior_mu"], s["prior_sigma"] = P["prior_mu"], P["prior_sigma"]
-                s["low"], s["high"], s["bounded"] = P["low"], P["high"], int(P["bounded"])
-                obs_parts.append(obs)
-                obs_off += obs.size
-                comp_off += obs.size + 1
-                max_obs = max(max_obs, obs.size)
-        n_comp = comp_off
-        obs_pool = np.concatenate(obs_parts) if obs_parts else np.zeros(1)
+        params = {i: _params(works[i].kind, works[i].args) for i in fit_ids}
+        nf = len(fit_ids)
+        segs = np.zeros(2 * nf, L.SEG_DTYPE)
+        obs_pool = None
+        n_obs_total = n_comp = max_obs = 0
+        if nf:
+            if hist_mode:
+                sizes = np.empty(2 * nf, np.int64)
+                for si, i in enumerate(fit_ids):
+                    sizes[2 * si] = np.asarray(works[i].obs_below).size
+                    sizes[2 * si + 1] = int(works[i].n_above)
+            else:
+                parts = [np.asarray(o, dtype=np.float64).reshape(-1) for i in fit_ids
+                         for o in (works[i].obs_below, works[i].obs_above)]
+                sizes = np.fromiter((o.size for o in parts), np.int64, 2 * nf)
+                obs_pool = np.concatenate(parts)
+            ends = np.cumsum(sizes)
+            obs_off = ends - sizes
+            comp_off = np.cumsum(sizes + 1) - (sizes + 1)
+            segs["obs_off"], segs["comp_off"], segs["n_obs"] = obs_off, comp_off, sizes
+            segs["lf"], segs["prior_weight"] = lf, prior_weight
+            pl = [params[i] for i in fit_ids]
+            for name in ("transform", "family", "floor", "prior_mu", "prior_sigma", "low", "high"):
+                segs[name] = np.repeat([p[name] for p in pl], 2)
+            segs["bounded"] = np.repeat([int(p["bounded"]) for p in pl], 2)
+            n_obs_total = int(ends[-1])
+            n_comp = n_obs_total + 2 * nf
+            max_obs = int(sizes.max())
+            if hist_mode:
+                for si, i in enumerate(fit_ids):
+                    for half in (0, 1):
+                        k = 2 * si + half
+                        gathers.append((works[i].col, 1 - half, int(obs_off[k]), 0, int(sizes[k]),
+                                        0))
+        if obs_pool is None:
+            obs_pool = np.zeros(1)
 
         # ---- categorical segments ------------------------------------------
         csegs = np.zeros(2 * len(cat), L.CAT_SEG_DTYPE)
@@ -253,15 +350,21 @@ class Engine:
                 prior_off = p_off
                 p_init.append(prior_p)
                 p_off += K
-            for half, obs in enumerate((w.obs_below, w.obs_above)):
-                obs = np.asarray(obs).reshape(-1).astype(np.int64) - offset
+            for half in (0, 1):
+                if hist_mode:
+                    n = np.asarray(w.obs_below).size if half == 0 else int(w.n_above)
+                    gathers.append((w.col, 1 - half, cobs_off, offset, n, 1))
+                else:
+                    obs = np.asarray(w.obs_below if half == 0 else w.obs_above).reshape(-1)
+                    obs = obs.astype(np.int64) - offset
+                    cobs_parts.append(obs)
+                    n = obs.size
                 c = csegs[2 * ci + half]
-                c["obs_off"], c["p_off"], c["n_obs"], c["n_cat"] = cobs_off, p_off, obs.size, K
+                c["obs_off"], c["p_off"], c["n_obs"], c["n_cat"] = cobs_off, p_off, n, K
                 c["lf"], c["mode"], c["prior_weight"], c["prior_p_off"] = lf, mode, prior_weight, \
                     max(prior_off, 0)
-                cobs_parts.append(obs)
                 p_init.append(np.zeros(K))
-                cobs_off += obs.size
+                cobs_off += n
                 p_off += K
         cobs_pool = np.concatenate(cobs_parts) if cobs_parts else np.zeros(1, np.int64)
         p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
@@ -306,60 +409,67 @@ class Engine:
             ("cat", [i for i in cat if not inj(i)]),
         ]
         order = [i for _, ids in groups for i in ids]
-        jobs = np.zeros(len(order), L.JOB_DTYPE)
+        nj_all = len(order)
+        jobs = np.zeros(nj_all, L.JOB_DTYPE)
+        J = {name: np.zeros(nj_all, L.JOB_DTYPE[name]) for name in L.JOB_DTYPE.names}
         cand_parts, cand_off, out_off, lat_off, qfb_off = [], 0, 0, 0, 0
         sort_off = cnt_off = tbl_off = 0
         seg_of = {i: si for si, i in enumerate(fit_ids)}
         cseg_of = {i: ci for ci, i in enumerate(cat)}
         for pos, i in enumerate(order):
-            w, j = works[i], jobs[pos]
-            j["key"] = np.uint64(int(w.key) & 0xFFFFFFFFFFFFFFFF)
-            j["cand_base"] = w.cand_base
+            w = works[i]
+            J["key"][pos] = int(w.key) & 0xFFFFFFFFFFFFFFFF
+            J["cand_base"][pos] = w.cand_base
             n = int(np.asarray(w.cand).size) if inj(i) else int(w.n_cand)
-            j["n_cand"] = n
-            j["out_off"] = out_off
+            J["n_cand"][pos] = n
+            J["out_off"][pos] = out_off
             out_off += n
+            flags = 0
             if inj(i):
                 # categorical candidates are category indices (0..K-1), as the
                 # reference's randint_via_categorical samples them (tpe.py:590)
                 c = np.asarray(w.cand, dtype=np.float64).reshape(-1)
-                j["cand_off"] = cand_off
+                J["cand_off"][pos] = cand_off
                 cand_parts.append(c)
                 cand_off += c.size
-                j["flags"] |= L.F_INJECTED
+                flags |= L.F_INJECTED
             if i in cat_meta:
-                j["family"] = L.CAT
-                j["below"], j["above"] = 2 * cseg_of[i], 2 * cseg_of[i] + 1
+                J["family"][pos] = L.CAT
+                J["below"][pos], J["above"][pos] = 2 * cseg_of[i], 2 * cseg_of[i] + 1
+                J["flags"][pos] = flags
                 continue
             P = params[i]
-            j["family"] = P["family"]
-            j["below"], j["above"] = 2 * seg_of[i], 2 * seg_of[i] + 1
+            J["family"][pos] = P["family"]
+            J["below"][pos], J["above"][pos] = 2 * seg_of[i], 2 * seg_of[i] + 1
             if P["bounded"]:
-                j["flags"] |= L.F_LOW | L.F_HIGH
-                j["low"], j["high"] = P["low"], P["high"]
+                flags |= L.F_LOW | L.F_HIGH
+                J["low"][pos], J["high"][pos] = P["low"], P["high"]
             if P["q"] is not None:
-                j["flags"] |= L.F_QUANT
-                j["q"] = P["q"]
+                flags |= L.F_QUANT
+                J["q"][pos] = P["q"]
                 if i in lat_ranges:
-                    j["lat_off"], j["lat_kmin"], j["lat_n"] = lat_off, *lat_ranges[i]
                     kmin, nk = lat_ranges[i]
+                    J["lat_off"][pos], J["lat_kmin"][pos], J["lat_n"][pos] = lat_off, kmin, nk
                     if precision == 32 and max(abs(kmin), abs(kmin + nk - 1)) <= DRAW32_MAX_SLOT:
-                        j["flags"] |= L.F_DRAW32
-                    lat_off += lat_ranges[i][1]
+                        flags |= L.F_DRAW32
+                    lat_off += nk
                 elif i in fallback:
-                    j["cand_off"] = qfb_off
+                    J["cand_off"][pos] = qfb_off
                     qfb_off += n
             elif modes[i] == "table":
-                j["tbl_off"], j["tbl_cap"] = tbl_off, TABLE_CAP
+                J["tbl_off"][pos], J["tbl_cap"][pos] = tbl_off, TABLE_CAP
                 tbl_off += TABLE_CAP
                 if inj(i):
-                    j["bin_lo"], j["bin_hi"] = _injected_range(w, P)
+                    J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P)
             elif modes[i] == "sorted":
-                j["bin_lo"], j["bin_hi"] = _support(w, P)
-                j["sort_off"], j["cnt_off"] = sort_off, cnt_off
+                J["bin_lo"][pos], J["bin_hi"][pos] = _support(w, P)
+                J["sort_off"][pos], J["cnt_off"][pos] = sort_off, cnt_off
                 slots = ctypes.c_int64(0)
                 cnt_off += lib.tpe_sort_layout(n, ctypes.byref(slots))
                 sort_off += slots.value
+            J["flags"][pos] = flags
+        for name, col in J.items():
+            jobs[name] = col
         cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
         # the dense fallback first materialises its draws: a job copy whose
         # out_off points into the scratch candidate buffer
@@ -369,10 +479,22 @@ class Engine:
 
         # ---- upload -------------------------------------------------------------
         o_segs = pack.add(segs) if segs.size else None
-        o_obs = pack.add(obs_pool)
         o_csegs = pack.add(csegs) if csegs.size else None
-        o_cobs = pack.add(cobs_pool)
         o_p = pack.add(p_pool)
+        if hist_mode:
+            g_arr = np.zeros(len(gathers), L.GATHER_DTYPE)
+            if gathers:
+                (g_arr["col"], g_arr["below"], g_arr["dst_off"], g_arr["offset"], g_arr["count"],
+                 g_arr["to_int"]) = (np.array(c) for c in zip(*gathers))
+            isb = np.ascontiguousarray(is_below, dtype=np.uint8)
+            n_rows = isb.size
+            o_g = pack.add(g_arr)
+            o_isb = pack.add(isb)
+            o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) if rows is not None \
+                else None
+        else:
+            o_obs = pack.add(obs_pool)
+            o_cobs = pack.add(cobs_pool)
         o_jobs = pack.add(jobs) if jobs.size else None
         o_fb = pack.add(fb_jobs) if fb_jobs.size else None
         o_cand = pack.add(cand_pool)
@@ -388,6 +510,18 @@ class Engine:
         err_t = self._bufs["err"]
         with torch.cuda.stream(stream):
             err_t[:16].zero_()
+        if hist_mode:
+            d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
+            d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
+            e0 = tick()
+            L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
+                                       history.ld, base + o_rows if o_rows is not None else None,
+                                       n_rows, base + o_isb, base + o_g,
+                                       g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr), d_obs,
+                                       d_cobs, d_err, sp), "tpe_gather_obs")
+            tock("gather", e0)
+        else:
+            d_obs, d_cobs = base + o_obs, base + o_cobs
         d_bl = d_al = d_x = None
         if outputs:
             d_bl = self._buf("out_bl", 8 * max(out_off, 1))
@@ -407,14 +541,13 @@ class Engine:
             d_w32 = self._buf("wide32", 16 * n_comp)
             d_pm = self._buf("pm", 4 * n_comp)
             d_sm = self._buf("sm", 4 * n_comp)
-            n_obs_total = int(obs_pool.size)
             d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
                                                                        n_obs_total))
             prune = any(k == "sorted" and ids for k, ids in groups)
             if not prune:
                 d_c32n = d_w32 = d_pm = d_sm = None
             e0 = tick()
-            L.check(lib.tpe_parzen_fit(base + o_obs, d_fs, d_segs, len(segs), max_obs,
+            L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
                                        n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
                                        d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
             tock("fit", e0)
@@ -427,7 +560,7 @@ class Engine:
                 pt = self._bufs["cat_p"]
                 st = self._bufs["stage"]
                 pt[:8 * p_pool.size].copy_(st[o_p:o_p + 8 * p_pool.size])
-            L.check(lib.tpe_cat_posterior(base + o_cobs, d_csegs, len(csegs),
+            L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
                                           int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, sp),
                     "tpe_cat_posterior")
             tock("cat_fit", e0)
@@ -556,6 +689,9 @@ class Engine:
             raise ValueError("negative arg to lognormal_cdf")  # tpe.py:196-197
         if err & 2:
             raise L.TpeHipError("lattice slot out of range (internal error)")
+        if err & 4:
+            raise L.TpeHipError("history gather: observation counts do not match the "
+                                "segment sizes given by the host")
         results = [None] * len(works)
         for pos, i in enumerate(order):
             b = best_h[pos]

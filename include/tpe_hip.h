@@ -152,6 +152,30 @@ int tpe_parzen_fit(const double* obs, void* scratch, tpe_seg* segs, int n_seg, i
                    double* coef64, float* coef32, float* coef32n, float* wide32, float* pm,
                    float* sm, void* stream);
 
+/* ---- observation lists from an HBM-resident history ---------------------
+ * Replaces the per-suggest rebuild of miscs_to_idxs_vals (base.py:200-214)
+ * and the list comprehensions of ap_split_trials (tpe.py:623-646, tid order
+ * kept).  vals / active: label-major matrices, element (col, row) at
+ * col * ld + row; rows (nullable = identity): the n_rows history rows in tid
+ * order; is_below: one flag per position of `rows` (1 = among the n_below
+ * best losses).  Each descriptor compacts the rows active for `col` on its
+ * side of the split into obs_f64 (Parzen fit pool) or, with to_int, into
+ * obs_i64 as (int64)value - offset (categorical pool), writing at most
+ * `count` elements; a different number of matches sets bit 4 of *err. */
+typedef struct tpe_gather {
+  int32_t col;          /* label column                                      */
+  int32_t below;        /* 1: below rows, 0: above rows                      */
+  int64_t dst_off;      /* first output element                              */
+  int64_t offset;       /* to_int: subtracted (randint low)                  */
+  int64_t count;        /* elements expected (the segment's n_obs)           */
+  int32_t to_int;       /* 1: int64 output, 0: fp64 output                   */
+  int32_t pad;
+} tpe_gather;
+int tpe_gather_obs(const double* vals, const uint8_t* active, int64_t ld, const int32_t* rows,
+                   int64_t n_rows, const uint8_t* is_below, const tpe_gather* gathers,
+                   const tpe_gather* host_gathers, int n_gathers, double* obs_f64,
+                   int64_t* obs_i64, int32_t* err, void* stream);
+
 /* ---- categorical posterior (tpe.py:578-615) ------------------------------ */
 /* p_pool: probabilities (mode 1 also reads the prior p from it at
  * prior_p_off); logp_pool / cdf_pool: log p and cumulative p at p_off.
@@ -293,7 +317,8 @@ int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* o
 
 const char* tpe_last_error(void);
 int tpe_abi_version(void);
-/* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table) to out[0..n) */
+/* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table, tpe_gather)
+ * to out[0..n) */
 int tpe_struct_sizes(int32_t* out, int n);
 
 #ifdef __cplusplus

@@ -31,10 +31,11 @@ def test_header_symbols_exported():
 def test_struct_sizes_and_abi():
     lib = L.load()
     assert lib.tpe_abi_version() == L.ABI_VERSION == 4
-    sizes = (ctypes.c_int32 * 5)()
-    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 5) == 5
+    sizes = (ctypes.c_int32 * 6)()
+    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 6) == 6
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
-                            L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize, L.TABLE_DTYPE.itemsize)
+                            L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize, L.TABLE_DTYPE.itemsize,
+                            L.GATHER_DTYPE.itemsize)
 
 
 def test_argument_errors_are_reported():
@@ -73,5 +74,13 @@ def test_argument_errors_are_reported():
     rc = lib.tpe_table_build(None, hp_, 1, *([None] * 11))
     assert rc == -1 and b"not an unquantized" in lib.tpe_last_error()
     assert lib.tpe_best_combine(None, 0, 1, None, None) == -1
+    g = np.zeros(1, L.GATHER_DTYPE)
+    g["to_int"] = 1
+    gp = g.ctypes.data_as(ctypes.c_void_p)
+    one = ctypes.c_void_p(1)
+    rc = lib.tpe_gather_obs(one, one, 10, None, 0, None, one, gp, 1, one, None, None, None)
+    assert rc == -1 and b"output pool" in lib.tpe_last_error()
+    assert lib.tpe_gather_obs(None, None, 10, None, 0, None, None, None, 0, None, None, None,
+                              None) == 0
     with pytest.raises(L.TpeHipError):
         L.check(-1, "probe")

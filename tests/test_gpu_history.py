@@ -1,0 +1,108 @@
+"""HBM-resident history (DeviceHistory + tpe_gather_obs) vs the upload path.
+
+The gathered observation lists must be exactly the ones ap_split_trials
+builds (tpe.py:623-646: active rows of the label, below / above by the
+n_below best losses, tid order), so every result of a history-mode run is
+bit-identical to the same run with the lists packed on the host.
+"""
+import numpy as np
+import pytest
+
+from oracle import tpe_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SPACE = [("u", "uniform", (-5.0, 5.0)), ("lu", "loguniform", (-5.0, 0.0)),
+         ("q", "quniform", (0.0, 20.0, 1.0)), ("n", "normal", (0.0, 2.0)),
+         ("c", "randint", (6,)), ("r", "randint", (3, 11))]
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from hyperopt_amd.engine import Engine
+    return Engine()
+
+
+def _history(T, seed, inactive=0.0):
+    rng = np.random.RandomState(seed)
+    cols = [rng.uniform(-5, 5, T), np.exp(rng.uniform(-5, 0, T)),
+            np.round(rng.uniform(0, 20, T)), rng.normal(0, 2, T),
+            rng.randint(0, 6, T).astype(float), rng.randint(3, 11, T).astype(float)]
+    mat = np.stack(cols, axis=1)
+    active = rng.uniform(size=mat.shape) >= inactive
+    losses = rng.normal(size=T)
+    return mat, active, losses
+
+
+def _works(mat, active, losses, rows, hist=None, n_cand=1 << 14):
+    from hyperopt_amd.engine import LabelWork
+    T = rows.size
+    n_below = min(int(np.ceil(0.25 * np.sqrt(T))), 25)
+    order = np.argsort(losses[rows], kind="stable")
+    isb = np.zeros(T, np.uint8)
+    isb[order[:n_below]] = 1
+    works = []
+    for j, (lab, kind, a) in enumerate(SPACE):
+        act = active[rows, j]
+        v = mat[rows, j]
+        below, above = v[act & (isb == 1)], v[act & (isb == 0)]
+        w = LabelWork(lab, kind, a, below, above, n_cand=n_cand, key=777 + j)
+        if hist is not None:
+            w.obs_above, w.col, w.n_above = None, j, above.size
+        works.append(w)
+    return works, isb
+
+
+@pytest.mark.parametrize("T,inactive,permute", [(40, 0.0, False), (3000, 0.0, False),
+                                                 (2500, 0.3, False), (1500, 0.2, True)])
+def test_history_gather_matches_upload(engine, T, inactive, permute):
+    from hyperopt_amd.engine import DeviceHistory
+    mat, active, losses = _history(T, T, inactive)
+    hist = DeviceHistory(engine, len(SPACE), cap=64)  # grows while appending
+    for a in range(0, T, 700):
+        hist.append(mat[a:a + 700], active[a:a + 700])
+    rows = np.random.RandomState(1).permutation(T) if permute else np.arange(T)
+    up, _ = _works(mat, active, losses, rows)
+    hw, isb = _works(mat, active, losses, rows, hist=hist)
+    kw = dict(rows=rows.astype(np.int32)) if permute else {}
+    for precision in (64, 32):
+        r_up = engine.run(up, precision=precision)
+        r_h = engine.run(hw, precision=precision, history=hist, is_below=isb, **kw)
+        for a, b in zip(r_up, r_h):
+            assert (a.index, a.value, a.score) == (b.index, b.value, b.score), (a, b)
+    post_up = engine.run(up, posteriors=True)
+    post_h = engine.run(hw, posteriors=True, history=hist, is_below=isb, **kw)
+    for a, b in zip(post_up, post_h):
+        for k in a.extra:
+            for x, y in zip(np.atleast_1d(a.extra[k]), np.atleast_1d(b.extra[k])):
+                np.testing.assert_array_equal(x, y)
+
+
+def test_history_posterior_matches_oracle(engine):
+    """The gathered lists feed the same Parzen fit the reference computes."""
+    from hyperopt_amd.engine import DeviceHistory
+    mat, active, losses = _history(2000, 5, 0.1)
+    hist = DeviceHistory(engine, len(SPACE))
+    hist.append(mat, active)
+    rows = np.arange(2000)
+    hw, isb = _works(mat, active, losses, rows, hist=hist)
+    res = engine.run(hw, posteriors=True, history=hist, is_below=isb)
+    j = 3  # normal(0, 2)
+    act = active[:, j]
+    below, above = O.ap_split_trials(np.flatnonzero(act), mat[act, j], rows, losses, 0.25)
+    for half, obs in (("below", below), ("above", above)):
+        ref = O.adaptive_parzen_normal(obs, 1.0, 0.0, 2.0)
+        for got, want in zip(res[j].extra[half], ref):
+            np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
+
+
+def test_history_count_mismatch_raises(engine):
+    from hyperopt_amd import _lib as L
+    from hyperopt_amd.engine import DeviceHistory
+    mat, active, losses = _history(500, 9)
+    hist = DeviceHistory(engine, len(SPACE))
+    hist.append(mat, active)
+    hw, isb = _works(mat, active, losses, np.arange(500), hist=hist)
+    hw[0].n_above -= 3  # the host claims fewer rows than the gather finds
+    with pytest.raises(L.TpeHipError, match="counts"):
+        engine.run(hw, history=hist, is_below=isb)
