@@ -20,10 +20,11 @@ HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main(src, kernel):
     c = json.load(open(src))[kernel]
     fetch = 2.0 * c["FETCH_SIZE"] * 1024.0
-    write = c["WRITE_SIZE"] * 1024.0
+    write = c.get("WRITE_SIZE", 0.0) * 1024.0  # not collected -> 0 (noted in "correction")
     out = {"kernel": kernel, "bytes_per_launch": fetch + write, "fetch_bytes": fetch,
            "write_bytes": write, "source": os.path.relpath(src, HERE),
-           "correction": "FETCH_SIZE x2 (gfx950 half-count), KiB -> B"}
+           "correction": "FETCH_SIZE x2 (gfx950 half-count), KiB -> B"
+                         + ("" if "WRITE_SIZE" in c else "; WRITE_SIZE not collected")}
     if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
         out["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4.0 / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0)
     if "SQ_INSTS_VALU" in c:
