@@ -32,22 +32,40 @@ struct Mix {  // sampler view of the below mixture (LDS or global)
   const double* cdf;
   const double* mu;
   const double* sg;
+  const uint32_t* thr;  // staged: component k takes words < thr[k] (fp32 draws)
+  const float* mu32;
+  const float* sg32;
   int n;
 };
 
-// stage the below mixture for sampling; returns the view (call by all threads)
+struct MixLds {  // LDS image of a below mixture of <= kStage components
+  double cdf[kStage], mu[kStage], sg[kStage];
+  uint32_t thr[kStage];
+  float mu32[kStage], sg32[kStage];
+};
+
+// stage the below mixture for sampling; returns the view (call by all threads).
+// thr[k] = ceil(cdf[k] / cdf[n-1] * 2^32): a 32-bit word w selects the first k
+// with w < thr[k] -- the same component as cdf[k] > w * 2^-32 * cdf[n-1].
 __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, const double* mu,
-                                         const double* sigma, double* s_cdf, double* s_mu,
-                                         double* s_sg) {
+                                         const double* sigma, MixLds& L) {
   const int n = S.n_obs + 1;
-  if (n > kStage) return Mix{wcdf + S.comp_off, mu + S.comp_off, sigma + S.comp_off, n};
+  if (n > kStage)
+    return Mix{wcdf + S.comp_off, mu + S.comp_off, sigma + S.comp_off, nullptr, nullptr,
+               nullptr, n};
+  const double total = wcdf[S.comp_off + n - 1];
   for (int k = threadIdx.x; k < n; k += kBS) {
-    s_cdf[k] = wcdf[S.comp_off + k];
-    s_mu[k] = mu[S.comp_off + k];
-    s_sg[k] = sigma[S.comp_off + k];
+    const double c = wcdf[S.comp_off + k], m = mu[S.comp_off + k], g = sigma[S.comp_off + k];
+    L.cdf[k] = c;
+    L.mu[k] = m;
+    L.sg[k] = g;
+    L.mu32[k] = (float)m;
+    L.sg32[k] = (float)g;
+    const double t = ceil(c / total * 4294967296.0);
+    L.thr[k] = (t >= 4294967295.0) ? 0xFFFFFFFFu : (t > 0.0 ? (uint32_t)t : 0u);
   }
   __syncthreads();
-  return Mix{s_cdf, s_mu, s_sg, n};
+  return Mix{L.cdf, L.mu, L.sg, L.thr, L.mu32, L.sg32, n};
 }
 
 // One draw from the (possibly truncated) below mixture: returns the value in
@@ -75,8 +93,22 @@ __device__ __forceinline__ double draw64(const Mix& M, uint64_t key, int64_t g, 
 // 2m+1's, and (y, z) give the Box-Muller pair (cos -> 2m, sin -> 2m+1).
 // Candidate g's value therefore depends on g alone, whichever kernel draws it.
 __device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
+  if (M.thr) {  // block-uniform: staged mixture, 32-bit integer search
+    int lo = 0, hi = M.n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (word < M.thr[mid]) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+  }
   const double u = (double)word * 0x1.0p-32 * M.cdf[M.n - 1];
   return upper_bound(M.cdf, M.n, u);
+}
+__device__ __forceinline__ float mu32_of(const Mix& M, int j) {
+  return M.mu32 ? M.mu32[j] : (float)M.mu[j];
+}
+__device__ __forceinline__ float sg32_of(const Mix& M, int j) {
+  return M.sg32 ? M.sg32[j] : (float)M.sg[j];
 }
 
 __device__ __forceinline__ void attempt32_pair(const Mix& M, uint64_t key, int64_t m, uint32_t a,
@@ -85,8 +117,8 @@ __device__ __forceinline__ void attempt32_pair(const Mix& M, uint64_t key, int64
   const int j0 = comp_of(M, r.x), j1 = comp_of(M, r.w);
   float z0, z1;
   normal_pair_f32(r.y, r.z, z0, z1);
-  y0 = fmaf((float)M.sg[j0], z0, (float)M.mu[j0]);
-  y1 = fmaf((float)M.sg[j1], z1, (float)M.mu[j1]);
+  y0 = fmaf(sg32_of(M, j0), z0, mu32_of(M, j0));
+  y1 = fmaf(sg32_of(M, j1), z1, mu32_of(M, j1));
 }
 
 // attempt `a` of candidate `g` alone (same value as attempt32_pair's half)
@@ -97,7 +129,7 @@ __device__ __forceinline__ float attempt32(const Mix& M, uint64_t key, int64_t g
   const float u2 = (float)(r.z >> 8) * 0x1.0p-24f;
   const float rr = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
   const float z = rr * ((g & 1) ? __builtin_amdgcn_sinf(u2) : __builtin_amdgcn_cosf(u2));
-  return fmaf((float)M.sg[j], z, (float)M.mu[j]);
+  return fmaf(sg32_of(M, j), z, mu32_of(M, j));
 }
 
 __device__ __forceinline__ bool accept32(float y, bool lo_on, bool hi_on, float lo, float hi) {

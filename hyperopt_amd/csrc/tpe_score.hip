@@ -262,7 +262,7 @@ __global__ __launch_bounds__(kBS) void k_score32(
     const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
     double* __restrict__ out_x, tpe_best* __restrict__ partial) {
   __shared__ float4 tile[kTile32];
-  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ MixLds s_mix;
   __shared__ BestT red[kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kBS) void k_score32(
       x[r] = li < J.n_cand ? (float)cand[J.cand_off + li] : 1.0f;
     }
   } else {
-    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
 #pragma unroll
     for (int r = 0; r < kR32; ++r) {
       const int64_t li = base + r * kBS + threadIdx.x;
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kBS) void k_score64(
     const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
     double* __restrict__ out_x, tpe_best* __restrict__ partial) {
   __shared__ double4 tile[kTile64];
-  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ MixLds s_mix;
   __shared__ BestT red[kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(kBS) void k_score64(
       x[r] = li < J.n_cand ? cand[J.cand_off + li] : 1.0;
     }
   } else {
-    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
 #pragma unroll
     for (int r = 0; r < kR64; ++r) {
       const int64_t li = base + r * kBS + threadIdx.x;
@@ -436,12 +436,12 @@ __global__ __launch_bounds__(kBS) void k_sort_count(
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, uint32_t* __restrict__ counts, float* __restrict__ gen) {
   __shared__ uint32_t h[kNB];
-  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ MixLds s_mix;
   const tpe_job J = jobs[blockIdx.y];
   const int64_t base = (int64_t)blockIdx.x * kSortPer;
   if (base >= J.n_cand) return;
   for (int i = threadIdx.x; i < kNB; i += kBS) h[i] = 0u;
-  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_mix);
   __syncthreads();
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
@@ -771,7 +771,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
     int32_t* __restrict__ err) {
   __shared__ uint32_t lfirst[kLatLds];
-  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ MixLds s_mix;
   __shared__ float s_stage[kLatR * kBS];
   const tpe_job J = jobs[blockIdx.y];
   const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
@@ -782,7 +782,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   const bool local = J.lat_n <= kLatLds;
   if (local)
     for (int s = threadIdx.x; s < J.lat_n; s += kBS) lfirst[s] = 0xFFFFFFFFu;
-  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
   __syncthreads();
   auto mark = [&](double v, int64_t li) {
     const int64_t slot = (int64_t)rint(v / J.q) - J.lat_kmin;  // np.round(x/q) (tpe.py:106)
@@ -970,11 +970,11 @@ __global__ __launch_bounds__(kBS) void k_sample(const tpe_job* __restrict__ jobs
                                                 const double* __restrict__ sigma,
                                                 const double* __restrict__ wcdf,
                                                 double* __restrict__ out_x) {
-  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ MixLds s_mix;
   const tpe_job J = jobs[blockIdx.y];
   const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
   if (base >= J.n_cand) return;
-  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_mix);
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
   for (int r = 0; r < kLatR; ++r) {

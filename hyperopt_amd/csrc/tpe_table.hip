@@ -429,7 +429,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
     const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
     double* __restrict__ out_x, tpe_best* __restrict__ partial,
     unsigned long long* __restrict__ stats) {
-  __shared__ double s_cdf[kStage], s_mu[kStage], s_sg[kStage];
+  __shared__ MixLds s_mix;
   // per wave: 64 rows of kRowF4 float4 (the lane's cell, transposed in from
   // its 8-lane group); also the sampler's staging buffer before scoring
   __shared__ float4 s_rows[(kBS / kWave) * kWave * kRowF4];
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
 #pragma unroll
     for (int r = 0; r < kTR; ++r) x[r] = t0 + r < J.n_cand ? (float)cand[J.cand_off + t0 + r] : 1.0f;
   } else {
-    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_cdf, s_mu, s_sg);
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
     const int nv = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
     draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
                       (float)J.high, lgmm, reinterpret_cast<float*>(s_rows), x);
@@ -462,24 +462,39 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   }
   const float g0 = (float)Tb.origin, inv_w = Tb.inv_w, inv_h = Tb.inv_h;
   const int nb = Tb.nb;
-  const float4* C4 = reinterpret_cast<const float4*>(cells) + J.tbl_off * (kCellF / 4);
+  // the job's cell table: a uniform base + 32-bit byte offsets (saddr loads)
+  const char* cbase = reinterpret_cast<const char*>(cells) + J.tbl_off * (kCellF * 4);
   const int lane = lane_id(), gi = lane & 7, gbase = lane & ~7;
   float4* rows = s_rows + (threadIdx.x / kWave) * (kWave * kRowF4);
-  BestT best{0.0, -1, 0.0};
+  // per-thread argmax in fp32 over the thread's candidates r = 0..kTR-1
+  // (np.argmax rules: larger score, NaN wins, ties -> smaller r)
+  float bs = 0.0f, bx = 0.0f;
+  int br = -1;
   int n_exact = 0;
   uint32_t exact_mask = 0;
-  // outputs + argmax of one scored candidate
-  auto finish = [&](float lb, float la, float y, float xv, int64_t li) {
-    double bl = lb, al = la;
-    if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
-      bl -= (double)y;
-      al -= (double)y;
+  const bool outs = out_bl || out_al || out_x;
+  // outputs + argmax of one scored candidate (the score is unaffected by
+  // lognormal_lpdf's -log(x), tpe.py:214-216, which both sides carry)
+  auto finish = [&](float lb, float la, float y, float xv, int r) {
+    const float sc = lb - la;
+    if (outs) {
+      double bl = lb, al = la;
+      if (lgmm) {
+        bl -= (double)y;
+        al -= (double)y;
+      }
+      const int64_t o = J.out_off + t0 + r;
+      if (out_bl) out_bl[o] = bl;
+      if (out_al) out_al[o] = al;
+      if (out_x) out_x[o] = (double)xv;
     }
-    const int64_t o = J.out_off + li;
-    if (out_bl) out_bl[o] = bl;
-    if (out_al) out_al[o] = al;
-    if (out_x) out_x[o] = (double)xv;
-    best_update(best, bl - al, J.cand_base + li, (double)xv);
+    const bool na = sc != sc, nb_ = bs != bs;
+    const bool take = (br < 0) || (na ? (!nb_ || r < br) : (!nb_ && (sc > bs || (sc == bs && r < br))));
+    if (take) {
+      bs = sc;
+      br = r;
+      bx = xv;
+    }
   };
 #pragma unroll
   for (int r = 0; r < kTR; ++r) {
@@ -498,7 +513,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int cj = __shfl(c, gbase | j, kWave);
-      v[j] = C4[(int64_t)cj * (kCellF / 4) + gi];
+      v[j] = *reinterpret_cast<const float4*>(cbase + (uint32_t)(cj * (kCellF * 4) + gi * 16));
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) rows[(gbase + j) * kRowF4 + gi] = v[j];
@@ -521,7 +536,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       exact_mask |= 1u << r;
       continue;
     }
-    finish(lb, la, y, x[r], li);
+    finish(lb, la, y, x[r], r);
   }
   // exact fp32 log-sum-exp for the (rare) candidates the table does not cover;
   // their values wait in the lane's own LDS row
@@ -537,10 +552,12 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       const float xv = stash[r];
       const float y = lgmm ? __logf(xv) : xv;
       finish(lse_exact32(coef32 + SB.comp_off, SB, y), lse_exact32(coef32 + SA.comp_off, SA, y),
-             y, xv, t0 + r);
+             y, xv, r);
       ++n_exact;
     }
   }
+  BestT best{0.0, -1, 0.0};
+  if (br >= 0) best = BestT{(double)bs, J.cand_base + t0 + br, (double)bx};
   best = block_best<kBS>(best, red);
   if (stats) {
     const int ne = block_sum<kBS, int>(n_exact, nred);
