@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32 = 1, 2, 4, 8, 16
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -41,7 +41,8 @@ JOB_DTYPE = np.dtype([
 TABLE_DTYPE = np.dtype([
     ("lo", "<f8"), ("hi", "<f8"), ("h_below", "<f8"), ("h_above", "<f8"), ("origin", "<f8"),
     ("h", "<f8"), ("inv_h", "<f4"), ("inv_w", "<f4"), ("nb", "<i4"), ("n_wide_below", "<i4"),
-    ("n_wide_above", "<i4"), ("pad", "<i4")], align=True)
+    ("n_wide_above", "<i4"), ("pad", "<i4"), ("T_below", "<f8"), ("T_above", "<f8")],
+    align=True)
 GATHER_DTYPE = np.dtype([
     ("col", "<i4"), ("below", "<i4"), ("dst_off", "<i8"), ("offset", "<i8"), ("count", "<i8"),
     ("to_int", "<i4"), ("pad", "<i4")], align=True)
@@ -68,7 +69,8 @@ _SIGNATURES = {
     "tpe_cat_posterior": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "tpe_gather_obs": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _P, _P, _P, _P]),
     "tpe_table_partials": (_I64, [_P, _I]),
-    "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_table_scratch_bytes": (_I64, [_I, _I]),
+    "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_table": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
                              _P, _P, _P]),
     "tpe_score_partials": (_I64, [_P, _I]),

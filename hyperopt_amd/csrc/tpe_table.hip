@@ -23,8 +23,10 @@
 // worst relative error of one component's truncated series.  By the Cauchy
 // estimate on |u| = 8, for |u| <= 1 that is
 //     exp(9|A| + 65|B|) * 8^-11 / 7  <=  5.5e-9   when 9|A| + 65|B| <= 5.8.
-// Components whose largest term on the cell is below exp(-25)/M of the
-// cell's smallest lower bound on S are left out (together < 1.4e-11 of S).
+// Components whose largest term anywhere in the candidate range is below
+// exp(-25)/M of the prior component's smallest term there (a lower bound of S
+// everywhere) are left out (together < 1.4e-11 of S); the rest are found per
+// cell through reach windows over the sorted means.
 // The plan step chooses h so that every component that can be included in
 // any cell satisfies the bound; if the cell budget (job.tbl_cap) forces a
 // larger h, failing cells are flagged and their candidates take the exact
@@ -93,29 +95,27 @@ __device__ __forceinline__ int block_scan_sum(int v, int* sh) {
 
 // ---------------------------------------------------------------------------
 // plan: coordinate range, admissible half-width, reach windows, wide list.
-// grid (2, n_jobs): blockIdx.x = 0 below mixture, 1 above mixture.
+// Two launches over (component tiles, 2 * n_jobs) -- y = 2*job + half, half 0
+// the below mixture, 1 the above: P1 does every component's reach / bound and
+// the tile-local scans, P2 applies the other tiles' carries.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBS) void k_table_reach(
-    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
-    const double* __restrict__ mu, const double* __restrict__ sigma,
-    const double* __restrict__ coef64, double* __restrict__ reach_hi,
-    double* __restrict__ reach_lo, int32_t* __restrict__ wide_idx, tpe_table* __restrict__ tables) {
-  __shared__ double red[kBS / kWave];
-  __shared__ int red_n[kBS / kWave];
-  __shared__ double scan_d[kBS / kWave];
-  __shared__ int scan_n[kBS / kWave];
-  const tpe_job J = jobs[blockIdx.y];
-  const tpe_seg SB = segs[J.below];
-  const tpe_seg S = segs[blockIdx.x ? J.above : J.below];
-  tpe_table* Tb = tables + blockIdx.y;
+constexpr int kPlanStride = 4;  // per tile: {max reach_hi, min reach_lo, #wide, min h}
 
-  // 1) range of the scoring coordinate: where the below sampler can put a
-  //    candidate (mu +- 5.8 sigma per component), clipped to the bounds
-  double a = INFINITY, b = -INFINITY;
+// range of the scoring coordinate (where the below sampler can put a
+// candidate: mu +- 5.8 sigma per component, clipped to the bounds) and the
+// global lower bound T of a term that can matter (the prior's smallest term
+// over the range, minus log(M) + kTauExtra); identical in every block
+__device__ __forceinline__ void plan_range(const tpe_job& J, const tpe_seg& SB, const tpe_seg& S,
+                                           const double* __restrict__ mu,
+                                           const double* __restrict__ sigma,
+                                           const double* __restrict__ coef64, double* red,
+                                           double& a, double& b, double& T) {
+  a = INFINITY;
+  b = -INFINITY;
   for (int k = threadIdx.x; k < SB.n_obs + 1; k += kBS) {
-    const double m = mu[SB.comp_off + k], s = sigma[SB.comp_off + k];
-    a = fmin(a, m - kDrawZ * s);
-    b = fmax(b, m + kDrawZ * s);
+    const double m = mu[SB.comp_off + k], sg = sigma[SB.comp_off + k];
+    a = fmin(a, m - kDrawZ * sg);
+    b = fmax(b, m + kDrawZ * sg);
   }
   a = -block_max<kBS, double>(-a, red);
   b = block_max<kBS, double>(b, red);
@@ -130,70 +130,123 @@ __global__ __launch_bounds__(kBS) void k_table_reach(
     const double c = isfinite(a) ? a : (isfinite(b) ? b : SB.prior_mu);
     a = b = c;
   }
-
-  // 2) global lower bound of log S over [a, b]: the prior component's smallest term
-  const int nc = S.n_obs + 1;
-  const int64_t off = S.comp_off;
-  const int pos = S.prior_pos;
-  const double ps = S.prior_sigma;
-  const double4 cp = ld4(coef64, off + pos);
+  const double4 cp = ld4(coef64, S.comp_off + S.prior_pos);
   const double far = fmax(fabs(a - cp.x), fabs(b - cp.x)) * cp.y;
-  const double T = cp.z - 0.5 * far * far - (log((double)nc) + kTauExtra);
+  T = cp.z - 0.5 * far * far - (log((double)(S.n_obs + 1)) + kTauExtra);
+}
 
-  // 3) per component: largest normalised distance at which it can matter,
-  //    admissible half-width and reach interval [mu - r, mu + r]; wide
-  //    components (the prior, sigma >= prior_sigma/4) are listed apart.
-  //    Coalesced 256-element tiles: prefix max of mu + r and the wide list
-  //    front to back, suffix min of mu - r back to front.
-  const int tid = threadIdx.x;
-  double hmin = INFINITY, carry_hi = -INFINITY;
-  int carry_n = 0;
-  for (int t0 = 0; t0 < nc; t0 += kBS) {
-    const int k = t0 + tid;
-    double hr = -INFINITY;
-    int wide = 0;
-    if (k < nc) {
-      const double4 c = ld4(coef64, off + k);
-      const double d = c.z - T;
-      const double z = d > 0.0 ? sqrt(2.0 * d) : 0.0;
-      if (d > 0.0) hmin = fmin(hmin, admissible_s(z) / c.y);
-      wide = (k == pos) || (sigma[off + k] >= 0.25 * ps);
-      if (!wide) hr = c.x + z / c.y * (1.0 + 1e-9) + 1e-12 * fabs(c.x);
-    }
-    hr = fmax(block_scan_max(hr, scan_d), carry_hi);
-    const int incl = block_scan_sum(wide, scan_n) + carry_n;
-    if (k < nc) {
-      reach_hi[off + k] = hr;
-      if (wide) wide_idx[off + incl - 1] = k;
-    }
-    carry_hi = block_max<kBS, double>(hr, red);  // the tile's last (largest) prefix
-    carry_n = block_max<kBS, int>(incl, red_n);
-  }
-  hmin = -block_max<kBS, double>(-hmin, red);
-  double carry_lo = INFINITY;
-  for (int t1 = nc - 1; t1 >= 0; t1 -= kBS) {
-    const int k = t1 - tid;
-    double lr = INFINITY;
-    if (k >= 0) {
-      const double4 c = ld4(coef64, off + k);
-      const double d = c.z - T;
-      const double z = d > 0.0 ? sqrt(2.0 * d) : 0.0;
-      const bool wide = (k == pos) || (sigma[off + k] >= 0.25 * ps);
-      if (!wide) lr = c.x - z / c.y * (1.0 + 1e-9) - 1e-12 * fabs(c.x);
-    }
-    lr = fmin(-block_scan_max(-lr, scan_d), carry_lo);
-    if (k >= 0) reach_lo[off + k] = lr;
-    carry_lo = -block_max<kBS, double>(-lr, red);
-  }
-  if (tid == 0) {
+// component k of mixture S: wide flag, reach interval, admissible half-width
+__device__ __forceinline__ void plan_comp(const tpe_seg& S, const double* __restrict__ sigma,
+                                          const double* __restrict__ coef64, double T, int k,
+                                          bool& wide, double& hr, double& lr, double& hk) {
+  const double4 c = ld4(coef64, S.comp_off + k);
+  const double d = c.z - T;
+  const double z = d > 0.0 ? sqrt(2.0 * d) : 0.0;
+  hk = d > 0.0 ? admissible_s(z) / c.y : INFINITY;
+  wide = (k == S.prior_pos) || (sigma[S.comp_off + k] >= 0.25 * S.prior_sigma);
+  const double r = z / c.y * (1.0 + 1e-9) + 1e-12 * fabs(c.x);
+  hr = wide ? -INFINITY : c.x + r;
+  lr = wide ? INFINITY : c.x - r;
+}
+
+__global__ __launch_bounds__(kBS) void k_table_plan1(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ coef64, double* __restrict__ reach_hi,
+    double* __restrict__ reach_lo, double* __restrict__ part, tpe_table* __restrict__ tables) {
+  __shared__ double red[kBS / kWave];
+  __shared__ double scan_d[kBS / kWave];
+  const int job = blockIdx.y >> 1, half = blockIdx.y & 1;
+  const tpe_job J = jobs[job];
+  const tpe_seg SB = segs[J.below];
+  const tpe_seg S = segs[half ? J.above : J.below];
+  const int nc = S.n_obs + 1;
+  if ((int)blockIdx.x * kBS >= nc) return;  // block-uniform
+  double a, b, T;
+  plan_range(J, SB, S, mu, sigma, coef64, red, a, b, T);
+  const int k = blockIdx.x * kBS + threadIdx.x;
+  bool wide = true;
+  double hr = -INFINITY, lr = INFINITY, hk = INFINITY;
+  if (k < nc) plan_comp(S, sigma, coef64, T, k, wide, hr, lr, hk);
+  hr = block_scan_max(hr, scan_d);  // tile-local prefix max
+  if (k < nc) reach_hi[S.comp_off + k] = hr;
+  // tile-local suffix min: thread t handles element tile_end - t
+  const int tend = min(nc, (int)(blockIdx.x + 1) * kBS) - 1;
+  const int kr = tend - (int)threadIdx.x;
+  bool wr;
+  double hr2, lr2 = INFINITY, hk2;
+  if (kr >= (int)blockIdx.x * kBS) plan_comp(S, sigma, coef64, T, kr, wr, hr2, lr2, hk2);
+  lr2 = -block_scan_max(-lr2, scan_d);
+  if (kr >= (int)blockIdx.x * kBS) reach_lo[S.comp_off + kr] = lr2;
+  const double tmax = block_max<kBS, double>(hr, red);
+  const double tmin = -block_max<kBS, double>(-lr2, red);
+  const double nw = block_sum<kBS, double>((k < nc && wide) ? 1.0 : 0.0, red);
+  const double hmin = -block_max<kBS, double>(-hk, red);
+  if (threadIdx.x == 0) {
+    double* P = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kPlanStride;
+    P[0] = tmax;
+    P[1] = tmin;
+    P[2] = nw;
+    P[3] = hmin;
     if (blockIdx.x == 0) {
-      Tb->lo = a;
-      Tb->hi = b;
-      Tb->h_below = hmin;
-      Tb->n_wide_below = carry_n;
+      if (half == 0) {
+        tables[job].lo = a;
+        tables[job].hi = b;
+        tables[job].T_below = T;
+      } else {
+        tables[job].T_above = T;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_table_plan2(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ coef64, double* __restrict__ reach_hi,
+    double* __restrict__ reach_lo, int32_t* __restrict__ wide_idx,
+    const double* __restrict__ part, tpe_table* __restrict__ tables) {
+  __shared__ double red[kBS / kWave];
+  __shared__ int scan_n[kBS / kWave];
+  const int job = blockIdx.y >> 1, half = blockIdx.y & 1;
+  const tpe_job J = jobs[job];
+  const tpe_seg S = segs[half ? J.above : J.below];
+  const int nc = S.n_obs + 1;
+  const int tiles = (nc + kBS - 1) / kBS;
+  const int t = blockIdx.x;
+  if (t >= tiles) return;  // block-uniform
+  const double* P = part + (int64_t)blockIdx.y * gridDim.x * kPlanStride;
+  double chi = -INFINITY, clo = INFINITY, woff = 0.0, hmin = INFINITY, nw = 0.0;
+  for (int q = threadIdx.x; q < tiles; q += kBS) {
+    if (q < t) {
+      chi = fmax(chi, P[q * kPlanStride]);
+      woff += P[q * kPlanStride + 2];
+    }
+    if (q > t) clo = fmin(clo, P[q * kPlanStride + 1]);
+    hmin = fmin(hmin, P[q * kPlanStride + 3]);
+    nw += P[q * kPlanStride + 2];
+  }
+  chi = block_max<kBS, double>(chi, red);
+  clo = -block_max<kBS, double>(-clo, red);
+  const int wbase = (int)block_sum<kBS, double>(woff, red);
+  hmin = -block_max<kBS, double>(-hmin, red);
+  const int ntot = (int)block_sum<kBS, double>(nw, red);
+  const int k = t * kBS + threadIdx.x;
+  bool wide = false;
+  if (k < nc) {
+    reach_hi[S.comp_off + k] = fmax(reach_hi[S.comp_off + k], chi);
+    reach_lo[S.comp_off + k] = fmin(reach_lo[S.comp_off + k], clo);
+    wide = (k == S.prior_pos) || (sigma[S.comp_off + k] >= 0.25 * S.prior_sigma);
+  }
+  const int incl = block_scan_sum(wide ? 1 : 0, scan_n);
+  if (wide) wide_idx[S.comp_off + wbase + incl - 1] = k;
+  if (t == 0 && threadIdx.x == 0) {
+    if (half == 0) {
+      tables[job].h_below = hmin;
+      tables[job].n_wide_below = ntot;
     } else {
-      Tb->h_above = hmin;
-      Tb->n_wide_above = carry_n;
+      tables[job].h_above = hmin;
+      tables[job].n_wide_above = ntot;
     }
   }
 }
@@ -263,14 +316,14 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
                                           const double* __restrict__ reach_hi,
                                           const double* __restrict__ reach_lo,
                                           const int32_t* __restrict__ wide_idx, int n_wide,
-                                          double y0, double h, float* out_p, float* out_m) {
+                                          double T, double y0, double h, float* out_p,
+                                          float* out_m) {
   const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
   const int pos = S.prior_pos;
   const double wide_sig = 0.25 * S.prior_sigma;
-  const double a = y0 - h, b = y0 + h;
-  const int k_lo = first_ge(reach_hi + off, nc, a);
-  const int k_hi = last_le(reach_lo + off, nc, b);
+  const int k_lo = first_ge(reach_hi + off, nc, y0 - h);
+  const int k_hi = last_le(reach_lo + off, nc, y0 + h);
   const int nwin = max(0, k_hi - k_lo + 1);
   const int items = nwin + n_wide;
   const int lane = lane_id();
@@ -283,42 +336,37 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     skip = false;
     return wide_idx[off + (it - nwin)];
   };
-  // pass 1: value at the centre (scale) and a lower bound of log S on the cell
-  double m0 = -INFINITY, lb = -INFINITY;
-  for (int it = lane; it < items; it += kWave) {
-    bool skip;
-    const int k = comp(it, skip);
-    if (skip) continue;
-    const double4 c = ld4(coef64, off + k);
-    const double zc = (y0 - c.x) * c.y;
-    const double zf = fmax(fabs(a - c.x), fabs(b - c.x)) * c.y;
-    m0 = fmax(m0, c.z - 0.5 * zc * zc);
-    lb = fmax(lb, c.z - 0.5 * zf * zf);
-  }
-  m0 = wave_max_d(m0);
-  lb = wave_max_d(lb);
-  const double thr = lb - (log((double)nc) + kTauExtra);
-  // pass 2: moments.  The exponent is formed in fp64, the series in fp32
-  // (each lane sums <= items/64 positive terms, then a 64-lane butterfly)
+  // One pass: every component inside the cell's reach window (components the
+  // plan's global bound admits; each satisfies the expansion bound by the
+  // choice of h).  The exponent is formed in fp64, the series in fp32; each
+  // lane keeps its own scale m_l (raised only when a term would exceed
+  // e^8 of it) and the lanes are merged at the end.
   float P[kP];
 #pragma unroll
   for (int n = 0; n < kP; ++n) P[n] = 0.0f;
+  double ml = -INFINITY;
   bool bad = false;
   for (int it = lane; it < items; it += kWave) {
     bool skip;
     const int k = comp(it, skip);
     if (skip) continue;
     const double4 c = ld4(coef64, off + k);
-    const double dn = (c.x < a) ? (a - c.x) : ((c.x > b) ? (c.x - b) : 0.0);
-    const double zn = dn * c.y;
-    if (c.z - 0.5 * zn * zn < thr) continue;
     const double dy = y0 - c.x;
+    const double zn = fmax(fabs(dy) - h, 0.0) * c.y;
+    if (c.z - 0.5 * zn * zn < T) continue;  // below the plan's floor on the whole cell
+    const double zc = dy * c.y;
+    const double v = c.z - 0.5 * zc * zc;
+    if (v > ml + 8.0) {  // new scale: rescale this lane's partial sums
+      const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - v));
+#pragma unroll
+      for (int n = 0; n < kP; ++n) P[n] *= r;
+      ml = v;
+    }
     const double hi2 = h * c.y * c.y;
     const double A = -dy * hi2;
     const double B = -0.5 * h * hi2;
     bad = bad || (9.0 * fabs(A) + 65.0 * fabs(B) > kRhoLim);
-    const double zc = dy * c.y;
-    const float e = __expf((float)(c.z - 0.5 * zc * zc - m0));
+    const float e = __expf((float)(v - ml));
     const float Af = (float)A, B2 = (float)(2.0 * B);
     float cm = 0.0f, cc = e;  // e * c_n
     P[0] += e;
@@ -329,6 +377,12 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
       cm = cc;
       cc = cn;
     }
+  }
+  const double m0 = wave_max_d(ml);
+  {
+    const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - m0));
+#pragma unroll
+    for (int n = 0; n < kP; ++n) P[n] *= r;
   }
 #pragma unroll
   for (int n = 0; n < kP; ++n) P[n] = wave_sum_f(P[n]);
@@ -368,9 +422,9 @@ __global__ __launch_bounds__(kBS) void k_table_build(
     const double y0 = (double)(float)(g.origin + (double)(2 * c + 1) * g.h);
     float* out = cells + (J.tbl_off + c) * kCellF;
     const bool bb = build_mix(SB, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below,
-                              y0, g.h, out, out + 24);
+                              Tb.T_below, y0, g.h, out, out + 24);
     const bool ba = build_mix(SA, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above,
-                              y0, g.h, out + kP, out + 25);
+                              Tb.T_above, y0, g.h, out + kP, out + 25);
     if (lane_id() == 0) {
       const int flags = (bb ? 1 : 0) | (ba ? 2 : 0);
       out[26] = (float)y0;
@@ -610,22 +664,35 @@ bool check_table_jobs(const char* fn, const tpe_job* hj, int n, bool* inj) {
 
 using namespace tpe;
 
+extern "C" int64_t tpe_table_scratch_bytes(int n_jobs, int max_comp) {
+  if (n_jobs < 0 || max_comp < 0) return -1;
+  const int64_t tiles = std::max(1, (max_comp + kBS - 1) / kBS);
+  return 8 * (int64_t)kPlanStride * tiles * 2 * std::max(n_jobs, 1);
+}
+
 extern "C" int tpe_table_build(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                                const tpe_seg* segs, const double* mu, const double* sigma,
-                               const double* coef64, double* reach_hi, double* reach_lo,
-                               int32_t* wide_idx, tpe_table* tables, float* cells,
-                               uint64_t* stats, void* stream) {
+                               const double* coef64, int max_comp, double* reach_hi,
+                               double* reach_lo, int32_t* wide_idx, double* scratch,
+                               tpe_table* tables, float* cells, uint64_t* stats, void* stream) {
   bool inj = false;
   if (!check_table_jobs("tpe_table_build", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
   if (n_jobs == 0) return TPE_OK;
   if (!jobs || !segs || !mu || !sigma || !coef64 || !reach_hi || !reach_lo || !wide_idx ||
-      !tables || !cells) {
+      !scratch || !tables || !cells) {
     set_error("tpe_table_build: null pointer");
     return TPE_E_ARG;
   }
+  if (max_comp < 1 || n_jobs > 32767) {
+    set_error("tpe_table_build: max_comp=%d n_jobs=%d", max_comp, n_jobs);
+    return TPE_E_ARG;
+  }
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_table_reach, dim3(2, n_jobs), dim3(kBS), 0, st, jobs, segs, mu, sigma,
-                     coef64, reach_hi, reach_lo, wide_idx, tables);
+  const dim3 pg((max_comp + kBS - 1) / kBS, 2 * n_jobs);
+  hipLaunchKernelGGL(k_table_plan1, pg, dim3(kBS), 0, st, jobs, segs, mu, sigma, coef64, reach_hi,
+                     reach_lo, scratch, tables);
+  hipLaunchKernelGGL(k_table_plan2, pg, dim3(kBS), 0, st, jobs, segs, mu, sigma, coef64, reach_hi,
+                     reach_lo, wide_idx, scratch, tables);
   hipLaunchKernelGGL(k_table_build, dim3(kBuildBlocks, n_jobs), dim3(kBS), 0, st, jobs, segs,
                      sigma, coef64, reach_hi, reach_lo, wide_idx, tables, cells,
                      (unsigned long long*)stats);

@@ -625,9 +625,11 @@ class Engine:
                 d_stats = self._buf("tstats", 16)
                 with torch.cuda.stream(stream):
                     self._bufs["tstats"][:16].zero_()
-                L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64, d_rh, d_rl,
-                                            d_wide, d_tab, d_cells, d_stats, sp),
-                        "tpe_table_build")
+                max_comp = max_obs + 1
+                d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
+                L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64, max_comp,
+                                            d_rh, d_rl, d_wide, d_tsc, d_tab, d_cells, d_stats,
+                                            sp), "tpe_table_build")
                 tock("table_build", e0)
                 e0 = tick()
                 L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32, d_tab,

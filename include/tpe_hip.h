@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 4
+#define TPE_ABI_VERSION 5
 
 enum {
   TPE_OK = 0,
@@ -254,15 +254,20 @@ typedef struct tpe_table {
   int32_t nb;           /* cells used (<= job.tbl_cap)                       */
   int32_t n_wide_below, n_wide_above;
   int32_t pad;
+  double T_below, T_above; /* log-term floor: components whose term stays
+                              below it on a cell are left out               */
 } tpe_table;
 
 /* partial-workspace entries tpe_score_table needs */
 int64_t tpe_table_partials(const tpe_job* host_jobs, int n_jobs);
+/* scratch: tpe_table_scratch_bytes(n_jobs, max_comp) bytes; max_comp = the
+ * largest component count (n_obs + 1) of the jobs' mixtures */
+int64_t tpe_table_scratch_bytes(int n_jobs, int max_comp);
 int tpe_table_build(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                     const tpe_seg* segs, const double* mu, const double* sigma,
-                    const double* coef64, double* reach_hi, double* reach_lo,
-                    int32_t* wide_idx, tpe_table* tables, float* cells, uint64_t* stats,
-                    void* stream);
+                    const double* coef64, int max_comp, double* reach_hi, double* reach_lo,
+                    int32_t* wide_idx, double* scratch, tpe_table* tables, float* cells,
+                    uint64_t* stats, void* stream);
 int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                     const tpe_seg* segs, const double* mu, const double* sigma,
                     const double* wcdf, const float* coef32, const tpe_table* tables,

@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 4
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 5
     sizes = (ctypes.c_int32 * 6)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 6) == 6
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -68,10 +68,11 @@ def test_argument_errors_are_reported():
     rc = lib.tpe_score_table(None, hp_, 1, *([None] * 12), 0, None, None, None)
     assert rc == -1 and b"no cell table" in lib.tpe_last_error()
     jobs["tbl_cap"] = 64
-    rc = lib.tpe_table_build(None, hp_, 1, *([None] * 11))
+    rc = lib.tpe_table_build(None, hp_, 1, None, None, None, None, 8, *([None] * 8))
     assert rc == -1 and b"null pointer" in lib.tpe_last_error()
+    assert lib.tpe_table_scratch_bytes(3, 1000) > 0 and lib.tpe_table_scratch_bytes(-1, 5) == -1
     jobs["flags"] = L.F_QUANT
-    rc = lib.tpe_table_build(None, hp_, 1, *([None] * 11))
+    rc = lib.tpe_table_build(None, hp_, 1, None, None, None, None, 8, *([None] * 8))
     assert rc == -1 and b"not an unquantized" in lib.tpe_last_error()
     assert lib.tpe_best_combine(None, 0, 1, None, None) == -1
     g = np.zeros(1, L.GATHER_DTYPE)
