@@ -15,6 +15,7 @@ constexpr int kBS = 256;       // block size of the candidate kernels
 constexpr int kStage = 64;     // below-mixture components staged in LDS for sampling
 constexpr uint32_t kMaxAttempts = 256;
 constexpr uint32_t kStreamSample = 0x53414D50u;  // "SAMP"
+constexpr int kGuide = 256;    // guide-table buckets (top 8 bits of the word)
 
 __device__ __forceinline__ tpe_best empty_best() { return tpe_best{0.0, -1, 0.0, 0}; }
 
@@ -33,6 +34,7 @@ struct Mix {  // sampler view of the below mixture (LDS or global)
   const double* mu;
   const double* sg;
   const uint32_t* thr;  // staged: component k takes words < thr[k] (fp32 draws)
+  const uint8_t* guide; // staged: first k with thr[k] > b * 2^24 for bucket b
   const float* mu32;
   const float* sg32;
   int n;
@@ -42,17 +44,21 @@ struct MixLds {  // LDS image of a below mixture of <= kStage components
   double cdf[kStage], mu[kStage], sg[kStage];
   uint32_t thr[kStage];
   float mu32[kStage], sg32[kStage];
+  uint8_t guide[kGuide];
 };
 
 // stage the below mixture for sampling; returns the view (call by all threads).
 // thr[k] = ceil(cdf[k] / cdf[n-1] * 2^32): a 32-bit word w selects the first k
 // with w < thr[k] -- the same component as cdf[k] > w * 2^-32 * cdf[n-1].
+// guide[b] (Chen & Asau guide table) is where that search starts for words of
+// bucket b = w >> 24; most buckets hold no threshold, so the walk is one
+// comparison.
 __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, const double* mu,
                                          const double* sigma, MixLds& L) {
   const int n = S.n_obs + 1;
   if (n > kStage)
     return Mix{wcdf + S.comp_off, mu + S.comp_off, sigma + S.comp_off, nullptr, nullptr,
-               nullptr, n};
+               nullptr, nullptr, n};
   const double total = wcdf[S.comp_off + n - 1];
   for (int k = threadIdx.x; k < n; k += kBS) {
     const double c = wcdf[S.comp_off + k], m = mu[S.comp_off + k], g = sigma[S.comp_off + k];
@@ -65,7 +71,17 @@ __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, c
     L.thr[k] = (t >= 4294967295.0) ? 0xFFFFFFFFu : (t > 0.0 ? (uint32_t)t : 0u);
   }
   __syncthreads();
-  return Mix{L.cdf, L.mu, L.sg, L.thr, L.mu32, L.sg32, n};
+  for (int b = threadIdx.x; b < kGuide; b += kBS) {
+    const uint32_t w = (uint32_t)b << 24;
+    int lo = 0, hi = n - 1;  // first k with thr[k] > w (n-1 if none)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (w < L.thr[mid]) hi = mid; else lo = mid + 1;
+    }
+    L.guide[b] = (uint8_t)lo;
+  }
+  __syncthreads();
+  return Mix{L.cdf, L.mu, L.sg, L.thr, L.guide, L.mu32, L.sg32, n};
 }
 
 // One draw from the (possibly truncated) below mixture: returns the value in
@@ -93,13 +109,10 @@ __device__ __forceinline__ double draw64(const Mix& M, uint64_t key, int64_t g, 
 // 2m+1's, and (y, z) give the Box-Muller pair (cos -> 2m, sin -> 2m+1).
 // Candidate g's value therefore depends on g alone, whichever kernel draws it.
 __device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
-  if (M.thr) {  // block-uniform: staged mixture, 32-bit integer search
-    int lo = 0, hi = M.n - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (word < M.thr[mid]) hi = mid; else lo = mid + 1;
-    }
-    return lo;
+  if (M.thr) {  // block-uniform: staged mixture, guide table + 32-bit walk
+    int k = M.guide[word >> 24];
+    while (k < M.n - 1 && word >= M.thr[k]) ++k;
+    return k;
   }
   const double u = (double)word * 0x1.0p-32 * M.cdf[M.n - 1];
   return upper_bound(M.cdf, M.n, u);
@@ -154,7 +167,8 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
 }
 
 // R consecutive candidates g0 .. g0+R-1 per thread (g0 even), n of them
-// valid, each exactly as draw32 draws it.  Every lane walks its own queue of
+// valid, each exactly as draw32 draws it (to_x: LGMM1 values as exp(y), as
+// draw32's callers store them; otherwise the mixture coordinate y).  Every lane walks its own queue of
 // candidate pairs: one Philox call per attempt serves both candidates of a
 // pair, and a rejection costs that lane one more step instead of stalling the
 // whole wave for a full draw.  Results go through `stage` (R*kBS floats of
@@ -162,7 +176,7 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
 template <int R>
 __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t g0, int n,
                                              bool lo_on, bool hi_on, float lo, float hi,
-                                             bool lgmm, float* stage, float (&x)[R]) {
+                                             bool to_x, float* stage, float (&x)[R]) {
   static_assert(R % 2 == 0, "pairs");
   const int tid = threadIdx.x;
   int p = 0;
@@ -180,7 +194,7 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
         const bool ok = accept32(y0, lo_on, hi_on, lo, hi);
         if (ok || last) {
           if (!ok) y0 = clamp32(y0, lo_on, hi_on, lo, hi);
-          stage[(2 * p) * kBS + tid] = lgmm ? __expf(y0) : y0;
+          stage[(2 * p) * kBS + tid] = to_x ? __expf(y0) : y0;
           d0 = true;
         }
       }
@@ -188,7 +202,7 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
         const bool ok = accept32(y1, lo_on, hi_on, lo, hi);
         if (ok || last) {
           if (!ok) y1 = clamp32(y1, lo_on, hi_on, lo, hi);
-          stage[(2 * p + 1) * kBS + tid] = lgmm ? __expf(y1) : y1;
+          stage[(2 * p + 1) * kBS + tid] = to_x ? __expf(y1) : y1;
           d1 = true;
         }
       }

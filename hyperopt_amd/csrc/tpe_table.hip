@@ -34,10 +34,12 @@
 // (injected values, rounding at the edges) take the exact path too.
 //
 // Layout.  One tpe_table per job plus 32 floats per cell:
-//     [0,12) below P_n   [12,24) above P_n   [24] m_below  [25] m_above
+//     [2n] below P_n, [2n+1] above P_n (n < 12)   [24] m_below  [25] m_above
 //     [26] y0            [27] flags (bit 0 below, bit 1 above failed)
-// 128 B = one cache line per cell, gathered once per candidate.
+// 128 B = one cache line per cell, gathered once per candidate; the pairs
+// (below P_n, above P_n) sit in adjacent registers for packed-FP32 Horner.
 #include <algorithm>
+#include <type_traits>
 
 #include "tpe_common.hpp"
 #include "tpe_sample.hpp"
@@ -50,8 +52,15 @@ constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
 constexpr double kTauExtra = 25.0;   // exclusion margin (nats) on top of log(M)
 constexpr double kDrawZ = 5.8;       // |z| of an fp32 Box-Muller draw is < 5.77
 constexpr float kULim = 1.05f;       // |u| accepted by the scorer (fp32 cell-centre rounding)
-constexpr int kTR = 8;               // candidates per thread in the scorer
-constexpr int kRowF4 = 9;            // LDS row stride (float4) of the gather transpose
+#ifndef TPE_TR
+#define TPE_TR 16
+#endif
+constexpr int kTR = TPE_TR;          // candidates per thread and tile in the scorer
+#ifndef TPE_TILES
+#define TPE_TILES 1
+#endif
+constexpr int kTiles = TPE_TILES;    // tiles (kBS * kTR candidates) per scorer block
+constexpr int64_t kTile = (int64_t)kBS * kTR;
 constexpr int kBuildBlocks = 512;    // build blocks per job (grid-stride over cells)
 constexpr float kLn2T = 0.6931471805599453f;
 
@@ -392,7 +401,7 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
 #pragma unroll
     for (int n = 1; n < kP; ++n)
       if (lane == n) v = P[n];
-    out_p[lane] = v;
+    out_p[2 * lane] = v;
   }
   if (lane == 0) *out_m = (float)m0;
   return bad;
@@ -424,7 +433,7 @@ __global__ __launch_bounds__(kBS) void k_table_build(
     const bool bb = build_mix(SB, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below,
                               Tb.T_below, y0, g.h, out, out + 24);
     const bool ba = build_mix(SA, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above,
-                              Tb.T_above, y0, g.h, out + kP, out + 25);
+                              Tb.T_above, y0, g.h, out + 1, out + 25);
     if (lane_id() == 0) {
       const int flags = (bb ? 1 : 0) | (ba ? 2 : 0);
       out[26] = (float)y0;
@@ -437,21 +446,30 @@ __global__ __launch_bounds__(kBS) void k_table_build(
 // ---------------------------------------------------------------------------
 // scoring
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float horner12(const float4 p0, const float4 p1, const float4 p2,
-                                          float u) {
-  float r = p2.w;
-  r = fmaf(r, u, p2.z);
-  r = fmaf(r, u, p2.y);
-  r = fmaf(r, u, p2.x);
-  r = fmaf(r, u, p1.w);
-  r = fmaf(r, u, p1.z);
-  r = fmaf(r, u, p1.y);
-  r = fmaf(r, u, p1.x);
-  r = fmaf(r, u, p0.w);
-  r = fmaf(r, u, p0.z);
-  r = fmaf(r, u, p0.y);
-  r = fmaf(r, u, p0.x);
-  return r;
+typedef float f4 __attribute__((ext_vector_type(4)));  // native vector (no memcpy copies)
+
+// f(integral_constant<int, R>) for R = B .. E-1, unrolled at compile time
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// both mixtures' degree-11 polynomials at u; q[k] = (b_2k, a_2k, b_2k+1, a_2k+1)
+// so every step is one packed FMA (v_pk_fma_f32) on adjacent registers
+__device__ __forceinline__ void horner12x2(const f4 q0, const f4 q1, const f4 q2,
+                                           const f4 q3, const f4 q4, const f4 q5,
+                                           float u, float& pb, float& pa) {
+  float b = q5.z, a = q5.w;
+#define TPE_H2(cb, ca) b = fmaf(b, u, cb); a = fmaf(a, u, ca);
+  TPE_H2(q5.x, q5.y) TPE_H2(q4.z, q4.w) TPE_H2(q4.x, q4.y) TPE_H2(q3.z, q3.w)
+  TPE_H2(q3.x, q3.y) TPE_H2(q2.z, q2.w) TPE_H2(q2.x, q2.y) TPE_H2(q1.z, q1.w)
+  TPE_H2(q1.x, q1.y) TPE_H2(q0.z, q0.w) TPE_H2(q0.x, q0.y)
+#undef TPE_H2
+  pb = b;
+  pa = a;
 }
 
 // exact fp32 log-sum-exp over every component (natural log), the dense
@@ -484,16 +502,16 @@ __global__ __launch_bounds__(kBS) void k_score_table(
     double* __restrict__ out_x, tpe_best* __restrict__ partial,
     unsigned long long* __restrict__ stats) {
   __shared__ MixLds s_mix;
-  // per wave: 64 rows of kRowF4 float4 (the lane's cell, transposed in from
-  // its 8-lane group); also the sampler's staging buffer before scoring
-  __shared__ float4 s_rows[(kBS / kWave) * kWave * kRowF4];
+  // per wave: 8 DMA slabs of 64 x 16 B, the gather's LDS image; also the
+  // sampler's staging buffer before scoring
+  __shared__ float4 s_rows[(kBS / kWave) * kWave * 8];
   __shared__ BestT red[kBS / kWave];
   __shared__ int nred[kBS / kWave];
   static_assert(sizeof(s_rows) >= kTR * kBS * sizeof(float), "staging alias");
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * (kBS * kTR);
-  if (base >= J.n_cand) {
+  const int64_t base0 = (int64_t)blockIdx.x * kTiles * kTile;
+  if (base0 >= J.n_cand) {
     if (threadIdx.x == 0) *P = empty_best();
     return;
   }
@@ -501,118 +519,165 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   const tpe_table Tb = tables[blockIdx.y];
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
-  // each thread owns kTR consecutive candidates (pairs share a Philox call)
-  const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
-  float x[kTR];
-  if (INJ) {
-#pragma unroll
-    for (int r = 0; r < kTR; ++r) x[r] = t0 + r < J.n_cand ? (float)cand[J.cand_off + t0 + r] : 1.0f;
-  } else {
-    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
-    const int nv = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
-    draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                      (float)J.high, lgmm, reinterpret_cast<float*>(s_rows), x);
-    __syncthreads();  // every wave has read its staged draws back
-  }
+  const bool log_in = INJ && lgmm, exp_out = !INJ && lgmm;
   const float g0 = (float)Tb.origin, inv_w = Tb.inv_w, inv_h = Tb.inv_h;
   const int nb = Tb.nb;
   // the job's cell table: a uniform base + 32-bit byte offsets (saddr loads)
   const char* cbase = reinterpret_cast<const char*>(cells) + J.tbl_off * (kCellF * 4);
   const int lane = lane_id(), gi = lane & 7, gbase = lane & ~7;
-  float4* rows = s_rows + (threadIdx.x / kWave) * (kWave * kRowF4);
-  // per-thread argmax in fp32 over the thread's candidates r = 0..kTR-1
-  // (np.argmax rules: larger score, NaN wins, ties -> smaller r)
-  float bs = 0.0f, bx = 0.0f;
-  int br = -1;
-  int n_exact = 0;
-  uint32_t exact_mask = 0;
+  float4* rows = s_rows + (threadIdx.x / kWave) * (kWave * 8);
   const bool outs = out_bl || out_al || out_x;
-  // outputs + argmax of one scored candidate (the score is unaffected by
-  // lognormal_lpdf's -log(x), tpe.py:214-216, which both sides carry)
-  auto finish = [&](float lb, float la, float y, float xv, int r) {
-    const float sc = lb - la;
-    if (outs) {
+  Mix M{};
+#ifndef TPE_DIAG_SKIP_SAMPLE
+  if (!INJ) M = stage_mix(SB, wcdf, mu, sigma, s_mix);  // once per block
+#endif
+  BestT run{0.0, -1, 0.0};
+  int n_exact = 0;
+  // the block's tiles in index order; a thread owns kTR consecutive candidates
+  // of each (pairs share a Philox call)
+  for (int tile = 0; tile < kTiles; ++tile) {
+    const int64_t base = base0 + tile * kTile;
+    if (base >= J.n_cand) break;
+    if (tile > 0) __syncthreads();  // the previous tile's slabs / stash are done
+    const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
+    // x[r]: the candidate in the scoring coordinate y for sampled jobs (log x for
+    // LGMM1; the value exp(y) is formed only for outputs and the winner), the
+    // given value for injected ones
+    float x[kTR];
+    if (INJ) {
+#pragma unroll
+      for (int r = 0; r < kTR; ++r) x[r] = t0 + r < J.n_cand ? (float)cand[J.cand_off + t0 + r] : 1.0f;
+    } else {
+#ifdef TPE_DIAG_SKIP_SAMPLE  // diagnostic builds only (tools/diag_variants.sh)
+      const float w = 2.0f * (float)Tb.h * (float)Tb.nb;
+#pragma unroll
+      for (int r = 0; r < kTR; ++r)
+        x[r] = (float)Tb.origin + w * __builtin_amdgcn_fractf((float)(t0 + r) * 0.6180339887f);
+#else
+      const int nv = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
+      draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
+                        (float)J.high, false, reinterpret_cast<float*>(s_rows), x);
+      __syncthreads();  // every wave has read its staged draws back
+#endif
+    }
+    // per-thread argmax in fp32 over the thread's candidates r = 0..kTR-1
+    // (np.argmax rules: larger score, NaN wins, ties -> smaller r)
+    float bs = -INFINITY, by = 0.0f;
+    int br = -1;
+    uint32_t exact_mask = 0;
+    auto outputs = [&](float lb, float la, float y, int r) {
       double bl = lb, al = la;
-      if (lgmm) {
+      if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216): in both, not in the score
         bl -= (double)y;
         al -= (double)y;
       }
       const int64_t o = J.out_off + t0 + r;
       if (out_bl) out_bl[o] = bl;
       if (out_al) out_al[o] = al;
-      if (out_x) out_x[o] = (double)xv;
-    }
-    const bool na = sc != sc, nb_ = bs != bs;
-    const bool take = (br < 0) || (na ? (!nb_ || r < br) : (!nb_ && (sc > bs || (sc == bs && r < br))));
-    if (take) {
-      bs = sc;
-      br = r;
-      bx = xv;
-    }
-  };
+      if (out_x) out_x[o] = (double)(exp_out ? __expf(y) : y);
+    };
+    // cell of every candidate of the thread (byte offset in the job's table)
+    float yv[kTR];
+    uint32_t co[kTR];
 #pragma unroll
-  for (int r = 0; r < kTR; ++r) {
-    const int64_t li = t0 + r;
-    const float y = lgmm ? __logf(x[r]) : x[r];
-    const float t = (y - g0) * inv_w;
-    int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
-    c = min(c, nb - 1);
-    // Cooperative gather: lane gi of each 8-lane group fetches 16-B chunk gi
-    // of every group member's cell, so one wave-instruction touches 8 cache
-    // lines instead of 64; rows are then transposed through LDS (row stride
-    // 144 B: conflict-free for these writes and for the row reads below).
-    // (chunk 7 is the cell's unused tail: loading and storing it keeps the
-    // code branch-free and v[] in registers)
-    float4 v[8];
+    for (int r = 0; r < kTR; ++r) {
+      yv[r] = log_in ? __logf(x[r]) : x[r];
+      const float t = (yv[r] - g0) * inv_w;
+      int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
+      co[r] = (uint32_t)min(c, nb - 1) * (kCellF * 4);
+    }
+    // Cooperative gather by LDS-DMA: lane gi of each 8-lane group fetches one
+    // 16-B chunk of every group member's cell (global_load_lds_dwordx4), so a
+    // wave-instruction touches 8 cache lines instead of 64 and the data lands
+    // in LDS without passing through VGPRs.  Slab j holds member j's cells:
+    // lane (g, gi) brings chunk gi^j, so lane (g, j) reads its chunk k from
+    // slab j, slot 8g + (k^j) -- conflict-free ds_read_b128.  Candidate r+1's
+    // DMA is issued as soon as candidate r's chunks are in registers, and runs
+    // under r's polynomial work.
+    typedef __attribute__((address_space(3))) void* lds_vp;
+    typedef const __attribute__((address_space(1))) void* glb_vp;
+    auto fetch = [&](int r) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int cj = __shfl(c, gbase | j, kWave);
-      v[j] = *reinterpret_cast<const float4*>(cbase + (uint32_t)(cj * (kCellF * 4) + gi * 16));
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) rows[(gbase + j) * kRowF4 + gi] = v[j];
-    __builtin_amdgcn_wave_barrier();
-    const float4* q = rows + lane * kRowF4;
-    const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6];
-    __builtin_amdgcn_wave_barrier();
-    if (li >= J.n_cand) continue;
-    const float u = (y - q6.z) * inv_h;
-    float lb, la;
-    bool ok = (__float_as_int(q6.w) == 0) && (fabsf(u) <= kULim);
-    if (ok) {
-      const float pb = horner12(q0, q1, q2, u);
-      const float pa = horner12(q3, q4, q5, u);
-      ok = (pb > 0.0f) && (pa > 0.0f);
-      lb = q6.x + __builtin_amdgcn_logf(pb) * kLn2T;
-      la = q6.y + __builtin_amdgcn_logf(pa) * kLn2T;
-    }
-    if (!ok) {  // off the table: scored exactly after the loop
-      exact_mask |= 1u << r;
-      continue;
-    }
-    finish(lb, la, y, x[r], r);
-  }
-  // exact fp32 log-sum-exp for the (rare) candidates the table does not cover;
-  // their values wait in the lane's own LDS row
-  if (__any(exact_mask != 0)) {
-    float* stash = reinterpret_cast<float*>(rows + lane * kRowF4);
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t cj = __shfl(co[r], gbase | j, kWave);
+        __builtin_amdgcn_global_load_lds((glb_vp)(cbase + (cj + ((gi ^ j) * 16))),
+                                         (lds_vp)(rows + j * kWave), 16, 0, 0);
+      }
+    };
+    const f4* slab = reinterpret_cast<const f4*>(rows) + gi * kWave;
+    auto score = [&](auto rc) __attribute__((always_inline)) {
+      constexpr int r = decltype(rc)::value;
+      const float y = yv[r];
+      const f4 q0 = slab[gbase | gi], q1 = slab[gbase | (1 ^ gi)], q2 = slab[gbase | (2 ^ gi)],
+               q3 = slab[gbase | (3 ^ gi)], q4 = slab[gbase | (4 ^ gi)], q5 = slab[gbase | (5 ^ gi)],
+               q6 = slab[gbase | (6 ^ gi)];
+      // the reads must land before the next candidate's DMA overwrites the slabs
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      if constexpr (r + 1 < kTR) fetch(r + 1);
+      const float u = (y - q6.z) * inv_h;
+      float pb, pa;
+      horner12x2(q0, q1, q2, q3, q4, q5, u, pb, pa);
+      const float lb = q6.x + __builtin_amdgcn_logf(pb) * kLn2T;
+      const float la = q6.y + __builtin_amdgcn_logf(pa) * kLn2T;
+      const bool valid = t0 + r < J.n_cand;
+      const bool ok = (__float_as_int(q6.w) == 0) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f);
+      exact_mask |= (valid && !ok) ? (1u << r) : 0u;
+      if (valid && ok) {
+        if (outs) outputs(lb, la, y, r);
+        // table scores are finite: strict > keeps the first of equal scores
+        const float sc = lb - la;
+        const bool take = sc > bs;
+        bs = take ? sc : bs;
+        by = take ? (INJ ? x[r] : y) : by;
+        br = take ? r : br;
+      }
+    };
+#ifdef TPE_DIAG_SKIP_SCORE  // diagnostic builds only: the sampler alone
 #pragma unroll
     for (int r = 0; r < kTR; ++r)
-      if (exact_mask & (1u << r)) stash[r] = x[r];
-    __builtin_amdgcn_wave_barrier();
-    while (exact_mask) {
-      const int r = __builtin_ctz(exact_mask);
-      exact_mask &= exact_mask - 1;
-      const float xv = stash[r];
-      const float y = lgmm ? __logf(xv) : xv;
-      finish(lse_exact32(coef32 + SB.comp_off, SB, y), lse_exact32(coef32 + SA.comp_off, SA, y),
-             y, xv, r);
-      ++n_exact;
+      if (t0 + r < J.n_cand && yv[r] > bs) {
+        bs = yv[r];
+        by = yv[r];
+        br = r;
+      }
+#else
+    fetch(0);
+    static_for<0, kTR>(score);
+#endif
+    // exact fp32 log-sum-exp for the (rare) candidates the table does not cover;
+    // their values wait in the lane's own LDS row
+    if (__any(exact_mask != 0)) {
+      float* stash = reinterpret_cast<float*>(rows + lane * (kTR / 4));
+#pragma unroll
+      for (int r = 0; r < kTR; ++r)
+        if (exact_mask & (1u << r)) stash[r] = x[r];
+      __builtin_amdgcn_wave_barrier();
+      while (exact_mask) {
+        const int r = __builtin_ctz(exact_mask);
+        exact_mask &= exact_mask - 1;
+        const float xv = stash[r];
+        const float y = log_in ? __logf(xv) : xv;
+        const float lb = lse_exact32(coef32 + SB.comp_off, SB, y);
+        const float la = lse_exact32(coef32 + SA.comp_off, SA, y);
+        if (outs) outputs(lb, la, y, r);
+        const float sc = lb - la;
+        const bool na = sc != sc, nb_ = bs != bs;
+        const bool take =
+            (br < 0) || (na ? (!nb_ || r < br) : (!nb_ && (sc > bs || (sc == bs && r < br))));
+        if (take) {
+          bs = sc;
+          br = r;
+          by = INJ ? xv : y;
+        }
+        ++n_exact;
+      }
     }
-  }
-  BestT best{0.0, -1, 0.0};
-  if (br >= 0) best = BestT{(double)bs, J.cand_base + t0 + br, (double)bx};
-  best = block_best<kBS>(best, red);
+    // the winner's value (by: the given value, or y of a sampled candidate --
+    // exp(y) for LGMM1, the same fp32 exp the other scorers store)
+    const float bx = exp_out ? __expf(by) : by;
+    if (br >= 0) best_update(run, (double)bs, J.cand_base + t0 + br, (double)bx);
+  }  // tiles
+  const BestT best = block_best<kBS>(run, red);
   if (stats) {
     const int ne = block_sum<kBS, int>(n_exact, nred);
     if (threadIdx.x == 0 && ne) atomicAdd(stats, (unsigned long long)ne);
@@ -716,7 +781,7 @@ extern "C" int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, in
   }
   int64_t gx = 1;
   for (int i = 0; i < n_jobs; ++i)
-    gx = std::max(gx, (host_jobs[i].n_cand + kBS * kTR - 1) / (kBS * kTR));
+    gx = std::max(gx, (host_jobs[i].n_cand + kTiles * kTile - 1) / (kTiles * kTile));
   if (gx * n_jobs > n_partial) {
     set_error("tpe_score_table: partial workspace %lld < %lld", (long long)n_partial,
               (long long)(gx * n_jobs));
@@ -739,6 +804,6 @@ extern "C" int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, in
 extern "C" int64_t tpe_table_partials(const tpe_job* host_jobs, int n_jobs) {
   int64_t gx = 1;
   for (int i = 0; i < n_jobs; ++i)
-    gx = std::max(gx, (host_jobs[i].n_cand + kBS * kTR - 1) / (kBS * kTR));
+    gx = std::max(gx, (host_jobs[i].n_cand + kTiles * kTile - 1) / (kTiles * kTile));
   return gx * n_jobs;
 }
