@@ -16,13 +16,17 @@
 // and exp(A u + B u^2) = sum_n c_n u^n with c_0 = 1, c_1 = A,
 // (n+1) c_{n+1} = A c_n + 2B c_{n-1}.  So on the cell
 //     S(y) = exp(m) * sum_{n<kP} P_n u^n,  P_n = sum_j exp(l_j(y0) - m) c_n^(j),
-// a degree-11 polynomial per cell and mixture: the per-candidate work is two
+// a degree-9 polynomial per cell and mixture: the per-candidate work is two
 // Horner evaluations and two logs, independent of the number of components.
 //
 // Error.  Every term is positive, so the relative error of S is at most the
-// worst relative error of one component's truncated series.  By the Cauchy
-// estimate on |u| = 8, for |u| <= 1 that is
-//     exp(9|A| + 65|B|) * 8^-11 / 7  <=  5.5e-9   when 9|A| + 65|B| <= 5.8.
+// worst relative error of one component's truncated series.  |c_n| is at most
+// the coefficient c~_n of exp(|A|u + |B|u^2) (same recurrence, all terms
+// positive), so for |u| <= 1.05 the truncation error is at most
+// e^{a+b} sum_{n>=10} c~_n 1.05^n (a = 1.05|A|, b = 1.05^2|B|); over
+// 9|A| + 65|B| <= 5.8 its maximum is 8.6e-8.  P_0..P_5 are stored in fp32 and
+// P_6..P_9 in fp16 (|P_n| <= e^{a+b} c~_n P_0, P_0 >= 1): the rounding adds at
+// most 1.4e-7 (tools/table_bounds.py evaluates both maxima).
 // Components whose largest term anywhere in the candidate range is below
 // exp(-25)/M of the prior component's smallest term there (a lower bound of S
 // everywhere) are left out (together < 1.4e-11 of S); the rest are found per
@@ -33,11 +37,13 @@
 // fp32 log-sum-exp over all components.  Candidates outside the grid
 // (injected values, rounding at the edges) take the exact path too.
 //
-// Layout.  One tpe_table per job plus 32 floats per cell:
-//     [2n] below P_n, [2n+1] above P_n (n < 12)   [24] m_below  [25] m_above
-//     [26] y0            [27] flags (bit 0 below, bit 1 above failed)
-// 128 B = one cache line per cell, gathered once per candidate; the pairs
-// (below P_n, above P_n) sit in adjacent registers for packed-FP32 Horner.
+// Layout.  One tpe_table per job plus one 128-B line per cell, of which the
+// scorer gathers the first 80 B (five 16-B chunks):
+//     floats [2n], [2n+1]: below / above P_n, n < 6                  chunks 0-2
+//     dword 12 + (n - 6): fp16 {below P_n (low half), above P_n}, n = 6..9   chunk 3
+//     [16] m_below  [17] m_above  [18] y0  [19] flags (bit 0 below, bit 1 above failed)
+// The pairs (below P_n, above P_n) sit in adjacent registers for packed-FP32
+// Horner.
 #include <algorithm>
 #include <type_traits>
 
@@ -46,8 +52,10 @@
 
 namespace tpe {
 namespace {
-constexpr int kP = 12;               // expansion terms per cell and mixture
-constexpr int kCellF = 32;           // floats per cell
+constexpr int kP = 10;               // expansion terms per cell and mixture
+constexpr int kP32 = 6;              // of which stored in fp32 (the rest in fp16)
+constexpr int kCellF = 32;           // floats per cell (line stride)
+constexpr int kChunks = 5;           // 16-B chunks of a cell the scorer reads
 constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
 constexpr double kTauExtra = 25.0;   // exclusion margin (nats) on top of log(M)
 constexpr double kDrawZ = 5.8;       // |z| of an fp32 Box-Muller draw is < 5.77
@@ -303,6 +311,27 @@ __device__ __forceinline__ int last_le(const double* a, int n, double v) {
   return lo - 1;
 }
 
+// first k with a[k] >= v (gt: a[k] > v), a non-decreasing, n if none; every
+// lane of the wave gets it.  64-ary narrowing: one probe load per lane per
+// step, so 10^4 components take 3 dependent loads instead of 14.
+__device__ __forceinline__ int wave_first(const double* a, int n, double v, bool gt) {
+  const int lane = lane_id();
+  int lo = 0, hi = n;  // answer in [lo, hi]
+  while (lo < hi) {
+    const int stride = (hi - lo + kWave - 1) / kWave;
+    const int idx = lo + lane * stride;
+    bool p = true;
+    if (idx < hi) p = gt ? (a[idx] > v) : (a[idx] >= v);
+    const uint64_t m = __ballot(p);
+    const int f = m ? __builtin_ctzll(m) : kWave;
+    if (f == 0) break;  // a[lo] qualifies
+    const int nlo = lo + (f - 1) * stride + 1;
+    hi = min(lo + f * stride, hi);
+    lo = nlo;
+  }
+  return lo;
+}
+
 __device__ __forceinline__ double wave_max_d(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
@@ -325,14 +354,19 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
                                           const double* __restrict__ reach_hi,
                                           const double* __restrict__ reach_lo,
                                           const int32_t* __restrict__ wide_idx, int n_wide,
-                                          double T, double y0, double h, float* out_p,
-                                          float* out_m) {
+                                          double T, double y0, double h, float* cell,
+                                          int mix) {
   const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
   const int pos = S.prior_pos;
   const double wide_sig = 0.25 * S.prior_sigma;
+#ifdef TPE_DIAG_BSEARCH
   const int k_lo = first_ge(reach_hi + off, nc, y0 - h);
   const int k_hi = last_le(reach_lo + off, nc, y0 + h);
+#else
+  const int k_lo = wave_first(reach_hi + off, nc, y0 - h, false);
+  const int k_hi = wave_first(reach_lo + off, nc, y0 + h, true) - 1;
+#endif
   const int nwin = max(0, k_hi - k_lo + 1);
   const int items = nwin + n_wide;
   const int lane = lane_id();
@@ -401,9 +435,12 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
 #pragma unroll
     for (int n = 1; n < kP; ++n)
       if (lane == n) v = P[n];
-    out_p[2 * lane] = v;
+    if (lane < kP32)
+      cell[2 * lane + mix] = v;
+    else
+      reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (lane - kP32) + mix] = (_Float16)v;
   }
-  if (lane == 0) *out_m = (float)m0;
+  if (lane == 0) cell[2 * kP32 + (kP - kP32) + mix] = (float)m0;
   return bad;
 }
 
@@ -431,13 +468,13 @@ __global__ __launch_bounds__(kBS) void k_table_build(
     const double y0 = (double)(float)(g.origin + (double)(2 * c + 1) * g.h);
     float* out = cells + (J.tbl_off + c) * kCellF;
     const bool bb = build_mix(SB, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below,
-                              Tb.T_below, y0, g.h, out, out + 24);
+                              Tb.T_below, y0, g.h, out, 0);
     const bool ba = build_mix(SA, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above,
-                              Tb.T_above, y0, g.h, out + 1, out + 25);
+                              Tb.T_above, y0, g.h, out, 1);
     if (lane_id() == 0) {
       const int flags = (bb ? 1 : 0) | (ba ? 2 : 0);
-      out[26] = (float)y0;
-      out[27] = __int_as_float(flags);
+      out[18] = (float)y0;
+      out[19] = __int_as_float(flags);
       if (flags && stats) atomicAdd(stats + 1, 1ull);
     }
   }
@@ -457,16 +494,26 @@ __device__ __forceinline__ void static_for(F& f) {
   }
 }
 
-// both mixtures' degree-11 polynomials at u; q[k] = (b_2k, a_2k, b_2k+1, a_2k+1)
-// so every step is one packed FMA (v_pk_fma_f32) on adjacent registers
-__device__ __forceinline__ void horner12x2(const f4 q0, const f4 q1, const f4 q2,
-                                           const f4 q3, const f4 q4, const f4 q5,
+__device__ __forceinline__ float half_lo(uint32_t d) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(d & 0xFFFFu));
+}
+__device__ __forceinline__ float half_hi(uint32_t d) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(d >> 16));
+}
+
+// both mixtures' degree-9 polynomials at u: q0..q2 = fp32 pairs
+// (b_2k, a_2k, b_2k+1, a_2k+1), q3 = fp16 pairs {b_n | a_n} for n = 6..9; the
+// fp32 steps are packed FMAs (v_pk_fma_f32) on adjacent registers
+__device__ __forceinline__ void horner10x2(const f4 q0, const f4 q1, const f4 q2, const f4 q3,
                                            float u, float& pb, float& pa) {
-  float b = q5.z, a = q5.w;
+  const uint32_t d6 = __float_as_uint(q3.x), d7 = __float_as_uint(q3.y),
+                 d8 = __float_as_uint(q3.z), d9 = __float_as_uint(q3.w);
+  float b = half_lo(d9), a = half_hi(d9);
 #define TPE_H2(cb, ca) b = fmaf(b, u, cb); a = fmaf(a, u, ca);
-  TPE_H2(q5.x, q5.y) TPE_H2(q4.z, q4.w) TPE_H2(q4.x, q4.y) TPE_H2(q3.z, q3.w)
-  TPE_H2(q3.x, q3.y) TPE_H2(q2.z, q2.w) TPE_H2(q2.x, q2.y) TPE_H2(q1.z, q1.w)
-  TPE_H2(q1.x, q1.y) TPE_H2(q0.z, q0.w) TPE_H2(q0.x, q0.y)
+  TPE_H2(half_lo(d8), half_hi(d8)) TPE_H2(half_lo(d7), half_hi(d7))
+  TPE_H2(half_lo(d6), half_hi(d6))
+  TPE_H2(q2.z, q2.w) TPE_H2(q2.x, q2.y) TPE_H2(q1.z, q1.w) TPE_H2(q1.x, q1.y)
+  TPE_H2(q0.z, q0.w) TPE_H2(q0.x, q0.y)
 #undef TPE_H2
   pb = b;
   pa = a;
@@ -600,27 +647,30 @@ __global__ __launch_bounds__(kBS) void k_score_table(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t cj = __shfl(co[r], gbase | j, kWave);
-        __builtin_amdgcn_global_load_lds((glb_vp)(cbase + (cj + ((gi ^ j) * 16))),
-                                         (lds_vp)(rows + j * kWave), 16, 0, 0);
+        if ((gi ^ j) < kChunks)
+          __builtin_amdgcn_global_load_lds((glb_vp)(cbase + (cj + ((gi ^ j) * 16))),
+                                           (lds_vp)(rows + j * kWave), 16, 0, 0);
       }
     };
     const f4* slab = reinterpret_cast<const f4*>(rows) + gi * kWave;
     auto score = [&](auto rc) __attribute__((always_inline)) {
       constexpr int r = decltype(rc)::value;
       const float y = yv[r];
+      // candidate r's DMA has landed (the compiler does not order LDS-DMA
+      // writes before later ds_reads by itself)
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       const f4 q0 = slab[gbase | gi], q1 = slab[gbase | (1 ^ gi)], q2 = slab[gbase | (2 ^ gi)],
-               q3 = slab[gbase | (3 ^ gi)], q4 = slab[gbase | (4 ^ gi)], q5 = slab[gbase | (5 ^ gi)],
-               q6 = slab[gbase | (6 ^ gi)];
+               q3 = slab[gbase | (3 ^ gi)], q4 = slab[gbase | (4 ^ gi)];
       // the reads must land before the next candidate's DMA overwrites the slabs
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       if constexpr (r + 1 < kTR) fetch(r + 1);
-      const float u = (y - q6.z) * inv_h;
+      const float u = (y - q4.z) * inv_h;
       float pb, pa;
-      horner12x2(q0, q1, q2, q3, q4, q5, u, pb, pa);
-      const float lb = q6.x + __builtin_amdgcn_logf(pb) * kLn2T;
-      const float la = q6.y + __builtin_amdgcn_logf(pa) * kLn2T;
+      horner10x2(q0, q1, q2, q3, u, pb, pa);
+      const float lb = q4.x + __builtin_amdgcn_logf(pb) * kLn2T;
+      const float la = q4.y + __builtin_amdgcn_logf(pa) * kLn2T;
       const bool valid = t0 + r < J.n_cand;
-      const bool ok = (__float_as_int(q6.w) == 0) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f);
+      const bool ok = (__float_as_int(q4.w) == 0) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f);
       exact_mask |= (valid && !ok) ? (1u << r) : 0u;
       if (valid && ok) {
         if (outs) outputs(lb, la, y, r);
