@@ -126,10 +126,24 @@ __device__ __forceinline__ float sg32_of(const Mix& M, int j) {
 
 __device__ __forceinline__ void attempt32_pair(const Mix& M, uint64_t key, int64_t m, uint32_t a,
                                                float& y0, float& y1) {
+#ifdef TPE_DIAG_NO_PHILOX  // diagnostic builds only (tools/diag_variants.sh)
+  const uint32_t hsh = (uint32_t)m * 0x9E3779B9u ^ a * 0x85EBCA6Bu ^ (uint32_t)key;
+  const U4 r{hsh, hsh * 0xC2B2AE35u, hsh ^ 0x27D4EB2Fu, hsh * 0x165667B1u};
+#else
   const U4 r = draw_words(key, m, a, kStreamSample);
+#endif
+#ifdef TPE_DIAG_NO_COMP
+  const int j0 = (int)(r.x & 7), j1 = (int)(r.w & 7);
+#else
   const int j0 = comp_of(M, r.x), j1 = comp_of(M, r.w);
+#endif
   float z0, z1;
+#ifdef TPE_DIAG_NO_BM
+  z0 = (float)(int)r.y * 0x1.0p-31f;
+  z1 = (float)(int)r.z * 0x1.0p-31f;
+#else
   normal_pair_f32(r.y, r.z, z0, z1);
+#endif
   y0 = fmaf(sg32_of(M, j0), z0, mu32_of(M, j0));
   y1 = fmaf(sg32_of(M, j1), z1, mu32_of(M, j1));
 }
@@ -168,55 +182,56 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
 
 // R consecutive candidates g0 .. g0+R-1 per thread (g0 even), n of them
 // valid, each exactly as draw32 draws it (to_x: LGMM1 values as exp(y), as
-// draw32's callers store them; otherwise the mixture coordinate y).  Every lane walks its own queue of
-// candidate pairs: one Philox call per attempt serves both candidates of a
-// pair, and a rejection costs that lane one more step instead of stalling the
-// whole wave for a full draw.  Results go through `stage` (R*kBS floats of
-// LDS; each thread reads back only its own slots).
+// draw32's callers store them; otherwise the mixture coordinate y).
+// Attempt 0 of every pair is drawn unrolled into registers (one Philox call
+// serves both candidates of a pair).  Bounded labels then retry their
+// rejected candidates one at a time, each lane walking its own queue (a
+// rejection costs that lane one more step instead of stalling the wave for a
+// whole draw); the retried values come back through `wstage`, the calling
+// wave's own R*64 floats of LDS (slot r of lane l at r*64 + l).
 template <int R>
 __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t g0, int n,
                                              bool lo_on, bool hi_on, float lo, float hi,
-                                             bool to_x, float* stage, float (&x)[R]) {
-  static_assert(R % 2 == 0, "pairs");
-  const int tid = threadIdx.x;
-  int p = 0;
-  uint32_t att = 0;
-  bool d0 = false, d1 = false;
-  while (true) {
-    const bool act = p < R / 2 && 2 * p < n;
-    if (!__any(act)) break;
-    if (act) {
-      float y0, y1;
-      attempt32_pair(M, key, (g0 >> 1) + p, att, y0, y1);
-      const bool last = att + 1 >= kMaxAttempts;
-      const bool has1 = 2 * p + 1 < n;
-      if (!d0) {
-        const bool ok = accept32(y0, lo_on, hi_on, lo, hi);
-        if (ok || last) {
-          if (!ok) y0 = clamp32(y0, lo_on, hi_on, lo, hi);
-          stage[(2 * p) * kBS + tid] = to_x ? __expf(y0) : y0;
-          d0 = true;
+                                             bool to_x, float* wstage, float (&x)[R]) {
+  static_assert(R % 2 == 0 && R <= 32, "pairs, one mask bit per candidate");
+  uint32_t rej = 0;
+#pragma unroll
+  for (int p = 0; p < R / 2; ++p) {
+    float y0, y1;
+    attempt32_pair(M, key, (g0 >> 1) + p, 0u, y0, y1);
+    x[2 * p] = y0;
+    x[2 * p + 1] = y1;
+    if (!accept32(y0, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p);
+    if (!accept32(y1, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p + 1);
+  }
+  rej &= n >= R ? ~0u : (n <= 0 ? 0u : (1u << n) - 1u);
+  if (__any(rej != 0)) {
+    float* st = wstage + lane_id();
+    uint32_t todo = rej, att = 1;
+    while (__any(todo != 0)) {
+      if (todo) {
+        const int r = __builtin_ctz(todo);
+        float y = attempt32(M, key, g0 + r, att);
+        const bool ok = accept32(y, lo_on, hi_on, lo, hi);
+        if (ok || att + 1 >= kMaxAttempts) {
+          if (!ok) y = clamp32(y, lo_on, hi_on, lo, hi);
+          st[r * kWave] = y;
+          todo &= todo - 1;
+          att = 1;
+        } else {
+          ++att;
         }
-      }
-      if (has1 && !d1) {
-        const bool ok = accept32(y1, lo_on, hi_on, lo, hi);
-        if (ok || last) {
-          if (!ok) y1 = clamp32(y1, lo_on, hi_on, lo, hi);
-          stage[(2 * p + 1) * kBS + tid] = to_x ? __expf(y1) : y1;
-          d1 = true;
-        }
-      }
-      if (d0 && (d1 || !has1)) {
-        ++p;
-        att = 0;
-        d0 = d1 = false;
-      } else {
-        ++att;
       }
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (rej & (1u << r)) x[r] = st[r * kWave];
   }
 #pragma unroll
-  for (int k = 0; k < R; ++k) x[k] = (k < n) ? stage[k * kBS + tid] : 1.0f;
+  for (int r = 0; r < R; ++r) {
+    if (to_x) x[r] = __expf(x[r]);
+    if (r >= n) x[r] = 1.0f;
+  }
 }
 
 }  // namespace

@@ -801,7 +801,8 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
     float x[kLatR];
     draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                        (float)J.high, lgmm, s_stage, x);
+                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
+                        x);
 #pragma unroll
     for (int r = 0; r < kLatR; ++r)
       if (r < nv) mark((double)x[r], t0 + r);

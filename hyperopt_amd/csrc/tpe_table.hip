@@ -554,7 +554,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   __shared__ float4 s_rows[(kBS / kWave) * kWave * 8];
   __shared__ BestT red[kBS / kWave];
   __shared__ int nred[kBS / kWave];
-  static_assert(sizeof(s_rows) >= kTR * kBS * sizeof(float), "staging alias");
+  static_assert(kTR * kWave * sizeof(float) <= kWave * 8 * sizeof(float4), "staging alias");
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t base0 = (int64_t)blockIdx.x * kTiles * kTile;
@@ -603,8 +603,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
 #else
       const int nv = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
       draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                        (float)J.high, false, reinterpret_cast<float*>(s_rows), x);
-      __syncthreads();  // every wave has read its staged draws back
+                        (float)J.high, false, reinterpret_cast<float*>(rows), x);
 #endif
     }
     // per-thread argmax in fp32 over the thread's candidates r = 0..kTR-1

@@ -1,4 +1,6 @@
-"""Host-side profile of bench.py's step (wall split + cProfile of Engine.run)."""
+"""Host-side profile of bench.py's step in history mode (diagnostic): wall time
+of the host parts and a cProfile of the whole step at a tiny candidate count
+(GPU time negligible, so what remains is launch + host work)."""
 import cProfile
 import os
 import pstats
@@ -10,35 +12,45 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from hyperopt_amd.engine import Engine  # noqa: E402
+from hyperopt_amd.engine import DeviceHistory, Engine  # noqa: E402
 
+torch.cuda.set_device(0)
 space = bench.c3_space()
 vals, losses = bench.c3_history(space)
+mat = bench.c3_matrix(space, vals)
 eng = Engine()
-for k in range(3):
-    eng.run(bench.make_works(space, bench.split(vals, losses), k, 1 << 22, 0))
-torch.cuda.synchronize()
-t0 = time.perf_counter()
-for k in range(5):
-    sp = bench.split(vals, losses)
-t1 = time.perf_counter()
-for k in range(5):
-    w = bench.make_works(space, sp, k, 1 << 22, 0)
-t2 = time.perf_counter()
-print("split %.3f ms  make_works %.3f ms" % ((t1 - t0) / 5e-3, (t2 - t1) / 5e-3))
-# launch-side cost: run with tiny candidate counts (GPU time negligible)
+hist = DeviceHistory(eng, len(space), cap=bench.T_HIST)
+hist.append(mat)
+
+
+def prep(k, n):
+    rb = bench.below_rows(losses)
+    isb = np.zeros(bench.T_HIST, np.uint8)
+    isb[rb] = 1
+    return bench.history_works(space, mat, hist, rb, k, n, 0), isb
+
+
+def step(k, n, timers=None):
+    works, isb = prep(k, n)
+    return eng.run(works, history=hist, is_below=isb, timers=timers)
+
+
 for n in (1 << 22, 1 << 10):
-    ws = [bench.make_works(space, sp, k, n, 0) for k in range(5)]
+    for k in range(3):
+        step(k, n)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for w in ws:
-        eng.run(w)
+    for k in range(10):
+        step(k, n)
     t1 = time.perf_counter()
-    print("run n=%d: %.3f ms/step" % (n, (t1 - t0) / 5e-3))
+    print("step n=%d: %.3f ms" % (n, (t1 - t0) / 10e-3))
+t0 = time.perf_counter()
+for k in range(10):
+    prep(k, 1 << 10)
+print("prep (below rows + works): %.3f ms" % ((time.perf_counter() - t0) / 10e-3))
 pr = cProfile.Profile()
-ws = [bench.make_works(space, sp, k, 1 << 10, 0) for k in range(5)]
 pr.enable()
-for w in ws:
-    eng.run(w)
+for k in range(10):
+    step(k, 1 << 10)
 pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+pstats.Stats(pr).sort_stats("tottime").print_stats(30)
