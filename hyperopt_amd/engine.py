@@ -22,6 +22,7 @@ from __future__ import annotations
 import ctypes
 import functools
 import math
+import time
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -213,7 +214,8 @@ class Engine:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
         self._bufs = {}
-        self._pinned = None
+        self._pinned = {}
+        self.host_marks = None  # set to a list to record host-side phase times (diagnostic)
 
     # -- memory --------------------------------------------------------------
     def _buf(self, name, nbytes):
@@ -225,18 +227,24 @@ class Engine:
             self._bufs[name] = t
         return t.data_ptr()
 
-    def _upload(self, pack, stream):
+    def _upload(self, pack, stream, slot=0):
+        """One host->device copy of ``pack`` through pinned buffer / device
+        staging area ``slot`` (a level uploads twice: descriptors for the fit,
+        then the job table, each into its own slot)."""
         torch = self.torch
-        if self._pinned is None or self._pinned.numel() < pack.size:
-            self._pinned = torch.empty(_align(int(pack.size * 1.25) + 1), dtype=torch.uint8,
-                                       pin_memory=True)
-        host = self._pinned.numpy()
+        pinned = self._pinned.get(slot)
+        if pinned is None or pinned.numel() < pack.size:
+            pinned = torch.empty(_align(int(pack.size * 1.25) + 1), dtype=torch.uint8,
+                                 pin_memory=True)
+            self._pinned[slot] = pinned
+        host = pinned.numpy()
         for off, arr in pack.parts:
             host[off:off + arr.nbytes] = arr.reshape(-1).view(np.uint8)
-        dev = self._buf("stage", pack.size)
-        dst = self._bufs["stage"]
+        name = "stage" if slot == 0 else "stage%d" % slot
+        dev = self._buf(name, pack.size)
+        dst = self._bufs[name]
         with torch.cuda.stream(stream):
-            dst[:pack.size].copy_(self._pinned[:pack.size], non_blocking=True)
+            dst[:pack.size].copy_(pinned[:pack.size], non_blocking=True)
         return dev
 
     # -- main entry ----------------------------------------------------------
@@ -270,6 +278,12 @@ class Engine:
         if scorer not in SCORERS:
             raise ValueError("scorer must be one of %s, got %r" % (SCORERS, scorer))
         torch = self.torch
+        hp = self.host_marks  # diagnostic: list of (name, perf_counter) or None
+
+        def _hmark(name):
+            if hp is not None:
+                hp.append((name, time.perf_counter()))
+        _hmark("start")
 
         def tick():
             if timers is None:
@@ -294,6 +308,7 @@ class Engine:
             else:
                 raise ValueError("unsupported prior %r for label %r" % (w.kind, w.label))
 
+        _hmark('prep')
         pack = _Pack()
         hist_mode = history is not None
         gathers = []  # history mode: (col, below, dst_off, offset, count, to_int)
@@ -336,6 +351,7 @@ class Engine:
         if obs_pool is None:
             obs_pool = np.zeros(1)
 
+        _hmark('segs')
         # ---- categorical segments ------------------------------------------
         csegs = np.zeros(2 * len(cat), L.CAT_SEG_DTYPE)
         cobs_parts, p_init = [], []
@@ -369,6 +385,7 @@ class Engine:
         cobs_pool = np.concatenate(cobs_parts) if cobs_parts else np.zeros(1, np.int64)
         p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
 
+        _hmark('cats')
         # ---- jobs, ordered so every kernel call takes a contiguous slice -----------
         inj = lambda i: works[i].cand is not None  # noqa: E731
         lat_ranges = {}
@@ -409,6 +426,92 @@ class Engine:
             ("cat", [i for i in cat if not inj(i)]),
         ]
         order = [i for _, ids in groups for i in ids]
+        _hmark('plan')
+        # ---- upload -------------------------------------------------------------
+        o_segs = pack.add(segs) if segs.size else None
+        o_csegs = pack.add(csegs) if csegs.size else None
+        o_p = pack.add(p_pool)
+        if hist_mode:
+            g_arr = np.zeros(len(gathers), L.GATHER_DTYPE)
+            if gathers:
+                (g_arr["col"], g_arr["below"], g_arr["dst_off"], g_arr["offset"], g_arr["count"],
+                 g_arr["to_int"]) = (np.array(c) for c in zip(*gathers))
+            isb = np.ascontiguousarray(is_below, dtype=np.uint8)
+            n_rows = isb.size
+            o_g = pack.add(g_arr)
+            o_isb = pack.add(isb)
+            o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) if rows is not None \
+                else None
+        else:
+            o_obs = pack.add(obs_pool)
+            o_cobs = pack.add(cobs_pool)
+        base = self._upload(pack, stream)
+        d_segs = base + o_segs if o_segs is not None else None
+        d_csegs = base + o_csegs if o_csegs is not None else None
+        # one result buffer, read back with one copy: [0,16) error bits,
+        # [16,32) table stats, [32,40) sorted-path pair count, [64,...) tpe_best
+        JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
+        n_jobs = len(order)
+        d_res = self._buf("res", 64 + n_jobs * BS)
+        res_t = self._bufs["res"]
+        d_err, d_stats, d_pairs, d_best = d_res, d_res + 16, d_res + 32, d_res + 64
+        with torch.cuda.stream(stream):
+            res_t[:64].zero_()
+        if hist_mode:
+            d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
+            d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
+            e0 = tick()
+            L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
+                                       history.ld, base + o_rows if o_rows is not None else None,
+                                       n_rows, base + o_isb, base + o_g,
+                                       g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr), d_obs,
+                                       d_cobs, d_err, sp), "tpe_gather_obs")
+            tock("gather", e0)
+        else:
+            d_obs, d_cobs = base + o_obs, base + o_cobs
+
+        _hmark('upload+gather')
+        # ---- posterior fit ------------------------------------------------------
+        d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
+        if fit_ids:
+            d_w = self._buf("w", 8 * n_comp)
+            d_mu = self._buf("mu", 8 * n_comp)
+            d_sig = self._buf("sigma", 8 * n_comp)
+            d_cdf = self._buf("wcdf", 8 * n_comp)
+            d_c64 = self._buf("coef64", 32 * n_comp)
+            d_c32 = self._buf("coef32", 16 * n_comp)
+            d_c32n = self._buf("coef32n", 16 * n_comp)
+            d_w32 = self._buf("wide32", 16 * n_comp)
+            d_pm = self._buf("pm", 4 * n_comp)
+            d_sm = self._buf("sm", 4 * n_comp)
+            d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
+                                                                       n_obs_total))
+            prune = any(k == "sorted" and ids for k, ids in groups)
+            if not prune:
+                d_c32n = d_w32 = d_pm = d_sm = None
+            e0 = tick()
+            L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
+                                       n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
+                                       d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
+            tock("fit", e0)
+        if cat:
+            d_logp = self._buf("cat_logp", 8 * p_pool.size)
+            d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
+            e0 = tick()
+            d_p = self._buf("cat_p", 8 * p_pool.size)
+            with torch.cuda.stream(stream):
+                pt = self._bufs["cat_p"]
+                st = self._bufs["stage"]
+                pt[:8 * p_pool.size].copy_(st[o_p:o_p + 8 * p_pool.size])
+            L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
+                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, sp),
+                    "tpe_cat_posterior")
+            tock("cat_fit", e0)
+
+        if posteriors:
+            return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
+                                         d_segs, stream)
+
         nj_all = len(order)
         jobs = np.zeros(nj_all, L.JOB_DTYPE)
         J = {name: np.zeros(nj_all, L.JOB_DTYPE[name]) for name in L.JOB_DTYPE.names}
@@ -477,98 +580,21 @@ class Engine:
         fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
         fb_jobs["out_off"] = fb_jobs["cand_off"]
 
-        # ---- upload -------------------------------------------------------------
-        o_segs = pack.add(segs) if segs.size else None
-        o_csegs = pack.add(csegs) if csegs.size else None
-        o_p = pack.add(p_pool)
-        if hist_mode:
-            g_arr = np.zeros(len(gathers), L.GATHER_DTYPE)
-            if gathers:
-                (g_arr["col"], g_arr["below"], g_arr["dst_off"], g_arr["offset"], g_arr["count"],
-                 g_arr["to_int"]) = (np.array(c) for c in zip(*gathers))
-            isb = np.ascontiguousarray(is_below, dtype=np.uint8)
-            n_rows = isb.size
-            o_g = pack.add(g_arr)
-            o_isb = pack.add(isb)
-            o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) if rows is not None \
-                else None
-        else:
-            o_obs = pack.add(obs_pool)
-            o_cobs = pack.add(cobs_pool)
-        o_jobs = pack.add(jobs) if jobs.size else None
-        o_fb = pack.add(fb_jobs) if fb_jobs.size else None
-        o_cand = pack.add(cand_pool)
-        base = self._upload(pack, stream)
-        d_segs = base + o_segs if o_segs is not None else None
-        d_csegs = base + o_csegs if o_csegs is not None else None
+        _hmark('jobs')
+        # ---- job table upload (the fit above is already running) ----------------
+        pack2 = _Pack()
+        o_jobs = pack2.add(jobs) if jobs.size else None
+        o_fb = pack2.add(fb_jobs) if fb_jobs.size else None
+        o_cand = pack2.add(cand_pool)
+        base = self._upload(pack2, stream, slot=1)
         d_cand = base + o_cand
-        JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
-
-        n_jobs = len(order)
-        d_best = self._buf("best", n_jobs * BS)
-        d_err = self._buf("err", 16)
-        err_t = self._bufs["err"]
-        with torch.cuda.stream(stream):
-            err_t[:16].zero_()
-        if hist_mode:
-            d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
-            d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
-            e0 = tick()
-            L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
-                                       history.ld, base + o_rows if o_rows is not None else None,
-                                       n_rows, base + o_isb, base + o_g,
-                                       g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr), d_obs,
-                                       d_cobs, d_err, sp), "tpe_gather_obs")
-            tock("gather", e0)
-        else:
-            d_obs, d_cobs = base + o_obs, base + o_cobs
         d_bl = d_al = d_x = None
         if outputs:
             d_bl = self._buf("out_bl", 8 * max(out_off, 1))
             d_al = self._buf("out_al", 8 * max(out_off, 1))
             d_x = self._buf("out_x", 8 * max(out_off, 1))
 
-        # ---- posterior fit ------------------------------------------------------
-        d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
-        if fit_ids:
-            d_w = self._buf("w", 8 * n_comp)
-            d_mu = self._buf("mu", 8 * n_comp)
-            d_sig = self._buf("sigma", 8 * n_comp)
-            d_cdf = self._buf("wcdf", 8 * n_comp)
-            d_c64 = self._buf("coef64", 32 * n_comp)
-            d_c32 = self._buf("coef32", 16 * n_comp)
-            d_c32n = self._buf("coef32n", 16 * n_comp)
-            d_w32 = self._buf("wide32", 16 * n_comp)
-            d_pm = self._buf("pm", 4 * n_comp)
-            d_sm = self._buf("sm", 4 * n_comp)
-            d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
-                                                                       n_obs_total))
-            prune = any(k == "sorted" and ids for k, ids in groups)
-            if not prune:
-                d_c32n = d_w32 = d_pm = d_sm = None
-            e0 = tick()
-            L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
-                                       n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
-                                       d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
-            tock("fit", e0)
-        if cat:
-            d_logp = self._buf("cat_logp", 8 * p_pool.size)
-            d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
-            e0 = tick()
-            d_p = self._buf("cat_p", 8 * p_pool.size)
-            with torch.cuda.stream(stream):
-                pt = self._bufs["cat_p"]
-                st = self._bufs["stage"]
-                pt[:8 * p_pool.size].copy_(st[o_p:o_p + 8 * p_pool.size])
-            L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
-                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, sp),
-                    "tpe_cat_posterior")
-            tock("cat_fit", e0)
-
-        if posteriors:
-            return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
-                                         d_segs, stream)
-
+        _hmark('fit')
         # ---- scoring, one call per group ----------------------------------------
         table_calls = []
         for g, (kind, ids) in enumerate(groups):
@@ -602,9 +628,6 @@ class Engine:
                 d_gen = self._buf("sort_gen", 4 * max(sort_off, 1))
                 d_sx = self._buf("sort_x", 4 * max(sort_off, 1))
                 d_si = self._buf("sort_i", 4 * max(sort_off, 1))
-                d_pairs = self._buf("pairs", 16)
-                with torch.cuda.stream(stream):
-                    self._bufs["pairs"][:8].zero_()
                 L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
                                                 d_gen, d_sx, d_si, sp), "tpe_sort_candidates")
                 tock("sort", e0)
@@ -622,9 +645,6 @@ class Engine:
                 d_rh = self._buf("reach_hi", 8 * n_comp)
                 d_rl = self._buf("reach_lo", 8 * n_comp)
                 d_wide = self._buf("wide_idx", 4 * n_comp)
-                d_stats = self._buf("tstats", 16)
-                with torch.cuda.stream(stream):
-                    self._bufs["tstats"][:16].zero_()
                 max_comp = max_obs + 1
                 d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
                 L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64, max_comp,
@@ -672,16 +692,18 @@ class Engine:
                         "tpe_score_categorical")
             tock(kind, e0)
 
+        _hmark('score launches')
         # ---- results (one device->host copy; syncs the stream) --------------------
         with torch.cuda.stream(stream):
-            best_h = self._bufs["best"][:n_jobs * BS].to("cpu").numpy().view(L.BEST_DTYPE)
-            err = int(err_t[:4].to("cpu").view(torch.int32).item())
+            res_h = res_t[:64 + n_jobs * BS].to("cpu").numpy()
+            best_h = res_h[64:].view(L.BEST_DTYPE)
+            err = int(res_h[:4].view(np.int32)[0])
             self.last_pairs = None
             if any(k == "sorted" and ids for k, ids in groups):
-                self.last_pairs = int(self._bufs["pairs"][:8].to("cpu").view(torch.int64).item())
+                self.last_pairs = int(res_h[32:40].view(np.int64)[0])
             self.last_table_stats = None
             if table_calls:
-                st = self._bufs["tstats"][:16].to("cpu").view(torch.int64).tolist()
+                st = res_h[16:32].view(np.int64).tolist()
                 self.last_table_stats = {"exact_candidates": st[0], "failed_cells": st[1]}
             outs = None
             if outputs:
@@ -694,6 +716,7 @@ class Engine:
         if err & 4:
             raise L.TpeHipError("history gather: observation counts do not match the "
                                 "segment sizes given by the host")
+        _hmark('readback')
         results = [None] * len(works)
         for pos, i in enumerate(order):
             b = best_h[pos]
@@ -706,6 +729,7 @@ class Engine:
                 r.above_llik = outs[1][o:o + n].copy()
                 r.cand = outs[2][o:o + n].copy()
             results[i] = r
+        _hmark("results")
         return results
 
 

@@ -54,3 +54,17 @@ for k in range(10):
     step(k, 1 << 10)
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+
+# host phase split of Engine.run (Engine.host_marks), full candidate count
+eng.host_marks = []
+acc = {}
+for k in range(20):
+    eng.host_marks.clear()
+    t0 = time.perf_counter()
+    step(k, 1 << 22)
+    m = eng.host_marks
+    for (a, ta), (b, tb) in zip(m, m[1:]):
+        acc[b] = acc.get(b, 0.0) + (tb - ta)
+    acc["prep (bench)"] = acc.get("prep (bench)", 0.0) + (m[0][1] - t0)
+for k, v in acc.items():
+    print("  %-16s %.3f ms" % (k, v / 20e-3))
