@@ -913,13 +913,34 @@ __global__ __launch_bounds__(kBS) void k_score_q(
 // ---------------------------------------------------------------------------
 // categorical labels
 // ---------------------------------------------------------------------------
-constexpr int kRC = 8;
-template <bool INJ>
-__global__ __launch_bounds__(kBS) void k_score_cat(
+constexpr int kRC = 16;      // categorical candidates per thread
+constexpr int kCatKey = 256;  // categories of the rank-key fast path (8-bit category field)
+
+// Categorical draws (randint / categorical priors sampled from the below
+// posterior, tpe.py:575-610): candidate g takes word (g & 3) of the Philox call
+// at counter (g >> 2, attempt 0) -- four candidates per call -- and its
+// category is the first k with word < thr[k], thr[k] = ceil(cdf[k] / cdf[K-1]
+// * 2^32): the inverse CDF at 2^-32 resolution, the same rule as the
+// continuous samplers' component choice.
+__device__ __forceinline__ uint32_t cat_thr(const double* cdf, int K, int k) {
+  const double t = ceil(cdf[k] / cdf[K - 1] * 4294967296.0);
+  return (t >= 4294967295.0) ? 0xFFFFFFFFu : (t > 0.0 ? (uint32_t)t : 0u);
+}
+__device__ __forceinline__ int cat_search(const double* cdf, int K, uint32_t w) {
+  int lo = 0, hi = K - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (w < cat_thr(cdf, K, mid)) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+// injected candidates (given category indices): per-candidate lookup + argmax
+__global__ __launch_bounds__(kBS) void k_score_cat_inj(
     const tpe_job* __restrict__ jobs, const tpe_cat_seg* __restrict__ csegs,
-    const double* __restrict__ logp, const double* __restrict__ cdf,
-    const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
-    double* __restrict__ out_x, tpe_best* __restrict__ partial) {
+    const double* __restrict__ logp, const double* __restrict__ cand,
+    double* __restrict__ out_bl, double* __restrict__ out_al, double* __restrict__ out_x,
+    tpe_best* __restrict__ partial) {
   __shared__ BestT red[kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -932,20 +953,11 @@ __global__ __launch_bounds__(kBS) void k_score_cat(
   const int K = CB.n_cat;
   const double* lb = logp + CB.p_off;
   const double* la = logp + CA.p_off;
-  const double* cb = cdf + CB.p_off;
   BestT b{0.0, -1, 0.0};
-#pragma unroll
   for (int r = 0; r < kRC; ++r) {
     const int64_t li = base + r * kBS + threadIdx.x;
-    if (li >= J.n_cand) continue;
-    const int64_t g = J.cand_base + li;
-    int64_t k;
-    if (INJ) {
-      k = (int64_t)cand[J.cand_off + li];
-    } else {
-      const U4 rw = draw_words(J.key, g, 0, kStreamSample);
-      k = upper_bound(cb, K, u01_f64(rw.x, rw.y) * cb[K - 1]);
-    }
+    if (li >= J.n_cand) break;
+    const int64_t k = (int64_t)cand[J.cand_off + li];
     double bl = NAN, al = NAN;
     if (k >= 0 && k < K) {
       bl = lb[k];
@@ -955,10 +967,144 @@ __global__ __launch_bounds__(kBS) void k_score_cat(
     if (out_bl) out_bl[o] = bl;
     if (out_al) out_al[o] = al;
     if (out_x) out_x[o] = (double)k;
-    best_update(b, bl - al, g, (double)k);
+    best_update(b, bl - al, J.cand_base + li, (double)k);
   }
   b = block_best<kBS>(b, red);
   if (threadIdx.x == 0) *P = tpe_best{b.score, b.index, b.value, 0};
+}
+
+// sampled candidates.  The score depends on the category alone, so every
+// category gets a rank (number of categories that beat it under np.argmax
+// rules: NaN first, then larger score; equal scores share a rank) and a
+// candidate's argmax key is rank << 48 | index << 8 | category: the smallest
+// key is the reference's winner (best score, first index).  K <= KR: the
+// thresholds sit in registers; KR < K <= kCatKey: binary search over the cdf
+// (thresholds formed on the fly, same values); K > kCatKey: per-candidate
+// fp64 argmax.  (The host picks KR from tpe_job.lat_n, the category count.)
+__device__ __forceinline__ uint32_t word_of(const U4& q, int sel) {
+  return sel == 0 ? q.x : sel == 1 ? q.y : sel == 2 ? q.z : q.w;
+}
+
+template <int KR>
+__global__ __launch_bounds__(kBS) void k_score_cat(
+    const tpe_job* __restrict__ jobs, const tpe_cat_seg* __restrict__ csegs,
+    const double* __restrict__ logp, const double* __restrict__ cdf,
+    double* __restrict__ out_bl, double* __restrict__ out_al, double* __restrict__ out_x,
+    tpe_best* __restrict__ partial) {
+  __shared__ double s_sc[kCatKey];
+  __shared__ uint64_t s_key[kCatKey];
+  __shared__ uint32_t s_thr[KR];
+  __shared__ uint64_t red[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kRC);
+  if (base >= J.n_cand) {
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
+  }
+  const tpe_cat_seg CB = csegs[J.below], CA = csegs[J.above];
+  const int K = CB.n_cat;
+  const double* lb = logp + CB.p_off;
+  const double* la = logp + CA.p_off;
+  const double* cb = cdf + CB.p_off;
+  const int64_t t0 = base + (int64_t)threadIdx.x * kRC;
+  const bool outs = out_bl || out_al || out_x;
+  auto put = [&](int64_t li, int k) __attribute__((always_inline)) {
+    if (outs) {
+      const int64_t o = J.out_off + li;
+      if (out_bl) out_bl[o] = lb[k];
+      if (out_al) out_al[o] = la[k];
+      if (out_x) out_x[o] = (double)k;
+    }
+  };
+  if (K > kCatKey) {  // block-uniform: many categories, plain fp64 argmax
+    BestT b{0.0, -1, 0.0};
+    for (int r = 0; r < kRC; ++r) {
+      const int64_t li = t0 + r;
+      if (li >= J.n_cand) break;
+      const int64_t g = J.cand_base + li;
+      const int k = cat_search(cb, K, word_of(draw_words(J.key, g >> 2, 0, kStreamSample),
+                                              (int)(g & 3)));
+      put(li, k);
+      best_update(b, lb[k] - la[k], g, (double)k);
+    }
+    b = block_best<kBS>(b, reinterpret_cast<BestT*>(s_sc));
+    if (threadIdx.x == 0) *P = tpe_best{b.score, b.index, b.value, 0};
+    return;
+  }
+  for (int k = threadIdx.x; k < K; k += kBS) {
+    s_sc[k] = lb[k] - la[k];
+    if (k < KR) s_thr[k] = cat_thr(cb, K, k);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += kBS) {
+    const double sk = s_sc[k];
+    uint32_t rank = 0;
+    for (int j = 0; j < K; ++j) {
+      const double sj = s_sc[j];
+      rank += (sj != sj) ? (sk == sk) : (sk == sk && sj > sk);
+    }
+    s_key[k] = ((uint64_t)rank << 48) | (uint64_t)k;
+  }
+  __syncthreads();
+  const bool in_regs = K <= KR;  // block-uniform
+  uint32_t thr[KR - 1];
+#pragma unroll
+  for (int j = 0; j + 1 < KR; ++j) thr[j] = (in_regs && j + 1 < K) ? s_thr[j] : 0xFFFFFFFFu;
+  auto category = [&](uint32_t w) __attribute__((always_inline)) -> int {
+    if (in_regs) {
+      int k = 0;
+#pragma unroll
+      for (int j = 0; j + 1 < KR; ++j) k += (w >= thr[j]) ? 1 : 0;
+      return min(k, K - 1);
+    }
+    return cat_search(cb, K, w);
+  };
+  uint64_t best = ~0ull;
+  auto take = [&](int64_t li, uint32_t w) __attribute__((always_inline)) {
+    const int k = category(w);
+    const int64_t g = J.cand_base + li;
+    best = min(best, s_key[k] | ((uint64_t)g << 8));
+    put(li, k);
+  };
+  const int64_t g0 = J.cand_base + t0;
+  if ((g0 & 3) == 0 && t0 + kRC <= J.n_cand) {  // four candidates per Philox call
+#pragma unroll
+    for (int c = 0; c < kRC / 4; ++c) {
+      const U4 r = draw_words(J.key, (g0 >> 2) + c, 0, kStreamSample);
+      take(t0 + 4 * c + 0, r.x);
+      take(t0 + 4 * c + 1, r.y);
+      take(t0 + 4 * c + 2, r.z);
+      take(t0 + 4 * c + 3, r.w);
+    }
+  } else {  // unaligned base or the job's last candidates: one call per candidate
+    for (int r = 0; r < kRC; ++r) {
+      const int64_t li = t0 + r;
+      if (li >= J.n_cand) break;
+      const int64_t g = J.cand_base + li;
+      take(li, word_of(draw_words(J.key, g >> 2, 0, kStreamSample), (int)(g & 3)));
+    }
+  }
+  // block min of the keys
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint64_t o = __shfl_xor(best, off, kWave);
+    best = min(best, o);
+  }
+  if (lane_id() == 0) red[threadIdx.x / kWave] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t b = red[0];
+#pragma unroll
+    for (int w = 1; w < kBS / kWave; ++w) b = min(b, red[w]);
+    if (b == ~0ull) {
+      *P = empty_best();
+    } else {
+      const int k = (int)(b & 0xFF);
+      const int64_t g = (int64_t)((b >> 8) & ((1ull << 40) - 1));
+      *P = tpe_best{s_sc[k], g, (double)k, 0};
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1229,12 +1375,21 @@ extern "C" int tpe_score_categorical(const tpe_job* jobs, const tpe_job* host_jo
   }
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)gx, (unsigned)n_jobs);
+  int kmax = 1;  // category counts (tpe_job.lat_n of categorical jobs; 0 = unknown)
+  for (int i = 0; i < n_jobs; ++i)
+    kmax = std::max(kmax, host_jobs[i].lat_n > 0 ? (int)host_jobs[i].lat_n : kCatKey);
   if (inj)
-    hipLaunchKernelGGL(k_score_cat<true>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool,
-                       cdf_pool, cand, out_bl, out_al, out_x, partial);
+    hipLaunchKernelGGL(k_score_cat_inj, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool, cand,
+                       out_bl, out_al, out_x, partial);
+  else if (kmax <= 4)
+    hipLaunchKernelGGL(k_score_cat<4>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool, cdf_pool,
+                       out_bl, out_al, out_x, partial);
+  else if (kmax <= 8)
+    hipLaunchKernelGGL(k_score_cat<8>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool, cdf_pool,
+                       out_bl, out_al, out_x, partial);
   else
-    hipLaunchKernelGGL(k_score_cat<false>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool,
-                       cdf_pool, cand, out_bl, out_al, out_x, partial);
+    hipLaunchKernelGGL(k_score_cat<16>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool, cdf_pool,
+                       out_bl, out_al, out_x, partial);
   hipLaunchKernelGGL(k_reduce, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
   return check_launch("tpe_score_categorical");
 }

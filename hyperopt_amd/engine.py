@@ -538,6 +538,7 @@ class Engine:
                 flags |= L.F_INJECTED
             if i in cat_meta:
                 J["family"][pos] = L.CAT
+                J["lat_n"][pos] = cat_meta[i][0]  # category count (sizes the sampler's path)
                 J["below"][pos], J["above"][pos] = 2 * cseg_of[i], 2 * cseg_of[i] + 1
                 J["flags"][pos] = flags
                 continue

@@ -118,7 +118,7 @@ typedef struct tpe_job {
   uint64_t key;         /* Philox key (seed mixed with label id)            */
   int64_t lat_off;      /* quantized: first lattice slot in the slot pool   */
   int64_t lat_kmin;     /* quantized: lattice index of slot 0               */
-  int64_t lat_n;        /* quantized: number of slots                       */
+  int64_t lat_n;        /* quantized: number of slots; categorical: K (0 = unknown) */
   int64_t out_off;      /* optional per-candidate outputs: first element    */
   double bin_lo, bin_hi;/* sorted path: candidate coordinate range to bin    */
   int64_t sort_off;     /* sorted path: first slot in the sorted pool        */

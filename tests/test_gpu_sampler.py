@@ -84,3 +84,38 @@ def test_chi2_quantized(engine, kind, args):
     table = table[:, table.sum(0) > 0]
     p = stats.chi2_contingency(table)[1]
     assert p > 1e-4, p
+
+
+@pytest.mark.parametrize("K,n_cand", [(3, N), (8, N), (40, N), (300, 1 << 17), (8, 1001)])
+def test_categorical_draws_and_argmax(engine, K, n_cand):
+    """Categorical draws follow the below posterior (chi^2 goodness of fit)
+    and the chosen candidate is np.argmax's over the drawn candidates' scores
+    (first index of the best-scoring category drawn) -- for K in registers,
+    K by binary search and K past the rank-key path; n_cand not a multiple
+    of the per-thread count exercises the tail."""
+    from hyperopt_amd.engine import LabelWork
+    rng = np.random.RandomState(K)
+    obs_b = rng.randint(0, K, 25)
+    obs_a = rng.randint(0, K, 400)
+    w = LabelWork("c", "randint", (K,), obs_b, obs_a, n_cand=n_cand, key=97 + K)
+    r, = engine.run([w], outputs=True)
+    k = r.cand.astype(np.int64)
+    assert k.min() >= 0 and k.max() < K
+    ref = O.categorical_label_scores("randint", (K,), obs_b, obs_a, k)
+    # p is bit-exact (test_gpu_posteriors); its log may differ from numpy's by an ulp
+    np.testing.assert_allclose(r.below_llik, ref["below_llik"], rtol=1e-14, atol=0)
+    np.testing.assert_allclose(r.above_llik, ref["above_llik"], rtol=1e-14, atol=0)
+    s = r.below_llik - r.above_llik
+    best = int(np.argmax(s))
+    assert (r.index, int(r.value), r.score) == (best, int(k[best]), s[best])
+    assert r.index == ref["best"] or abs(s[r.index] - s[ref["best"]]) < 1e-12
+    if n_cand >= 1 << 17:
+        counts = np.bincount(k, minlength=K)
+        expect = ref["p_below"] * n_cand
+        keep = expect >= 20
+        obs_c = np.append(counts[keep], counts[~keep].sum())
+        exp_c = np.append(expect[keep], expect[~keep].sum())
+        if exp_c[-1] == 0:
+            obs_c, exp_c = obs_c[:-1], exp_c[:-1]
+        p = stats.chisquare(obs_c, exp_c)[1]
+        assert p > 1e-4, p
