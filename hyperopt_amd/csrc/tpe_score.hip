@@ -790,9 +790,12 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
       atomicOr(err, 2);
       return;
     }
-    if (local)
-      atomicMin(&lfirst[slot], (uint32_t)(li - base));
-    else
+    if (local) {
+      // most draws land on slots already holding a smaller index: a plain
+      // read first keeps the atomics (and their same-address serialisation) rare
+      const uint32_t rel = (uint32_t)(li - base);
+      if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
+    } else
       atomicMin(&slot_first[J.lat_off + slot], (unsigned long long)(J.cand_base + li));
   };
   if (J.flags & TPE_F_DRAW32) {
@@ -839,14 +842,14 @@ __global__ __launch_bounds__(kBS) void k_lattice_compact(
   firsts[J.lat_off + pos] = (int64_t)f;
 }
 
-// quantized mixture log-mass of one value, one wave, lanes stride components.
+// quantized mixture log-mass of one value, one block, threads stride components.
 // tpe.py:159-174 (GMM1) and :288-305 (LGMM1): sum_k w_k*cdf(ub) - w_k*cdf(lb),
 // then log(prob) - log(p_accept).
 __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
                                         const double* __restrict__ w,
                                         const double* __restrict__ mu,
                                         const double* __restrict__ sigma, double x,
-                                        int32_t* err) {
+                                        int32_t* err, double* sh) {
   const bool lg = J.family == TPE_LGMM1;
   const double hq = J.q / 2.0;
   double ub = x + hq, lb = x - hq;
@@ -855,13 +858,13 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
   double lub = 0.0, llb = 0.0;
   if (lg) {
     lb = fmax(0.0, lb);
-    if (ub < 0.0 && lane_id() == 0) atomicOr(err, 1);  // tpe.py:196-197
+    if (ub < 0.0 && threadIdx.x == 0) atomicOr(err, 1);  // tpe.py:196-197
     lub = log(ub < kEps ? kEps : ub);
     llb = log(lb < kEps ? kEps : lb);
   }
   const int nc = S.n_obs + 1;
   double acc = 0.0;
-  for (int k = lane_id(); k < nc; k += kWave) {
+  for (int k = threadIdx.x; k < nc; k += kBS) {
     const double wk = w[S.comp_off + k], m = mu[S.comp_off + k], s = sigma[S.comp_off + k];
     double cu, cl;
     if (lg) {
@@ -873,13 +876,13 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
     }
     acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, kWave);
-  acc = __shfl(acc, 0, kWave);
+  acc = block_sum<kBS, double>(acc, sh);
   return log(acc) - log(S.p_accept);
 }
 
-constexpr int kQW = kBS / kWave;  // values per block (one wave each)
+// one block per value: 256 threads share its ~10^4 component CDF pairs, so a
+// level's ~10^3 present values keep every SIMD busy
+constexpr int kQW = 1;
 
 __global__ __launch_bounds__(kBS) void k_score_q(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
@@ -888,26 +891,25 @@ __global__ __launch_bounds__(kBS) void k_score_q(
     const int64_t* __restrict__ firsts, const unsigned long long* __restrict__ counts,
     double* __restrict__ out_bl, double* __restrict__ out_al, tpe_best* __restrict__ partial,
     int32_t* __restrict__ err) {
-  __shared__ BestT red[kBS / kWave];
+  __shared__ double sh[kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
   const int64_t cnt = counts ? (int64_t)counts[blockIdx.y] : J.n_cand;
-  const int64_t pos = (int64_t)blockIdx.x * kQW + threadIdx.x / kWave;
-  BestT b{0.0, -1, 0.0};
-  if (pos < cnt) {  // wave-uniform
-    const int64_t voff = counts ? J.lat_off : J.cand_off;
-    const double v = vals[voff + pos];
-    const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err);
-    const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err);
-    const int64_t idx = firsts ? firsts[J.lat_off + pos] : J.cand_base + pos;
-    if (lane_id() == 0) {
-      if (out_bl) out_bl[J.out_off + pos] = bl;
-      if (out_al) out_al[J.out_off + pos] = al;
-    }
-    b = BestT{bl - al, idx, v};
+  const int64_t pos = blockIdx.x;
+  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  if (pos >= cnt) {  // block-uniform
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
   }
-  b = block_best<kBS>(b, red);
-  if (threadIdx.x == 0)
-    partial[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = tpe_best{b.score, b.index, b.value, 0};
+  const int64_t voff = counts ? J.lat_off : J.cand_off;
+  const double v = vals[voff + pos];
+  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err, sh);
+  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err, sh);
+  if (threadIdx.x == 0) {
+    const int64_t idx = firsts ? firsts[J.lat_off + pos] : J.cand_base + pos;
+    if (out_bl) out_bl[J.out_off + pos] = bl;
+    if (out_al) out_al[J.out_off + pos] = al;
+    *P = tpe_best{bl - al, idx, v, 0};
+  }
 }
 
 // ---------------------------------------------------------------------------
