@@ -72,24 +72,49 @@ __device__ double np_pairwise_sum(const double* a, int64_t n) {
 constexpr int kCatBS = 256;
 constexpr int kCatWaves = kCatBS / kWave;
 
-// Weighted counts, one wave per (segment, category): the wave scans the
-// observations 64 at a time, ballots the matches, and adds their LF weights
-// in observation order -- exactly np.bincount's sequential sum
-// (pyll/base.py:1053-1060), but the dependent fp64 chain is only as long as
-// the category's own count.
+// Weighted counts, one wave per (segment, category): np.bincount's sum
+// (pyll/base.py:1053-1060) adds the LF weights of a category's observations
+// sequentially in observation order, so the fp64 chain itself cannot be
+// split.  The wave scans 64 observations per step, ballots the matches, and
+// every matching lane writes its weight (computed in parallel) into the
+// wave's LDS list at its rank; when the list fills, lane 0 folds it into the
+// running count in list order -- the only serial work left is one fp64 add
+// per match.
+constexpr int kCatList = 512;  // weights buffered per wave before a fold
+
 __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict__ obs,
                                                        const tpe_cat_seg* __restrict__ segs,
                                                        double* __restrict__ p) {
+  __shared__ double s_list[kCatWaves][kCatList];
   const tpe_cat_seg& S = segs[blockIdx.y];
   const int k = blockIdx.x * kCatWaves + threadIdx.x / kWave;
   if (k >= S.n_cat) return;  // wave-uniform
+  double* list = s_list[threadIdx.x / kWave];
   const int n = S.n_obs, lane = lane_id();
   // linear-forgetting ramp (np.linspace(1/N, 1, N-LF), tpe.py:380-392)
   const bool ramp = S.lf > 0 && S.lf < n;
   const int64_t num = n - S.lf;
   const double start = 1.0 / (double)n;
   const double step = (ramp && num > 1) ? (1.0 - start) / (double)(num - 1) : 0.0;
+  const uint64_t lt = (1ull << lane) - 1ull;
   double cnt = 0.0;
+  int filled = 0;
+  auto fold = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      int j = 0;
+      for (; j + 4 <= filled; j += 4) {
+        const double a = list[j], b = list[j + 1], c = list[j + 2], d = list[j + 3];
+        cnt = __dadd_rn(cnt, a);
+        cnt = __dadd_rn(cnt, b);
+        cnt = __dadd_rn(cnt, c);
+        cnt = __dadd_rn(cnt, d);
+      }
+      for (; j < filled; ++j) cnt = __dadd_rn(cnt, list[j]);
+    }
+    filled = 0;
+    __builtin_amdgcn_wave_barrier();
+  };
   constexpr int kDepth = 8;  // tiles of 64 observations loaded per step
   for (int t0 = 0; t0 < n; t0 += kDepth * kWave) {
     int64_t cur[kDepth];
@@ -100,20 +125,24 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
     }
 #pragma unroll
     for (int b = 0; b < kDepth; ++b) {
-      uint64_t m = __ballot(cur[b] == (int64_t)k);
-      while (m) {  // wave-uniform, in observation order
-        const int64_t i = t0 + b * kWave + __builtin_ctzll(m);
-        m &= m - 1;
+      const bool hit = cur[b] == (int64_t)k;
+      const uint64_t m = __ballot(hit);
+      if (m == 0) continue;  // wave-uniform
+      if (filled + kWave > kCatList) fold();
+      if (hit) {
+        const int64_t i = t0 + b * kWave + lane;
         double wt = 1.0;
         if (ramp && i < num) {
           if (num == 1) wt = start;
           else if (i == num - 1) wt = 1.0;
           else wt = __dadd_rn(__dmul_rn((double)i, step), start);
         }
-        cnt = __dadd_rn(cnt, wt);
+        list[filled + __popcll(m & lt)] = wt;
       }
+      filled += __popcll(m);
     }
   }
+  fold();
   if (lane == 0) {
     double pseudo;
     if (S.mode == 0) {
