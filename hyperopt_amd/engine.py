@@ -357,6 +357,7 @@ class Engine:
         cobs_parts, p_init = [], []
         cobs_off = p_off = 0
         cat_meta = {}
+        ccols = []
         for ci, i in enumerate(cat):
             w = works[i]
             K, offset, mode, prior_p = categorical_params(w.kind, w.args)
@@ -375,13 +376,15 @@ class Engine:
                     obs = obs.astype(np.int64) - offset
                     cobs_parts.append(obs)
                     n = obs.size
-                c = csegs[2 * ci + half]
-                c["obs_off"], c["p_off"], c["n_obs"], c["n_cat"] = cobs_off, p_off, n, K
-                c["lf"], c["mode"], c["prior_weight"], c["prior_p_off"] = lf, mode, prior_weight, \
-                    max(prior_off, 0)
+                ccols.append((cobs_off, p_off, n, K, mode, max(prior_off, 0)))
                 p_init.append(np.zeros(K))
                 cobs_off += n
                 p_off += K
+        if cat:  # one column assignment per field instead of per segment
+            cc = np.array(ccols, dtype=np.int64)
+            (csegs["obs_off"], csegs["p_off"], csegs["n_obs"], csegs["n_cat"], csegs["mode"],
+             csegs["prior_p_off"]) = cc.T
+            csegs["lf"], csegs["prior_weight"] = lf, prior_weight
         cobs_pool = np.concatenate(cobs_parts) if cobs_parts else np.zeros(1, np.int64)
         p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
 
