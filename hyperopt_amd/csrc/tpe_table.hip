@@ -572,7 +572,10 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   // the job's cell table: a uniform base + 32-bit byte offsets (saddr loads)
   const char* cbase = reinterpret_cast<const char*>(cells) + J.tbl_off * (kCellF * 4);
   const int lane = lane_id(), gi = lane & 7, gbase = lane & ~7;
-  float4* rows = s_rows + (threadIdx.x / kWave) * (kWave * 8);
+  // wave-uniform (scalar) base of the wave's LDS region: the DMA destinations need no
+  // per-instruction readfirstlane
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  float4* rows = s_rows + wave * (kWave * 8);
   const bool outs = out_bl || out_al || out_x;
   Mix M{};
 #ifndef TPE_DIAG_SKIP_SAMPLE
@@ -646,9 +649,10 @@ __global__ __launch_bounds__(kBS) void k_score_table(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t cj = __shfl(co[r], gbase | j, kWave);
-        if ((gi ^ j) < kChunks)
-          __builtin_amdgcn_global_load_lds((glb_vp)(cbase + (cj + ((gi ^ j) * 16))),
-                                           (lds_vp)(rows + j * kWave), 16, 0, 0);
+        // (lanes whose chunk gi^j >= kChunks bring bytes of the same line nobody
+        // reads: cheaper than masking them)
+        __builtin_amdgcn_global_load_lds((glb_vp)(cbase + (cj + ((gi ^ j) * 16))),
+                                         (lds_vp)(rows + j * kWave), 16, 0, 0);
       }
     };
     const f4* slab = reinterpret_cast<const f4*>(rows) + gi * kWave;
