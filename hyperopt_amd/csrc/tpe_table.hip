@@ -662,6 +662,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       // candidate r's DMA has landed (the compiler does not order LDS-DMA
       // writes before later ds_reads by itself)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      static_assert(kChunks == 5, "the reads below take chunks 0..4");
       const f4 q0 = slab[gbase | gi], q1 = slab[gbase | (1 ^ gi)], q2 = slab[gbase | (2 ^ gi)],
                q3 = slab[gbase | (3 ^ gi)], q4 = slab[gbase | (4 ^ gi)];
       // the reads must land before the next candidate's DMA overwrites the slabs
