@@ -31,3 +31,11 @@ for kind in kinds:
         g = {k: round(float(np.mean([a.elapsed_time(b) for a, b in v])), 4)
              for k, v in timers.items()}
         print(kind, scorer, n, g, eng.last_table_stats, flush=True)
+
+# cell-grid geometry of the last run (tpe_table records)
+from hyperopt_amd import _lib as L  # noqa: E402
+nt = len([s for s in space if s[1] in kinds])
+raw = eng._bufs["tables"][:L.TABLE_DTYPE.itemsize * nt].cpu().numpy().view(L.TABLE_DTYPE)
+for t in raw[:nt]:
+    print("  nb %6d  h %.3g  span %.3g  wide b/a %d/%d" % (t["nb"], t["h"], t["hi"] - t["lo"],
+                                                        t["n_wide_below"], t["n_wide_above"]))
