@@ -784,8 +784,15 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     for (int s = threadIdx.x; s < J.lat_n; s += kBS) lfirst[s] = 0xFFFFFFFFu;
   const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
   __syncthreads();
+  // np.round(x / q) (tpe.py:106) without a division per draw: t = x * (1/q) is
+  // within 3.4e-16 |t| of fl(x / q), so rint(t) == rint(fl(x / q)) unless
+  // fl(x / q) sits that close to a half-integer -- those few redo the division
+  const double inv_q = 1.0 / J.q;
   auto mark = [&](double v, int64_t li) {
-    const int64_t slot = (int64_t)rint(v / J.q) - J.lat_kmin;  // np.round(x/q) (tpe.py:106)
+    const double t = v * inv_q;
+    double k = rint(t);
+    if (fabs(fabs(t - k) - 0.5) <= 8e-16 * fabs(t)) k = rint(v / J.q);
+    const int64_t slot = (int64_t)k - J.lat_kmin;
     if (slot < 0 || slot >= J.lat_n) {
       atomicOr(err, 2);
       return;
