@@ -119,12 +119,12 @@ def make_works(space, splits, step, n_cand, cand_base):
 
 def cpu_baseline(space, vals, losses, seconds_hint=True):
     """The oracle (numpy restatement of tpe.suggest's per-label pipeline) on a
-    bounded sample: one label of each kind, 2048 candidates each, same 10k
+    bounded sample (~10 s): one label of each kind, 20480 candidates each, same 10k
     history.  Test infrastructure only -- never on the product path."""
     from oracle import tpe_oracle as O
     sp = split(vals, losses)
     picks = [s for s in space if s[0] in ("u0", "lu0", "qu0", "n0", "c0")]
-    n = 8192
+    n = 20480
     rng = np.random.RandomState(5)
     t0 = time.perf_counter()
     for lab, kind, a in picks:
@@ -173,6 +173,58 @@ def readme_suggest_p50():
     t = np.array(times[20:]) * 1e3
     return {"p50_ms": float(np.median(t)), "p90_ms": float(np.percentile(t, 90)),
             "calls": int(t.size), "config": "README space, max_evals=100, n_EI=24"}
+
+
+def c3_trials(space, vals, losses):
+    """The C3 history as a drop-in ``Trials`` of T finished documents (and its
+    Domain), in the reference's document format (base.py:459-482)."""
+    from hyperopt_amd import Trials, hp
+    from hyperopt_amd.base import JOB_STATE_DONE, Domain
+    hps = {lab: (hp.randint(lab, a[0]) if kind == "randint" else getattr(hp, kind)(lab, *a))
+           for lab, kind, a in space}
+    domain = Domain(lambda p: 0.0, hps)
+    trials = Trials()
+    T = losses.size
+    ints = {lab for lab, kind, _ in space if kind == "randint"}
+    cols = {lab: (vals[lab].astype(np.int64).tolist() if lab in ints else vals[lab].tolist())
+            for lab, _, _ in space}
+    miscs = [{"tid": i, "cmd": domain.cmd, "workdir": None,
+              "idxs": {lab: [i] for lab in cols}, "vals": {lab: [cols[lab][i]] for lab in cols}}
+             for i in range(T)]
+    docs = trials.new_trial_docs(list(range(T)), [None] * T,
+                                 [{"status": "ok", "loss": float(x)} for x in losses], miscs)
+    for d in docs:
+        d["state"] = JOB_STATE_DONE
+    trials.insert_trial_docs(docs)
+    trials.refresh()
+    return domain, trials
+
+
+def dropin_suggest_p50(space, vals, losses, n_cand, calls=8, warmup=2):
+    """suggest p50 through the drop-in API on C3: ``tpe.suggest(new_ids,
+    domain, trials, seed, n_EI_candidates=n_cand)`` on the 10k-document Trials
+    (per-tid history, split, HBM mirror of the columnar cache appended with the
+    previous call's document, every level's kernels, the returned document).
+    Each call's document is completed with a loss and inserted, as fmin does."""
+    from hyperopt_amd import tpe
+    from hyperopt_amd.base import JOB_STATE_DONE
+    domain, trials = c3_trials(space, vals, losses)
+    rng = np.random.RandomState(9)
+    times = []
+    for k in range(warmup + calls):
+        tid = losses.size + k
+        t0 = time.perf_counter()
+        docs = tpe.suggest([tid], domain, trials, k, n_EI_candidates=n_cand, verbose=False)
+        times.append(time.perf_counter() - t0)
+        docs[0]["state"] = JOB_STATE_DONE
+        docs[0]["result"] = {"status": "ok", "loss": float(rng.normal())}
+        trials.insert_trial_docs(docs)
+        trials.refresh()
+    t = np.array(times[warmup:]) * 1e3
+    return {"p50_ms": float(np.median(t)), "p90_ms": float(np.percentile(t, 90)),
+            "calls": int(t.size),
+            "config": "C3 through tpe.suggest: %d-document Trials, n_EI_candidates=2^%d"
+                      % (losses.size, int(round(math.log2(n_cand))))}
 
 
 def main():
@@ -326,6 +378,7 @@ def main():
         "group_ms": group_ms,
     }
     if rank == 0 and world == 1:
+        line["dropin_suggest"] = dropin_suggest_p50(space, vals, losses, n_cand)
         line["readme_suggest"] = readme_suggest_p50()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(space, vals, losses)

@@ -132,7 +132,12 @@ class Columnar(object):
 
     Row r holds document r of ``Trials._dynamic_trials`` (documents are
     append-only there); ``vals[r, j]`` is the value of label j (NaN when the
-    label is inactive in that trial, ``active[r, j]`` False).
+    label is inactive in that trial, ``active[r, j]`` False).  Per row it also
+    keeps the tid the row's loss is filed under (``misc.from_tid`` or ``tid``,
+    tpe.py:879) and the tid its observations are filed under (``misc.tid``),
+    the per-label active counts, and -- once tpe.suggest asks for it -- a
+    mirror of the matrix in HBM per device (``device_history``), appended with
+    the new rows only.
     """
 
     def __init__(self, labels):
@@ -143,6 +148,11 @@ class Columnar(object):
         self.row_of = {}
         self.vals = np.zeros((0, len(self.labels)))
         self.active = np.zeros((0, len(self.labels)), bool)
+        self.key_tid = np.zeros(0, np.int64)
+        self.obs_tid = np.zeros(0, np.int64)
+        self.n_active = np.zeros(len(self.labels), np.int64)
+        self.keys_increasing = True  # key_tid strictly increasing: one document per tid
+        self._device = {}
 
     def extend(self, docs):
         new = docs[self.rows:]
@@ -153,23 +163,52 @@ class Columnar(object):
             cap = max(need, 2 * self.vals.shape[0], 64)
             v = np.full((cap, len(self.labels)), np.nan)
             a = np.zeros((cap, len(self.labels)), bool)
+            kt = np.zeros(cap, np.int64)
+            ot = np.zeros(cap, np.int64)
             v[:self.rows] = self.vals[:self.rows]
             a[:self.rows] = self.active[:self.rows]
-            self.vals, self.active = v, a
+            kt[:self.rows] = self.key_tid[:self.rows]
+            ot[:self.rows] = self.obs_tid[:self.rows]
+            self.vals, self.active, self.key_tid, self.obs_tid = v, a, kt, ot
         col = self.col
+        last = self.key_tid[self.rows - 1] if self.rows else None
+        inc = self.keys_increasing
         for r, doc in enumerate(new, start=self.rows):
-            for lab, vv in doc["misc"]["vals"].items():
+            misc = doc["misc"]
+            for lab, vv in misc["vals"].items():
                 j = col.get(lab)
                 if j is not None and len(vv):
                     self.vals[r, j] = float(vv[0])
                     self.active[r, j] = True
+            key = misc.get("from_tid", doc["tid"])
+            self.key_tid[r] = key
+            self.obs_tid[r] = misc["tid"]
+            if inc and last is not None and not key > last:
+                inc = False
+            last = key
             self.row_of[id(doc)] = r
+        self.keys_increasing = inc
+        self.n_active += self.active[self.rows:need].sum(0)
         self.docs.extend(new)
         self.rows = need
 
     def valid_for(self, docs):
         n = min(self.rows, len(docs))
         return n == 0 or (docs[n - 1] is self.docs[n - 1] and docs[0] is self.docs[0])
+
+    def device_history(self, engine):
+        """The HBM mirror of rows [0, rows) on ``engine``'s device
+        (engine.DeviceHistory, device row r == row r here), brought up to date
+        by appending the rows added since the last call."""
+        from .engine import DeviceHistory
+        key = str(engine.device)
+        dh = self._device.get(key)
+        if dh is None or dh.rows > self.rows:
+            dh = self._device[key] = DeviceHistory(engine, len(self.labels),
+                                                   cap=max(self.rows, 1024))
+        if dh.rows < self.rows:
+            dh.append(self.vals[dh.rows:self.rows], self.active[dh.rows:self.rows])
+        return dh
 
 
 class Trials(object):

@@ -46,6 +46,7 @@ _default_n_startup_jobs = 20
 _default_linear_forgetting = DEFAULT_LF
 
 _engines = {}
+USE_DEVICE_HISTORY = True  # gather observation lists from the HBM mirror (LevelInputs)
 
 
 def engine():
@@ -71,47 +72,98 @@ def label_key(seed, label):
 
 
 class History(object):
-    """The history tpe.suggest conditions on, one row per distinct tid."""
+    """The history tpe.suggest conditions on, one row per distinct tid.
 
-    def __init__(self, tids, losses, obs_tids, vals, active):
+    ``vals`` / ``active`` (T, L) are views or gathers of the trials' columnar
+    cache when there is one (``col`` + ``rows``: row i of the history is
+    columnar row ``rows[i]``, or row i itself when ``rows`` is None), so the
+    device path can gather from the HBM mirror of the same rows instead.
+    """
+
+    def __init__(self, tids, losses, obs_tids, vals=None, active=None, col=None, rows=None):
         self.tids = tids          # (T,) loss tids, sorted
         self.losses = losses      # (T,) float64, +inf for unfinished/failed
         self.obs_tids = obs_tids  # (T,) the tid each row's observations are filed under
-        self.vals = vals          # (T, L) float64
-        self.active = active      # (T, L) bool
+        self.col = col            # base.Columnar or None
+        self.rows = rows          # (T,) int64 columnar rows, or None (= arange(T))
+        self._vals, self._active = vals, active
+
+    def _gather(self):
+        T = self.tids.size
+        if self.rows is None:
+            self._vals, self._active = self.col.vals[:T], self.col.active[:T]
+        else:
+            self._vals, self._active = self.col.vals[self.rows], self.col.active[self.rows]
+
+    @property
+    def vals(self):
+        if self._vals is None:
+            self._gather()
+        return self._vals    # (T, L) float64
+
+    @property
+    def active(self):
+        if self._active is None:
+            self._gather()
+        return self._active  # (T, L) bool
+
+    def label_counts(self):
+        """Active observations per label over the history's rows."""
+        if self.col is not None and self.rows is None and self.tids.size == self.col.rows:
+            return self.col.n_active
+        return self.active.sum(0)
+
+
+def _loss(doc):
+    loss = doc["result"].get("loss")
+    return float("inf") if loss is None else float(loss)
 
 
 def collect_history(trials, labels):
-    """Best document per tid, sorted by tid (tpe.py:874-896), as columns."""
+    """Best document per tid, sorted by tid (tpe.py:874-896), as columns.
+
+    Reference rule, kept exactly: ``best_docs_loss.setdefault(tid, loss)``
+    then ``if loss <= best_docs_loss[tid]`` -- so a tid whose first document
+    has a NaN loss never gets a document and drops out of the history.
+    """
+    docs = trials.trials
+    col = trials.columnar(labels) if hasattr(trials, "columnar") else None
+    n = len(docs)
+    if col is not None and n == col.rows and col.keys_increasing:
+        # trials.trials is every cached row (a filtered subsequence of
+        # _dynamic_trials of the same length) and each tid has one document
+        losses = np.fromiter((_loss(d) for d in docs), dtype=np.float64, count=n)
+        keep = ~np.isnan(losses)
+        if keep.all():
+            return History(col.key_tid[:n].copy(), losses, col.obs_tid[:n].copy(), col=col)
+        rows = np.flatnonzero(keep)
+        return History(col.key_tid[rows], losses[rows], col.obs_tid[rows], col=col, rows=rows)
     best_loss, best_doc = {}, {}
-    for doc in trials.trials:
+    for doc in docs:
         tid = doc["misc"].get("from_tid", doc["tid"])
-        loss = doc["result"].get("loss")
-        loss = float("inf") if loss is None else float(loss)
-        prev = best_loss.get(tid)
-        if prev is None or loss <= prev:
+        loss = _loss(doc)
+        if loss <= best_loss.setdefault(tid, loss):
             best_loss[tid] = loss
             best_doc[tid] = doc
     tids = sorted(best_doc)
-    docs = [best_doc[t] for t in tids]
+    bdocs = [best_doc[t] for t in tids]
     losses = np.array([best_loss[t] for t in tids], dtype=np.float64)
-    obs_tids = np.array([d["misc"]["tid"] for d in docs], dtype=np.int64)
+    obs_tids = np.array([d["misc"]["tid"] for d in bdocs], dtype=np.int64)
+    tids = np.asarray(tids, dtype=np.int64)
+    if col is not None and all(id(d) in col.row_of for d in bdocs):
+        rows = np.fromiter((col.row_of[id(d)] for d in bdocs), dtype=np.int64, count=len(bdocs))
+        return History(tids, losses, obs_tids, col=col, rows=rows)
     L = len(labels)
-    col = trials.columnar(labels) if hasattr(trials, "columnar") else None
-    if col is not None and all(id(d) in col.row_of for d in docs):
-        rows = np.fromiter((col.row_of[id(d)] for d in docs), dtype=np.int64, count=len(docs))
-        vals, active = col.vals[rows], col.active[rows]
-    else:
-        index = {lab: j for j, lab in enumerate(labels)}
-        vals = np.full((len(docs), L), np.nan)
-        active = np.zeros((len(docs), L), bool)
-        for r, d in enumerate(docs):
-            for lab, vv in d["misc"]["vals"].items():
-                j = index.get(lab)
-                if j is not None and len(vv):
-                    vals[r, j] = float(vv[0])
-                    active[r, j] = True
-    return History(np.asarray(tids, dtype=np.int64), losses, obs_tids, vals, active)
+    index = {lab: j for j, lab in enumerate(labels)}
+    vals = np.full((len(bdocs), L), np.nan)
+    active = np.zeros((len(bdocs), L), bool)
+    for r, d in enumerate(bdocs):
+        for lab, vv in d["misc"]["vals"].items():
+            j = index.get(lab)
+            if j is not None and len(vv):
+                vals[r, j] = float(vv[0])
+                active[r, j] = True
+    return History(tids, losses, obs_tids, vals, active)
 
 
 def split_masks(hist, gamma, gamma_cap=DEFAULT_LF):
@@ -173,6 +225,52 @@ def _decode(spec, value):
     return float(value), float(value)
 
 
+class LevelInputs(object):
+    """The observation inputs of every label for Engine.run.
+
+    When the trials carry a columnar cache (``History.col``) the lists are
+    gathered on the device: the cache is mirrored in HBM
+    (``Columnar.device_history``, appended with new rows only) and a suggest
+    uploads one split flag per history row (1 below, 0 above, 2 neither --
+    from_tid rows outside both sets) plus, when the history is not every cached
+    row, the row list; only the <= 25 below rows are read on the host (their
+    sizes size the fit).  Without a cache (foreign Trials classes) the lists
+    are sliced on the host and uploaded.  Both give bit-identical lists in tid
+    order (tests/test_gpu_history.py).
+    """
+
+    def __init__(self, hist, isb, isa, eng=None, device=True):
+        self.hist, self.isb, self.isa = hist, isb, isa
+        self.device = bool(device) and hist.col is not None and eng is not None
+        self.run_kwargs = {}
+        if not self.device:
+            return
+        c = hist.col
+        T = hist.tids.size
+        flags = np.full(T, 2, np.uint8)
+        flags[isa] = 0
+        flags[isb] = 1
+        below_pos = np.flatnonzero(isb)
+        crow = below_pos if hist.rows is None else hist.rows[below_pos]
+        self.vb, self.ab = c.vals[crow], c.active[crow]
+        nb = self.ab.sum(0)
+        if T - below_pos.size == int(np.count_nonzero(isa)):  # every other row is above
+            self.n_above = hist.label_counts() - nb
+        else:
+            self.n_above = hist.active[isa].sum(0)
+        rows = None if hist.rows is None else hist.rows.astype(np.int32)
+        self.run_kwargs = dict(history=c.device_history(eng), rows=rows, is_below=flags)
+
+    def work(self, label, spec, j, **kw):
+        if self.device:
+            return LabelWork(label=label, kind=spec.kind, args=spec.args,
+                             obs_below=self.vb[self.ab[:, j], j], obs_above=None, col=j,
+                             n_above=int(self.n_above[j]), **kw)
+        act, v = self.hist.active[:, j], self.hist.vals[:, j]
+        return LabelWork(label=label, kind=spec.kind, args=spec.args,
+                         obs_below=v[act & self.isb], obs_above=v[act & self.isa], **kw)
+
+
 def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
             n_startup_jobs=_default_n_startup_jobs, n_EI_candidates=_default_n_EI_candidates,
             gamma=_default_gamma, verbose=True, linear_forgetting=_default_linear_forgetting,
@@ -201,22 +299,16 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
     live = []
     if n_EI_candidates > 0:
         eng = engine()
+        obs = LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY)
         while True:
             live = domain.reachable(walk)
             level = [lab for lab in live if lab not in walk]
             if not level:
                 break
-            works = []
-            for lab in level:
-                spec = domain.specs[lab]
-                j = col[lab]
-                act = hist.active[:, j]
-                v = hist.vals[:, j]
-                works.append(LabelWork(label=lab, kind=spec.kind, args=spec.args,
-                                       obs_below=v[act & isb], obs_above=v[act & isa],
-                                       n_cand=count, key=label_key(seed, lab), cand_base=start))
+            works = [obs.work(lab, domain.specs[lab], col[lab], n_cand=count,
+                              key=label_key(seed, lab), cand_base=start) for lab in level]
             res = eng.run(works, prior_weight=prior_weight, lf=linear_forgetting,
-                          precision=prec)
+                          precision=prec, **obs.run_kwargs)
             if ws > 1:
                 hdist.allreduce_best(res)
             for lab, r in zip(level, res):
@@ -267,7 +359,8 @@ def suggest_many(requests, shard_studies=False):
         isb, isa = split_masks(hist, kw["gamma"])
         n_ei = max(int(kw["n_EI_candidates"]), 0)
         start, count = (0, n_ei) if (shard_studies or ws == 1) else hdist.shard(n_ei, rank, ws)
-        states.append(dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist, isb=isb, isa=isa,
+        states.append(dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist,
+                           obs=LevelInputs(hist, isb, isa, device=False),
                            col={lab: j for j, lab in enumerate(labels)}, walk={}, stored={},
                            live=[], start=start, count=count, done=n_ei == 0,
                            prec=_precision(kw["precision"], n_ei, hist.tids.size)))
@@ -287,11 +380,8 @@ def suggest_many(requests, shard_studies=False):
             for lab in level:
                 spec = st["rq"].domain.specs[lab]
                 j = st["col"][lab]
-                act, v = st["hist"].active[:, j], st["hist"].vals[:, j]
-                w = LabelWork(label=lab, kind=spec.kind, args=spec.args,
-                              obs_below=v[act & st["isb"]], obs_above=v[act & st["isa"]],
-                              n_cand=st["count"], key=label_key(st["rq"].seed, lab),
-                              cand_base=st["start"])
+                w = st["obs"].work(lab, spec, j, n_cand=st["count"],
+                                   key=label_key(st["rq"].seed, lab), cand_base=st["start"])
                 batches.setdefault(key, []).append((st, lab, w))
         if not batches:
             break

@@ -106,3 +106,53 @@ def test_history_count_mismatch_raises(engine):
     hw[0].n_above -= 3  # the host claims fewer rows than the gather finds
     with pytest.raises(L.TpeHipError, match="counts"):
         engine.run(hw, history=hist, is_below=isb)
+
+
+def _suggest_both(monkeypatch, trials, domain, n_ei, seed=7):
+    from hyperopt_amd import tpe
+    out = []
+    for dev in (True, False):
+        monkeypatch.setattr(tpe, "USE_DEVICE_HISTORY", dev)
+        docs = tpe.suggest([100_000], domain, trials, seed, n_EI_candidates=n_ei, verbose=False)
+        out.append(docs[0]["misc"]["vals"])
+    return out
+
+
+@pytest.mark.parametrize("kw", [{}, {"dup": 0.3, "nan": 0.1, "none": 0.1},
+                                {"cancel": 0.2, "dup": 0.1}])
+@pytest.mark.parametrize("n_ei", [24, 1 << 16])
+def test_suggest_device_history_matches_host_lists(monkeypatch, kw, n_ei):
+    """tpe.suggest gathering from the HBM mirror of the trials' columnar cache
+    == tpe.suggest with host-sliced lists (same Philox streams => identical
+    documents), on histories with from_tid duplicates, NaN / None losses and
+    cancelled documents (fp64 path at n_EI=24, fp32 table path at 2^16)."""
+    from hyperopt_amd import hp
+    from hyperopt_amd.base import Domain
+    from tests.test_history_cache import _random_trials
+    domain = Domain(lambda p: 0.0, {"x": hp.uniform("x", -5, 5), "y": hp.loguniform("y", -3, 0),
+                                    "k": hp.randint("k", 4)})
+    rng = np.random.RandomState(n_ei + len(kw))
+    for T in (30, 700):
+        trials = _random_trials(rng, T, **kw)
+        dev, host = _suggest_both(monkeypatch, trials, domain, n_ei)
+        assert dev == host, (T, dev, host)
+
+
+def test_fmin_device_history_incremental(monkeypatch):
+    """fmin appends one row per iteration to the HBM mirror; the whole run is
+    identical to the host-list run."""
+    from hyperopt_amd import Trials, fmin, hp, tpe
+    space = {"x": hp.uniform("x", -5, 5), "c": hp.choice("c", [0, 1, 2]),
+             "q": hp.quniform("q", 0, 10, 1)}
+
+    def run(dev):
+        monkeypatch.setattr(tpe, "USE_DEVICE_HISTORY", dev)
+        t = Trials()
+        fmin(lambda p: (p["x"] - 1) ** 2 + p["c"] + 0.1 * p["q"], space, algo=tpe.suggest,
+             max_evals=45, trials=t, rstate=np.random.RandomState(4), show_progressbar=False)
+        return t
+    t_dev, t_host = run(True), run(False)
+    assert [d["misc"]["vals"] for d in t_dev.trials] == [d["misc"]["vals"] for d in t_host.trials]
+    col = next(iter(t_dev._columnar.values()))
+    (dh,) = col._device.values()
+    assert dh.rows == 44  # mirrored up to the last suggest's history

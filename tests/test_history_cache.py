@@ -1,0 +1,143 @@
+"""The columnar history cache behind tpe.suggest (CPU): per-tid best documents
+(tpe.py:874-896) on the fast one-document-per-tid path and the general path,
+and the device-mode observation inputs (split flags, counts, below lists)
+against the host-sliced lists they replace."""
+import numpy as np
+import pytest
+
+from hyperopt_amd import Trials
+from hyperopt_amd import tpe
+from hyperopt_amd.base import Columnar
+
+LABELS = ["x", "y", "k"]
+
+
+def _doc(tid, loss, vals, from_tid=None, state=2):
+    misc = {"tid": tid, "cmd": None, "workdir": None,
+            "idxs": {lab: ([tid] if lab in vals else []) for lab in LABELS},
+            "vals": {lab: ([vals[lab]] if lab in vals else []) for lab in LABELS}}
+    if from_tid is not None:
+        misc["from_tid"] = from_tid
+    result = {"status": "ok", "loss": loss} if loss is not None else {"status": "new"}
+    return {"state": state, "tid": tid, "spec": None, "result": result, "misc": misc,
+            "exp_key": None, "owner": None, "version": 0, "book_time": None,
+            "refresh_time": None}
+
+
+def _reference_rule(trials):
+    """tpe.py:876-896 restated: best document per tid, then sorted by tid."""
+    best_docs, best_docs_loss = {}, {}
+    for doc in trials.trials:
+        tid = doc["misc"].get("from_tid", doc["tid"])
+        loss = doc["result"].get("loss")
+        loss = float("inf") if loss is None else float(loss)
+        best_docs_loss.setdefault(tid, loss)
+        if loss <= best_docs_loss[tid]:
+            best_docs_loss[tid] = loss
+            best_docs[tid] = doc
+    tid_docs = sorted(best_docs.items())
+    return ([t for t, _ in tid_docs], [best_docs_loss[t] for t, _ in tid_docs],
+            [d for _, d in tid_docs])
+
+
+def _random_trials(rng, T, dup=0.0, nan=0.0, none=0.0, cancel=0.0):
+    t = Trials()
+    docs = []
+    for tid in range(T):
+        vals = {}
+        if rng.rand() < 0.8:
+            vals["x"] = float(rng.uniform(-5, 5))
+        if rng.rand() < 0.6:
+            vals["y"] = float(np.exp(rng.uniform(-3, 0)))
+        vals["k"] = int(rng.randint(4))
+        u = rng.rand()
+        loss = None if u < none else (float("nan") if u < none + nan else float(rng.normal()))
+        src = int(rng.randint(tid)) if tid and rng.rand() < dup else None
+        docs.append(_doc(tid, loss, vals, from_tid=src,
+                         state=4 if rng.rand() < cancel else 2))
+    t.insert_trial_docs(docs)
+    t.refresh()
+    return t
+
+
+def _check(trials):
+    tids, losses, docs = _reference_rule(trials)
+    h = tpe.collect_history(trials, LABELS)
+    np.testing.assert_array_equal(h.tids, tids)
+    np.testing.assert_array_equal(h.losses, losses)
+    np.testing.assert_array_equal(h.obs_tids, [d["misc"]["tid"] for d in docs])
+    for j, lab in enumerate(LABELS):
+        want_a = [bool(d["misc"]["vals"][lab]) for d in docs]
+        np.testing.assert_array_equal(h.active[:, j], want_a)
+        want_v = [d["misc"]["vals"][lab][0] for d in docs if d["misc"]["vals"][lab]]
+        np.testing.assert_array_equal(h.vals[h.active[:, j], j], want_v)
+    np.testing.assert_array_equal(h.label_counts(), h.active.sum(0))
+    return h
+
+
+@pytest.mark.parametrize("kw", [{}, {"nan": 0.1}, {"none": 0.2}, {"dup": 0.2},
+                                {"dup": 0.3, "nan": 0.1, "none": 0.1}, {"cancel": 0.2},
+                                {"cancel": 0.1, "nan": 0.05, "dup": 0.1}])
+def test_collect_history_matches_reference_rule(kw):
+    rng = np.random.RandomState(len(str(kw)))
+    for T in (0, 1, 7, 300):
+        _check(_random_trials(rng, T, **kw))
+
+
+def test_first_nan_loss_drops_the_tid():
+    """A tid whose first document has a NaN loss has no best document
+    (best_docs_loss.setdefault(tid, nan); nan <= nan is False)."""
+    t = Trials()
+    t.insert_trial_docs([_doc(0, 1.0, {"x": 0.1}), _doc(1, float("nan"), {"x": 0.2}),
+                         _doc(2, 3.0, {"x": 0.3}), _doc(3, 0.5, {"x": 0.4}, from_tid=1)])
+    t.refresh()
+    h = _check(t)
+    assert list(h.tids) == [0, 2]
+
+
+def test_columnar_tid_cache_incremental():
+    rng = np.random.RandomState(3)
+    t = _random_trials(rng, 50)
+    c = t.columnar(LABELS)
+    assert c.keys_increasing and c.rows == 50
+    more = [_doc(50 + i, float(i), {"x": 0.5}) for i in range(5)]
+    t.insert_trial_docs(more)
+    t.refresh()
+    c2 = t.columnar(LABELS)
+    assert c2 is c and c.rows == 55 and c.keys_increasing
+    np.testing.assert_array_equal(c.key_tid[:55], np.arange(55))
+    np.testing.assert_array_equal(c.n_active, c.active[:55].sum(0))
+    t.insert_trial_docs([_doc(55, 1.0, {"x": 0.1}, from_tid=3)])
+    t.refresh()
+    assert not t.columnar(LABELS).keys_increasing
+    _check(t)
+
+
+@pytest.mark.parametrize("kw", [{}, {"dup": 0.3, "nan": 0.1}, {"cancel": 0.2, "none": 0.1}])
+def test_device_inputs_match_host_lists(monkeypatch, kw):
+    """LevelInputs in device mode: the split flags + row list, gathered the
+    way tpe_gather_obs does (active rows on the flagged side, in row order),
+    give the host-sliced below/above lists; counts and below lists match."""
+    monkeypatch.setattr(Columnar, "device_history", lambda self, eng: "HBM")
+    rng = np.random.RandomState(11)
+    for T in (25, 400):
+        trials = _random_trials(rng, T, **kw)
+        h = tpe.collect_history(trials, LABELS)
+        isb, isa = tpe.split_masks(h, 0.25)
+        dev = tpe.LevelInputs(h, isb, isa, eng=object())
+        host = tpe.LevelInputs(h, isb, isa, device=False)
+        assert dev.device and not host.device
+        kw_run = dev.run_kwargs
+        assert kw_run["history"] == "HBM"
+        flags = kw_run["is_below"]
+        rows = kw_run["rows"] if kw_run["rows"] is not None else np.arange(flags.size)
+        assert rows.size == flags.size == h.tids.size
+        col = h.col
+        for j, lab in enumerate(LABELS):
+            wd = dev.work(lab, type("S", (), {"kind": "uniform", "args": (0, 1)}), j)
+            wh = host.work(lab, type("S", (), {"kind": "uniform", "args": (0, 1)}), j)
+            np.testing.assert_array_equal(wd.obs_below, wh.obs_below)
+            assert wd.n_above == wh.obs_above.size and wd.col == j and wd.obs_above is None
+            for side, want in ((1, wh.obs_below), (0, wh.obs_above)):
+                sel = (flags == side) & col.active[rows, j]
+                np.testing.assert_array_equal(col.vals[rows[sel], j], want)
