@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32 = 1, 2, 4, 8, 16
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -45,7 +45,10 @@ TABLE_DTYPE = np.dtype([
     align=True)
 GATHER_DTYPE = np.dtype([
     ("col", "<i4"), ("below", "<i4"), ("dst_off", "<i8"), ("offset", "<i8"), ("count", "<i8"),
-    ("to_int", "<i4"), ("pad", "<i4")], align=True)
+    ("to_int", "<i4"), ("hist", "<i4")], align=True)
+HISTORY_DTYPE = np.dtype([
+    ("vals", "<u8"), ("active", "<u8"), ("ld", "<i8"), ("n_cols", "<i8"), ("n_rows", "<i8"),
+    ("rows_off", "<i8"), ("isb_off", "<i8")], align=True)
 BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
                        ("n_scored", "<i8")], align=True)
 
@@ -68,6 +71,7 @@ _SIGNATURES = {
                               _P]),
     "tpe_cat_posterior": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "tpe_gather_obs": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _P, _P, _P, _P]),
+    "tpe_gather_obs_multi": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P]),
     "tpe_table_partials": (_I64, [_P, _I]),
     "tpe_table_scratch_bytes": (_I64, [_I, _I]),
     "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -110,10 +114,10 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    sizes = (ctypes.c_int32 * 6)()
-    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 6)
+    sizes = (ctypes.c_int32 * 7)()
+    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 7)
     want = (SEG_DTYPE.itemsize, CAT_SEG_DTYPE.itemsize, JOB_DTYPE.itemsize, BEST_DTYPE.itemsize,
-            TABLE_DTYPE.itemsize, GATHER_DTYPE.itemsize)
+            TABLE_DTYPE.itemsize, GATHER_DTYPE.itemsize, HISTORY_DTYPE.itemsize)
     if lib.tpe_abi_version() != ABI_VERSION:
         raise ImportError("hyperopt_amd: libtpe_hip.so ABI %d, expected %d (rebuild with make)"
                           % (lib.tpe_abi_version(), ABI_VERSION))

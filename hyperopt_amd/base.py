@@ -127,6 +127,12 @@ def validate_loss_threshold(loss_threshold):
                         "Given value: {loss_threshold}".format(loss_threshold=loss_threshold))
 
 
+def doc_loss(doc):
+    """A document's loss for tpe.suggest: result['loss'], None -> +inf (tpe.py:880-882)."""
+    loss = doc["result"].get("loss")
+    return float("inf") if loss is None else float(loss)
+
+
 class Columnar(object):
     """Cached columnar view of a trials history for a fixed label tuple.
 
@@ -152,6 +158,8 @@ class Columnar(object):
         self.obs_tid = np.zeros(0, np.int64)
         self.n_active = np.zeros(len(self.labels), np.int64)
         self.keys_increasing = True  # key_tid strictly increasing: one document per tid
+        self.loss = np.zeros(0)
+        self.n_final = 0  # rows [0, n_final) are DONE and their losses cached
         self._device = {}
 
     def extend(self, docs):
@@ -165,11 +173,13 @@ class Columnar(object):
             a = np.zeros((cap, len(self.labels)), bool)
             kt = np.zeros(cap, np.int64)
             ot = np.zeros(cap, np.int64)
+            ls = np.zeros(cap)
             v[:self.rows] = self.vals[:self.rows]
             a[:self.rows] = self.active[:self.rows]
             kt[:self.rows] = self.key_tid[:self.rows]
             ot[:self.rows] = self.obs_tid[:self.rows]
-            self.vals, self.active, self.key_tid, self.obs_tid = v, a, kt, ot
+            ls[:self.n_final] = self.loss[:self.n_final]
+            self.vals, self.active, self.key_tid, self.obs_tid, self.loss = v, a, kt, ot, ls
         col = self.col
         last = self.key_tid[self.rows - 1] if self.rows else None
         inc = self.keys_increasing
@@ -195,6 +205,24 @@ class Columnar(object):
     def valid_for(self, docs):
         n = min(self.rows, len(docs))
         return n == 0 or (docs[n - 1] is self.docs[n - 1] and docs[0] is self.docs[0])
+
+    def losses(self):
+        """Loss of every row (tpe.py:880-882: None -> +inf), as a new array.
+
+        A document's loss is read once it is DONE and cached from then on:
+        hyperopt's evaluation flow sets ``result`` and then ``state = DONE``
+        and never touches a finished document again.  Rows not yet DONE
+        (NEW / RUNNING, loss usually None) are re-read on every call.
+        """
+        docs, n, k = self.docs, self.rows, self.n_final
+        while k < n and docs[k]["state"] == JOB_STATE_DONE:
+            self.loss[k] = doc_loss(docs[k])
+            k += 1
+        self.n_final = k
+        out = self.loss[:n].copy()
+        for r in range(k, n):
+            out[r] = doc_loss(docs[r])
+        return out
 
     def device_history(self, engine):
         """The HBM mirror of rows [0, rows) on ``engine``'s device

@@ -18,20 +18,14 @@ namespace {
 constexpr int kGBS = 1024;
 constexpr int kGWaves = kGBS / kWave;
 
-__global__ __launch_bounds__(kGBS) void k_gather_obs(const double* __restrict__ vals,
-                                                     const uint8_t* __restrict__ active,
-                                                     int64_t ld, const int32_t* __restrict__ rows,
-                                                     int64_t n_rows,
-                                                     const uint8_t* __restrict__ is_below,
-                                                     const tpe_gather* __restrict__ gs,
-                                                     double* __restrict__ out_f,
-                                                     int64_t* __restrict__ out_i,
-                                                     int32_t* __restrict__ err) {
-  __shared__ int wsum[kGWaves];
-  __shared__ int64_t carry_s;
-  const tpe_gather G = gs[blockIdx.x];
-  const double* V = vals + (int64_t)G.col * ld;
-  const uint8_t* A = active + (int64_t)G.col * ld;
+// compacts one descriptor's rows (block-wide, in position order)
+__device__ __forceinline__ void gather_one(const double* __restrict__ V,
+                                           const uint8_t* __restrict__ A,
+                                           const int32_t* __restrict__ rows, int64_t n_rows,
+                                           const uint8_t* __restrict__ is_below,
+                                           const tpe_gather& G, double* __restrict__ out_f,
+                                           int64_t* __restrict__ out_i, int32_t* __restrict__ err,
+                                           int* wsum, int64_t& carry_s) {
   const uint8_t side = G.below ? 1 : 0;
   const int lane = lane_id(), wid = threadIdx.x / kWave;
   if (threadIdx.x == 0) carry_s = 0;
@@ -69,6 +63,39 @@ __global__ __launch_bounds__(kGBS) void k_gather_obs(const double* __restrict__ 
   }
   if (threadIdx.x == 0 && carry_s != G.count && err) atomicOr(err, 4);
 }
+
+__global__ __launch_bounds__(kGBS) void k_gather_obs(const double* __restrict__ vals,
+                                                     const uint8_t* __restrict__ active,
+                                                     int64_t ld, const int32_t* __restrict__ rows,
+                                                     int64_t n_rows,
+                                                     const uint8_t* __restrict__ is_below,
+                                                     const tpe_gather* __restrict__ gs,
+                                                     double* __restrict__ out_f,
+                                                     int64_t* __restrict__ out_i,
+                                                     int32_t* __restrict__ err) {
+  __shared__ int wsum[kGWaves];
+  __shared__ int64_t carry_s;
+  const tpe_gather G = gs[blockIdx.x];
+  gather_one(vals + (int64_t)G.col * ld, active + (int64_t)G.col * ld, rows, n_rows, is_below, G,
+             out_f, out_i, err, wsum, carry_s);
+}
+
+// one block per descriptor; descriptor g reads history hs[g.hist]
+__global__ __launch_bounds__(kGBS) void k_gather_obs_multi(const tpe_history* __restrict__ hs,
+                                                           const uint8_t* __restrict__ aux,
+                                                           const tpe_gather* __restrict__ gs,
+                                                           double* __restrict__ out_f,
+                                                           int64_t* __restrict__ out_i,
+                                                           int32_t* __restrict__ err) {
+  __shared__ int wsum[kGWaves];
+  __shared__ int64_t carry_s;
+  const tpe_gather G = gs[blockIdx.x];
+  const tpe_history H = hs[G.hist];
+  const int32_t* rows =
+      H.rows_off >= 0 ? reinterpret_cast<const int32_t*>(aux + H.rows_off) : nullptr;
+  gather_one(H.vals + (int64_t)G.col * H.ld, H.active + (int64_t)G.col * H.ld, rows, H.n_rows,
+             aux + H.isb_off, G, out_f, out_i, err, wsum, carry_s);
+}
 }  // namespace
 }  // namespace tpe
 
@@ -99,4 +126,41 @@ extern "C" int tpe_gather_obs(const double* vals, const uint8_t* active, int64_t
   hipLaunchKernelGGL(k_gather_obs, dim3(n_gathers), dim3(kGBS), 0, (hipStream_t)stream, vals,
                      active, ld, rows, n_rows, is_below, gathers, obs_f64, obs_i64, err);
   return check_launch("tpe_gather_obs");
+}
+
+extern "C" int tpe_gather_obs_multi(const tpe_history* hists, const tpe_history* host_hists,
+                                    int n_hists, const void* aux, const tpe_gather* gathers,
+                                    const tpe_gather* host_gathers, int n_gathers,
+                                    double* obs_f64, int64_t* obs_i64, int32_t* err,
+                                    void* stream) {
+  if (n_gathers < 0 || n_gathers > 2147483647 || n_hists < 0) {
+    set_error("tpe_gather_obs_multi: n_gathers=%d n_hists=%d", n_gathers, n_hists);
+    return TPE_E_ARG;
+  }
+  if (n_gathers == 0) return TPE_OK;
+  if (!hists || !host_hists || !aux || !gathers || !host_gathers || n_hists == 0) {
+    set_error("tpe_gather_obs_multi: null pointer or no history");
+    return TPE_E_ARG;
+  }
+  for (int h = 0; h < n_hists; ++h) {
+    const tpe_history& H = host_hists[h];
+    if (!H.vals || !H.active || H.ld < 0 || H.n_cols < 0 || H.n_rows < 0 || H.isb_off < 0 ||
+        (H.rows_off < 0 && H.n_rows > H.ld)) {
+      set_error("tpe_gather_obs_multi: history %d has a bad pointer / size / offset", h);
+      return TPE_E_ARG;
+    }
+  }
+  for (int i = 0; i < n_gathers; ++i) {
+    const tpe_gather& g = host_gathers[i];
+    if (g.hist < 0 || g.hist >= n_hists || g.col < 0 || g.col >= host_hists[g.hist].n_cols ||
+        g.dst_off < 0 || g.count < 0 || (g.to_int ? !obs_i64 : !obs_f64)) {
+      set_error("tpe_gather_obs_multi: gather %d has a bad history / column / offset / count "
+                "/ output pool", i);
+      return TPE_E_ARG;
+    }
+  }
+  hipLaunchKernelGGL(k_gather_obs_multi, dim3((unsigned)n_gathers), dim3(kGBS), 0,
+                     (hipStream_t)stream, hists, (const uint8_t*)aux, gathers, obs_f64, obs_i64,
+                     err);
+  return check_launch("tpe_gather_obs_multi");
 }

@@ -205,6 +205,12 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
     if (!accept32(y1, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p + 1);
   }
   rej &= n >= R ? ~0u : (n <= 0 ? 0u : (1u << n) - 1u);
+#ifdef TPE_DIAG_NO_RETRY  // diagnostic builds only: rejected draws clamped, no retries
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (rej & (1u << r)) x[r] = clamp32(x[r], lo_on, hi_on, lo, hi);
+  rej = 0;
+#endif
   if (__any(rej != 0)) {
     float* st = wstage + lane_id();
     uint32_t todo = rej, att = 1;

@@ -62,6 +62,7 @@ class LabelWork:
     # the host (it is small) and obs_above is None with its size in n_above
     col: Optional[int] = None
     n_above: int = 0
+    hist: int = 0             # Engine.run(histories=...): index of this work's history
 
 
 @dataclass
@@ -251,7 +252,7 @@ class Engine:
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
             outputs=False, stream=None, timers=None, sample_only=False,
             pruned=True, scorer=None, posteriors=False, history=None, rows=None,
-            is_below=None) -> List[LabelResult]:
+            is_below=None, histories=None) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``.
         ``sample_only``: fit, then only draw the candidates of the continuous
@@ -270,7 +271,10 @@ class Engine:
         ``history`` (DeviceHistory) + ``is_below`` (uint8 per position of
         ``rows``, or of the history rows when ``rows`` is None): every work
         names its label column (``col``) and the observation lists are
-        gathered on the device (tpe_gather_obs) instead of being uploaded."""
+        gathered on the device (tpe_gather_obs) instead of being uploaded.
+        ``histories``: a list of (DeviceHistory, rows or None, is_below) for
+        batches of independent studies; each work names its history by
+        ``hist`` (one tpe_gather_obs_multi launch gathers every list)."""
         if sample_only:
             outputs = True
         if scorer is None:
@@ -310,8 +314,10 @@ class Engine:
 
         _hmark('prep')
         pack = _Pack()
-        hist_mode = history is not None
-        gathers = []  # history mode: (col, below, dst_off, offset, count, to_int)
+        if history is not None and histories is not None:
+            raise ValueError("give either history or histories")
+        hist_mode = history is not None or histories is not None
+        gathers = []  # history mode: (col, below, dst_off, offset, count, to_int, hist)
         # ---- continuous / quantized segments --------------------------------
         fit_ids = cont + quant
         params = {i: _params(works[i].kind, works[i].args) for i in fit_ids}
@@ -347,7 +353,7 @@ class Engine:
                     for half in (0, 1):
                         k = 2 * si + half
                         gathers.append((works[i].col, 1 - half, int(obs_off[k]), 0, int(sizes[k]),
-                                        0))
+                                        0, works[i].hist))
         if obs_pool is None:
             obs_pool = np.zeros(1)
 
@@ -370,7 +376,7 @@ class Engine:
             for half in (0, 1):
                 if hist_mode:
                     n = np.asarray(w.obs_below).size if half == 0 else int(w.n_above)
-                    gathers.append((w.col, 1 - half, cobs_off, offset, n, 1))
+                    gathers.append((w.col, 1 - half, cobs_off, offset, n, 1, w.hist))
                 else:
                     obs = np.asarray(w.obs_below if half == 0 else w.obs_above).reshape(-1)
                     obs = obs.astype(np.int64) - offset
@@ -438,13 +444,25 @@ class Engine:
             g_arr = np.zeros(len(gathers), L.GATHER_DTYPE)
             if gathers:
                 (g_arr["col"], g_arr["below"], g_arr["dst_off"], g_arr["offset"], g_arr["count"],
-                 g_arr["to_int"]) = (np.array(c) for c in zip(*gathers))
-            isb = np.ascontiguousarray(is_below, dtype=np.uint8)
-            n_rows = isb.size
+                 g_arr["to_int"], g_arr["hist"]) = (np.array(c) for c in zip(*gathers))
             o_g = pack.add(g_arr)
-            o_isb = pack.add(isb)
-            o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) if rows is not None \
-                else None
+            if histories is None:
+                isb = np.ascontiguousarray(is_below, dtype=np.uint8)
+                n_rows = isb.size
+                o_isb = pack.add(isb)
+                o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) \
+                    if rows is not None else None
+            else:  # row lists / flags at offsets of the staged pack (the `aux` base)
+                h_arr = np.zeros(len(histories), L.HISTORY_DTYPE)
+                for h, (dh, h_rows, h_isb) in enumerate(histories):
+                    h_isb = np.ascontiguousarray(h_isb, dtype=np.uint8)
+                    h_arr[h] = (dh.vals.data_ptr(), dh.active.data_ptr(), dh.ld, dh.n_labels,
+                                h_isb.size, pack.add(np.ascontiguousarray(h_rows, np.int32))
+                                if h_rows is not None else -1, pack.add(h_isb))
+                    if h_rows is None and h_isb.size > dh.rows:
+                        raise ValueError("history %d: %d split flags for %d rows"
+                                         % (h, h_isb.size, dh.rows))
+                o_h = pack.add(h_arr)
         else:
             o_obs = pack.add(obs_pool)
             o_cobs = pack.add(cobs_pool)
@@ -464,11 +482,19 @@ class Engine:
             d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
             d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
             e0 = tick()
-            L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
-                                       history.ld, base + o_rows if o_rows is not None else None,
-                                       n_rows, base + o_isb, base + o_g,
-                                       g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr), d_obs,
-                                       d_cobs, d_err, sp), "tpe_gather_obs")
+            if histories is None:
+                L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
+                                           history.ld,
+                                           base + o_rows if o_rows is not None else None,
+                                           n_rows, base + o_isb, base + o_g,
+                                           g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr),
+                                           d_obs, d_cobs, d_err, sp), "tpe_gather_obs")
+            else:
+                L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
+                                                 len(h_arr), base, base + o_g,
+                                                 g_arr.ctypes.data_as(ctypes.c_void_p),
+                                                 len(g_arr), d_obs, d_cobs, d_err, sp),
+                        "tpe_gather_obs_multi")
             tock("gather", e0)
         else:
             d_obs, d_cobs = base + o_obs, base + o_cobs

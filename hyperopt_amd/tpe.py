@@ -34,6 +34,7 @@ import numpy as np
 
 from . import dist as hdist
 from . import rand
+from .base import doc_loss
 from .engine import DEFAULT_LF, Engine, LabelWork
 
 logger = logging.getLogger(__name__)
@@ -114,11 +115,6 @@ class History(object):
         return self.active.sum(0)
 
 
-def _loss(doc):
-    loss = doc["result"].get("loss")
-    return float("inf") if loss is None else float(loss)
-
-
 def collect_history(trials, labels):
     """Best document per tid, sorted by tid (tpe.py:874-896), as columns.
 
@@ -131,8 +127,9 @@ def collect_history(trials, labels):
     n = len(docs)
     if col is not None and n == col.rows and col.keys_increasing:
         # trials.trials is every cached row (a filtered subsequence of
-        # _dynamic_trials of the same length) and each tid has one document
-        losses = np.fromiter((_loss(d) for d in docs), dtype=np.float64, count=n)
+        # _dynamic_trials of the same length) and each tid has one document;
+        # finished documents' losses come from the cache (Columnar.losses)
+        losses = col.losses()
         keep = ~np.isnan(losses)
         if keep.all():
             return History(col.key_tid[:n].copy(), losses, col.obs_tid[:n].copy(), col=col)
@@ -141,7 +138,7 @@ def collect_history(trials, labels):
     best_loss, best_doc = {}, {}
     for doc in docs:
         tid = doc["misc"].get("from_tid", doc["tid"])
-        loss = _loss(doc)
+        loss = doc_loss(doc)
         if loss <= best_loss.setdefault(tid, loss):
             best_loss[tid] = loss
             best_doc[tid] = doc
@@ -340,10 +337,15 @@ def suggest_many(requests, shard_studies=False):
     ``shard_studies`` under torch.distributed, rank r serves studies r::world
     (no collective on the data path) and returns None for the others.
     Returns one list of trial documents per request.
+
+    Studies whose trials carry a columnar cache are gathered on the device:
+    each keeps its own HBM mirror (Columnar.device_history) and a batch's lists
+    come from one tpe_gather_obs_multi launch over all of them.
     """
     rank, ws = hdist.world()
     out = [None] * len(requests)
     states = []
+    eng = None
     for qi, rq in enumerate(requests):
         if shard_studies and ws > 1 and qi % ws != rank:
             continue
@@ -359,14 +361,15 @@ def suggest_many(requests, shard_studies=False):
         isb, isa = split_masks(hist, kw["gamma"])
         n_ei = max(int(kw["n_EI_candidates"]), 0)
         start, count = (0, n_ei) if (shard_studies or ws == 1) else hdist.shard(n_ei, rank, ws)
+        if eng is None and n_ei > 0:
+            eng = engine()
         states.append(dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist,
-                           obs=LevelInputs(hist, isb, isa, device=False),
+                           obs=LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY),
                            col={lab: j for j, lab in enumerate(labels)}, walk={}, stored={},
                            live=[], start=start, count=count, done=n_ei == 0,
                            prec=_precision(kw["precision"], n_ei, hist.tids.size)))
-    eng = engine() if states else None
     while True:
-        batches = {}  # (prior_weight, lf, precision) -> [(state, label, work)]
+        batches = {}  # (prior_weight, lf, precision, device) -> [(state, label, work)]
         for st in states:
             if st["done"]:
                 continue
@@ -376,7 +379,8 @@ def suggest_many(requests, shard_studies=False):
             if not level:
                 st["done"] = True
                 continue
-            key = (st["kw"]["prior_weight"], st["kw"]["linear_forgetting"], st["prec"])
+            key = (st["kw"]["prior_weight"], st["kw"]["linear_forgetting"], st["prec"],
+                   st["obs"].device)
             for lab in level:
                 spec = st["rq"].domain.specs[lab]
                 j = st["col"][lab]
@@ -385,8 +389,20 @@ def suggest_many(requests, shard_studies=False):
                 batches.setdefault(key, []).append((st, lab, w))
         if not batches:
             break
-        for (pw, lf, prec), items in batches.items():
-            res = eng.run([w for _, _, w in items], prior_weight=pw, lf=lf, precision=prec)
+        for (pw, lf, prec, dev), items in batches.items():
+            kw_run = {}
+            if dev:  # one history per study of the batch
+                slot, hists = {}, []
+                for st, _, w in items:
+                    h = slot.get(st["qi"])
+                    if h is None:
+                        h = slot[st["qi"]] = len(hists)
+                        rk = st["obs"].run_kwargs
+                        hists.append((rk["history"], rk["rows"], rk["is_below"]))
+                    w.hist = h
+                kw_run["histories"] = hists
+            res = eng.run([w for _, _, w in items], prior_weight=pw, lf=lf, precision=prec,
+                          **kw_run)
             if ws > 1 and not shard_studies:
                 hdist.allreduce_best(res)
             for (st, lab, _), r in zip(items, res):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 5
+#define TPE_ABI_VERSION 6
 
 enum {
   TPE_OK = 0,
@@ -169,12 +169,30 @@ typedef struct tpe_gather {
   int64_t offset;       /* to_int: subtracted (randint low)                  */
   int64_t count;        /* elements expected (the segment's n_obs)           */
   int32_t to_int;       /* 1: int64 output, 0: fp64 output                   */
-  int32_t pad;
+  int32_t hist;         /* tpe_gather_obs_multi: index of the history (else 0) */
 } tpe_gather;
 int tpe_gather_obs(const double* vals, const uint8_t* active, int64_t ld, const int32_t* rows,
                    int64_t n_rows, const uint8_t* is_below, const tpe_gather* gathers,
                    const tpe_gather* host_gathers, int n_gathers, double* obs_f64,
                    int64_t* obs_i64, int32_t* err, void* stream);
+
+/* Many histories in one launch (batched independent studies, the C4 shape of
+ * SURVEY §8(f) row 3): gather g reads history hists[g.hist].  A history's
+ * row list (rows_off < 0: identity) and split flags live in the caller's
+ * `aux` buffer at byte offsets rows_off / isb_off; n_cols bounds `col`. */
+typedef struct tpe_history {
+  const double* vals;     /* label-major values, (col, row) at col * ld + row    */
+  const uint8_t* active;  /* same layout, 1 = label active in that row          */
+  int64_t ld;
+  int64_t n_cols;
+  int64_t n_rows;         /* positions (length of the row list / flags)         */
+  int64_t rows_off;       /* byte offset of int32 rows in aux, or -1 (identity) */
+  int64_t isb_off;        /* byte offset of the uint8 split flags in aux        */
+} tpe_history;
+int tpe_gather_obs_multi(const tpe_history* hists, const tpe_history* host_hists, int n_hists,
+                         const void* aux, const tpe_gather* gathers,
+                         const tpe_gather* host_gathers, int n_gathers, double* obs_f64,
+                         int64_t* obs_i64, int32_t* err, void* stream);
 
 /* ---- categorical posterior (tpe.py:578-615) ------------------------------ */
 /* p_pool: probabilities (mode 1 also reads the prior p from it at
@@ -322,8 +340,8 @@ int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* o
 
 const char* tpe_last_error(void);
 int tpe_abi_version(void);
-/* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table, tpe_gather)
- * to out[0..n) */
+/* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table, tpe_gather,
+ * tpe_history) to out[0..n); returns 7 */
 int tpe_struct_sizes(int32_t* out, int n);
 
 #ifdef __cplusplus

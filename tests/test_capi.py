@@ -30,12 +30,12 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 5
-    sizes = (ctypes.c_int32 * 6)()
-    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 6) == 6
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 6
+    sizes = (ctypes.c_int32 * 7)()
+    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 7) == 7
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
                             L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize, L.TABLE_DTYPE.itemsize,
-                            L.GATHER_DTYPE.itemsize)
+                            L.GATHER_DTYPE.itemsize, L.HISTORY_DTYPE.itemsize)
 
 
 def test_argument_errors_are_reported():
@@ -83,5 +83,21 @@ def test_argument_errors_are_reported():
     assert rc == -1 and b"output pool" in lib.tpe_last_error()
     assert lib.tpe_gather_obs(None, None, 10, None, 0, None, None, None, 0, None, None, None,
                               None) == 0
+    h = np.zeros(1, L.HISTORY_DTYPE)
+    h["vals"] = h["active"] = 1
+    h["ld"], h["n_cols"], h["n_rows"], h["rows_off"] = 10, 3, 10, -1
+    hp2 = h.ctypes.data_as(ctypes.c_void_p)
+    g["hist"], g["col"], g["to_int"] = 0, 3, 0
+    rc = lib.tpe_gather_obs_multi(one, hp2, 1, one, one, gp, 1, one, None, None, None)
+    assert rc == -1 and b"column" in lib.tpe_last_error()
+    g["col"], g["hist"] = 2, 1
+    rc = lib.tpe_gather_obs_multi(one, hp2, 1, one, one, gp, 1, one, None, None, None)
+    assert rc == -1 and b"history" in lib.tpe_last_error()
+    h["n_rows"] = 11  # identity rows beyond the leading dimension
+    g["hist"] = 0
+    rc = lib.tpe_gather_obs_multi(one, hp2, 1, one, one, gp, 1, one, None, None, None)
+    assert rc == -1 and b"history 0" in lib.tpe_last_error()
+    assert lib.tpe_gather_obs_multi(None, None, 0, None, None, None, 0, None, None, None,
+                                    None) == 0
     with pytest.raises(L.TpeHipError):
         L.check(-1, "probe")

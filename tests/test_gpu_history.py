@@ -156,3 +156,25 @@ def test_fmin_device_history_incremental(monkeypatch):
     col = next(iter(t_dev._columnar.values()))
     (dh,) = col._device.values()
     assert dh.rows == 44  # mirrored up to the last suggest's history
+
+
+def test_suggest_many_multi_history_matches_host_lists(monkeypatch):
+    """suggest_many gathering every study's lists from its own HBM mirror in one
+    tpe_gather_obs_multi launch == suggest_many with host-sliced lists, for
+    studies of different sizes and history shapes (duplicates, NaN / None
+    losses, cancelled documents) in one batch."""
+    from hyperopt_amd import hp, tpe
+    from hyperopt_amd.base import Domain
+    from tests.test_history_cache import _random_trials
+    domain = Domain(lambda p: 0.0, {"x": hp.uniform("x", -5, 5), "y": hp.loguniform("y", -3, 0),
+                                    "k": hp.randint("k", 4)})
+    rng = np.random.RandomState(21)
+    kws = [{}, {"dup": 0.3, "nan": 0.1}, {"cancel": 0.2, "none": 0.1}, {}, {"dup": 0.1}]
+    studies = [_random_trials(rng, T, **kw) for T, kw in zip((40, 300, 120, 900, 64), kws)]
+    out = {}
+    for dev in (True, False):
+        monkeypatch.setattr(tpe, "USE_DEVICE_HISTORY", dev)
+        reqs = [tpe.SuggestRequest([10_000], domain, t, 5 + s, n_EI_candidates=n)
+                for s, t in enumerate(studies) for n in (24, 1 << 14)]
+        out[dev] = [d[0]["misc"]["vals"] for d in tpe.suggest_many(reqs)]
+    assert out[True] == out[False]

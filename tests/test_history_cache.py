@@ -141,3 +141,24 @@ def test_device_inputs_match_host_lists(monkeypatch, kw):
             for side, want in ((1, wh.obs_below), (0, wh.obs_above)):
                 sel = (flags == side) & col.active[rows, j]
                 np.testing.assert_array_equal(col.vals[rows[sel], j], want)
+
+
+def test_loss_cache_follows_finishing_documents():
+    """Rows are re-read until DONE; a finished document's loss is cached."""
+    t = Trials()
+    docs = [_doc(i, float(i), {"x": 0.1 * i}) for i in range(6)]
+    for d in docs[3:]:
+        d["state"], d["result"] = 1, {"status": "running"}  # RUNNING, no loss yet
+    t.insert_trial_docs(docs)
+    t.refresh()
+    docs = t._dynamic_trials  # the stored (SONified) documents
+    h = _check(t)
+    assert list(h.losses) == [0.0, 1.0, 2.0, np.inf, np.inf, np.inf]
+    assert t.columnar(LABELS).n_final == 3
+    docs[4]["result"], docs[4]["state"] = {"status": "ok", "loss": -1.0}, 2
+    h = _check(t)
+    assert list(h.losses) == [0.0, 1.0, 2.0, np.inf, -1.0, np.inf]
+    assert t.columnar(LABELS).n_final == 3  # row 3 still running
+    docs[3]["result"], docs[3]["state"] = {"status": "ok", "loss": 5.0}, 2
+    _check(t)
+    assert t.columnar(LABELS).n_final == 5

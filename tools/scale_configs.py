@@ -1,0 +1,137 @@
+"""Configs C4 and C5 (BASELINE.json configs[3], [4]) at their stated sizes on one
+GPU, through the drop-in API (diagnostic / measurement; run on the GPU box).
+
+C5: 3-level nested hp.choice space (tests/golden/spaces.py:nested), 100k-trial
+    history drawn from the prior (seed 0), N(0,1) losses (seed 1),
+    n_EI_candidates = 2^24 per live label, tpe.suggest (one GPU's view of the
+    8-GPU run: the same per-label candidate count, no combine).
+C4: the per-GPU share of 4096 studies over 8 GPUs = 512 independent studies,
+    20-dim each (4 x uniform / loguniform / quniform / normal / choice(8)),
+    2k trials each (prior draws, seed = study), n_EI = 2^12 per label,
+    one suggest_many call.
+Prints one JSON line per config.
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from hyperopt_amd import Trials, hp, rand, tpe  # noqa: E402
+from hyperopt_amd.base import JOB_STATE_DONE, Domain  # noqa: E402
+from tests.golden import spaces  # noqa: E402
+
+
+def finished(trials, docs, losses):
+    for d, x in zip(docs, losses):
+        d["state"] = JOB_STATE_DONE
+        d["result"] = {"status": "ok", "loss": float(x)}
+    trials.insert_trial_docs(docs)
+    trials.refresh()
+
+
+def prior_trials(domain, T, seed):
+    t = Trials()
+    docs = rand.suggest(list(range(T)), domain, t, seed)
+    finished(t, docs, np.random.RandomState(seed + 1).normal(size=T))
+    return t
+
+
+def flat_trials(domain, T, seed):
+    """prior_trials for a flat space, each column drawn at once (fast)."""
+    rng = np.random.RandomState(seed)
+    cols = {}
+    for lab in domain.params:
+        sp = domain.specs[lab]
+        a = sp.args
+        if sp.kind == "uniform":
+            v = rng.uniform(a[0], a[1], T)
+        elif sp.kind == "loguniform":
+            v = np.exp(rng.uniform(a[0], a[1], T))
+        elif sp.kind == "quniform":
+            v = np.round(rng.uniform(a[0], a[1], T) / a[2]) * a[2]
+        elif sp.kind == "normal":
+            v = rng.normal(a[0], a[1], T)
+        elif sp.kind == "randint":
+            v = rng.randint(a[0], a[1], T) if a[1] is not None else rng.randint(a[0], size=T)
+        else:
+            p = np.asarray(a[0], float)
+            v = rng.choice(p.size, size=T, p=p / p.sum())
+        cols[lab] = v.tolist()
+    t = Trials()
+    miscs = [{"tid": i, "cmd": domain.cmd, "workdir": None,
+              "idxs": {lab: [i] for lab in cols}, "vals": {lab: [cols[lab][i]] for lab in cols}}
+             for i in range(T)]
+    docs = t.new_trial_docs(list(range(T)), [None] * T, [domain.new_result()] * T, miscs)
+    finished(t, docs, np.random.RandomState(seed + 1).normal(size=T))
+    return t
+
+
+def timed(fn, calls, warmup):
+    out, ts = None, []
+    for k in range(warmup + calls):
+        t0 = time.perf_counter()
+        out = fn(k)
+        ts.append(time.perf_counter() - t0)
+    return out, np.array(ts[warmup:]) * 1e3
+
+
+def c5(T=100_000, n_ei=1 << 24):
+    domain = Domain(lambda p: 0.0, spaces.nested(hp))
+    t0 = time.perf_counter()
+    trials = prior_trials(domain, T, 0)
+    build_s = time.perf_counter() - t0
+    docs, ms = timed(lambda k: tpe.suggest([T + k], domain, trials, k, n_EI_candidates=n_ei,
+                                           verbose=False), 5, 2)
+    live = [lab for lab, v in docs[0]["misc"]["vals"].items() if v]
+    return {"config": "C5", "history": T, "n_EI_candidates": n_ei, "labels": len(domain.params),
+            "live_labels_last": live, "suggest_p50_ms": float(np.median(ms)),
+            "suggest_ms": ms.round(3).tolist(),
+            "EI_candidates_per_s_p50": len(live) * n_ei / (np.median(ms) * 1e-3),
+            "history_build_s": round(build_s, 1)}
+
+
+def c4_space(s):
+    sp = {}
+    for i in range(4):
+        sp["u%d" % i] = hp.uniform("u%d" % i, -5, 5)
+        sp["lu%d" % i] = hp.loguniform("lu%d" % i, -5, 0)
+        sp["qu%d" % i] = hp.quniform("qu%d" % i, 0, 100, 1)
+        sp["n%d" % i] = hp.normal("n%d" % i, 0, 2)
+        sp["c%d" % i] = hp.choice("c%d" % i, list(range(8)))
+    return sp
+
+
+def c4(studies=512, T=2000, n_ei=1 << 12):
+    t0 = time.perf_counter()
+    doms, trs = [], []
+    for s in range(studies):
+        d = Domain(lambda p: 0.0, c4_space(s))
+        doms.append(d)
+        trs.append(flat_trials(d, T, s))
+        if s % 128 == 127:
+            print("c4: %d studies built, %.0f s" % (s + 1, time.perf_counter() - t0),
+                  file=sys.stderr, flush=True)
+    build_s = time.perf_counter() - t0
+
+    def call(k):
+        reqs = [tpe.SuggestRequest([T + k], d, t, s + k, n_EI_candidates=n_ei)
+                for s, (d, t) in enumerate(zip(doms, trs))]
+        return tpe.suggest_many(reqs)
+    out, ms = timed(call, 3, 1)
+    assert all(len(o) == 1 for o in out)
+    return {"config": "C4 (one GPU's share)", "studies": studies, "history": T, "dims": 20,
+            "n_EI_candidates": n_ei, "suggest_many_p50_ms": float(np.median(ms)),
+            "suggest_many_ms": ms.round(3).tolist(),
+            "EI_candidates_per_s_p50": studies * 20 * n_ei / (np.median(ms) * 1e-3),
+            "history_build_s": round(build_s, 1)}
+
+
+if __name__ == "__main__":
+    import torch
+    torch.cuda.set_device(0)
+    which = sys.argv[1:] or ["c5", "c4"]
+    for w in which:
+        print(json.dumps({"c5": c5, "c4": c4}[w]()), flush=True)
