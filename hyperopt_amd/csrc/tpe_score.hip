@@ -827,10 +827,15 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   }
   if (local) {
     __syncthreads();
+    // blocks run roughly in index order, so the global slot mostly holds a
+    // smaller index already: an agent-scope load first keeps the (cross-XCD)
+    // atomics to the blocks that improve a slot
     for (int s = threadIdx.x; s < J.lat_n; s += kBS) {
       const uint32_t f = lfirst[s];
-      if (f != 0xFFFFFFFFu)
-        atomicMin(&slot_first[J.lat_off + s], (unsigned long long)(J.cand_base + base + f));
+      if (f == 0xFFFFFFFFu) continue;
+      unsigned long long* dst = &slot_first[J.lat_off + s];
+      const unsigned long long g = (unsigned long long)(J.cand_base + base + f);
+      if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
     }
   }
 }

@@ -22,6 +22,7 @@ from __future__ import annotations
 import ctypes
 import functools
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -38,6 +39,7 @@ TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
 SORTED_MIN_CAND = 1 << 12  # auto scorer: sorted/pruned path from this many (below: dense)
 SCORERS = ("auto", "dense", "sorted", "table")
+SIDE_KINDS = ("lat", "qfb", "qinj", "cat")  # groups scored on the side stream
 _ALIGN = 256
 
 CONTINUOUS = ("uniform", "quniform", "loguniform", "qloguniform",
@@ -215,14 +217,24 @@ class Engine:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
         self._bufs = {}
+        self._retired = []
         self._pinned = {}
         self.host_marks = None  # set to a list to record host-side phase times (diagnostic)
+        # quantized / categorical scoring runs on a second stream, concurrently
+        # with the cell-table path (the two share no buffers); TPE_SIDE_STREAM=0
+        # puts everything on the caller's stream (diagnostic)
+        # "2": the table scorer waits for the side stream (side work overlaps the
+        # table build only); "1": join at the end of the level
+        self.side_stream = os.environ.get("TPE_SIDE_STREAM", "0")
+        self._side = None
 
     # -- memory --------------------------------------------------------------
     def _buf(self, name, nbytes):
         t = self._bufs.get(name)
         nbytes = max(int(nbytes), 16)
         if t is None or t.numel() < nbytes:
+            if t is not None:  # may still be in use on the side stream: freed after the run
+                self._retired.append(t)
             t = self.torch.empty(_align(int(nbytes * 1.25)), dtype=self.torch.uint8,
                                  device=self.device)
             self._bufs[name] = t
@@ -282,6 +294,7 @@ class Engine:
         if scorer not in SCORERS:
             raise ValueError("scorer must be one of %s, got %r" % (SCORERS, scorer))
         torch = self.torch
+        self._retired.clear()  # every earlier run ended with a synchronising readback
         hp = self.host_marks  # diagnostic: list of (name, perf_counter) or None
 
         def _hmark(name):
@@ -289,16 +302,16 @@ class Engine:
                 hp.append((name, time.perf_counter()))
         _hmark("start")
 
-        def tick():
+        def tick(on=None):
             if timers is None:
                 return None
             e = torch.cuda.Event(enable_timing=True)
-            e.record(stream)
+            e.record(stream if on is None else on)
             return e
 
-        def tock(name, e0):
+        def tock(name, e0, on=None):
             if timers is not None:
-                timers.setdefault(name, []).append((e0, tick()))
+                timers.setdefault(name, []).append((e0, tick(on)))
         lib = self.lib
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
@@ -626,8 +639,25 @@ class Engine:
 
         _hmark('fit')
         # ---- scoring, one call per group ----------------------------------------
+        # quantized and categorical groups go to the side stream (after the job
+        # table has landed); continuous groups stay on `stream`
+        side = None
+        if self.side_stream != "0" and not sample_only and any(
+                ids for k, ids in groups if k in SIDE_KINDS):
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            side = self._side
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            side.wait_event(ev)
+        side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
         table_calls = []
-        for g, (kind, ids) in enumerate(groups):
+        g_order = list(range(len(groups)))
+        if side is not None:  # side groups launched first
+            g_order.sort(key=lambda g: groups[g][0] not in SIDE_KINDS)
+        joined = side is None
+        for g in g_order:
+            kind, ids = groups[g]
             if not ids:
                 continue
             if sample_only:
@@ -644,7 +674,11 @@ class Engine:
             dj = base + o_jobs + a * JS
             db = d_best + a * BS
             nj = b - a
-            e0 = tick()
+            on_side = side is not None and kind in SIDE_KINDS
+            ks = side_p if on_side else sp
+            kst = side if on_side else None
+            pname = "partial_side" if on_side else "partial"
+            e0 = tick(kst)
             if kind == "cont":
                 npart = lib.tpe_score_partials(hjp, nj)
                 d_part = self._buf("partial", 32 * max(npart, 1))
@@ -681,6 +715,11 @@ class Engine:
                                             d_rh, d_rl, d_wide, d_tsc, d_tab, d_cells, d_stats,
                                             sp), "tpe_table_build")
                 tock("table_build", e0)
+                if not joined and self.side_stream == "2":
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    stream.wait_event(ev)
+                    joined = True
                 e0 = tick()
                 L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32, d_tab,
                                             d_cells, d_cand, d_bl, d_al, d_x, d_part, npart, db,
@@ -692,36 +731,40 @@ class Engine:
                 d_first = self._buf("lat_first", 8 * lat_off)
                 d_cnt = self._buf("lat_cnt", 8 * nj)
                 L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_slot,
-                                               d_err, sp), "tpe_lattice_sample")
-                L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt, sp),
+                                               d_err, ks), "tpe_lattice_sample")
+                L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt, ks),
                         "tpe_lattice_compact")
                 max_vals = int(hj["lat_n"].max())
                 npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_part = self._buf(pname, 32 * max(npart, 1))
                 L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_vals,
                                                 d_first, d_cnt, max_vals, None, None, d_part,
-                                                npart, db, d_err, sp), "tpe_score_quantized")
+                                                npart, db, d_err, ks), "tpe_score_quantized")
             elif kind in ("qfb", "qinj"):
                 vals = d_cand
                 if kind == "qfb":
                     vals = self._buf("q_cand", 8 * max(qfb_off, 1))
                     L.check(lib.tpe_sample(base + o_fb, fb_jobs.ctypes.data_as(ctypes.c_void_p),
-                                           nj, d_segs, d_mu, d_sig, d_cdf, 64, vals, sp),
+                                           nj, d_segs, d_mu, d_sig, d_cdf, 64, vals, ks),
                             "tpe_sample")
                 max_vals = int(hj["n_cand"].max())
                 npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_part = self._buf(pname, 32 * max(npart, 1))
                 L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, vals, None,
                                                 None, max_vals, d_bl, d_al, d_part, npart, db,
-                                                d_err, sp), "tpe_score_quantized")
+                                                d_err, ks), "tpe_score_quantized")
             else:
                 npart = lib.tpe_categorical_partials(hjp, nj)
-                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_part = self._buf(pname, 32 * max(npart, 1))
                 L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf, d_cand,
-                                                  d_bl, d_al, d_x, d_part, npart, db, sp),
+                                                  d_bl, d_al, d_x, d_part, npart, db, ks),
                         "tpe_score_categorical")
-            tock(kind, e0)
+            tock(kind, e0, kst)
 
+        if not joined:  # join before the readback
+            ev = torch.cuda.Event()
+            ev.record(side)
+            stream.wait_event(ev)
         _hmark('score launches')
         # ---- results (one device->host copy; syncs the stream) --------------------
         with torch.cuda.stream(stream):
