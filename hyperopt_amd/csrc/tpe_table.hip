@@ -26,7 +26,8 @@
 // e^{a+b} sum_{n>=10} c~_n 1.05^n (a = 1.05|A|, b = 1.05^2|B|); over
 // 9|A| + 65|B| <= 5.8 its maximum is 8.6e-8.  P_0..P_5 are stored in fp32 and
 // P_6..P_9 in fp16 (|P_n| <= e^{a+b} c~_n P_0, P_0 >= 1): the rounding adds at
-// most 1.4e-7 (tools/table_bounds.py evaluates both maxima).
+// most 1.4e-7; the scorer evaluates that fp16 tail in fp16 arithmetic, which
+// adds at most 5.8e-7 (tools/table_bounds.py evaluates the three maxima).
 // Components whose largest term anywhere in the candidate range is below
 // exp(-25)/M of the prior component's smallest term there (a lower bound of S
 // everywhere) are left out (together < 1.4e-11 of S); the rest are found per
@@ -494,24 +495,24 @@ __device__ __forceinline__ void static_for(F& f) {
   }
 }
 
-__device__ __forceinline__ float half_lo(uint32_t d) {
-  return (float)__builtin_bit_cast(_Float16, (unsigned short)(d & 0xFFFFu));
-}
-__device__ __forceinline__ float half_hi(uint32_t d) {
-  return (float)__builtin_bit_cast(_Float16, (unsigned short)(d >> 16));
-}
-
 // both mixtures' degree-9 polynomials at u: q0..q2 = fp32 pairs
-// (b_2k, a_2k, b_2k+1, a_2k+1), q3 = fp16 pairs {b_n | a_n} for n = 6..9; the
-// fp32 steps are packed FMAs (v_pk_fma_f32) on adjacent registers
+// (b_2k, a_2k, b_2k+1, a_2k+1), q3 = fp16 pairs {b_n | a_n} for n = 6..9.  The
+// fp16 tail P_6 + u(P_7 + u(P_8 + u P_9)) is evaluated in packed fp16
+// (v_pk_fma_f16, both mixtures per instruction; its rounding is bounded in
+// tools/table_bounds.py), the fp32 steps are packed FMAs (v_pk_fma_f32) on
+// adjacent registers
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void horner10x2(const f4 q0, const f4 q1, const f4 q2, const f4 q3,
                                            float u, float& pb, float& pa) {
-  const uint32_t d6 = __float_as_uint(q3.x), d7 = __float_as_uint(q3.y),
-                 d8 = __float_as_uint(q3.z), d9 = __float_as_uint(q3.w);
-  float b = half_lo(d9), a = half_hi(d9);
+  const h2_t c6 = __builtin_bit_cast(h2_t, q3.x), c7 = __builtin_bit_cast(h2_t, q3.y),
+             c8 = __builtin_bit_cast(h2_t, q3.z), c9 = __builtin_bit_cast(h2_t, q3.w);
+  const _Float16 uh = (_Float16)u;
+  const h2_t uu = {uh, uh};
+  h2_t t = __builtin_elementwise_fma(c9, uu, c8);
+  t = __builtin_elementwise_fma(t, uu, c7);
+  t = __builtin_elementwise_fma(t, uu, c6);
+  float b = (float)t.x, a = (float)t.y;
 #define TPE_H2(cb, ca) b = fmaf(b, u, cb); a = fmaf(a, u, ca);
-  TPE_H2(half_lo(d8), half_hi(d8)) TPE_H2(half_lo(d7), half_hi(d7))
-  TPE_H2(half_lo(d6), half_hi(d6))
   TPE_H2(q2.z, q2.w) TPE_H2(q2.x, q2.y) TPE_H2(q1.z, q1.w) TPE_H2(q1.x, q1.y)
   TPE_H2(q0.z, q0.w) TPE_H2(q0.x, q0.y)
 #undef TPE_H2
@@ -849,7 +850,10 @@ extern "C" int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, in
     hipLaunchKernelGGL(k_score_table<true>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
                        c, tables, cells, cand, out_bl, out_al, out_x, partial, s);
   else
-    hipLaunchKernelGGL(k_score_table<false>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
+#ifndef TPE_DIAG_EXTRA_LDS  // diagnostic builds: dynamic LDS padding to lower occupancy
+#define TPE_DIAG_EXTRA_LDS 0
+#endif
+    hipLaunchKernelGGL(k_score_table<false>, grid, dim3(kBS), TPE_DIAG_EXTRA_LDS, st, jobs, segs, mu, sigma, wcdf,
                        c, tables, cells, cand, out_bl, out_al, out_x, partial, s);
   hipLaunchKernelGGL(k_reduce_t, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
   return check_launch("tpe_score_table");

@@ -5,7 +5,11 @@ coefficients of exp(|A| u + |B| u^2) (same recurrence, all terms positive).
 On |u| <= 1.05 and over the admissible set 9|A| + 65|B| <= 5.8 this prints
   * the truncation bound  e^{a+b} sum_{n>=P} c~_n 1.05^n   (a = 1.05|A|, b = 1.05^2|B|)
   * the fp16 rounding bound of the stored P_6..P_{P-1}: 2^-11 e^{a+b} sum c~_n 1.05^n
-both relative to the mixture density (every term positive, P_0 >= 1).
+  * the fp16 Horner bound of the tail P_6 + u(P_7 + u(P_8 + u P_9)), evaluated
+    in fp16 (u rounded to fp16, one rounding per packed FMA): a relative error
+    of (k + n - 6) 2^-11 on term n for k = P-6 FMAs, i.e.
+    2^-11 e^{a+b} sum_n (n - 6 + P - 6) c~_n 1.05^n
+all relative to the mixture density (every term positive, P_0 >= 1).
 
     python tools/table_bounds.py [P] [n_fp32]
 """
@@ -22,20 +26,22 @@ def majorant(a, b, n_terms=60):
 
 
 def bounds(P=10, n32=6, lim=5.8, ulim=1.05, steps=801):
-    trunc = fp16 = 0.0
+    trunc = fp16 = horner = 0.0
     for t in np.linspace(0.0, 1.0, steps):
         A, B = t * lim / 9.0, (1.0 - t) * lim / 65.0
         a, b = A * ulim, B * ulim * ulim
         c = majorant(a, b)
         e = np.exp(a + b)
         trunc = max(trunc, e * c[P:].sum())
+        n = np.arange(n32, P)
         fp16 = max(fp16, e * 2.0 ** -11 * c[n32:P].sum())
-    return trunc, fp16
+        horner = max(horner, e * 2.0 ** -11 * ((n - n32 + P - n32) * c[n32:P]).sum())
+    return trunc, fp16, horner
 
 
 if __name__ == "__main__":
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     n32 = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-    tr, h = bounds(P, n32)
-    print("P=%d (fp32 terms %d): truncation <= %.2e, fp16 rounding <= %.2e, total <= %.2e"
-          % (P, n32, tr, h, tr + h))
+    tr, h, hh = bounds(P, n32)
+    print("P=%d (fp32 terms %d): truncation <= %.2e, fp16 storage <= %.2e, fp16 Horner <= %.2e, "
+          "total <= %.2e" % (P, n32, tr, h, hh, tr + h + hh))
