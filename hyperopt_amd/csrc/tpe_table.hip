@@ -16,18 +16,18 @@
 // and exp(A u + B u^2) = sum_n c_n u^n with c_0 = 1, c_1 = A,
 // (n+1) c_{n+1} = A c_n + 2B c_{n-1}.  So on the cell
 //     S(y) = exp(m) * sum_{n<kP} P_n u^n,  P_n = sum_j exp(l_j(y0) - m) c_n^(j),
-// a degree-9 polynomial per cell and mixture: the per-candidate work is two
+// a degree-8 polynomial per cell and mixture: the per-candidate work is two
 // Horner evaluations and two logs, independent of the number of components.
 //
 // Error.  Every term is positive, so the relative error of S is at most the
 // worst relative error of one component's truncated series.  |c_n| is at most
 // the coefficient c~_n of exp(|A|u + |B|u^2) (same recurrence, all terms
 // positive), so for |u| <= 1.05 the truncation error is at most
-// e^{a+b} sum_{n>=10} c~_n 1.05^n (a = 1.05|A|, b = 1.05^2|B|); over
-// 9|A| + 65|B| <= 5.8 its maximum is 8.6e-8.  P_0..P_5 are stored in fp32 and
-// P_6..P_9 in fp16 (|P_n| <= e^{a+b} c~_n P_0, P_0 >= 1): the rounding adds at
+// e^{a+b} sum_{n>=9} c~_n 1.05^n (a = 1.05|A|, b = 1.05^2|B|); over
+// 9|A| + 65|B| <= 5.8 its maximum is 4.3e-7.  P_0..P_5 are stored in fp32 and
+// P_6..P_8 in fp16 (|P_n| <= e^{a+b} c~_n P_0, P_0 >= 1): the rounding adds at
 // most 1.4e-7; the scorer evaluates that fp16 tail in fp16 arithmetic, which
-// adds at most 5.8e-7 (tools/table_bounds.py evaluates the three maxima).
+// adds at most 4.4e-7 (tools/table_bounds.py 9 evaluates the three maxima).
 // Components whose largest term anywhere in the candidate range is below
 // exp(-25)/M of the prior component's smallest term there (a lower bound of S
 // everywhere) are left out (together < 1.4e-11 of S); the rest are found per
@@ -38,13 +38,16 @@
 // fp32 log-sum-exp over all components.  Candidates outside the grid
 // (injected values, rounding at the edges) take the exact path too.
 //
-// Layout.  One tpe_table per job plus one 128-B line per cell, of which the
-// scorer gathers the first 80 B (five 16-B chunks):
+// Layout.  One tpe_table per job plus a 128-B slot per cell: the job's region
+// holds tbl_cap 64-B cells (four 16-B chunks, the scorer's whole gather), then
+// tbl_cap (m_below, m_above) fp32 pairs (per-candidate outputs only):
 //     floats [2n], [2n+1]: below / above P_n, n < 6                  chunks 0-2
-//     dword 12 + (n - 6): fp16 {below P_n (low half), above P_n}, n = 6..9   chunk 3
-//     [16] m_below  [17] m_above  [18] y0  [19] flags (bit 0 below, bit 1 above failed)
-// The pairs (below P_n, above P_n) sit in adjacent registers for packed-FP32
-// Horner.
+//     dword 12 + (n - 6): fp16 {below P_n (low half), above P_n}, n = 6..8
+//     [15] m_below - m_above (the score offset); NaN marks a cell that failed
+//          the bound                                                  chunk 3
+// The cell centre is not stored: both sides form it from the cell index
+// (cell_centre).  The pairs (below P_n, above P_n) sit in adjacent registers
+// for packed-FP32 Horner.
 #include <algorithm>
 #include <type_traits>
 
@@ -53,10 +56,11 @@
 
 namespace tpe {
 namespace {
-constexpr int kP = 10;               // expansion terms per cell and mixture
+constexpr int kP = 9;                // expansion terms per cell and mixture
 constexpr int kP32 = 6;              // of which stored in fp32 (the rest in fp16)
-constexpr int kCellF = 32;           // floats per cell (line stride)
-constexpr int kChunks = 5;           // 16-B chunks of a cell the scorer reads
+constexpr int kCellF = 16;           // floats per cell (64 B: four 16-B chunks)
+constexpr int kSlotB = 128;          // bytes per cell slot of a job's region (cells + m pairs)
+constexpr int kChunks = 4;           // 16-B chunks of a cell the scorer reads
 constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
 constexpr double kTauExtra = 25.0;   // exclusion margin (nats) on top of log(M)
 constexpr double kDrawZ = 5.8;       // |z| of an fp32 Box-Muller draw is < 5.77
@@ -275,6 +279,11 @@ struct Grid {
   int nb;
 };
 
+// centre of cell c, rounded to fp32 (the build expands around exactly this
+// point; the scorer recomputes it from the cell index with the same ops)
+__device__ __forceinline__ double cell_centre(double origin, double h, int c) {
+  return (double)(float)(origin + (double)(2 * c + 1) * h);
+}
 __device__ __forceinline__ Grid grid_of(const tpe_table& Tb, int64_t cap) {
   const double span = Tb.hi - Tb.lo;
   double hn = fmin(Tb.h_below, Tb.h_above);
@@ -356,7 +365,7 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
                                           const double* __restrict__ reach_lo,
                                           const int32_t* __restrict__ wide_idx, int n_wide,
                                           double T, double y0, double h, float* cell,
-                                          int mix) {
+                                          int mix, double& m_out) {
   const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
   const int pos = S.prior_pos;
@@ -441,7 +450,7 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     else
       reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (lane - kP32) + mix] = (_Float16)v;
   }
-  if (lane == 0) cell[2 * kP32 + (kP - kP32) + mix] = (float)m0;
+  m_out = m0;
   return bad;
 }
 
@@ -466,17 +475,21 @@ __global__ __launch_bounds__(kBS) void k_table_build(
   const int wid = threadIdx.x / kWave;
   for (int64_t c = (int64_t)blockIdx.x * (kBS / kWave) + wid; c < g.nb;
        c += (int64_t)gridDim.x * (kBS / kWave)) {
-    const double y0 = (double)(float)(g.origin + (double)(2 * c + 1) * g.h);
-    float* out = cells + (J.tbl_off + c) * kCellF;
+    const double y0 = cell_centre(g.origin, g.h, (int)c);
+    float* region = cells + J.tbl_off * (kSlotB / 4);
+    float* out = region + c * kCellF;
+    double mb, ma;
     const bool bb = build_mix(SB, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below,
-                              Tb.T_below, y0, g.h, out, 0);
+                              Tb.T_below, y0, g.h, out, 0, mb);
     const bool ba = build_mix(SA, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above,
-                              Tb.T_above, y0, g.h, out, 1);
+                              Tb.T_above, y0, g.h, out, 1, ma);
     if (lane_id() == 0) {
-      const int flags = (bb ? 1 : 0) | (ba ? 2 : 0);
-      out[18] = (float)y0;
-      out[19] = __int_as_float(flags);
-      if (flags && stats) atomicAdd(stats + 1, 1ull);
+      // dword 15: the score offset m_below - m_above, NaN marks a failed cell
+      out[15] = (bb || ba) ? __int_as_float(0x7FC00000) : (float)(mb - ma);
+      float* mp = region + (int64_t)J.tbl_cap * kCellF + 2 * c;  // (m_below, m_above)
+      mp[0] = (float)mb;
+      mp[1] = (float)ma;
+      if ((bb || ba) && stats) atomicAdd(stats + 1, 1ull);
     }
   }
 }
@@ -495,21 +508,21 @@ __device__ __forceinline__ void static_for(F& f) {
   }
 }
 
-// both mixtures' degree-9 polynomials at u: q0..q2 = fp32 pairs
-// (b_2k, a_2k, b_2k+1, a_2k+1), q3 = fp16 pairs {b_n | a_n} for n = 6..9.  The
-// fp16 tail P_6 + u(P_7 + u(P_8 + u P_9)) is evaluated in packed fp16
-// (v_pk_fma_f16, both mixtures per instruction; its rounding is bounded in
-// tools/table_bounds.py), the fp32 steps are packed FMAs (v_pk_fma_f32) on
-// adjacent registers
+// both mixtures' degree-8 polynomials at u: q0..q2 = fp32 pairs
+// (b_2k, a_2k, b_2k+1, a_2k+1), q3 = fp16 pairs {b_n | a_n} for n = 6..8 (and
+// the score offset in q3.w).  The fp16 tail P_6 + u(P_7 + u P_8) is evaluated
+// in packed fp16 (v_pk_fma_f16, both mixtures per instruction; its rounding is
+// bounded in tools/table_bounds.py), the fp32 steps are packed FMAs
+// (v_pk_fma_f32) on adjacent registers
 typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void horner10x2(const f4 q0, const f4 q1, const f4 q2, const f4 q3,
-                                           float u, float& pb, float& pa) {
+__device__ __forceinline__ void horner9x2(const f4 q0, const f4 q1, const f4 q2, const f4 q3,
+                                          float u, float& pb, float& pa) {
+  static_assert(kP == 9 && kP32 == 6, "six fp32 and three fp16 terms");
   const h2_t c6 = __builtin_bit_cast(h2_t, q3.x), c7 = __builtin_bit_cast(h2_t, q3.y),
-             c8 = __builtin_bit_cast(h2_t, q3.z), c9 = __builtin_bit_cast(h2_t, q3.w);
+             c8 = __builtin_bit_cast(h2_t, q3.z);
   const _Float16 uh = (_Float16)u;
   const h2_t uu = {uh, uh};
-  h2_t t = __builtin_elementwise_fma(c9, uu, c8);
-  t = __builtin_elementwise_fma(t, uu, c7);
+  h2_t t = __builtin_elementwise_fma(c8, uu, c7);
   t = __builtin_elementwise_fma(t, uu, c6);
   float b = (float)t.x, a = (float)t.y;
 #define TPE_H2(cb, ca) b = fmaf(b, u, cb); a = fmaf(a, u, ca);
@@ -550,12 +563,12 @@ __global__ __launch_bounds__(kBS) void k_score_table(
     double* __restrict__ out_x, tpe_best* __restrict__ partial,
     unsigned long long* __restrict__ stats) {
   __shared__ MixLds s_mix;
-  // per wave: 8 DMA slabs of 64 x 16 B, the gather's LDS image; also the
+  // per wave: 4 DMA slabs of 64 x 16 B, the gather's LDS image; also the
   // sampler's staging buffer before scoring
-  __shared__ float4 s_rows[(kBS / kWave) * kWave * 8];
+  __shared__ float4 s_rows[(kBS / kWave) * kWave * kChunks];
   __shared__ BestT red[kBS / kWave];
   __shared__ int nred[kBS / kWave];
-  static_assert(kTR * kWave * sizeof(float) <= kWave * 8 * sizeof(float4), "staging alias");
+  static_assert(kTR * kWave * sizeof(float) <= kWave * kChunks * sizeof(float4), "staging alias");
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t base0 = (int64_t)blockIdx.x * kTiles * kTile;
@@ -571,12 +584,14 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   const float g0 = (float)Tb.origin, inv_w = Tb.inv_w, inv_h = Tb.inv_h;
   const int nb = Tb.nb;
   // the job's cell table: a uniform base + 32-bit byte offsets (saddr loads)
-  const char* cbase = reinterpret_cast<const char*>(cells) + J.tbl_off * (kCellF * 4);
-  const int lane = lane_id(), gi = lane & 7, gbase = lane & ~7;
+  const char* cbase = reinterpret_cast<const char*>(cells) + J.tbl_off * kSlotB;
+  const float* mpairs = reinterpret_cast<const float*>(cbase) + J.tbl_cap * kCellF;
+  const double g0d = Tb.origin, hd = Tb.h;
+  const int lane = lane_id(), gi = lane & (kChunks - 1), gbase = lane & ~(kChunks - 1);
   // wave-uniform (scalar) base of the wave's LDS region: the DMA destinations need no
   // per-instruction readfirstlane
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  float4* rows = s_rows + wave * (kWave * 8);
+  float4* rows = s_rows + wave * (kWave * kChunks);
   const bool outs = out_bl || out_al || out_x;
   Mix M{};
 #ifndef TPE_DIAG_SKIP_SAMPLE
@@ -636,22 +651,20 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
       co[r] = (uint32_t)min(c, nb - 1) * (kCellF * 4);
     }
-    // Cooperative gather by LDS-DMA: lane gi of each 8-lane group fetches one
-    // 16-B chunk of every group member's cell (global_load_lds_dwordx4), so a
-    // wave-instruction touches 8 cache lines instead of 64 and the data lands
+    // Cooperative gather by LDS-DMA: lane gi of each 4-lane group fetches one
+    // 16-B chunk of every group member's 64-B cell (global_load_lds_dwordx4),
+    // so a wave-instruction touches 16 cells instead of 64 and the data lands
     // in LDS without passing through VGPRs.  Slab j holds member j's cells:
     // lane (g, gi) brings chunk gi^j, so lane (g, j) reads its chunk k from
-    // slab j, slot 8g + (k^j) -- conflict-free ds_read_b128.  Candidate r+1's
+    // slab j, slot 4g + (k^j) -- conflict-free ds_read_b128.  Candidate r+1's
     // DMA is issued as soon as candidate r's chunks are in registers, and runs
     // under r's polynomial work.
     typedef __attribute__((address_space(3))) void* lds_vp;
     typedef const __attribute__((address_space(1))) void* glb_vp;
     auto fetch = [&](int r) __attribute__((always_inline)) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < kChunks; ++j) {
         const uint32_t cj = __shfl(co[r], gbase | j, kWave);
-        // (lanes whose chunk gi^j >= kChunks bring bytes of the same line nobody
-        // reads: cheaper than masking them)
         __builtin_amdgcn_global_load_lds((glb_vp)(cbase + (cj + ((gi ^ j) * 16))),
                                          (lds_vp)(rows + j * kWave), 16, 0, 0);
       }
@@ -663,24 +676,27 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       // candidate r's DMA has landed (the compiler does not order LDS-DMA
       // writes before later ds_reads by itself)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      static_assert(kChunks == 5, "the reads below take chunks 0..4");
+      static_assert(kChunks == 4, "the reads below take chunks 0..3");
       const f4 q0 = slab[gbase | gi], q1 = slab[gbase | (1 ^ gi)], q2 = slab[gbase | (2 ^ gi)],
-               q3 = slab[gbase | (3 ^ gi)], q4 = slab[gbase | (4 ^ gi)];
+               q3 = slab[gbase | (3 ^ gi)];
       // the reads must land before the next candidate's DMA overwrites the slabs
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       if constexpr (r + 1 < kTR) fetch(r + 1);
-      const float u = (y - q4.z) * inv_h;
+      const int cell = (int)(co[r] / (kCellF * 4));
+      const float u = (y - (float)cell_centre(g0d, hd, cell)) * inv_h;
       float pb, pa;
-      horner10x2(q0, q1, q2, q3, u, pb, pa);
-      const float lb = q4.x + __builtin_amdgcn_logf(pb) * kLn2T;
-      const float la = q4.y + __builtin_amdgcn_logf(pa) * kLn2T;
+      horner9x2(q0, q1, q2, q3, u, pb, pa);
+      const float dlog = (__builtin_amdgcn_logf(pb) - __builtin_amdgcn_logf(pa)) * kLn2T;
       const bool valid = t0 + r < J.n_cand;
-      const bool ok = (__float_as_int(q4.w) == 0) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f);
+      // q3.w: m_below - m_above, NaN for a cell that failed the bound
+      const bool ok = (q3.w == q3.w) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f);
       exact_mask |= (valid && !ok) ? (1u << r) : 0u;
       if (valid && ok) {
-        if (outs) outputs(lb, la, y, r);
+        if (outs)
+          outputs(mpairs[2 * cell] + __builtin_amdgcn_logf(pb) * kLn2T,
+                  mpairs[2 * cell + 1] + __builtin_amdgcn_logf(pa) * kLn2T, y, r);
         // table scores are finite: strict > keeps the first of equal scores
-        const float sc = lb - la;
+        const float sc = q3.w + dlog;
         const bool take = sc > bs;
         bs = take ? sc : bs;
         by = take ? (INJ ? x[r] : y) : by;

@@ -254,11 +254,12 @@ int tpe_score_sorted(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
  * every component that can reach 2^-36 of the sum on that cell
  * (tpe_table_build).  Each component's factor exp(A u + B u^2) is expanded
  * only where 9|A| + 65|B| <= 5.8, which bounds the truncation error of the
- * whole sum by 6e-9 relative (Cauchy estimate).  A
- * candidate whose cell fails the bound, or that lies outside the grid, is
+ * degree-8 series by 1.0e-6 relative (Cauchy estimate).
+ * A candidate whose cell fails the bound, or that lies outside the grid, is
  * scored by the exact fp32 log-sum-exp over all components instead.
- * tables: one tpe_table per job (device); cells: float pool, 32 floats per
- * cell at 32 * (job.tbl_off + c); reach_hi / reach_lo: fp64 per-component
+ * tables: one tpe_table per job (device); cells: byte pool, 128 B per cell
+ * slot: job j's region starts at 128 * job.tbl_off and holds tbl_cap 64-B
+ * cells, then tbl_cap (m_below, m_above) fp32 pairs; reach_hi / reach_lo: fp64 per-component
  * workspace (size of the mixture pool); wide_idx: int32, same size.
  * stats (nullable, 2 x u64): [0] candidates scored by the exact fallback,
  * [1] cells that failed the bound. */

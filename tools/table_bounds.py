@@ -40,7 +40,7 @@ def bounds(P=10, n32=6, lim=5.8, ulim=1.05, steps=801):
 
 
 if __name__ == "__main__":
-    P = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 9
     n32 = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     tr, h, hh = bounds(P, n32)
     print("P=%d (fp32 terms %d): truncation <= %.2e, fp16 storage <= %.2e, fp16 Horner <= %.2e, "
