@@ -35,7 +35,7 @@ T_HIST = 10_000
 N_CAND = 1 << 22
 FP32_PEAK_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 FLOPS_PER_PAIR = 9  # unquantized GMM1/LGMM1 pair
-OPS_PER_TABLE_CAND = 97  # cell-table scorer (degree-9 cells), per candidate
+OPS_PER_TABLE_CAND = 97  # cell-table scorer (degree-8 cells), per candidate
 DIRECT_PAIR_CEILING = 9.81e12  # pairs/s of the exp-bound direct loop (profiles/r01_valu_microbench.txt)
 
 
@@ -320,7 +320,7 @@ def main():
     sec = avg_ms * 1e-3
     if group == "table":
         # algorithmic operations per candidate of the
-        # cell-table scorer (sample + cell lookup + two degree-9 polynomials)
+        # cell-table scorer (sample + cell lookup + two degree-8 polynomials)
         ops = OPS_PER_TABLE_CAND * n_cont
         work = {"ops_per_candidate": OPS_PER_TABLE_CAND, "candidates_per_launch": n_cont}
     else:
@@ -353,7 +353,7 @@ def main():
                 "valu_busy": prof.get("valu_busy"), "traffic_source": prof.get("source")}
     roofline.update(work)
     if group == "table":
-        roofline["l2_gather_bytes_per_launch"] = 128 * n_cont
+        roofline["l2_gather_bytes_per_launch"] = 64 * n_cont  # one 64-B cell per candidate
         roofline["build_ms"] = group_ms.get("table_build")
     line = {
         "metric": "EI candidates scored/sec (50-dim, 10k trials)",

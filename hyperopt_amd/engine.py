@@ -217,6 +217,7 @@ class Engine:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
         self._bufs = {}
+        self._plans = {}  # level structure -> static descriptor arrays (_plan_record)
         self._retired = []
         self._pinned = {}
         self.host_marks = None  # set to a list to record host-side phase times (diagnostic)
@@ -259,6 +260,89 @@ class Engine:
         with torch.cuda.stream(stream):
             dst[:pack.size].copy_(pinned[:pack.size], non_blocking=True)
         return dev
+
+    # -- level plans -----------------------------------------------------------
+    # A level's descriptor arrays (segments, categorical segments, gathers,
+    # jobs) depend on the level's structure -- kinds, prior arguments,
+    # candidate counts, history columns, lattice ranges, run options -- and,
+    # per call, only on the observation counts and the Philox keys.  The first
+    # call of a structure builds them in Python; later calls copy the recorded
+    # arrays and fill the per-call columns with a few vectorised operations.
+    def _plan_key(self, works, prior_weight, lf, precision, scorer, outputs, sample_only,
+                  hist_mode, multi):
+        if not hist_mode or outputs or sample_only:
+            return None
+        parts = []
+        for w in works:
+            if w.cand is not None or w.kind not in CONTINUOUS + CATEGORICAL:
+                return None
+            lat = None
+            if w.kind in CONTINUOUS and w.kind.startswith("q"):
+                P = _params(w.kind, w.args)
+                if not P["bounded"]:  # the lattice range follows the below set
+                    lat = _lattice_range(w, P)
+            parts.append((w.kind, w.args, int(w.n_cand), w.col, w.hist, lat))
+        key = (tuple(parts), float(prior_weight), int(lf), int(precision), scorer, multi)
+        try:
+            hash(key)
+        except TypeError:  # unhashable prior arguments (e.g. a probability list)
+            return None
+        if len(self._plans) > 64:
+            self._plans.clear()
+        return key
+
+    def _plan_record(self, works, cont, quant, cat, fit_ids, params, segs, csegs, p_pool,
+                     cat_meta, lat_ranges, fallback, modes, groups, order, gathers, jobs,
+                     fb_slice, out_off, lat_off, qfb_off, sort_off, cnt_off, tbl_off):
+        g = np.zeros(len(gathers), L.GATHER_DTYPE)
+        if gathers:
+            (g["col"], g["below"], g["dst_off"], g["offset"], g["count"], g["to_int"],
+             g["hist"]) = (np.array(c) for c in zip(*gathers))
+        return dict(cont=cont, quant=quant, cat=cat, fit_ids=fit_ids, params=params,
+                    segs=segs.copy(), csegs=csegs.copy(), p_pool=p_pool.copy(),
+                    cat_meta=cat_meta, lat_ranges=lat_ranges, fallback=fallback, modes=modes,
+                    groups=groups, order=order, g=g, jobs=jobs.copy(), fb_slice=fb_slice,
+                    counts=(out_off, lat_off, qfb_off, sort_off, cnt_off, tbl_off))
+
+    def _plan_fast(self, P, works):
+        fit_ids, cat = P["fit_ids"], P["cat"]
+        nf = len(fit_ids)
+        segs = P["segs"].copy()
+        sizes = np.empty(2 * nf, np.int64)
+        sizes[0::2] = [np.size(works[i].obs_below) for i in fit_ids]
+        sizes[1::2] = [works[i].n_above for i in fit_ids]
+        ends = np.cumsum(sizes)
+        obs_off = ends - sizes
+        segs["obs_off"], segs["n_obs"] = obs_off, sizes
+        segs["comp_off"] = np.cumsum(sizes + 1) - (sizes + 1)
+        n_obs_total = int(ends[-1]) if nf else 0
+        n_comp = n_obs_total + 2 * nf
+        max_obs = int(sizes.max()) if nf else 0
+        csegs = P["csegs"].copy()
+        csizes = np.empty(2 * len(cat), np.int64)
+        csizes[0::2] = [np.size(works[i].obs_below) for i in cat]
+        csizes[1::2] = [works[i].n_above for i in cat]
+        cends = np.cumsum(csizes)
+        coff = cends - csizes
+        csegs["obs_off"], csegs["n_obs"] = coff, csizes
+        cobs_off = int(cends[-1]) if cat else 0
+        g_arr = P["g"].copy()
+        g_arr["dst_off"] = np.concatenate([obs_off, coff])
+        g_arr["count"] = np.concatenate([sizes, csizes])
+        return (P["cont"], P["quant"], cat, fit_ids, P["params"], nf, segs, np.zeros(1),
+                n_obs_total, n_comp, max_obs, csegs, np.zeros(1, np.int64), P["p_pool"],
+                P["cat_meta"], cobs_off, P["lat_ranges"], P["fallback"], P["modes"],
+                P["groups"], P["order"], g_arr)
+
+    def _jobs_fast(self, P, works):
+        order = P["order"]
+        jobs = P["jobs"].copy()
+        jobs["key"] = [int(works[i].key) & 0xFFFFFFFFFFFFFFFF for i in order]
+        jobs["cand_base"] = [works[i].cand_base for i in order]
+        a, b = P["fb_slice"]
+        fb_jobs = jobs[a:b].copy()
+        fb_jobs["out_off"] = fb_jobs["cand_off"]
+        return (jobs, np.zeros(1), fb_jobs, P["fb_slice"]) + tuple(P["counts"])
 
     # -- main entry ----------------------------------------------------------
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
@@ -316,146 +400,156 @@ class Engine:
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        cont, quant, cat = [], [], []
-        for i, w in enumerate(works):
-            if w.kind in CONTINUOUS:
-                (quant if w.kind.startswith("q") else cont).append(i)
-            elif w.kind in CATEGORICAL:
-                cat.append(i)
-            else:
-                raise ValueError("unsupported prior %r for label %r" % (w.kind, w.label))
-
-        _hmark('prep')
-        pack = _Pack()
         if history is not None and histories is not None:
             raise ValueError("give either history or histories")
         hist_mode = history is not None or histories is not None
-        gathers = []  # history mode: (col, below, dst_off, offset, count, to_int, hist)
-        # ---- continuous / quantized segments --------------------------------
-        fit_ids = cont + quant
-        params = {i: _params(works[i].kind, works[i].args) for i in fit_ids}
-        nf = len(fit_ids)
-        segs = np.zeros(2 * nf, L.SEG_DTYPE)
-        obs_pool = None
-        n_obs_total = n_comp = max_obs = 0
-        if nf:
-            if hist_mode:
-                sizes = np.empty(2 * nf, np.int64)
-                for si, i in enumerate(fit_ids):
-                    sizes[2 * si] = np.asarray(works[i].obs_below).size
-                    sizes[2 * si + 1] = int(works[i].n_above)
-            else:
-                parts = [np.asarray(o, dtype=np.float64).reshape(-1) for i in fit_ids
-                         for o in (works[i].obs_below, works[i].obs_above)]
-                sizes = np.fromiter((o.size for o in parts), np.int64, 2 * nf)
-                obs_pool = np.concatenate(parts)
-            ends = np.cumsum(sizes)
-            obs_off = ends - sizes
-            comp_off = np.cumsum(sizes + 1) - (sizes + 1)
-            segs["obs_off"], segs["comp_off"], segs["n_obs"] = obs_off, comp_off, sizes
-            segs["lf"], segs["prior_weight"] = lf, prior_weight
-            pl = [params[i] for i in fit_ids]
-            for name in ("transform", "family", "floor", "prior_mu", "prior_sigma", "low", "high"):
-                segs[name] = np.repeat([p[name] for p in pl], 2)
-            segs["bounded"] = np.repeat([int(p["bounded"]) for p in pl], 2)
-            n_obs_total = int(ends[-1])
-            n_comp = n_obs_total + 2 * nf
-            max_obs = int(sizes.max())
-            if hist_mode:
-                for si, i in enumerate(fit_ids):
-                    for half in (0, 1):
-                        k = 2 * si + half
-                        gathers.append((works[i].col, 1 - half, int(obs_off[k]), 0, int(sizes[k]),
-                                        0, works[i].hist))
-        if obs_pool is None:
-            obs_pool = np.zeros(1)
+        pkey = self._plan_key(works, prior_weight, lf, precision, scorer, outputs, sample_only,
+                              hist_mode, histories is not None)
+        cached = self._plans.get(pkey) if pkey is not None else None
+        pack = _Pack()
+        if cached is not None:
+            (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp, max_obs,
+             csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes, groups,
+             order, g_arr) = self._plan_fast(cached, works)
+            inj = lambda i: works[i].cand is not None  # noqa: E731
+        else:
+            cont, quant, cat = [], [], []
+            for i, w in enumerate(works):
+                if w.kind in CONTINUOUS:
+                    (quant if w.kind.startswith("q") else cont).append(i)
+                elif w.kind in CATEGORICAL:
+                    cat.append(i)
+                else:
+                    raise ValueError("unsupported prior %r for label %r" % (w.kind, w.label))
 
-        _hmark('segs')
-        # ---- categorical segments ------------------------------------------
-        csegs = np.zeros(2 * len(cat), L.CAT_SEG_DTYPE)
-        cobs_parts, p_init = [], []
-        cobs_off = p_off = 0
-        cat_meta = {}
-        ccols = []
-        for ci, i in enumerate(cat):
-            w = works[i]
-            K, offset, mode, prior_p = categorical_params(w.kind, w.args)
-            cat_meta[i] = (K, offset)
-            prior_off = -1
-            if mode == 1:
-                prior_off = p_off
-                p_init.append(prior_p)
-                p_off += K
-            for half in (0, 1):
+            _hmark('prep')
+            gathers = []  # history mode: (col, below, dst_off, offset, count, to_int, hist)
+            # ---- continuous / quantized segments --------------------------------
+            fit_ids = cont + quant
+            params = {i: _params(works[i].kind, works[i].args) for i in fit_ids}
+            nf = len(fit_ids)
+            segs = np.zeros(2 * nf, L.SEG_DTYPE)
+            obs_pool = None
+            n_obs_total = n_comp = max_obs = 0
+            if nf:
                 if hist_mode:
-                    n = np.asarray(w.obs_below).size if half == 0 else int(w.n_above)
-                    gathers.append((w.col, 1 - half, cobs_off, offset, n, 1, w.hist))
+                    sizes = np.empty(2 * nf, np.int64)
+                    for si, i in enumerate(fit_ids):
+                        sizes[2 * si] = np.asarray(works[i].obs_below).size
+                        sizes[2 * si + 1] = int(works[i].n_above)
                 else:
-                    obs = np.asarray(w.obs_below if half == 0 else w.obs_above).reshape(-1)
-                    obs = obs.astype(np.int64) - offset
-                    cobs_parts.append(obs)
-                    n = obs.size
-                ccols.append((cobs_off, p_off, n, K, mode, max(prior_off, 0)))
-                p_init.append(np.zeros(K))
-                cobs_off += n
-                p_off += K
-        if cat:  # one column assignment per field instead of per segment
-            cc = np.array(ccols, dtype=np.int64)
-            (csegs["obs_off"], csegs["p_off"], csegs["n_obs"], csegs["n_cat"], csegs["mode"],
-             csegs["prior_p_off"]) = cc.T
-            csegs["lf"], csegs["prior_weight"] = lf, prior_weight
-        cobs_pool = np.concatenate(cobs_parts) if cobs_parts else np.zeros(1, np.int64)
-        p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
+                    parts = [np.asarray(o, dtype=np.float64).reshape(-1) for i in fit_ids
+                             for o in (works[i].obs_below, works[i].obs_above)]
+                    sizes = np.fromiter((o.size for o in parts), np.int64, 2 * nf)
+                    obs_pool = np.concatenate(parts)
+                ends = np.cumsum(sizes)
+                obs_off = ends - sizes
+                comp_off = np.cumsum(sizes + 1) - (sizes + 1)
+                segs["obs_off"], segs["comp_off"], segs["n_obs"] = obs_off, comp_off, sizes
+                segs["lf"], segs["prior_weight"] = lf, prior_weight
+                pl = [params[i] for i in fit_ids]
+                for name in ("transform", "family", "floor", "prior_mu", "prior_sigma", "low", "high"):
+                    segs[name] = np.repeat([p[name] for p in pl], 2)
+                segs["bounded"] = np.repeat([int(p["bounded"]) for p in pl], 2)
+                n_obs_total = int(ends[-1])
+                n_comp = n_obs_total + 2 * nf
+                max_obs = int(sizes.max())
+                if hist_mode:
+                    for si, i in enumerate(fit_ids):
+                        for half in (0, 1):
+                            k = 2 * si + half
+                            gathers.append((works[i].col, 1 - half, int(obs_off[k]), 0, int(sizes[k]),
+                                            0, works[i].hist))
+            if obs_pool is None:
+                obs_pool = np.zeros(1)
 
-        _hmark('cats')
-        # ---- jobs, ordered so every kernel call takes a contiguous slice -----------
-        inj = lambda i: works[i].cand is not None  # noqa: E731
-        lat_ranges = {}
-        fallback = []
-        for i in quant:
-            if not inj(i):
-                kmin, kmax = _lattice_range(works[i], params[i])
-                if kmax - kmin + 1 > LATTICE_CAP:
-                    fallback.append(i)
-                else:
-                    lat_ranges[i] = (kmin, kmax - kmin + 1)
-        def cont_mode(i):
-            if precision != 32 or sample_only:
-                return "cont"
-            n = int(np.asarray(works[i].cand).size) if inj(i) else int(works[i].n_cand)
-            mode = scorer
-            if mode == "auto":
-                mode = "cont"
+            _hmark('segs')
+            # ---- categorical segments ------------------------------------------
+            csegs = np.zeros(2 * len(cat), L.CAT_SEG_DTYPE)
+            cobs_parts, p_init = [], []
+            cobs_off = p_off = 0
+            cat_meta = {}
+            ccols = []
+            for ci, i in enumerate(cat):
+                w = works[i]
+                K, offset, mode, prior_p = categorical_params(w.kind, w.args)
+                cat_meta[i] = (K, offset)
+                prior_off = -1
+                if mode == 1:
+                    prior_off = p_off
+                    p_init.append(prior_p)
+                    p_off += K
+                for half in (0, 1):
+                    if hist_mode:
+                        n = np.asarray(w.obs_below).size if half == 0 else int(w.n_above)
+                        gathers.append((w.col, 1 - half, cobs_off, offset, n, 1, w.hist))
+                    else:
+                        obs = np.asarray(w.obs_below if half == 0 else w.obs_above).reshape(-1)
+                        obs = obs.astype(np.int64) - offset
+                        cobs_parts.append(obs)
+                        n = obs.size
+                    ccols.append((cobs_off, p_off, n, K, mode, max(prior_off, 0)))
+                    p_init.append(np.zeros(K))
+                    cobs_off += n
+                    p_off += K
+            if cat:  # one column assignment per field instead of per segment
+                cc = np.array(ccols, dtype=np.int64)
+                (csegs["obs_off"], csegs["p_off"], csegs["n_obs"], csegs["n_cat"], csegs["mode"],
+                 csegs["prior_p_off"]) = cc.T
+                csegs["lf"], csegs["prior_weight"] = lf, prior_weight
+            cobs_pool = np.concatenate(cobs_parts) if cobs_parts else np.zeros(1, np.int64)
+            p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
+
+            _hmark('cats')
+            # ---- jobs, ordered so every kernel call takes a contiguous slice -----------
+            inj = lambda i: works[i].cand is not None  # noqa: E731
+            lat_ranges = {}
+            fallback = []
+            for i in quant:
                 if not inj(i):
-                    if n >= TABLE_MIN_CAND:
-                        mode = "table"
-                    elif n >= SORTED_MIN_CAND and not outputs:
-                        mode = "sorted"
-            if mode == "sorted" and (inj(i) or outputs):
-                mode = "cont"
-            return "cont" if mode == "dense" else mode
-        modes = {i: cont_mode(i) for i in cont}
-        groups = [
-            ("cont", [i for i in cont if inj(i) and modes[i] == "cont"]),
-            ("cont", [i for i in cont if not inj(i) and modes[i] == "cont"]),
-            ("sorted", [i for i in cont if modes[i] == "sorted"]),
-            ("table", [i for i in cont if inj(i) and modes[i] == "table"]),
-            ("table", [i for i in cont if not inj(i) and modes[i] == "table"]),
-            ("lat", [i for i in quant if i in lat_ranges]),
-            ("qfb", fallback),
-            ("qinj", [i for i in quant if inj(i)]),
-            ("cat", [i for i in cat if inj(i)]),
-            ("cat", [i for i in cat if not inj(i)]),
-        ]
-        order = [i for _, ids in groups for i in ids]
+                    kmin, kmax = _lattice_range(works[i], params[i])
+                    if kmax - kmin + 1 > LATTICE_CAP:
+                        fallback.append(i)
+                    else:
+                        lat_ranges[i] = (kmin, kmax - kmin + 1)
+            def cont_mode(i):
+                if precision != 32 or sample_only:
+                    return "cont"
+                n = int(np.asarray(works[i].cand).size) if inj(i) else int(works[i].n_cand)
+                mode = scorer
+                if mode == "auto":
+                    mode = "cont"
+                    if not inj(i):
+                        if n >= TABLE_MIN_CAND:
+                            mode = "table"
+                        elif n >= SORTED_MIN_CAND and not outputs:
+                            mode = "sorted"
+                if mode == "sorted" and (inj(i) or outputs):
+                    mode = "cont"
+                return "cont" if mode == "dense" else mode
+            modes = {i: cont_mode(i) for i in cont}
+            groups = [
+                ("cont", [i for i in cont if inj(i) and modes[i] == "cont"]),
+                ("cont", [i for i in cont if not inj(i) and modes[i] == "cont"]),
+                ("sorted", [i for i in cont if modes[i] == "sorted"]),
+                ("table", [i for i in cont if inj(i) and modes[i] == "table"]),
+                ("table", [i for i in cont if not inj(i) and modes[i] == "table"]),
+                ("lat", [i for i in quant if i in lat_ranges]),
+                ("qfb", fallback),
+                ("qinj", [i for i in quant if inj(i)]),
+                ("cat", [i for i in cat if inj(i)]),
+                ("cat", [i for i in cat if not inj(i)]),
+            ]
+            order = [i for _, ids in groups for i in ids]
         _hmark('plan')
         # ---- upload -------------------------------------------------------------
         o_segs = pack.add(segs) if segs.size else None
         o_csegs = pack.add(csegs) if csegs.size else None
         o_p = pack.add(p_pool)
         if hist_mode:
-            g_arr = np.zeros(len(gathers), L.GATHER_DTYPE)
-            if gathers:
+            if cached is None:
+                g_arr = np.zeros(len(gathers), L.GATHER_DTYPE)
+            if cached is None and gathers:
                 (g_arr["col"], g_arr["below"], g_arr["dst_off"], g_arr["offset"], g_arr["count"],
                  g_arr["to_int"], g_arr["hist"]) = (np.array(c) for c in zip(*gathers))
             o_g = pack.add(g_arr)
@@ -554,75 +648,85 @@ class Engine:
             return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
                                          d_segs, stream)
 
-        nj_all = len(order)
-        jobs = np.zeros(nj_all, L.JOB_DTYPE)
-        J = {name: np.zeros(nj_all, L.JOB_DTYPE[name]) for name in L.JOB_DTYPE.names}
-        cand_parts, cand_off, out_off, lat_off, qfb_off = [], 0, 0, 0, 0
-        sort_off = cnt_off = tbl_off = 0
-        seg_of = {i: si for si, i in enumerate(fit_ids)}
-        cseg_of = {i: ci for ci, i in enumerate(cat)}
-        for pos, i in enumerate(order):
-            w = works[i]
-            J["key"][pos] = int(w.key) & 0xFFFFFFFFFFFFFFFF
-            J["cand_base"][pos] = w.cand_base
-            n = int(np.asarray(w.cand).size) if inj(i) else int(w.n_cand)
-            J["n_cand"][pos] = n
-            J["out_off"][pos] = out_off
-            out_off += n
-            flags = 0
-            if inj(i):
-                # categorical candidates are category indices (0..K-1), as the
-                # reference's randint_via_categorical samples them (tpe.py:590)
-                c = np.asarray(w.cand, dtype=np.float64).reshape(-1)
-                J["cand_off"][pos] = cand_off
-                cand_parts.append(c)
-                cand_off += c.size
-                flags |= L.F_INJECTED
-            if i in cat_meta:
-                J["family"][pos] = L.CAT
-                J["lat_n"][pos] = cat_meta[i][0]  # category count (sizes the sampler's path)
-                J["below"][pos], J["above"][pos] = 2 * cseg_of[i], 2 * cseg_of[i] + 1
-                J["flags"][pos] = flags
-                continue
-            P = params[i]
-            J["family"][pos] = P["family"]
-            J["below"][pos], J["above"][pos] = 2 * seg_of[i], 2 * seg_of[i] + 1
-            if P["bounded"]:
-                flags |= L.F_LOW | L.F_HIGH
-                J["low"][pos], J["high"][pos] = P["low"], P["high"]
-            if P["q"] is not None:
-                flags |= L.F_QUANT
-                J["q"][pos] = P["q"]
-                if i in lat_ranges:
-                    kmin, nk = lat_ranges[i]
-                    J["lat_off"][pos], J["lat_kmin"][pos], J["lat_n"][pos] = lat_off, kmin, nk
-                    if precision == 32 and max(abs(kmin), abs(kmin + nk - 1)) <= DRAW32_MAX_SLOT:
-                        flags |= L.F_DRAW32
-                    lat_off += nk
-                elif i in fallback:
-                    J["cand_off"][pos] = qfb_off
-                    qfb_off += n
-            elif modes[i] == "table":
-                J["tbl_off"][pos], J["tbl_cap"][pos] = tbl_off, TABLE_CAP
-                tbl_off += TABLE_CAP
+        if cached is not None:
+            (jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off, sort_off, cnt_off,
+             tbl_off) = self._jobs_fast(cached, works)
+        else:
+            nj_all = len(order)
+            jobs = np.zeros(nj_all, L.JOB_DTYPE)
+            J = {name: np.zeros(nj_all, L.JOB_DTYPE[name]) for name in L.JOB_DTYPE.names}
+            cand_parts, cand_off, out_off, lat_off, qfb_off = [], 0, 0, 0, 0
+            sort_off = cnt_off = tbl_off = 0
+            seg_of = {i: si for si, i in enumerate(fit_ids)}
+            cseg_of = {i: ci for ci, i in enumerate(cat)}
+            for pos, i in enumerate(order):
+                w = works[i]
+                J["key"][pos] = int(w.key) & 0xFFFFFFFFFFFFFFFF
+                J["cand_base"][pos] = w.cand_base
+                n = int(np.asarray(w.cand).size) if inj(i) else int(w.n_cand)
+                J["n_cand"][pos] = n
+                J["out_off"][pos] = out_off
+                out_off += n
+                flags = 0
                 if inj(i):
-                    J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P)
-            elif modes[i] == "sorted":
-                J["bin_lo"][pos], J["bin_hi"][pos] = _support(w, P)
-                J["sort_off"][pos], J["cnt_off"][pos] = sort_off, cnt_off
-                slots = ctypes.c_int64(0)
-                cnt_off += lib.tpe_sort_layout(n, ctypes.byref(slots))
-                sort_off += slots.value
-            J["flags"][pos] = flags
-        for name, col in J.items():
-            jobs[name] = col
-        cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
-        # the dense fallback first materialises its draws: a job copy whose
-        # out_off points into the scratch candidate buffer
-        fb_slice = _slice_of(groups, [k for k, _ in groups].index("qfb"))
-        fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
-        fb_jobs["out_off"] = fb_jobs["cand_off"]
+                    # categorical candidates are category indices (0..K-1), as the
+                    # reference's randint_via_categorical samples them (tpe.py:590)
+                    c = np.asarray(w.cand, dtype=np.float64).reshape(-1)
+                    J["cand_off"][pos] = cand_off
+                    cand_parts.append(c)
+                    cand_off += c.size
+                    flags |= L.F_INJECTED
+                if i in cat_meta:
+                    J["family"][pos] = L.CAT
+                    J["lat_n"][pos] = cat_meta[i][0]  # category count (sizes the sampler's path)
+                    J["below"][pos], J["above"][pos] = 2 * cseg_of[i], 2 * cseg_of[i] + 1
+                    J["flags"][pos] = flags
+                    continue
+                P = params[i]
+                J["family"][pos] = P["family"]
+                J["below"][pos], J["above"][pos] = 2 * seg_of[i], 2 * seg_of[i] + 1
+                if P["bounded"]:
+                    flags |= L.F_LOW | L.F_HIGH
+                    J["low"][pos], J["high"][pos] = P["low"], P["high"]
+                if P["q"] is not None:
+                    flags |= L.F_QUANT
+                    J["q"][pos] = P["q"]
+                    if i in lat_ranges:
+                        kmin, nk = lat_ranges[i]
+                        J["lat_off"][pos], J["lat_kmin"][pos], J["lat_n"][pos] = lat_off, kmin, nk
+                        if precision == 32 and max(abs(kmin), abs(kmin + nk - 1)) <= DRAW32_MAX_SLOT:
+                            flags |= L.F_DRAW32
+                        lat_off += nk
+                    elif i in fallback:
+                        J["cand_off"][pos] = qfb_off
+                        qfb_off += n
+                elif modes[i] == "table":
+                    J["tbl_off"][pos], J["tbl_cap"][pos] = tbl_off, TABLE_CAP
+                    tbl_off += TABLE_CAP
+                    if inj(i):
+                        J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P)
+                elif modes[i] == "sorted":
+                    J["bin_lo"][pos], J["bin_hi"][pos] = _support(w, P)
+                    J["sort_off"][pos], J["cnt_off"][pos] = sort_off, cnt_off
+                    slots = ctypes.c_int64(0)
+                    cnt_off += lib.tpe_sort_layout(n, ctypes.byref(slots))
+                    sort_off += slots.value
+                J["flags"][pos] = flags
+            for name, col in J.items():
+                jobs[name] = col
+            cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
+            # the dense fallback first materialises its draws: a job copy whose
+            # out_off points into the scratch candidate buffer
+            fb_slice = _slice_of(groups, [k for k, _ in groups].index("qfb"))
+            fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
+            fb_jobs["out_off"] = fb_jobs["cand_off"]
+            if pkey is not None and not any(k == "sorted" and ids for k, ids in groups):
+                self._plans[pkey] = self._plan_record(
+                    works, cont, quant, cat, fit_ids, params, segs, csegs, p_pool, cat_meta,
+                    lat_ranges, fallback, modes, groups, order, gathers, jobs, fb_slice, out_off,
+                    lat_off, qfb_off, sort_off, cnt_off, tbl_off)
 
+        self.last_plan = (segs, csegs, g_arr if hist_mode else None, jobs, cached is not None)
         _hmark('jobs')
         # ---- job table upload (the fit above is already running) ----------------
         pack2 = _Pack()

@@ -258,3 +258,31 @@ def test_smallest_rows_matches_stable_argsort():
             losses = rng.normal(size=T)
         want = set(np.argsort(losses, kind="stable")[:n].tolist())
         assert set(_smallest_rows(losses, n).tolist()) == want, (losses, n)
+
+
+def test_plan_key_rules():
+    """Level-plan cache key (engine.Engine._plan_key): history-mode levels of
+    hashable structure only; injected candidates, per-candidate outputs, the
+    sampler hook and upload mode always plan from scratch; the key follows
+    kinds, arguments, candidate counts and columns but not the Philox keys."""
+    from hyperopt_amd.engine import Engine, LabelWork
+    eng = Engine.__new__(Engine)  # key logic only: no device state
+    eng._plans = {}
+
+    def work(**kw):
+        base = dict(label="u", kind="uniform", args=(-5.0, 5.0), obs_below=np.zeros(3),
+                    obs_above=None, n_cand=24, col=0, n_above=5)
+        base.update(kw)
+        return LabelWork(**base)
+
+    k = lambda ws, **o: eng._plan_key(ws, 1.0, 25, 32, "auto", o.get("outputs", False),  # noqa
+                                      o.get("sample_only", False), o.get("hist", True), False)
+    assert k([work()]) is not None
+    assert k([work()]) == k([work(key=99, cand_base=7, n_above=9, obs_below=np.ones(5))])
+    assert k([work()]) != k([work(n_cand=48)])
+    assert k([work()]) != k([work(col=1)])
+    assert k([work(cand=np.zeros(4))]) is None
+    assert k([work()], outputs=True) is None
+    assert k([work()], sample_only=True) is None
+    assert k([work()], hist=False) is None
+    assert k([work(kind="categorical", args=([0.5, 0.5],))]) is None  # unhashable args
