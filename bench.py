@@ -104,10 +104,10 @@ def history_works(space, mat, hist, rows_b, step, n_cand, cand_base):
 
 
 def label_key(seed, step, lab):
-    h = 1469598103934665603
-    for ch in ("%d/%d/%s" % (seed, step, lab)).encode():
-        h = ((h ^ ch) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
-    return h
+    """Philox key of (seed, step, label): the drop-in's key rule (tpe.label_key)
+    with the step folded into the seed."""
+    from hyperopt_amd.tpe import label_key as key
+    return key(seed * 1000003 + step, lab)
 
 
 def make_works(space, splits, step, n_cand, cand_base):

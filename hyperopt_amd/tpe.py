@@ -25,6 +25,7 @@ all-gather + device max-loc (hyperopt_amd/dist.py).
 """
 from __future__ import annotations
 
+import functools
 import logging
 import math
 import os
@@ -60,16 +61,29 @@ def engine():
     return eng
 
 
-def label_key(seed, label):
-    """64-bit Philox key for (suggest seed, label): FNV-1a then a splitmix finaliser."""
+@functools.lru_cache(maxsize=1 << 16)
+def _label_hash(label):
+    """FNV-1a of the label (cached: labels repeat on every call)."""
     h = 0xCBF29CE484222325
-    for ch in ("%d:%s" % (int(seed), label)).encode():
+    for ch in str(label).encode():
         h = ((h ^ ch) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def _mix64(h):
+    """splitmix64 finaliser."""
     h ^= h >> 30
     h = (h * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
     h ^= h >> 27
     h = (h * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
     return h ^ (h >> 31)
+
+
+def label_key(seed, label):
+    """64-bit Philox key for (suggest seed, label): the label's FNV-1a hash
+    xor the mixed seed, through a splitmix finaliser."""
+    return _mix64(_label_hash(label) ^ _mix64((int(seed) * 0x9E3779B97F4A7C15 + 1)
+                                             & 0xFFFFFFFFFFFFFFFF))
 
 
 class History(object):
