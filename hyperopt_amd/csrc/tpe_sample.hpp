@@ -34,39 +34,39 @@ struct Mix {  // sampler view of the below mixture (LDS or global)
   const double* mu;
   const double* sg;
   const uint32_t* thr;  // staged: component k takes words < thr[k] (fp32 draws)
-  const uint8_t* guide; // staged: first k with thr[k] > b * 2^24 for bucket b
-  const float* mu32;
-  const float* sg32;
+  const uint2* gd;      // staged: guide entry of bucket b (see stage_mix)
+  const float2* ms32;   // staged: (mu, sigma) in fp32
   int n;
 };
 
 struct MixLds {  // LDS image of a below mixture of <= kStage components
   double cdf[kStage], mu[kStage], sg[kStage];
   uint32_t thr[kStage];
-  float mu32[kStage], sg32[kStage];
-  uint8_t guide[kGuide];
+  float2 ms32[kStage];
+  uint2 gd[kGuide];
 };
 
 // stage the below mixture for sampling; returns the view (call by all threads).
 // thr[k] = ceil(cdf[k] / cdf[n-1] * 2^32): a 32-bit word w selects the first k
 // with w < thr[k] -- the same component as cdf[k] > w * 2^-32 * cdf[n-1].
-// guide[b] (Chen & Asau guide table) is where that search starts for words of
-// bucket b = w >> 24; most buckets hold no threshold, so the walk is one
-// comparison.
+// Guide table (Chen & Asau) over buckets b = w >> 24: g = the first k with
+// thr[k] > b * 2^24 is the smallest component a word of the bucket can take.
+// Entry gd[b] = {thr[g], g | step << 8 | multi << 9}: step = (g < n-1), and
+// the component is g + step * (w >= thr[g]) unless a second threshold falls
+// inside the bucket (multi), where the walk over thr[] finishes the search.
 __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, const double* mu,
                                          const double* sigma, MixLds& L) {
   const int n = S.n_obs + 1;
   if (n > kStage)
     return Mix{wcdf + S.comp_off, mu + S.comp_off, sigma + S.comp_off, nullptr, nullptr,
-               nullptr, nullptr, n};
+               nullptr, n};
   const double total = wcdf[S.comp_off + n - 1];
   for (int k = threadIdx.x; k < n; k += kBS) {
     const double c = wcdf[S.comp_off + k], m = mu[S.comp_off + k], g = sigma[S.comp_off + k];
     L.cdf[k] = c;
     L.mu[k] = m;
     L.sg[k] = g;
-    L.mu32[k] = (float)m;
-    L.sg32[k] = (float)g;
+    L.ms32[k] = make_float2((float)m, (float)g);
     const double t = ceil(c / total * 4294967296.0);
     L.thr[k] = (t >= 4294967295.0) ? 0xFFFFFFFFu : (t > 0.0 ? (uint32_t)t : 0u);
   }
@@ -78,10 +78,13 @@ __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, c
       const int mid = (lo + hi) >> 1;
       if (w < L.thr[mid]) hi = mid; else lo = mid + 1;
     }
-    L.guide[b] = (uint8_t)lo;
+    const uint32_t top = w | 0xFFFFFFu;  // largest word of the bucket
+    const uint32_t step = lo < n - 1 ? 1u : 0u;
+    const uint32_t multi = (lo + 1 < n - 1 && L.thr[lo + 1] <= top) ? 1u : 0u;
+    L.gd[b] = make_uint2(L.thr[lo], (uint32_t)lo | step << 8 | multi << 9);
   }
   __syncthreads();
-  return Mix{L.cdf, L.mu, L.sg, L.thr, L.guide, L.mu32, L.sg32, n};
+  return Mix{L.cdf, L.mu, L.sg, L.thr, L.gd, L.ms32, n};
 }
 
 // One draw from the (possibly truncated) below mixture: returns the value in
@@ -109,19 +112,18 @@ __device__ __forceinline__ double draw64(const Mix& M, uint64_t key, int64_t g, 
 // 2m+1's, and (y, z) give the Box-Muller pair (cos -> 2m, sin -> 2m+1).
 // Candidate g's value therefore depends on g alone, whichever kernel draws it.
 __device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
-  if (M.thr) {  // block-uniform: staged mixture, guide table + 32-bit walk
-    int k = M.guide[word >> 24];
-    while (k < M.n - 1 && word >= M.thr[k]) ++k;
+  if (M.thr) {  // block-uniform: staged mixture, one guide entry (+ rare walk)
+    const uint2 e = M.gd[word >> 24];
+    int k = (int)(e.y & 0xFFu) + ((word >= e.x) ? (int)((e.y >> 8) & 1u) : 0);
+    if (e.y & 0x200u)
+      while (k < M.n - 1 && word >= M.thr[k]) ++k;
     return k;
   }
   const double u = (double)word * 0x1.0p-32 * M.cdf[M.n - 1];
   return upper_bound(M.cdf, M.n, u);
 }
-__device__ __forceinline__ float mu32_of(const Mix& M, int j) {
-  return M.mu32 ? M.mu32[j] : (float)M.mu[j];
-}
-__device__ __forceinline__ float sg32_of(const Mix& M, int j) {
-  return M.sg32 ? M.sg32[j] : (float)M.sg[j];
+__device__ __forceinline__ float2 ms32_of(const Mix& M, int j) {  // (mu, sigma)
+  return M.ms32 ? M.ms32[j] : make_float2((float)M.mu[j], (float)M.sg[j]);
 }
 
 __device__ __forceinline__ void attempt32_pair(const Mix& M, uint64_t key, int64_t m, uint32_t a,
@@ -144,8 +146,9 @@ __device__ __forceinline__ void attempt32_pair(const Mix& M, uint64_t key, int64
 #else
   normal_pair_f32(r.y, r.z, z0, z1);
 #endif
-  y0 = fmaf(sg32_of(M, j0), z0, mu32_of(M, j0));
-  y1 = fmaf(sg32_of(M, j1), z1, mu32_of(M, j1));
+  const float2 c0 = ms32_of(M, j0), c1 = ms32_of(M, j1);
+  y0 = fmaf(c0.y, z0, c0.x);
+  y1 = fmaf(c1.y, z1, c1.x);
 }
 
 // attempt `a` of candidate `g` alone (same value as attempt32_pair's half)
@@ -156,7 +159,8 @@ __device__ __forceinline__ float attempt32(const Mix& M, uint64_t key, int64_t g
   const float u2 = (float)(r.z >> 8) * 0x1.0p-24f;
   const float rr = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
   const float z = rr * ((g & 1) ? __builtin_amdgcn_sinf(u2) : __builtin_amdgcn_cosf(u2));
-  return fmaf(sg32_of(M, j), z, mu32_of(M, j));
+  const float2 c = ms32_of(M, j);
+  return fmaf(c.y, z, c.x);
 }
 
 __device__ __forceinline__ bool accept32(float y, bool lo_on, bool hi_on, float lo, float hi) {

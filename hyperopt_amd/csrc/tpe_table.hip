@@ -279,10 +279,11 @@ struct Grid {
   int nb;
 };
 
-// centre of cell c, rounded to fp32 (the build expands around exactly this
-// point; the scorer recomputes it from the cell index with the same ops)
-__device__ __forceinline__ double cell_centre(double origin, double h, int c) {
-  return (double)(float)(origin + (double)(2 * c + 1) * h);
+// centre of cell c in fp32 from the fp32 origin and half-width (the build
+// expands around exactly this point; the scorer recomputes it from the cell
+// index with the same two operations)
+__device__ __forceinline__ float cell_centre(float origin, float h, int c) {
+  return fmaf((float)(2 * c + 1), h, origin);
 }
 __device__ __forceinline__ Grid grid_of(const tpe_table& Tb, int64_t cap) {
   const double span = Tb.hi - Tb.lo;
@@ -475,7 +476,7 @@ __global__ __launch_bounds__(kBS) void k_table_build(
   const int wid = threadIdx.x / kWave;
   for (int64_t c = (int64_t)blockIdx.x * (kBS / kWave) + wid; c < g.nb;
        c += (int64_t)gridDim.x * (kBS / kWave)) {
-    const double y0 = cell_centre(g.origin, g.h, (int)c);
+    const double y0 = (double)cell_centre((float)g.origin, (float)g.h, (int)c);
     float* region = cells + J.tbl_off * (kSlotB / 4);
     float* out = region + c * kCellF;
     double mb, ma;
@@ -586,7 +587,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   // the job's cell table: a uniform base + 32-bit byte offsets (saddr loads)
   const char* cbase = reinterpret_cast<const char*>(cells) + J.tbl_off * kSlotB;
   const float* mpairs = reinterpret_cast<const float*>(cbase) + J.tbl_cap * kCellF;
-  const double g0d = Tb.origin, hd = Tb.h;
+  const float h32 = (float)Tb.h;
   const int lane = lane_id(), gi = lane & (kChunks - 1), gbase = lane & ~(kChunks - 1);
   // wave-uniform (scalar) base of the wave's LDS region: the DMA destinations need no
   // per-instruction readfirstlane
@@ -641,6 +642,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       if (out_al) out_al[o] = al;
       if (out_x) out_x[o] = (double)(exp_out ? __expf(y) : y);
     };
+    const int nvalid = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
     // cell of every candidate of the thread (byte offset in the job's table)
     float yv[kTR];
     uint32_t co[kTR];
@@ -683,11 +685,11 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       if constexpr (r + 1 < kTR) fetch(r + 1);
       const int cell = (int)(co[r] / (kCellF * 4));
-      const float u = (y - (float)cell_centre(g0d, hd, cell)) * inv_h;
+      const float u = (y - cell_centre(g0, h32, cell)) * inv_h;
       float pb, pa;
       horner9x2(q0, q1, q2, q3, u, pb, pa);
       const float dlog = (__builtin_amdgcn_logf(pb) - __builtin_amdgcn_logf(pa)) * kLn2T;
-      const bool valid = t0 + r < J.n_cand;
+      const bool valid = r < nvalid;
       // q3.w: m_below - m_above, NaN for a cell that failed the bound
       const bool ok = (q3.w == q3.w) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f);
       exact_mask |= (valid && !ok) ? (1u << r) : 0u;
