@@ -157,6 +157,13 @@ __device__ __forceinline__ void plan_range(const tpe_job& J, const tpe_seg& SB, 
   T = cp.z - 0.5 * far * far - (log((double)(S.n_obs + 1)) + kTauExtra);
 }
 
+// wide components (the prior, and any with sigma >= prior_sigma / 4) are not
+// windowed but listed; decided from the coefficient's 1/sigma everywhere
+// (plan and build agree by construction)
+__device__ __forceinline__ bool is_wide(const tpe_seg& S, int k, double inv) {
+  return (k == S.prior_pos) || (inv <= 4.0 / S.prior_sigma);
+}
+
 // component k of mixture S: wide flag, reach interval, admissible half-width
 __device__ __forceinline__ void plan_comp(const tpe_seg& S, const double* __restrict__ sigma,
                                           const double* __restrict__ coef64, double T, int k,
@@ -165,7 +172,7 @@ __device__ __forceinline__ void plan_comp(const tpe_seg& S, const double* __rest
   const double d = c.z - T;
   const double z = d > 0.0 ? sqrt(2.0 * d) : 0.0;
   hk = d > 0.0 ? admissible_s(z) / c.y : INFINITY;
-  wide = (k == S.prior_pos) || (sigma[S.comp_off + k] >= 0.25 * S.prior_sigma);
+  wide = is_wide(S, k, c.y);
   const double r = z / c.y * (1.0 + 1e-9) + 1e-12 * fabs(c.x);
   hr = wide ? -INFINITY : c.x + r;
   lr = wide ? INFINITY : c.x - r;
@@ -258,7 +265,7 @@ __global__ __launch_bounds__(kBS) void k_table_plan2(
   if (k < nc) {
     reach_hi[S.comp_off + k] = fmax(reach_hi[S.comp_off + k], chi);
     reach_lo[S.comp_off + k] = fmin(reach_lo[S.comp_off + k], clo);
-    wide = (k == S.prior_pos) || (sigma[S.comp_off + k] >= 0.25 * S.prior_sigma);
+    wide = is_wide(S, k, ld4(coef64, S.comp_off + k).y);
   }
   const int incl = block_scan_sum(wide ? 1 : 0, scan_n);
   if (wide) wide_idx[S.comp_off + wbase + incl - 1] = k;
@@ -369,8 +376,6 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
                                           int mix, double& m_out) {
   const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
-  const int pos = S.prior_pos;
-  const double wide_sig = 0.25 * S.prior_sigma;
 #ifdef TPE_DIAG_BSEARCH
   const int k_lo = first_ge(reach_hi + off, nc, y0 - h);
   const int k_hi = last_le(reach_lo + off, nc, y0 + h);
@@ -381,56 +386,60 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   const int nwin = max(0, k_hi - k_lo + 1);
   const int items = nwin + n_wide;
   const int lane = lane_id();
-  auto comp = [&](int it, bool& skip) -> int {
-    if (it < nwin) {
-      const int k = k_lo + it;
-      skip = (k == pos) || (sigma[off + k] >= wide_sig);  // wide: taken from the list
-      return k;
-    }
-    skip = false;
-    return wide_idx[off + (it - nwin)];
+  // component of work item `it` (window first, then the wide list)
+  auto comp = [&](int it) -> int {
+    return it < nwin ? k_lo + it : wide_idx[off + (it - nwin)];
   };
   // One pass: every component inside the cell's reach window (components the
   // plan's global bound admits; each satisfies the expansion bound by the
-  // choice of h).  The exponent is formed in fp64, the series in fp32; each
-  // lane keeps its own scale m_l (raised only when a term would exceed
-  // e^8 of it) and the lanes are merged at the end.
+  // choice of h).  The exponent is formed in fp64, the series and the
+  // per-component tests in fp32; each lane keeps its own scale m_l (raised
+  // only when a term would exceed e^8 of it) and the lanes are merged at the
+  // end.  The next item's coefficients are loaded before this item's work.
   float P[kP];
 #pragma unroll
   for (int n = 0; n < kP; ++n) P[n] = 0.0f;
   double ml = -INFINITY;
   bool bad = false;
-  for (int it = lane; it < items; it += kWave) {
-    bool skip;
-    const int k = comp(it, skip);
-    if (skip) continue;
-    const double4 c = ld4(coef64, off + k);
+  const float hf = (float)h, Tf = (float)T;
+  int it = lane;
+  int k = it < items ? comp(it) : 0;
+  double4 c = it < items ? ld4(coef64, off + k) : make_double4(0.0, 0.0, 0.0, 0.0);
+  for (; it < items; it += kWave) {
+    const int itn = it + kWave;
+    const int kn = itn < items ? comp(itn) : 0;
+    const double4 cn = itn < items ? ld4(coef64, off + kn) : c;
+    // window items that are wide come from the list instead
+    const bool skip = it < nwin && is_wide(S, k, c.y);
     const double dy = y0 - c.x;
-    const double zn = fmax(fabs(dy) - h, 0.0) * c.y;
-    if (c.z - 0.5 * zn * zn < T) continue;  // below the plan's floor on the whole cell
-    const double zc = dy * c.y;
-    const double v = c.z - 0.5 * zc * zc;
-    if (v > ml + 8.0) {  // new scale: rescale this lane's partial sums
-      const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - v));
+    const float dyf = (float)dy, inv = (float)c.y;
+    const float zn = fmaxf(fabsf(dyf) - hf, 0.0f) * inv;
+    // below the plan's floor on the whole cell: left out
+    if (!skip && (float)c.z - 0.5f * zn * zn >= Tf) {
+      const double zc = dy * c.y;
+      const double v = c.z - 0.5 * zc * zc;
+      if (v > ml + 8.0) {  // new scale: rescale this lane's partial sums
+        const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - v));
 #pragma unroll
-      for (int n = 0; n < kP; ++n) P[n] *= r;
-      ml = v;
-    }
-    const double hi2 = h * c.y * c.y;
-    const double A = -dy * hi2;
-    const double B = -0.5 * h * hi2;
-    bad = bad || (9.0 * fabs(A) + 65.0 * fabs(B) > kRhoLim);
-    const float e = __expf((float)(v - ml));
-    const float Af = (float)A, B2 = (float)(2.0 * B);
-    float cm = 0.0f, cc = e;  // e * c_n
-    P[0] += e;
+        for (int n = 0; n < kP; ++n) P[n] *= r;
+        ml = v;
+      }
+      const float hi2 = hf * inv * inv;
+      const float Af = -dyf * hi2, B2 = -hf * hi2;  // A and 2B
+      bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > kRhoLim * (1.0 + 1e-5));
+      const float e = __expf((float)(v - ml));
+      float cm = 0.0f, cc = e;  // e * c_n
+      P[0] += e;
 #pragma unroll
-    for (int n = 0; n + 1 < kP; ++n) {
-      const float cn = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
-      P[n + 1] += cn;
-      cm = cc;
-      cc = cn;
+      for (int n = 0; n + 1 < kP; ++n) {
+        const float cnx = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
+        P[n + 1] += cnx;
+        cm = cc;
+        cc = cnx;
+      }
     }
+    k = kn;
+    c = cn;
   }
   const double m0 = wave_max_d(ml);
   {
