@@ -813,9 +813,28 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
                         (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
                         x);
+    int qe;
+    if (frexp(J.q, &qe) == 0.5 && qe > -100 && qe < 100 && local) {
+      // q a power of two: x * (1/q) is exact in fp32, so rintf gives np.round(x / q)
+      // exactly and the slot needs no fp64 work
+      const float inv_q32 = (float)inv_q;
 #pragma unroll
-    for (int r = 0; r < kLatR; ++r)
-      if (r < nv) mark((double)x[r], t0 + r);
+      for (int r = 0; r < kLatR; ++r) {
+        if (r >= nv) continue;
+        const float t = rintf(x[r] * inv_q32);
+        const int64_t slot = (fabsf(t) < 2147483648.0f) ? (int64_t)t - J.lat_kmin : -1;
+        if (slot < 0 || slot >= J.lat_n) {
+          atomicOr(err, 2);
+          continue;
+        }
+        const uint32_t rel = (uint32_t)(t0 + r - base);
+        if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kLatR; ++r)
+        if (r < nv) mark((double)x[r], t0 + r);
+    }
   } else {
     for (int r = 0; r < kLatR; ++r) {
       const int64_t li = base + r * kBS + threadIdx.x;
