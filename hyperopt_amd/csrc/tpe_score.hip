@@ -895,8 +895,13 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
   }
   const int nc = S.n_obs + 1;
   double acc = 0.0;
+  const double xu = lg ? lub : ub, xl = lg ? llb : lb;
   for (int k = threadIdx.x; k < nc; k += kBS) {
     const double wk = w[S.comp_off + k], m = mu[S.comp_off + k], s = sigma[S.comp_off + k];
+    // both erf arguments beyond +-6.5 (erf exactly +-1 in fp64): the two cdf
+    // values are equal and the term w*cu - w*cl is exactly 0 -- skip it
+    const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
+    if (xl - m >= b65 || xu - m <= -b65) continue;
     double cu, cl;
     if (lg) {
       cu = lognormal_cdf_logx(lub, m, s);
