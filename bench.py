@@ -230,8 +230,8 @@ def dropin_suggest_p50(space, vals, losses, n_cand, calls=8, warmup=2):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", type=int, default=32)
     ap.add_argument("--n-cand", type=int, default=N_CAND)
     ap.add_argument("--no-cpu-baseline", action="store_true")
