@@ -96,10 +96,11 @@ def history_works(space, mat, hist, rows_b, step, n_cand, cand_base):
     sets are read on the host; the above sets are gathered on the GPU."""
     from hyperopt_amd.engine import LabelWork
     below = mat[rows_b]
-    n_b = hist.active_host[rows_b].sum(0)
+    n_above = (hist.n_active - hist.active_host[rows_b].sum(0)).tolist()
+    keys = label_keys(0, step, [lab for lab, _, _ in space])
     return [LabelWork(label=lab, kind=kind, args=a, obs_below=below[:, j], obs_above=None,
-                      n_cand=n_cand, key=label_key(0, step, lab), cand_base=cand_base, col=j,
-                      n_above=int(hist.n_active[j] - n_b[j]))
+                      n_cand=n_cand, key=keys[j], cand_base=cand_base, col=j,
+                      n_above=n_above[j])
             for j, (lab, kind, a) in enumerate(space)]
 
 
@@ -108,6 +109,12 @@ def label_key(seed, step, lab):
     with the step folded into the seed."""
     from hyperopt_amd.tpe import label_key as key
     return key(seed * 1000003 + step, lab)
+
+
+def label_keys(seed, step, labels):
+    """label_key for a list of labels (vectorised, tpe.label_keys)."""
+    from hyperopt_amd.tpe import label_keys as keys
+    return keys(seed * 1000003 + step, labels)
 
 
 def make_works(space, splits, step, n_cand, cand_base):

@@ -47,7 +47,7 @@ CONTINUOUS = ("uniform", "quniform", "loguniform", "qloguniform",
 CATEGORICAL = ("randint", "categorical")
 
 
-@dataclass
+@dataclass(slots=True)
 class LabelWork:
     """One label's inputs for one suggest level."""
     label: str
@@ -67,7 +67,7 @@ class LabelWork:
     hist: int = 0             # Engine.run(histories=...): index of this work's history
 
 
-@dataclass
+@dataclass(slots=True)
 class LabelResult:
     label: str
     index: int                # global candidate index of the winner (-1: none)

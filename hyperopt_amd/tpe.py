@@ -86,6 +86,23 @@ def label_key(seed, label):
                                              & 0xFFFFFFFFFFFFFFFF))
 
 
+def _mix64_np(h):
+    h = h ^ (h >> np.uint64(30))
+    h = h * np.uint64(0xBF58476D1CE4E5B9)
+    h = h ^ (h >> np.uint64(27))
+    h = h * np.uint64(0x94D049BB133111EB)
+    return h ^ (h >> np.uint64(31))
+
+
+def label_keys(seed, labels):
+    """label_key(seed, lab) for every label at once (uint64 array arithmetic
+    wraps like the masked Python integers)."""
+    s = np.uint64(_mix64((int(seed) * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF))
+    h = np.fromiter((_label_hash(lab) for lab in labels), np.uint64, len(labels))
+    with np.errstate(over="ignore"):
+        return _mix64_np(h ^ s).tolist()
+
+
 class History(object):
     """The history tpe.suggest conditions on, one row per distinct tid.
 
@@ -316,8 +333,9 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
             level = [lab for lab in live if lab not in walk]
             if not level:
                 break
-            works = [obs.work(lab, domain.specs[lab], col[lab], n_cand=count,
-                              key=label_key(seed, lab), cand_base=start) for lab in level]
+            works = [obs.work(lab, domain.specs[lab], col[lab], n_cand=count, key=k,
+                              cand_base=start)
+                     for lab, k in zip(level, label_keys(seed, level))]
             res = eng.run(works, prior_weight=prior_weight, lf=linear_forgetting,
                           precision=prec, **obs.run_kwargs)
             if ws > 1:

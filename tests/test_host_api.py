@@ -286,3 +286,9 @@ def test_plan_key_rules():
     assert k([work()], sample_only=True) is None
     assert k([work()], hist=False) is None
     assert k([work(kind="categorical", args=([0.5, 0.5],))]) is None  # unhashable args
+
+
+def test_label_keys_match_label_key():
+    labs = ["x", "lr", "a_b", "ü", "c%d" % 7]
+    for seed in (0, 1, 12345, 2 ** 40 + 7):
+        assert tpe.label_keys(seed, labs) == [tpe.label_key(seed, lab) for lab in labs]
