@@ -51,8 +51,18 @@ def coarse_utcnow():
     return now.replace(microsecond=(now.microsecond // 1000) * 1000)
 
 
+_SON_PLAIN = (float, int, str, bool, type(None))
+
+
 def SONify(arg, memo=None):  # noqa: N802
     """Convert numpy scalars/arrays to plain Python (base.py:128-169, no bson)."""
+    t = type(arg)
+    if t in _SON_PLAIN:  # the common leaves, returned as they are
+        return arg
+    if t is dict:
+        return {SONify(k): SONify(v) for k, v in arg.items()}
+    if t is list:
+        return [SONify(a) for a in arg]
     if isinstance(arg, np.floating):
         return float(arg)
     if isinstance(arg, np.integer):
