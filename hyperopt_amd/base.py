@@ -637,7 +637,31 @@ class Domain(object):
         Walks the space from the root; a ``switch`` whose index depends on an
         undecided label contributes that label but none of its branches
         (the level structure of vectorize.py:321-363 / pyll/base.py:863-881).
+        The result depends only on the decided values of switch-selector
+        labels, so it is memoised on those.
         """
+        sel_labels = self.__dict__.get("_selector_labels")
+        if sel_labels is None:
+            sel_labels = set()
+            for n in pyll.dfs(self.expr):
+                if n.name == "switch":
+                    sel_labels.update(m.pos_args[0].obj for m in pyll.dfs(n.pos_args[0])
+                                      if m.name == "hyperopt_param")
+            self._selector_labels = sel_labels = tuple(sorted(sel_labels))
+            self._reach_memo = {}
+        try:
+            key = tuple((lab, decided[lab]) for lab in sel_labels if lab in decided)
+            hit = self._reach_memo.get(key)
+        except TypeError:  # unhashable decided value: walk
+            key, hit = None, None
+        if hit is not None:
+            return list(hit)
+        live = self._reachable_walk(decided)
+        if key is not None and len(self._reach_memo) < 4096:
+            self._reach_memo[key] = tuple(live)
+        return live
+
+    def _reachable_walk(self, decided):
         live, seen = [], set()
         order = {lab: i for i, lab in enumerate(self.params)}
         stack = [self.expr]

@@ -292,3 +292,19 @@ def test_label_keys_match_label_key():
     labs = ["x", "lr", "a_b", "ü", "c%d" % 7]
     for seed in (0, 1, 12345, 2 ** 40 + 7):
         assert tpe.label_keys(seed, labs) == [tpe.label_key(seed, lab) for lab in labs]
+
+
+def test_reachable_memo_matches_walk():
+    """Domain.reachable is memoised on the decided selector values; every
+    answer equals a fresh walk of the space."""
+    from hyperopt_amd import hp
+    space = hp.choice("a", [("x", hp.uniform("u", 0, 1)),
+                            ("y", hp.choice("b", [hp.normal("n", 0, 1),
+                                                  {"z": hp.loguniform("lz", -3, 0)}])),
+                            ("w", hp.randint("r", 5))])
+    dom = Domain(lambda p: 0.0, space)
+    cases = [{}, {"a": 0}, {"a": 1}, {"a": 1, "b": 0}, {"a": 1, "b": 1}, {"a": 2},
+             {"a": 1, "b": 1, "lz": 0.3}, {"a": np.int64(1), "b": 0}]
+    for _ in range(2):  # second pass served from the memo
+        for d in cases:
+            assert dom.reachable(d) == dom._reachable_walk(d), d
