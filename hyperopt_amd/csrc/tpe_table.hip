@@ -355,6 +355,50 @@ __device__ __forceinline__ double wave_max_d(double v) {
   for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
   return v;
 }
+
+// Wave reductions without the LDS crossbar (all 64 lanes active): DPP within
+// each 16-lane row (quad perms, half-row and row mirrors leave the row total
+// in every lane of the row), then the four row totals by readlane.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
+                                                            0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF,
+                                                         true);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<kDppXor1>(v);
+  v += dpp_f<kDppXor2>(v);
+  v += dpp_f<kDppHalfMirror>(v);
+  v += dpp_f<kDppMirror>(v);
+  const int b = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
+}
+__device__ __forceinline__ double wave_max_dpp(double v) {
+  v = fmax(v, dpp_d<kDppXor1>(v));
+  v = fmax(v, dpp_d<kDppXor2>(v));
+  v = fmax(v, dpp_d<kDppHalfMirror>(v));
+  v = fmax(v, dpp_d<kDppMirror>(v));
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  double r = -INFINITY;
+#pragma unroll
+  for (int row = 0; row < 4; ++row) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, row * 16);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), row * 16);
+    r = fmax(r, __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo));
+  }
+  return r;
+}
 __device__ __forceinline__ float wave_sum_f(float v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -441,14 +485,14 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     k = kn;
     c = cn;
   }
-  const double m0 = wave_max_d(ml);
+  const double m0 = wave_max_dpp(ml);
   {
     const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - m0));
 #pragma unroll
     for (int n = 0; n < kP; ++n) P[n] *= r;
   }
 #pragma unroll
-  for (int n = 0; n < kP; ++n) P[n] = wave_sum_f(P[n]);
+  for (int n = 0; n < kP; ++n) P[n] = wave_sum_dpp(P[n]);
   bad = __any(bad);
   if (lane < kP) {
     float v = P[0];
