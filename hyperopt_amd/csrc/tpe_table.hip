@@ -717,12 +717,15 @@ __global__ __launch_bounds__(kBS) void k_score_table(
     typedef __attribute__((address_space(3))) void* lds_vp;
     typedef const __attribute__((address_space(1))) void* glb_vp;
     auto fetch = [&](int r) __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < kChunks; ++j) {
-        const uint32_t cj = __shfl(co[r], gbase | j, kWave);
+      auto one = [&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        // member j's cell offset: a quad-perm broadcast inside the 4-lane group
+        const uint32_t cj = (uint32_t)__builtin_amdgcn_mov_dpp(
+            (int)co[r], j | (j << 2) | (j << 4) | (j << 6), 0xF, 0xF, true);
         __builtin_amdgcn_global_load_lds((glb_vp)(cbase + (cj + ((gi ^ j) * 16))),
                                          (lds_vp)(rows + j * kWave), 16, 0, 0);
-      }
+      };
+      static_for<0, kChunks>(one);
     };
     const f4* slab = reinterpret_cast<const f4*>(rows) + gi * kWave;
     auto score = [&](auto rc) __attribute__((always_inline)) {
