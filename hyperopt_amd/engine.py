@@ -541,113 +541,6 @@ class Engine:
                 ("cat", [i for i in cat if not inj(i)]),
             ]
             order = [i for _, ids in groups for i in ids]
-        _hmark('plan')
-        # ---- upload -------------------------------------------------------------
-        o_segs = pack.add(segs) if segs.size else None
-        o_csegs = pack.add(csegs) if csegs.size else None
-        o_p = pack.add(p_pool)
-        if hist_mode:
-            if cached is None:
-                g_arr = np.zeros(len(gathers), L.GATHER_DTYPE)
-            if cached is None and gathers:
-                (g_arr["col"], g_arr["below"], g_arr["dst_off"], g_arr["offset"], g_arr["count"],
-                 g_arr["to_int"], g_arr["hist"]) = (np.array(c) for c in zip(*gathers))
-            o_g = pack.add(g_arr)
-            if histories is None:
-                isb = np.ascontiguousarray(is_below, dtype=np.uint8)
-                n_rows = isb.size
-                o_isb = pack.add(isb)
-                o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) \
-                    if rows is not None else None
-            else:  # row lists / flags at offsets of the staged pack (the `aux` base)
-                h_arr = np.zeros(len(histories), L.HISTORY_DTYPE)
-                for h, (dh, h_rows, h_isb) in enumerate(histories):
-                    h_isb = np.ascontiguousarray(h_isb, dtype=np.uint8)
-                    h_arr[h] = (dh.vals.data_ptr(), dh.active.data_ptr(), dh.ld, dh.n_labels,
-                                h_isb.size, pack.add(np.ascontiguousarray(h_rows, np.int32))
-                                if h_rows is not None else -1, pack.add(h_isb))
-                    if h_rows is None and h_isb.size > dh.rows:
-                        raise ValueError("history %d: %d split flags for %d rows"
-                                         % (h, h_isb.size, dh.rows))
-                o_h = pack.add(h_arr)
-        else:
-            o_obs = pack.add(obs_pool)
-            o_cobs = pack.add(cobs_pool)
-        base = self._upload(pack, stream)
-        d_segs = base + o_segs if o_segs is not None else None
-        d_csegs = base + o_csegs if o_csegs is not None else None
-        # one result buffer, read back with one copy: [0,16) error bits,
-        # [16,32) table stats, [32,40) sorted-path pair count, [64,...) tpe_best
-        JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
-        n_jobs = len(order)
-        d_res = self._buf("res", 64 + n_jobs * BS)
-        res_t = self._bufs["res"]
-        d_err, d_stats, d_pairs, d_best = d_res, d_res + 16, d_res + 32, d_res + 64
-        with torch.cuda.stream(stream):
-            res_t[:64].zero_()
-        if hist_mode:
-            d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
-            d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
-            e0 = tick()
-            if histories is None:
-                L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
-                                           history.ld,
-                                           base + o_rows if o_rows is not None else None,
-                                           n_rows, base + o_isb, base + o_g,
-                                           g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr),
-                                           d_obs, d_cobs, d_err, sp), "tpe_gather_obs")
-            else:
-                L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
-                                                 len(h_arr), base, base + o_g,
-                                                 g_arr.ctypes.data_as(ctypes.c_void_p),
-                                                 len(g_arr), d_obs, d_cobs, d_err, sp),
-                        "tpe_gather_obs_multi")
-            tock("gather", e0)
-        else:
-            d_obs, d_cobs = base + o_obs, base + o_cobs
-
-        _hmark('upload+gather')
-        # ---- posterior fit ------------------------------------------------------
-        d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
-        if fit_ids:
-            d_w = self._buf("w", 8 * n_comp)
-            d_mu = self._buf("mu", 8 * n_comp)
-            d_sig = self._buf("sigma", 8 * n_comp)
-            d_cdf = self._buf("wcdf", 8 * n_comp)
-            d_c64 = self._buf("coef64", 32 * n_comp)
-            d_c32 = self._buf("coef32", 16 * n_comp)
-            d_c32n = self._buf("coef32n", 16 * n_comp)
-            d_w32 = self._buf("wide32", 16 * n_comp)
-            d_pm = self._buf("pm", 4 * n_comp)
-            d_sm = self._buf("sm", 4 * n_comp)
-            d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
-                                                                       n_obs_total))
-            prune = any(k == "sorted" and ids for k, ids in groups)
-            if not prune:
-                d_c32n = d_w32 = d_pm = d_sm = None
-            e0 = tick()
-            L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
-                                       n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
-                                       d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
-            tock("fit", e0)
-        if cat:
-            d_logp = self._buf("cat_logp", 8 * p_pool.size)
-            d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
-            e0 = tick()
-            d_p = self._buf("cat_p", 8 * p_pool.size)
-            with torch.cuda.stream(stream):
-                pt = self._bufs["cat_p"]
-                st = self._bufs["stage"]
-                pt[:8 * p_pool.size].copy_(st[o_p:o_p + 8 * p_pool.size])
-            L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
-                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, sp),
-                    "tpe_cat_posterior")
-            tock("cat_fit", e0)
-
-        if posteriors:
-            return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
-                                         d_segs, stream)
-
         if cached is not None:
             (jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off, sort_off, cnt_off,
              tbl_off) = self._jobs_fast(cached, works)
@@ -726,14 +619,114 @@ class Engine:
                     lat_ranges, fallback, modes, groups, order, gathers, jobs, fb_slice, out_off,
                     lat_off, qfb_off, sort_off, cnt_off, tbl_off)
 
+        _hmark('plan')
+        # ---- upload (descriptors, jobs, injected candidates: one copy) -----------
+        o_segs = pack.add(segs) if segs.size else None
+        o_csegs = pack.add(csegs) if csegs.size else None
+        o_p = pack.add(p_pool)
+        if hist_mode:
+            if cached is None:
+                g_arr = np.zeros(len(gathers), L.GATHER_DTYPE)
+            if cached is None and gathers:
+                (g_arr["col"], g_arr["below"], g_arr["dst_off"], g_arr["offset"], g_arr["count"],
+                 g_arr["to_int"], g_arr["hist"]) = (np.array(c) for c in zip(*gathers))
+            o_g = pack.add(g_arr)
+            if histories is None:
+                isb = np.ascontiguousarray(is_below, dtype=np.uint8)
+                n_rows = isb.size
+                o_isb = pack.add(isb)
+                o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) \
+                    if rows is not None else None
+            else:  # row lists / flags at offsets of the staged pack (the `aux` base)
+                h_arr = np.zeros(len(histories), L.HISTORY_DTYPE)
+                for h, (dh, h_rows, h_isb) in enumerate(histories):
+                    h_isb = np.ascontiguousarray(h_isb, dtype=np.uint8)
+                    h_arr[h] = (dh.vals.data_ptr(), dh.active.data_ptr(), dh.ld, dh.n_labels,
+                                h_isb.size, pack.add(np.ascontiguousarray(h_rows, np.int32))
+                                if h_rows is not None else -1, pack.add(h_isb))
+                    if h_rows is None and h_isb.size > dh.rows:
+                        raise ValueError("history %d: %d split flags for %d rows"
+                                         % (h, h_isb.size, dh.rows))
+                o_h = pack.add(h_arr)
+        else:
+            o_obs = pack.add(obs_pool)
+            o_cobs = pack.add(cobs_pool)
+        o_jobs = pack.add(jobs) if jobs.size else None
+        o_fb = pack.add(fb_jobs) if fb_jobs.size else None
+        o_cand = pack.add(cand_pool)
+        base = self._upload(pack, stream)
+        d_segs = base + o_segs if o_segs is not None else None
+        d_csegs = base + o_csegs if o_csegs is not None else None
+        # one result buffer, read back with one copy: [0,16) error bits,
+        # [16,32) table stats, [32,40) sorted-path pair count, [64,...) tpe_best
+        JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
+        n_jobs = len(order)
+        d_res = self._buf("res", 64 + n_jobs * BS)
+        res_t = self._bufs["res"]
+        d_err, d_stats, d_pairs, d_best = d_res, d_res + 16, d_res + 32, d_res + 64
+        with torch.cuda.stream(stream):
+            res_t[:64].zero_()
+        if hist_mode:
+            d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
+            d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
+            e0 = tick()
+            if histories is None:
+                L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
+                                           history.ld,
+                                           base + o_rows if o_rows is not None else None,
+                                           n_rows, base + o_isb, base + o_g,
+                                           g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr),
+                                           d_obs, d_cobs, d_err, sp), "tpe_gather_obs")
+            else:
+                L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
+                                                 len(h_arr), base, base + o_g,
+                                                 g_arr.ctypes.data_as(ctypes.c_void_p),
+                                                 len(g_arr), d_obs, d_cobs, d_err, sp),
+                        "tpe_gather_obs_multi")
+            tock("gather", e0)
+        else:
+            d_obs, d_cobs = base + o_obs, base + o_cobs
+
+        _hmark('upload+gather')
+        # ---- posterior fit ------------------------------------------------------
+        d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
+        if fit_ids:
+            d_w = self._buf("w", 8 * n_comp)
+            d_mu = self._buf("mu", 8 * n_comp)
+            d_sig = self._buf("sigma", 8 * n_comp)
+            d_cdf = self._buf("wcdf", 8 * n_comp)
+            d_c64 = self._buf("coef64", 32 * n_comp)
+            d_c32 = self._buf("coef32", 16 * n_comp)
+            d_c32n = self._buf("coef32n", 16 * n_comp)
+            d_w32 = self._buf("wide32", 16 * n_comp)
+            d_pm = self._buf("pm", 4 * n_comp)
+            d_sm = self._buf("sm", 4 * n_comp)
+            d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
+                                                                       n_obs_total))
+            prune = any(k == "sorted" and ids for k, ids in groups)
+            if not prune:
+                d_c32n = d_w32 = d_pm = d_sm = None
+            e0 = tick()
+            L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
+                                       n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
+                                       d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
+            tock("fit", e0)
+        if cat:
+            d_logp = self._buf("cat_logp", 8 * p_pool.size)
+            d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
+            e0 = tick()
+            d_p = base + o_p  # the posterior is formed in place in the staged pool
+            L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
+                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, sp),
+                    "tpe_cat_posterior")
+            tock("cat_fit", e0)
+
+        if posteriors:
+            return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
+                                         d_segs, stream, o_p)
+
         self.last_plan = (segs, csegs, g_arr if hist_mode else None, jobs, cached is not None)
         _hmark('jobs')
-        # ---- job table upload (the fit above is already running) ----------------
-        pack2 = _Pack()
-        o_jobs = pack2.add(jobs) if jobs.size else None
-        o_fb = pack2.add(fb_jobs) if fb_jobs.size else None
-        o_cand = pack2.add(cand_pool)
-        base = self._upload(pack2, stream, slot=1)
         d_cand = base + o_cand
         d_bl = d_al = d_x = None
         if outputs:
@@ -895,11 +888,11 @@ class Engine:
                                 "segment sizes given by the host")
         _hmark('readback')
         results = [None] * len(works)
+        b_idx, b_val = best_h["index"].tolist(), best_h["value"].tolist()
+        b_sc, b_ns = best_h["score"].tolist(), best_h["n_scored"].tolist()
         for pos, i in enumerate(order):
-            b = best_h[pos]
             w = works[i]
-            r = LabelResult(w.label, int(b["index"]), float(b["value"]), float(b["score"]),
-                            int(b["n_scored"]))
+            r = LabelResult(w.label, b_idx[pos], b_val[pos], b_sc[pos], b_ns[pos])
             if outputs:
                 o, n = int(jobs[pos]["out_off"]), int(jobs[pos]["n_cand"])
                 r.below_llik = outs[0][o:o + n].copy()
@@ -910,7 +903,8 @@ class Engine:
         return results
 
 
-    def _read_posteriors(self, works, fit_ids, cat, segs, csegs, n_comp, n_p, d_segs, stream):
+    def _read_posteriors(self, works, fit_ids, cat, segs, csegs, n_comp, n_p, d_segs, stream,
+                         o_p):
         torch = self.torch
         with torch.cuda.stream(stream):
             host = {}
@@ -924,7 +918,8 @@ class Engine:
                 raw.copy_(seg_t[off:off + segs.nbytes])
                 dsegs = raw.numpy().view(L.SEG_DTYPE)
             if cat:
-                host["p"] = self._bufs["cat_p"][:8 * n_p].to("cpu").numpy().view(np.float64)
+                host["p"] = self._bufs["stage"][o_p:o_p + 8 * n_p].to("cpu").numpy() \
+                    .view(np.float64)
         results = [LabelResult(w.label, -1, 0.0, 0.0, 0) for w in works]
         for si, i in enumerate(fit_ids):
             post = {}
