@@ -654,18 +654,39 @@ class Engine:
         o_jobs = pack.add(jobs) if jobs.size else None
         o_fb = pack.add(fb_jobs) if fb_jobs.size else None
         o_cand = pack.add(cand_pool)
+        # one result block, zeroed by the upload and read back with one copy:
+        # [0,16) error bits, [16,32) table stats, [32,40) sorted-path pair
+        # count, [64,...) tpe_best per job
+        JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
+        n_jobs = len(order)
+        o_res = pack.add(np.zeros(64 + n_jobs * BS, np.uint8))
         base = self._upload(pack, stream)
         d_segs = base + o_segs if o_segs is not None else None
         d_csegs = base + o_csegs if o_csegs is not None else None
-        # one result buffer, read back with one copy: [0,16) error bits,
-        # [16,32) table stats, [32,40) sorted-path pair count, [64,...) tpe_best
-        JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
-        n_jobs = len(order)
-        d_res = self._buf("res", 64 + n_jobs * BS)
-        res_t = self._bufs["res"]
+        d_res = base + o_res
         d_err, d_stats, d_pairs, d_best = d_res, d_res + 16, d_res + 32, d_res + 64
-        with torch.cuda.stream(stream):
-            res_t[:64].zero_()
+        # every workspace pointer before the first launch: the launches then
+        # follow each other without host work in between
+        d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
+        if fit_ids:
+            d_w = self._buf("w", 8 * n_comp)
+            d_mu = self._buf("mu", 8 * n_comp)
+            d_sig = self._buf("sigma", 8 * n_comp)
+            d_cdf = self._buf("wcdf", 8 * n_comp)
+            d_c64 = self._buf("coef64", 32 * n_comp)
+            d_c32 = self._buf("coef32", 16 * n_comp)
+            d_c32n = self._buf("coef32n", 16 * n_comp)
+            d_w32 = self._buf("wide32", 16 * n_comp)
+            d_pm = self._buf("pm", 4 * n_comp)
+            d_sm = self._buf("sm", 4 * n_comp)
+            d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
+                                                                       n_obs_total))
+            prune = any(k == "sorted" and ids for k, ids in groups)
+            if not prune:
+                d_c32n = d_w32 = d_pm = d_sm = None
+        if cat:
+            d_logp = self._buf("cat_logp", 8 * p_pool.size)
+            d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
         if hist_mode:
             d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
             d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
@@ -689,31 +710,13 @@ class Engine:
 
         _hmark('upload+gather')
         # ---- posterior fit ------------------------------------------------------
-        d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
         if fit_ids:
-            d_w = self._buf("w", 8 * n_comp)
-            d_mu = self._buf("mu", 8 * n_comp)
-            d_sig = self._buf("sigma", 8 * n_comp)
-            d_cdf = self._buf("wcdf", 8 * n_comp)
-            d_c64 = self._buf("coef64", 32 * n_comp)
-            d_c32 = self._buf("coef32", 16 * n_comp)
-            d_c32n = self._buf("coef32n", 16 * n_comp)
-            d_w32 = self._buf("wide32", 16 * n_comp)
-            d_pm = self._buf("pm", 4 * n_comp)
-            d_sm = self._buf("sm", 4 * n_comp)
-            d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
-                                                                       n_obs_total))
-            prune = any(k == "sorted" and ids for k, ids in groups)
-            if not prune:
-                d_c32n = d_w32 = d_pm = d_sm = None
             e0 = tick()
             L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
                                        n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
                                        d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
             tock("fit", e0)
         if cat:
-            d_logp = self._buf("cat_logp", 8 * p_pool.size)
-            d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
             e0 = tick()
             d_p = base + o_p  # the posterior is formed in place in the staged pool
             L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
@@ -865,7 +868,7 @@ class Engine:
         _hmark('score launches')
         # ---- results (one device->host copy; syncs the stream) --------------------
         with torch.cuda.stream(stream):
-            res_h = res_t[:64 + n_jobs * BS].to("cpu").numpy()
+            res_h = self._bufs["stage"][o_res:o_res + 64 + n_jobs * BS].to("cpu").numpy()
             best_h = res_h[64:].view(L.BEST_DTYPE)
             err = int(res_h[:4].view(np.int32)[0])
             self.last_pairs = None
