@@ -207,7 +207,7 @@ def c3_trials(space, vals, losses):
     return domain, trials
 
 
-def dropin_suggest_p50(space, vals, losses, n_cand, calls=8, warmup=2):
+def dropin_suggest_p50(space, vals, losses, n_cand, calls=20, warmup=3):
     """suggest p50 through the drop-in API on C3: ``tpe.suggest(new_ids,
     domain, trials, seed, n_EI_candidates=n_cand)`` on the 10k-document Trials
     (per-tid history, split, HBM mirror of the columnar cache appended with the
