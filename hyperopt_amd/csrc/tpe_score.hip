@@ -779,9 +779,11 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   const tpe_seg SB = segs[J.below];
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
-  const bool local = J.lat_n <= kLatLds;
-  if (local)
-    for (int s = threadIdx.x; s < J.lat_n; s += kBS) lfirst[s] = 0xFFFFFFFFu;
+  // the first kLatLds slots of the lattice are deduplicated in LDS (for the
+  // wide lattices of unbounded labels that is where the mass sits); slots
+  // beyond go to the global marks directly, each read before its atomic
+  const int n_loc = (int)min((int64_t)kLatLds, J.lat_n);
+  for (int s = threadIdx.x; s < n_loc; s += kBS) lfirst[s] = 0xFFFFFFFFu;
   const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
   __syncthreads();
   // np.round(x / q) (tpe.py:106) without a division per draw: t = x * (1/q) is
@@ -797,13 +799,16 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
       atomicOr(err, 2);
       return;
     }
-    if (local) {
+    if (slot < n_loc) {
       // most draws land on slots already holding a smaller index: a plain
       // read first keeps the atomics (and their same-address serialisation) rare
       const uint32_t rel = (uint32_t)(li - base);
       if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
-    } else
-      atomicMin(&slot_first[J.lat_off + slot], (unsigned long long)(J.cand_base + li));
+    } else {
+      unsigned long long* dst = &slot_first[J.lat_off + slot];
+      const unsigned long long g = (unsigned long long)(J.cand_base + li);
+      if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
+    }
   };
   if (J.flags & TPE_F_DRAW32) {
     // kLatR consecutive candidates per thread, pair-shared Philox draws
@@ -814,7 +819,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
                         (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
                         x);
     int qe;
-    if (frexp(J.q, &qe) == 0.5 && qe > -100 && qe < 100 && local) {
+    if (frexp(J.q, &qe) == 0.5 && qe > -100 && qe < 100 && J.lat_n <= kLatLds) {
       // q a power of two: x * (1/q) is exact in fp32, so rintf gives np.round(x / q)
       // exactly and the slot needs no fp64 work
       const float inv_q32 = (float)inv_q;
@@ -844,12 +849,12 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
       mark(v, li);
     }
   }
-  if (local) {
+  {
     __syncthreads();
     // blocks run roughly in index order, so the global slot mostly holds a
     // smaller index already: an agent-scope load first keeps the (cross-XCD)
     // atomics to the blocks that improve a slot
-    for (int s = threadIdx.x; s < J.lat_n; s += kBS) {
+    for (int s = threadIdx.x; s < n_loc; s += kBS) {
       const uint32_t f = lfirst[s];
       if (f == 0xFFFFFFFFu) continue;
       unsigned long long* dst = &slot_first[J.lat_off + s];
