@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
     filled = 0;
     __builtin_amdgcn_wave_barrier();
   };
-  constexpr int kDepth = 8;  // tiles of 64 observations loaded per step
+  constexpr int kDepth = 32;  // tiles of 64 observations in flight per step (latency-bound scan)
   for (int t0 = 0; t0 < n; t0 += kDepth * kWave) {
     int64_t cur[kDepth];
 #pragma unroll

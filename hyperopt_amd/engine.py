@@ -348,9 +348,11 @@ class Engine:
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
             outputs=False, stream=None, timers=None, sample_only=False,
             pruned=True, scorer=None, posteriors=False, history=None, rows=None,
-            is_below=None, histories=None) -> List[LabelResult]:
+            is_below=None, histories=None, timer_groups=None) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
-        per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``.
+        per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``;
+        ``timer_groups`` (optional set) limits them to those groups (each event
+        pair costs the stream a ~10 us timestamp barrier).
         ``sample_only``: fit, then only draw the candidates of the continuous
         labels (tpe_sample) into ``LabelResult.cand`` -- the sampler test hook.
         ``scorer`` picks the fp32 kernel for unquantized labels: "dense"
@@ -386,16 +388,16 @@ class Engine:
                 hp.append((name, time.perf_counter()))
         _hmark("start")
 
-        def tick(on=None):
-            if timers is None:
+        def tick(name, on=None):
+            if timers is None or (timer_groups is not None and name not in timer_groups):
                 return None
             e = torch.cuda.Event(enable_timing=True)
             e.record(stream if on is None else on)
             return e
 
         def tock(name, e0, on=None):
-            if timers is not None:
-                timers.setdefault(name, []).append((e0, tick(on)))
+            if e0 is not None:
+                timers.setdefault(name, []).append((e0, tick(name, on)))
         lib = self.lib
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
@@ -690,7 +692,7 @@ class Engine:
         if hist_mode:
             d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
             d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
-            e0 = tick()
+            e0 = tick("gather")
             if histories is None:
                 L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
                                            history.ld,
@@ -711,13 +713,13 @@ class Engine:
         _hmark('upload+gather')
         # ---- posterior fit ------------------------------------------------------
         if fit_ids:
-            e0 = tick()
+            e0 = tick("fit")
             L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
                                        n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
                                        d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
             tock("fit", e0)
         if cat:
-            e0 = tick()
+            e0 = tick("cat_fit")
             d_p = base + o_p  # the posterior is formed in place in the staged pool
             L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
                                           int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, sp),
@@ -778,7 +780,7 @@ class Engine:
             ks = side_p if on_side else sp
             kst = side if on_side else None
             pname = "partial_side" if on_side else "partial"
-            e0 = tick(kst)
+            e0 = tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst)
             if kind == "cont":
                 npart = lib.tpe_score_partials(hjp, nj)
                 d_part = self._buf("partial", 32 * max(npart, 1))
@@ -795,7 +797,7 @@ class Engine:
                 L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
                                                 d_gen, d_sx, d_si, sp), "tpe_sort_candidates")
                 tock("sort", e0)
-                e0 = tick()
+                e0 = tick("sorted")
                 L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,
                                              d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
                         "tpe_score_sorted")
@@ -820,7 +822,7 @@ class Engine:
                     ev.record(side)
                     stream.wait_event(ev)
                     joined = True
-                e0 = tick()
+                e0 = tick("table")
                 L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32, d_tab,
                                             d_cells, d_cand, d_bl, d_al, d_x, d_part, npart, db,
                                             d_stats, sp), "tpe_score_table")

@@ -1,5 +1,8 @@
-"""Configs C4 and C5 (BASELINE.json configs[3], [4]) at their stated sizes on one
-GPU, through the drop-in API (diagnostic / measurement; run on the GPU box).
+"""Configs C2, C4 and C5 (BASELINE.json configs[2], [3], [4]) at their stated
+sizes on one GPU, through the drop-in API (measurement; run on the GPU box).
+
+C2: 1-D hp.uniform('x', -5, 5), 10k-trial history (x ~ U(-5,5) seed 0, losses
+    N(0,1) seed 1), n_EI_candidates = 2^20, tpe.suggest p50 over 20 calls.
 
 C5: 3-level nested hp.choice space (tests/golden/spaces.py:nested), 100k-trial
     history drawn from the prior (seed 0), N(0,1) losses (seed 1),
@@ -93,6 +96,18 @@ def c5(T=100_000, n_ei=1 << 24):
             "history_build_s": round(build_s, 1)}
 
 
+def c2(T=10_000, n_ei=1 << 20):
+    """C2: hp.uniform('x', -5, 5), x_t ~ U(-5, 5) (seed 0), losses N(0,1) (seed 1)."""
+    domain = Domain(lambda p: 0.0, {"x": hp.uniform("x", -5, 5)})
+    trials = flat_trials(domain, T, 0)
+    docs, ms = timed(lambda k: tpe.suggest([T + k], domain, trials, k, n_EI_candidates=n_ei,
+                                           verbose=False), 20, 3)
+    return {"config": "C2", "history": T, "n_EI_candidates": n_ei,
+            "suggest_p50_ms": float(np.median(ms)), "suggest_p90_ms": float(np.percentile(ms, 90)),
+            "EI_candidates_per_s_p50": n_ei / (np.median(ms) * 1e-3),
+            "value_last": docs[0]["misc"]["vals"]["x"]}
+
+
 def c4_space(s):
     sp = {}
     for i in range(4):
@@ -132,6 +147,6 @@ def c4(studies=512, T=2000, n_ei=1 << 12):
 if __name__ == "__main__":
     import torch
     torch.cuda.set_device(0)
-    which = sys.argv[1:] or ["c5", "c4"]
+    which = sys.argv[1:] or ["c2", "c5", "c4"]
     for w in which:
-        print(json.dumps({"c5": c5, "c4": c4}[w]()), flush=True)
+        print(json.dumps({"c2": c2, "c5": c5, "c4": c4}[w]()), flush=True)
