@@ -30,7 +30,7 @@ def step(k, timers=None, groups=None):
 
 
 for rep in range(2):
-    for mode in ("none", "all", "table", "fit"):
+    for mode in sys.argv[1:] or ("none", "all", "table", "fit"):
         for k in range(3):
             step(k)
         torch.cuda.synchronize()
