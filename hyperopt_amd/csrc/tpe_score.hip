@@ -238,12 +238,13 @@ __device__ __forceinline__ void lse64(const double4* __restrict__ coef, const tp
       for (int r = 0; r < R; ++r) {
         const double t = (y[r] - c.x) * c.y;
         const double v = -0.5 * (t * t) + c.z;
-        if (v > m[r]) {
-          s[r] = s[r] * exp(m[r] - v) + 1.0;
-          m[r] = v;
-        } else {
-          s[r] += exp(v - m[r]);
-        }
+        // one exp per pair on every lane: a branch per lane would run the
+        // (software) fp64 exp twice whenever the wave diverges.  Same values
+        // as s*exp(m-v)+1 (new max) / s+exp(v-m), NaN included.
+        const bool up = v > m[r];
+        const double e = exp(up ? m[r] - v : v - m[r]);
+        s[r] = up ? s[r] * e + 1.0 : s[r] + e;
+        m[r] = up ? v : m[r];
       }
     }
   }
