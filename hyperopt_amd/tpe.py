@@ -413,11 +413,11 @@ def suggest_many(requests, shard_studies=False):
                 continue
             key = (st["kw"]["prior_weight"], st["kw"]["linear_forgetting"], st["prec"],
                    st["obs"].device)
-            for lab in level:
+            for lab, k in zip(level, label_keys(st["rq"].seed, level)):
                 spec = st["rq"].domain.specs[lab]
                 j = st["col"][lab]
-                w = st["obs"].work(lab, spec, j, n_cand=st["count"],
-                                   key=label_key(st["rq"].seed, lab), cand_base=st["start"])
+                w = st["obs"].work(lab, spec, j, n_cand=st["count"], key=k,
+                                   cand_base=st["start"])
                 batches.setdefault(key, []).append((st, lab, w))
         if not batches:
             break
