@@ -184,11 +184,15 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
   return clamp32(y, lo_on, hi_on, lo, hi);
 }
 
-// R consecutive candidates g0 .. g0+R-1 per thread (g0 even), n of them
-// valid, each exactly as draw32 draws it (to_x: LGMM1 values as exp(y), as
-// draw32's callers store them; otherwise the mixture coordinate y).
+// R consecutive candidates g0 .. g0+R-1 per thread, n of them valid, each
+// exactly as draw32 draws it (to_x: LGMM1 values as exp(y), as draw32's
+// callers store them; otherwise the mixture coordinate y).
 // Attempt 0 of every pair is drawn unrolled into registers (one Philox call
-// serves both candidates of a pair).  Bounded labels then retry their
+// serves both candidates of a pair).  An odd g0 (a shard that starts inside a
+// pair -- g0 is cand_base + an even offset, so the test is job-uniform)
+// draws attempt 0 of each candidate alone instead: same values, since
+// attempt32(g) is the half of attempt32_pair(g >> 1) that g owns.  Bounded
+// labels then retry their
 // rejected candidates one at a time, each lane walking its own queue (a
 // rejection costs that lane one more step instead of stalling the wave for a
 // whole draw); the retried values come back through `wstage`, the calling
@@ -199,14 +203,22 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
                                              bool to_x, float* wstage, float (&x)[R]) {
   static_assert(R % 2 == 0 && R <= 32, "pairs, one mask bit per candidate");
   uint32_t rej = 0;
+  if (g0 & 1) {
 #pragma unroll
-  for (int p = 0; p < R / 2; ++p) {
-    float y0, y1;
-    attempt32_pair(M, key, (g0 >> 1) + p, 0u, y0, y1);
-    x[2 * p] = y0;
-    x[2 * p + 1] = y1;
-    if (!accept32(y0, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p);
-    if (!accept32(y1, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p + 1);
+    for (int r = 0; r < R; ++r) {
+      x[r] = attempt32(M, key, g0 + r, 0u);
+      if (!accept32(x[r], lo_on, hi_on, lo, hi)) rej |= 1u << r;
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < R / 2; ++p) {
+      float y0, y1;
+      attempt32_pair(M, key, (g0 >> 1) + p, 0u, y0, y1);
+      x[2 * p] = y0;
+      x[2 * p + 1] = y1;
+      if (!accept32(y0, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p);
+      if (!accept32(y1, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p + 1);
+    }
   }
   rej &= n >= R ? ~0u : (n <= 0 ? 0u : (1u << n) - 1u);
 #ifdef TPE_DIAG_NO_RETRY  // diagnostic builds only: rejected draws clamped, no retries

@@ -1162,23 +1162,36 @@ __global__ __launch_bounds__(kBS) void k_sample(const tpe_job* __restrict__ jobs
                                                 const double* __restrict__ wcdf,
                                                 double* __restrict__ out_x) {
   __shared__ MixLds s_mix;
+  __shared__ float s_stage[kLatR * kBS];
   const tpe_job J = jobs[blockIdx.y];
   const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
   if (base >= J.n_cand) return;
   const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_mix);
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  if (sizeof(T) == 4) {
+    // the fp32 stream exactly as the scorers draw it: kLatR consecutive
+    // candidates per thread through draw32_pairs (the table scorer's and the
+    // DRAW32 lattice sampler's code), LGMM1 values as __expf(y)
+    const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
+    const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
+    float x[kLatR];
+    draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
+                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), x);
+#pragma unroll
+    for (int r = 0; r < kLatR; ++r) {
+      if (r >= nv) continue;
+      double v = (double)x[r];
+      if (J.flags & TPE_F_QUANT) v = rint(v / J.q) * J.q;
+      out_x[J.out_off + t0 + r] = v;
+    }
+    return;
+  }
   for (int r = 0; r < kLatR; ++r) {
     const int64_t li = base + r * kBS + threadIdx.x;
     if (li >= J.n_cand) break;
-    double v;
-    if (sizeof(T) == 4) {
-      float f = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
-      v = lgmm ? (double)__expf(f) : (double)f;
-    } else {
-      v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
-      if (lgmm) v = exp(v);
-    }
+    double v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+    if (lgmm) v = exp(v);
     if (J.flags & TPE_F_QUANT) v = rint(v / J.q) * J.q;
     out_x[J.out_off + li] = v;
   }

@@ -65,6 +65,10 @@ class LabelWork:
     col: Optional[int] = None
     n_above: int = 0
     hist: int = 0             # Engine.run(histories=...): index of this work's history
+    # candidates of the label over all devices (0: n_cand).  The automatic
+    # scorer choice follows it, so every shard of a label runs the same
+    # kernel and the winner does not depend on the number of ranks
+    n_total: int = 0
 
 
 @dataclass(slots=True)
@@ -281,7 +285,7 @@ class Engine:
                 P = _params(w.kind, w.args)
                 if not P["bounded"]:  # the lattice range follows the below set
                     lat = _lattice_range(w, P)
-            parts.append((w.kind, w.args, int(w.n_cand), w.col, w.hist, lat))
+            parts.append((w.kind, w.args, int(w.n_cand), int(w.n_total), w.col, w.hist, lat))
         key = (tuple(parts), float(prior_weight), int(lf), int(precision), scorer, multi)
         try:
             hash(key)
@@ -373,6 +377,8 @@ class Engine:
         ``histories``: a list of (DeviceHistory, rows or None, is_below) for
         batches of independent studies; each work names its history by
         ``hist`` (one tpe_gather_obs_multi launch gathers every list)."""
+        if not works:
+            return []
         if sample_only:
             outputs = True
         if scorer is None:
@@ -517,7 +523,8 @@ class Engine:
             def cont_mode(i):
                 if precision != 32 or sample_only:
                     return "cont"
-                n = int(np.asarray(works[i].cand).size) if inj(i) else int(works[i].n_cand)
+                n = int(np.asarray(works[i].cand).size) if inj(i) else \
+                    int(works[i].n_total or works[i].n_cand)
                 mode = scorer
                 if mode == "auto":
                     mode = "cont"
@@ -989,8 +996,12 @@ def _lattice_range(w: LabelWork, P):
     else:
         obs = np.asarray(w.obs_below, dtype=np.float64)
         if P["transform"] == L.OBS_LOG:
-            obs = np.log(np.maximum(obs, P["floor"])) if obs.size else obs
-        pts = np.concatenate([obs, [P["prior_mu"]]])
+            with np.errstate(all="ignore"):
+                obs = np.log(np.maximum(obs, P["floor"])) if obs.size else obs
+        # non-finite observations (as _support drops them): the fit places
+        # components at them, but the lattice spans the finite draws only --
+        # a draw off the lattice is reported (err bit 2), never written
+        pts = np.concatenate([obs[np.isfinite(obs)], [P["prior_mu"]]])
         lo = float(pts.min()) - 9.0 * P["prior_sigma"]
         hi = float(pts.max()) + 9.0 * P["prior_sigma"]
     if P["family"] == L.LGMM1:

@@ -27,7 +27,6 @@ from __future__ import annotations
 
 import functools
 import logging
-import math
 import os
 import time
 
@@ -320,12 +319,12 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
     isb, isa = split_masks(hist, gamma)
     prec = _precision(precision, n_EI_candidates, hist.tids.size)
     rank, ws = hdist.world()
-    start, count = hdist.shard(max(int(n_EI_candidates), 0), rank, ws)
+    n_ei = max(int(n_EI_candidates), 0)
     col = {lab: j for j, lab in enumerate(labels)}
 
     walk, stored = {}, {}
     live = []
-    if n_EI_candidates > 0:
+    if n_ei > 0:
         eng = engine()
         obs = LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY)
         while True:
@@ -333,15 +332,23 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
             level = [lab for lab in live if lab not in walk]
             if not level:
                 break
-            works = [obs.work(lab, domain.specs[lab], col[lab], n_cand=count, key=k,
-                              cand_base=start)
-                     for lab, k in zip(level, label_keys(seed, level))]
+            keys = label_keys(seed, level)
+            # under torch.distributed this rank scores its units of the level
+            # (whole labels, or candidate ranges when labels < ranks) and the
+            # winners are combined across ranks (hyperopt_amd/dist.py)
+            units = hdist.plan_units([domain.specs[lab].kind for lab in level], n_ei, ws)[rank]
+            works = [obs.work(level[i], domain.specs[level[i]], col[level[i]], n_cand=count,
+                              key=keys[i], cand_base=start, n_total=n_ei)
+                     for i, start, count in units]
             res = eng.run(works, prior_weight=prior_weight, lf=linear_forgetting,
                           precision=prec, **obs.run_kwargs)
             if ws > 1:
-                hdist.allreduce_best(res)
-            for lab, r in zip(level, res):
-                walk[lab], stored[lab] = _decode(domain.specs[lab], r.value)
+                best = hdist.gather_best(len(level), [(u[0], r) for u, r in zip(units, res)])
+                values = [b[2] for b in best]
+            else:
+                values = [r.value for r in res]
+            for lab, v in zip(level, values):
+                walk[lab], stored[lab] = _decode(domain.specs[lab], v)
     live = set(live)
     misc = {"tid": first_new_id, "cmd": domain.cmd, "workdir": domain.workdir,
             "idxs": {lab: ([first_new_id] if lab in live else []) for lab in labels},
@@ -398,7 +405,7 @@ def suggest_many(requests, shard_studies=False):
         states.append(dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist,
                            obs=LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY),
                            col={lab: j for j, lab in enumerate(labels)}, walk={}, stored={},
-                           live=[], start=start, count=count, done=n_ei == 0,
+                           live=[], start=start, count=count, n_ei=n_ei, done=n_ei == 0,
                            prec=_precision(kw["precision"], n_ei, hist.tids.size)))
     while True:
         batches = {}  # (prior_weight, lf, precision, device) -> [(state, label, work)]
@@ -417,7 +424,7 @@ def suggest_many(requests, shard_studies=False):
                 spec = st["rq"].domain.specs[lab]
                 j = st["col"][lab]
                 w = st["obs"].work(lab, spec, j, n_cand=st["count"], key=k,
-                                   cand_base=st["start"])
+                                   cand_base=st["start"], n_total=st["n_ei"])
                 batches.setdefault(key, []).append((st, lab, w))
         if not batches:
             break
@@ -449,5 +456,3 @@ def suggest_many(requests, shard_studies=False):
         out[st["qi"]] = rq.trials.new_trial_docs([tid], [None], [rq.domain.new_result()], [misc])
     return out
 
-
-_ = math
