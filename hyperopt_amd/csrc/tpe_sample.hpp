@@ -202,24 +202,29 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
                                              bool lo_on, bool hi_on, float lo, float hi,
                                              bool to_x, float* wstage, float (&x)[R]) {
   static_assert(R % 2 == 0 && R <= 32, "pairs, one mask bit per candidate");
-  uint32_t rej = 0;
-  if (g0 & 1) {
+  // pair m = (g0 >> 1) + p holds candidates 2m (cos half) and 2m+1 (sin
+  // half).  Aligned: x[2p], x[2p+1] = pair p.  Odd g0: x[2p] is pair p's
+  // sin half and x[2p-1] pair p's cos half; x[R-1] needs one more pair.
+  // Selects, not a second unrolled draw loop: the register footprint (and
+  // so the occupancy of the scorer) stays that of the aligned loop.
+  const bool odd = (g0 & 1) != 0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      x[r] = attempt32(M, key, g0 + r, 0u);
-      if (!accept32(x[r], lo_on, hi_on, lo, hi)) rej |= 1u << r;
-    }
-  } else {
-#pragma unroll
-    for (int p = 0; p < R / 2; ++p) {
-      float y0, y1;
-      attempt32_pair(M, key, (g0 >> 1) + p, 0u, y0, y1);
-      x[2 * p] = y0;
-      x[2 * p + 1] = y1;
-      if (!accept32(y0, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p);
-      if (!accept32(y1, lo_on, hi_on, lo, hi)) rej |= 1u << (2 * p + 1);
-    }
+  for (int p = 0; p < R / 2; ++p) {
+    float c, s;
+    attempt32_pair(M, key, (g0 >> 1) + p, 0u, c, s);
+    x[2 * p] = odd ? s : c;
+    x[2 * p + 1] = s;  // odd: replaced by the next pair's cos half
+    if (p > 0 && odd) x[2 * p - 1] = c;
   }
+  if (odd) {
+    float c, s;
+    attempt32_pair(M, key, (g0 >> 1) + R / 2, 0u, c, s);
+    x[R - 1] = c;
+  }
+  uint32_t rej = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (!accept32(x[r], lo_on, hi_on, lo, hi)) rej |= 1u << r;
   rej &= n >= R ? ~0u : (n <= 0 ? 0u : (1u << n) - 1u);
 #ifdef TPE_DIAG_NO_RETRY  // diagnostic builds only: rejected draws clamped, no retries
 #pragma unroll

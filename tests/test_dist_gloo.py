@@ -97,3 +97,76 @@ def test_combine_host_records():
     out = hdist.combine_host(np.stack([a.view(np.uint8), b.view(np.uint8)]))
     assert out[0]["index"] == 2 and out[0]["n_scored"] == 20
     assert out[1]["index"] == 9
+
+
+def _unit_worker(rank, world, port, q):
+    """Label-sharded level: each rank 'scores' only its units (synthetic
+    winners derived from the unit) and gather_best combines them."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kinds = ["uniform", "randint", "quniform", "normal", "loguniform"]
+    units = hdist.plan_units(kinds, 1000, world)[rank]
+    local = []
+    for i, start, count in units:
+        # winner of a unit: global index start + (7 * i) % count, score by label;
+        # label 1 is a NaN label whose first NaN must win
+        idx = start + (7 * i) % count
+        score = float("nan") if i == 1 else float(i)
+        local.append((i, LabelResult("l%d" % i, idx, 0.5 * idx, score, count)))
+    best = hdist.gather_best(len(kinds), local)
+    q.put((rank, best))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_best_label_sharded_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_unit_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # every rank agrees, and each label's winner is its unit's (whole labels:
+    # 5 labels >= ranks, so each label lives on one rank)
+    for r in range(1, world):
+        assert [tuple(np.nan_to_num(b)) for b in out[r]] == \
+               [tuple(np.nan_to_num(b)) for b in out[0]]
+    for i, (score, index, value, n) in enumerate(out[0]):
+        assert n == 1000 and index == (7 * i) % 1000 and value == 0.5 * index
+        assert (np.isnan(score) if i == 1 else score == float(i))
+
+
+def test_plan_units_partition():
+    kinds = ["uniform"] * 10 + ["loguniform"] * 10 + ["quniform"] * 10 + ["normal"] * 10 + \
+            ["randint"] * 10
+    for n_total in (1, 24, 4097, 1 << 22):
+        for ws in (1, 2, 3, 4, 7, 8, 64):
+            for ks in (kinds, kinds[:3], kinds[:1], []):
+                plan = hdist.plan_units(ks, n_total, ws)
+                assert len(plan) == ws
+                assert plan == hdist.plan_units(ks, n_total, ws)  # deterministic
+                cover = {}
+                for units in plan:
+                    for i, s, c in units:
+                        cover.setdefault(i, []).append((s, c))
+                assert sorted(cover) == list(range(len(ks)))
+                for i, parts in cover.items():
+                    parts.sort()
+                    pos = 0
+                    for s, c in parts:
+                        assert s == pos and c > 0
+                        pos += c
+                    assert pos == n_total
+    # C3 on 8 ranks: whole labels, the costliest rank within one table label
+    # of the mean
+    plan = hdist.plan_units(kinds, 1 << 22, 8)
+    cost = [sum(hdist.UNIT_COST[hdist.kind_class(kinds[i])] for i, _, _ in u) for u in plan]
+    mean = sum(cost) / 8
+    assert max(cost) - mean <= 1.0
+    assert all(c == 1 << 22 for u in plan for _, _, c in u)

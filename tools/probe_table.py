@@ -20,8 +20,11 @@ eng = Engine()
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 22
 kinds = sys.argv[2].split(",") if len(sys.argv) > 2 else ["uniform", "loguniform", "normal"]
 scorers = sys.argv[3].split(",") if len(sys.argv) > 3 else ["table"]
-for kind in kinds:
-    sub = [s for s in space if s[1] == kind]
+groups = [[s for s in space if s[1] == kind] for kind in kinds]
+if len(kinds) > 1:  # and all of them in one launch (the bench's shape)
+    groups.append([s for s in space if s[1] in kinds])
+for sub in groups:
+    kind = "+".join(sorted({s[1] for s in sub}))
     for scorer in scorers:
         eng.run(bench.make_works(sub, sp, 0, n, 0), scorer=scorer)
         timers = {}
@@ -34,7 +37,7 @@ for kind in kinds:
 
 # cell-grid geometry of the last run (tpe_table records)
 from hyperopt_amd import _lib as L  # noqa: E402
-nt = len([s for s in space if s[1] in kinds])
+nt = len(groups[-1])
 raw = eng._bufs["tables"][:L.TABLE_DTYPE.itemsize * nt].cpu().numpy().view(L.TABLE_DTYPE)
 for t in raw[:nt]:
     print("  nb %6d  h %.3g  span %.3g  wide b/a %d/%d" % (t["nb"], t["h"], t["hi"] - t["lo"],

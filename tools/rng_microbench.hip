@@ -33,6 +33,34 @@ __device__ __forceinline__ U4 philox_hilo(U4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+// Threefry-4x32 (Random123 rotation constants), ROUNDS rounds, key injection
+// every 4 rounds: only adds, rotates (v_alignbit) and xors
+template <int ROUNDS>
+__device__ __forceinline__ U4 threefry(U4 c, uint32_t k0, uint32_t k1) {
+  constexpr int R0[8] = {10, 11, 13, 23, 6, 17, 25, 18};
+  constexpr int R1[8] = {26, 21, 27, 5, 20, 11, 10, 20};
+  const uint32_t k2 = 0, k3 = 0, k4 = 0x1BD11BDAu ^ k0 ^ k1;
+  const uint32_t ks[5] = {k0, k1, k2, k3, k4};
+  uint32_t x0 = c.x + k0, x1 = c.y + k1, x2 = c.z + k2, x3 = c.w + k3;
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    if ((r & 1) == 0) {
+      x0 += x1; x1 = rotl(x1, R0[r & 7]); x1 ^= x0;
+      x2 += x3; x3 = rotl(x3, R1[r & 7]); x3 ^= x2;
+    } else {
+      x0 += x3; x3 = rotl(x3, R0[r & 7]); x3 ^= x0;
+      x2 += x1; x1 = rotl(x1, R1[r & 7]); x1 ^= x2;
+    }
+    if ((r & 3) == 3) {
+      const int s = (r + 1) / 4;
+      x0 += ks[s % 5]; x1 += ks[(s + 1) % 5]; x2 += ks[(s + 2) % 5];
+      x3 += ks[(s + 3) % 5] + (uint32_t)s;
+    }
+  }
+  return U4{x0, x1, x2, x3};
+}
+
 template <int V>
 __global__ void k_philox(uint32_t* out, uint32_t key) {
   uint32_t acc[4] = {0, 0, 0, 0};
@@ -41,8 +69,12 @@ __global__ void k_philox(uint32_t* out, uint32_t key) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       U4 ctr{t, (uint32_t)it, (uint32_t)c, 0x53414D50u};
-      U4 r = V == 0 ? philox_mad64<10>(ctr, key, ~key)
-                    : (V == 1 ? philox_hilo(ctr, key, ~key) : philox_mad64<7>(ctr, key, ~key));
+      U4 r;
+      if (V == 0) r = philox_mad64<10>(ctr, key, ~key);
+      else if (V == 1) r = philox_hilo(ctr, key, ~key);
+      else if (V == 2) r = philox_mad64<7>(ctr, key, ~key);
+      else if (V == 3) r = threefry<13>(ctr, key, ~key);
+      else r = threefry<20>(ctr, key, ~key);
       acc[c] ^= r.x ^ r.y ^ r.z ^ r.w;
     }
   }
@@ -77,7 +109,8 @@ int main() {
   const double n = (double)blocks * threads * ITERS * 4;
   struct K { const char* name; void (*fn)(uint32_t*, uint32_t); } ks[] = {
       {"philox4x32-10 (v_mad_u64_u32)", k_philox<0>}, {"philox4x32-10 (mul_hi/mul_lo)", k_philox<1>},
-      {"philox4x32-7 (v_mad_u64_u32)", k_philox<2>}};
+      {"philox4x32-7 (v_mad_u64_u32)", k_philox<2>}, {"threefry4x32-13", k_philox<3>},
+      {"threefry4x32-20", k_philox<4>}};
   for (auto& k : ks) {
     float ms = 0;
     for (int rep = 0; rep < 3; ++rep) {
