@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32 = 1, 2, 4, 8, 16
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -77,6 +77,8 @@ _SIGNATURES = {
     "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_table": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
                              _P, _P, _P]),
+    "tpe_score_table_fast": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P,
+                                  _P, _P]),
     "tpe_score_partials": (_I64, [_P, _I]),
     "tpe_score_continuous": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P,
                                   _P, _I64, _P, _P]),

@@ -2,9 +2,10 @@
 //
 // GMM1 / LGMM1 draws (hyperopt/tpe.py:79-106, 229-257): component by inverse
 // CDF of the below mixture's weights, then N(mu, sigma) by Box-Muller, with
-// the reference's acceptance test low <= y < high.  Draw `a` of candidate `g`
-// is Philox4x32-10 at counter (g, a, "SAMP") under the label key, so every
-// kernel that draws candidate g sees the same value.
+// the reference's acceptance test low <= y < high.  Every draw is a function
+// of (label key, global candidate index, attempt) through Philox4x32-10, so
+// every kernel that draws candidate g sees the same value; the fp64 and fp32
+// streams differ (draw64 / attempt32_*).
 #pragma once
 
 #include "tpe_common.hpp"
@@ -15,6 +16,7 @@ constexpr int kBS = 256;       // block size of the candidate kernels
 constexpr int kStage = 64;     // below-mixture components staged in LDS for sampling
 constexpr uint32_t kMaxAttempts = 256;
 constexpr uint32_t kStreamSample = 0x53414D50u;  // "SAMP"
+constexpr uint32_t kStreamRetry = 0x52455452u;   // "RETR": fp32 retries
 constexpr int kGuide = 256;    // guide-table buckets (top 8 bits of the word)
 
 __device__ __forceinline__ tpe_best empty_best() { return tpe_best{0.0, -1, 0.0, 0}; }
@@ -35,14 +37,14 @@ struct Mix {  // sampler view of the below mixture (LDS or global)
   const double* sg;
   const uint32_t* thr;  // staged: component k takes words < thr[k] (fp32 draws)
   const uint2* gd;      // staged: guide entry of bucket b (see stage_mix)
-  const float2* ms32;   // staged: (mu, sigma) in fp32
+  const float4* cw;     // staged: {mu, sigma, bits of thr[k-1], 1 / (thr[k] - thr[k-1])}
   int n;
 };
 
 struct MixLds {  // LDS image of a below mixture of <= kStage components
   double cdf[kStage], mu[kStage], sg[kStage];
   uint32_t thr[kStage];
-  float2 ms32[kStage];
+  float4 cw[kStage];
   uint2 gd[kGuide];
 };
 
@@ -54,6 +56,8 @@ struct MixLds {  // LDS image of a below mixture of <= kStage components
 // Entry gd[b] = {thr[g], g | step << 8 | multi << 9}: step = (g < n-1), and
 // the component is g + step * (w >= thr[g]) unless a second threshold falls
 // inside the bucket (multi), where the walk over thr[] finishes the search.
+// cw[k] also carries component k's word interval [thr[k-1], thr[k]) so the
+// fp32 sampler can read the word's position inside it (comp_res).
 __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, const double* mu,
                                          const double* sigma, MixLds& L) {
   const int n = S.n_obs + 1;
@@ -66,7 +70,6 @@ __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, c
     L.cdf[k] = c;
     L.mu[k] = m;
     L.sg[k] = g;
-    L.ms32[k] = make_float2((float)m, (float)g);
     const double t = ceil(c / total * 4294967296.0);
     L.thr[k] = (t >= 4294967295.0) ? 0xFFFFFFFFu : (t > 0.0 ? (uint32_t)t : 0u);
   }
@@ -83,8 +86,13 @@ __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, c
     const uint32_t multi = (lo + 1 < n - 1 && L.thr[lo + 1] <= top) ? 1u : 0u;
     L.gd[b] = make_uint2(L.thr[lo], (uint32_t)lo | step << 8 | multi << 9);
   }
+  for (int k = threadIdx.x; k < n; k += kBS) {
+    const uint32_t lo = k ? L.thr[k - 1] : 0u, width = L.thr[k] - lo;
+    L.cw[k] = make_float4((float)L.mu[k], (float)L.sg[k], __uint_as_float(lo),
+                          width ? 1.0f / (float)width : 0.0f);
+  }
   __syncthreads();
-  return Mix{L.cdf, L.mu, L.sg, L.thr, L.gd, L.ms32, n};
+  return Mix{L.cdf, L.mu, L.sg, L.thr, L.gd, L.cw, n};
 }
 
 // One draw from the (possibly truncated) below mixture: returns the value in
@@ -107,10 +115,17 @@ __device__ __forceinline__ double draw64(const Mix& M, uint64_t key, int64_t g, 
   return y;
 }
 
-// fp32 draws come in pairs: attempt `a` of candidates 2m and 2m+1 is ONE
-// Philox call at counter (m, a): word x picks 2m's component, word w picks
-// 2m+1's, and (y, z) give the Box-Muller pair (cos -> 2m, sin -> 2m+1).
-// Candidate g's value therefore depends on g alone, whichever kernel draws it.
+// fp32 draws.  Attempt 0 of candidates 4m .. 4m+3 is ONE Philox call at
+// counter (m, 0): word k picks candidate 4m+k's component by inverse CDF, and
+// the word's position inside that component's interval -- a uniform of its
+// own, independent of which component it picked -- feeds Box-Muller: the
+// residuals of words 0 / 1 give radius / angle of the pair (4m, 4m+1) (cos ->
+// 4m, sin -> 4m+1), words 2 / 3 those of (4m+2, 4m+3).  Four candidates per
+// call, so the sampler spends half as many Philox rounds (quarter-rate
+// v_mad_u64_u32) per candidate as a pair-per-call scheme.  Retries (attempt
+// a >= 1, bounded labels) take one call per candidate at counter (g, a) in a
+// stream of their own.  Candidate g's value depends on g alone, whichever
+// kernel draws it.
 __device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
   if (M.thr) {  // block-uniform: staged mixture, one guide entry (+ rare walk)
     const uint2 e = M.gd[word >> 24];
@@ -122,45 +137,99 @@ __device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
   const double u = (double)word * 0x1.0p-32 * M.cdf[M.n - 1];
   return upper_bound(M.cdf, M.n, u);
 }
-__device__ __forceinline__ float2 ms32_of(const Mix& M, int j) {  // (mu, sigma)
-  return M.ms32 ? M.ms32[j] : make_float2((float)M.mu[j], (float)M.sg[j]);
+
+// component (mu, sigma) of `word` and the word's residual uniform in [0, 1)
+// (clamped below 1, so 1 - res >= 2^-24 and a Box-Muller radius stays < 5.77)
+__device__ __forceinline__ void comp_res(const Mix& M, uint32_t word, float& mu, float& sg,
+                                         float& res) {
+#ifdef TPE_DIAG_NO_COMP  // diagnostic builds only (tools/diag_variants.sh)
+  const float4 c = M.cw ? M.cw[word & 7] : make_float4(0.0f, 1.0f, 0.0f, 0x1.0p-32f);
+  mu = c.x;
+  sg = c.y;
+  res = (float)word * 0x1.0p-32f;
+#else
+  if (M.cw) {
+    const float4 c = M.cw[comp_of(M, word)];
+    mu = c.x;
+    sg = c.y;
+    res = (float)(word - __float_as_uint(c.z)) * c.w;
+  } else {
+    const double total = M.cdf[M.n - 1];
+    const double u = (double)word * 0x1.0p-32 * total;
+    const int k = upper_bound(M.cdf, M.n, u);
+    const double lo = k ? M.cdf[k - 1] : 0.0, wk = M.cdf[k] - lo;
+    res = wk > 0.0 ? (float)((u - lo) / wk) : 0.0f;
+    mu = (float)M.mu[k];
+    sg = (float)M.sg[k];
+  }
+#endif
+  res = fminf(res, 0x1.fffffep-1f);
 }
 
-__device__ __forceinline__ void attempt32_pair(const Mix& M, uint64_t key, int64_t m, uint32_t a,
-                                               float& y0, float& y1) {
-#ifdef TPE_DIAG_NO_PHILOX  // diagnostic builds only (tools/diag_variants.sh)
-  const uint32_t hsh = (uint32_t)m * 0x9E3779B9u ^ a * 0x85EBCA6Bu ^ (uint32_t)key;
-  const U4 r{hsh, hsh * 0xC2B2AE35u, hsh ^ 0x27D4EB2Fu, hsh * 0x165667B1u};
-#else
-  const U4 r = draw_words(key, m, a, kStreamSample);
-#endif
-#ifdef TPE_DIAG_NO_COMP
-  const int j0 = (int)(r.x & 7), j1 = (int)(r.w & 7);
-#else
-  const int j0 = comp_of(M, r.x), j1 = comp_of(M, r.w);
-#endif
-  float z0, z1;
+// Box-Muller pair from two residual uniforms: radius from ra, angle from rb
+__device__ __forceinline__ void bm_pair(float ra, float rb, float& z0, float& z1) {
 #ifdef TPE_DIAG_NO_BM
-  z0 = (float)(int)r.y * 0x1.0p-31f;
-  z1 = (float)(int)r.z * 0x1.0p-31f;
+  z0 = ra - 0.5f;
+  z1 = rb - 0.5f;
 #else
-  normal_pair_f32(r.y, r.z, z0, z1);
+  const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(1.0f - ra));
+  z0 = r * __builtin_amdgcn_cosf(rb);
+  z1 = r * __builtin_amdgcn_sinf(rb);
 #endif
-  const float2 c0 = ms32_of(M, j0), c1 = ms32_of(M, j1);
-  y0 = fmaf(c0.y, z0, c0.x);
-  y1 = fmaf(c1.y, z1, c1.x);
 }
 
-// attempt `a` of candidate `g` alone (same value as attempt32_pair's half)
+__device__ __forceinline__ U4 quad_words(uint64_t key, int64_t m) {
+#ifdef TPE_DIAG_NO_PHILOX  // diagnostic builds only
+  const uint32_t hsh = (uint32_t)m * 0x9E3779B9u ^ (uint32_t)key;
+  return U4{hsh, hsh * 0xC2B2AE35u, hsh ^ 0x27D4EB2Fu, hsh * 0x165667B1u};
+#else
+  return draw_words(key, m, 0u, kStreamSample);
+#endif
+}
+
+// attempt 0 of candidates 4m .. 4m+3
+__device__ __forceinline__ void attempt32_quad(const Mix& M, uint64_t key, int64_t m, float& y0,
+                                               float& y1, float& y2, float& y3) {
+  const U4 r = quad_words(key, m);
+  float mu0, sg0, r0, mu1, sg1, r1, mu2, sg2, r2, mu3, sg3, r3;
+  comp_res(M, r.x, mu0, sg0, r0);
+  comp_res(M, r.y, mu1, sg1, r1);
+  comp_res(M, r.z, mu2, sg2, r2);
+  comp_res(M, r.w, mu3, sg3, r3);
+  float z0, z1, z2, z3;
+  bm_pair(r0, r1, z0, z1);
+  bm_pair(r2, r3, z2, z3);
+  y0 = fmaf(sg0, z0, mu0);
+  y1 = fmaf(sg1, z1, mu1);
+  y2 = fmaf(sg2, z2, mu2);
+  y3 = fmaf(sg3, z3, mu3);
+}
+
+// attempt 0 of candidate g alone (its share of attempt32_quad at m = g >> 2)
+__device__ __forceinline__ float attempt32_first(const Mix& M, uint64_t key, int64_t g) {
+  const U4 r = quad_words(key, g >> 2);
+  const bool hi_pair = (g & 2) != 0, second = (g & 1) != 0;
+  float mua, sga, ra, mub, sgb, rb;
+  comp_res(M, hi_pair ? r.z : r.x, mua, sga, ra);
+  comp_res(M, hi_pair ? r.w : r.y, mub, sgb, rb);
+  float z0, z1;
+  bm_pair(ra, rb, z0, z1);
+  return second ? fmaf(sgb, z1, mub) : fmaf(sga, z0, mua);
+}
+
+// attempt a >= 1 of candidate g: one Philox call of the retry stream
+__device__ __forceinline__ float attempt32_retry(const Mix& M, uint64_t key, int64_t g,
+                                                 uint32_t a) {
+  const U4 r = draw_words(key, g, a, kStreamRetry);
+  float mu, sg, res;
+  comp_res(M, r.x, mu, sg, res);
+  float z0, z1;
+  bm_pair(u01_f32(r.y), u01_f32(r.z), z0, z1);
+  return fmaf(sg, z0, mu);
+}
+
 __device__ __forceinline__ float attempt32(const Mix& M, uint64_t key, int64_t g, uint32_t a) {
-  const U4 r = draw_words(key, g >> 1, a, kStreamSample);
-  const int j = comp_of(M, (g & 1) ? r.w : r.x);
-  const float u1 = 1.0f - u01_f32(r.y);
-  const float u2 = (float)(r.z >> 8) * 0x1.0p-24f;
-  const float rr = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-  const float z = rr * ((g & 1) ? __builtin_amdgcn_sinf(u2) : __builtin_amdgcn_cosf(u2));
-  const float2 c = ms32_of(M, j);
-  return fmaf(c.y, z, c.x);
+  return a == 0 ? attempt32_first(M, key, g) : attempt32_retry(M, key, g, a);
 }
 
 __device__ __forceinline__ bool accept32(float y, bool lo_on, bool hi_on, float lo, float hi) {
@@ -186,40 +255,31 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
 
 // R consecutive candidates g0 .. g0+R-1 per thread, n of them valid, each
 // exactly as draw32 draws it (to_x: LGMM1 values as exp(y), as draw32's
-// callers store them; otherwise the mixture coordinate y).
-// Attempt 0 of every pair is drawn unrolled into registers (one Philox call
-// serves both candidates of a pair).  An odd g0 (a shard that starts inside a
-// pair -- g0 is cand_base + an even offset, so the test is job-uniform)
-// draws attempt 0 of each candidate alone instead: same values, since
-// attempt32(g) is the half of attempt32_pair(g >> 1) that g owns.  Bounded
-// labels then retry their
-// rejected candidates one at a time, each lane walking its own queue (a
-// rejection costs that lane one more step instead of stalling the wave for a
-// whole draw); the retried values come back through `wstage`, the calling
-// wave's own R*64 floats of LDS (slot r of lane l at r*64 + l).
+// callers store them; otherwise the mixture coordinate y).  Attempt 0 is
+// drawn unrolled into registers, one Philox call per four candidates.  A
+// start inside a call (g0 not a multiple of 4 -- only at a shard boundary;
+// g0 is cand_base + a multiple of R, so the test is job-uniform) draws
+// attempt 0 one candidate at a time in a rolled loop through `wstage`, which
+// keeps the register footprint of the aligned loop.  Bounded labels then
+// retry their rejected candidates one at a time, each lane walking its own
+// queue (a rejection costs that lane one more step instead of stalling the
+// wave for a whole draw); retried values come back through `wstage`, the
+// calling wave's own R*64 floats of LDS (slot r of lane l at r*64 + l).
 template <int R>
 __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t g0, int n,
                                              bool lo_on, bool hi_on, float lo, float hi,
                                              bool to_x, float* wstage, float (&x)[R]) {
-  static_assert(R % 2 == 0 && R <= 32, "pairs, one mask bit per candidate");
-  // pair m = (g0 >> 1) + p holds candidates 2m (cos half) and 2m+1 (sin
-  // half).  Aligned: x[2p], x[2p+1] = pair p.  Odd g0: x[2p] is pair p's
-  // sin half and x[2p-1] pair p's cos half; x[R-1] needs one more pair.
-  // Selects, not a second unrolled draw loop: the register footprint (and
-  // so the occupancy of the scorer) stays that of the aligned loop.
-  const bool odd = (g0 & 1) != 0;
+  static_assert(R % 4 == 0 && R <= 32, "quads, one mask bit per candidate");
+  float* st = wstage + lane_id();
+  if ((g0 & 3) == 0) {
 #pragma unroll
-  for (int p = 0; p < R / 2; ++p) {
-    float c, s;
-    attempt32_pair(M, key, (g0 >> 1) + p, 0u, c, s);
-    x[2 * p] = odd ? s : c;
-    x[2 * p + 1] = s;  // odd: replaced by the next pair's cos half
-    if (p > 0 && odd) x[2 * p - 1] = c;
-  }
-  if (odd) {
-    float c, s;
-    attempt32_pair(M, key, (g0 >> 1) + R / 2, 0u, c, s);
-    x[R - 1] = c;
+    for (int q = 0; q < R / 4; ++q)
+      attempt32_quad(M, key, (g0 >> 2) + q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+  } else {
+#pragma unroll 1
+    for (int r = 0; r < R; ++r) st[r * kWave] = attempt32_first(M, key, g0 + r);
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = st[r * kWave];
   }
   uint32_t rej = 0;
 #pragma unroll
@@ -233,12 +293,11 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
   rej = 0;
 #endif
   if (__any(rej != 0)) {
-    float* st = wstage + lane_id();
     uint32_t todo = rej, att = 1;
     while (__any(todo != 0)) {
       if (todo) {
         const int r = __builtin_ctz(todo);
-        float y = attempt32(M, key, g0 + r, att);
+        float y = attempt32_retry(M, key, g0 + r, att);
         const bool ok = accept32(y, lo_on, hi_on, lo, hi);
         if (ok || att + 1 >= kMaxAttempts) {
           if (!ok) y = clamp32(y, lo_on, hi_on, lo, hi);

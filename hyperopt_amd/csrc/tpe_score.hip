@@ -770,12 +770,19 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, int n_tiles, int n_jobs) {
   __shared__ uint32_t lfirst[kLatLds];
   __shared__ MixLds s_mix;
   __shared__ float s_stage[kLatR * kBS];
-  const tpe_job J = jobs[blockIdx.y];
-  const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
+  // XCD-aware work order (as k_score_table): each XCD sweeps a contiguous
+  // eighth of the (job, tile) list, so a job's first-index atomics stay in
+  // few XCDs' L2s
+  const int64_t W = (int64_t)n_tiles * n_jobs, per = (W + 7) / 8;
+  const int64_t wi = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (wi >= W) return;
+  const int job = (int)(wi / n_tiles);
+  const tpe_job J = jobs[job];
+  const int64_t base = (wi - (int64_t)job * n_tiles) * (kBS * kLatR);
   if (base >= J.n_cand) return;
   const tpe_seg SB = segs[J.below];
   const bool lgmm = J.family == TPE_LGMM1;
@@ -1333,8 +1340,13 @@ extern "C" int tpe_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
   if (hipMemsetAsync(slot_first, 0xFF, (size_t)end * sizeof(uint64_t), st) != hipSuccess)
     return check_launch("tpe_lattice_sample memset");
   const int64_t gx = max_blocks(host_jobs, n_jobs, (int64_t)kBS * kLatR, -1);
-  hipLaunchKernelGGL(k_lattice_sample, dim3((unsigned)gx, (unsigned)n_jobs), dim3(kBS), 0, st,
-                     jobs, segs, mu, sigma, wcdf, (unsigned long long*)slot_first, err);
+  const int64_t per = (gx * n_jobs + 7) / 8;
+  if (gx > INT32_MAX || 8 * per > INT32_MAX) {
+    set_error("tpe_lattice_sample: %lld work items", (long long)(gx * n_jobs));
+    return TPE_E_UNSUPPORTED;
+  }
+  hipLaunchKernelGGL(k_lattice_sample, dim3((unsigned)(8 * per)), dim3(kBS), 0, st, jobs, segs,
+                     mu, sigma, wcdf, (unsigned long long*)slot_first, err, (int)gx, n_jobs);
   return check_launch("tpe_lattice_sample");
 }
 

@@ -508,6 +508,97 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   return bad;
 }
 
+// ---------------------------------------------------------------------------
+// score cells.  The argmax needs only the score
+//     f(u) = (m_b - m_a) + log P_b(u) - log P_a(u)
+// per candidate, and on a cell f is far smoother than either mixture (a
+// difference of two log-densities, sampled at half-widths of ~0.06 of the
+// narrowest bandwidth): a cubic interpolant at four Chebyshev nodes of
+// [-1.05, 1.05] reproduces it to ~1e-7 on C3's histories.
+// k_table_score gives each cell 16 lanes: lanes 0-3 evaluate f at the
+// nodes, lanes 4-15 at 12 check points, from the cell's STORED coefficients
+// (what the two-polynomial scorer evaluates; fp32 Horner, the log of the
+// ratio as exponent + v_log_f32 of the mantissa, < 3e-7 in all); the nodes'
+// values are broadcast, every lane forms the same cubic (fp64 divided
+// differences), rounds it to fp32 and checks it at its point.  A cell whose
+// cubic misses f by more than kScoreTol (absolute, + 2^-22 relative), or
+// whose P is not positive, is flagged (NaN c0) and its candidates take the
+// two-polynomial cell.  16 B per cell, after the job's cells and m pairs in
+// its 128-B-per-cell region.
+// ---------------------------------------------------------------------------
+constexpr double kScoreTol = 1.0e-6;  // absolute fit error allowed (nats)
+constexpr int kScoreLanes = 16;       // lanes per cell: 4 nodes + 12 check points
+constexpr int kScoreChecks = kScoreLanes - 4;
+constexpr int kScoreCellsPerBlock = kBS / kScoreLanes;
+constexpr int kScoreBlocks = 256;     // per job (grid-stride over cells)
+
+__device__ __forceinline__ const float4* score_cells_of(const char* region, int64_t cap) {
+  return reinterpret_cast<const float4*>(region + ((cap * (int64_t)(kCellF * 4 + 8) + 15) & ~15ll));
+}
+
+__global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__ jobs,
+                                                     const tpe_table* __restrict__ tables,
+                                                     float* __restrict__ cells,
+                                                     unsigned long long* __restrict__ stats) {
+  const tpe_job J = jobs[blockIdx.y];
+  const int nb = tables[blockIdx.y].nb;
+  char* region = reinterpret_cast<char*>(cells) + J.tbl_off * kSlotB;
+  float4* outs = const_cast<float4*>(score_cells_of(region, J.tbl_cap));
+  const int sub = threadIdx.x / kScoreLanes, l = threadIdx.x % kScoreLanes;
+  const int gbase = lane_id() & ~(kScoreLanes - 1);  // first lane of this cell's group
+  constexpr double kU = (double)kULim;
+  const double nd0 = kU * 0.92387953251128674, nd1 = kU * 0.38268343236508978, nd2 = -nd1,
+               nd3 = -nd0;
+  const double u = l == 0 ? nd0 : l == 1 ? nd1 : l == 2 ? nd2 : l == 3 ? nd3
+                 : -kU + 2.0 * kU * (double)(l - 4) / (kScoreChecks - 1);
+  const float uf = (float)u;
+  // group-uniform trip count: every lane of a group runs the shuffles
+  for (int64_t c = (int64_t)blockIdx.x * kScoreCellsPerBlock + sub; c < nb;
+       c += (int64_t)gridDim.x * kScoreCellsPerBlock) {
+    const float* cell = reinterpret_cast<const float*>(region) + c * kCellF;
+    const double off = (double)cell[15];
+    const _Float16* tail = reinterpret_cast<const _Float16*>(cell + 2 * kP32);
+    float pb = 0.0f, pa = 0.0f;
+#pragma unroll
+    for (int n = kP - 1; n >= kP32; --n) {
+      pb = fmaf(pb, uf, (float)tail[2 * (n - kP32)]);
+      pa = fmaf(pa, uf, (float)tail[2 * (n - kP32) + 1]);
+    }
+#pragma unroll
+    for (int n = kP32 - 1; n >= 0; --n) {
+      pb = fmaf(pb, uf, cell[2 * n]);
+      pa = fmaf(pa, uf, cell[2 * n + 1]);
+    }
+    const bool ok_pt = (pb > 0.0f) && (pa > 0.0f) && isfinite(pb) && isfinite(pa);
+    // log(pb / pa) = ln2 * (e + log2(m)), m = the ratio's mantissa in [0.5, 1)
+    int e = 0;
+    const float m = ok_pt ? frexpf(pb / pa, &e) : 1.0f;
+    const double f = off + kLn2 * ((double)e + (double)__builtin_amdgcn_logf(m));
+    const double f0 = __shfl(f, gbase + 0, kWave), f1 = __shfl(f, gbase + 1, kWave),
+                 f2 = __shfl(f, gbase + 2, kWave), f3 = __shfl(f, gbase + 3, kWave);
+    // Newton divided differences -> monomial coefficients of the cubic
+    const double d01 = (f1 - f0) / (nd1 - nd0), d12 = (f2 - f1) / (nd2 - nd1),
+                 d23 = (f3 - f2) / (nd3 - nd2);
+    const double d012 = (d12 - d01) / (nd2 - nd0), d123 = (d23 - d12) / (nd3 - nd1);
+    const double d0123 = (d123 - d012) / (nd3 - nd0);
+    const double c3 = d0123;
+    const double c2 = d012 - d0123 * (nd0 + nd1 + nd2);
+    const double c1 = d01 - d012 * (nd0 + nd1) + d0123 * (nd0 * nd1 + nd0 * nd2 + nd1 * nd2);
+    const double c0 = f0 - d01 * nd0 + d012 * nd0 * nd1 - d0123 * nd0 * nd1 * nd2;
+    const float4 q = make_float4((float)c0, (float)c1, (float)c2, (float)c3);
+    const double p = (((double)q.w * u + (double)q.z) * u + (double)q.y) * u + (double)q.x;
+    bool fail = !ok_pt || (l >= 4 && !(fabs(p - f) <= kScoreTol + fabs(f) * 0x1.0p-22));
+    fail = fail || !(off == off) || !isfinite(q.x) || !isfinite(q.y) || !isfinite(q.z) ||
+           !isfinite(q.w);
+    const uint64_t mk = __ballot(fail) >> gbase;
+    if (l == 0) {
+      const bool bad = (mk & ((1ull << kScoreLanes) - 1)) != 0;
+      outs[c] = bad ? make_float4(__int_as_float(0x7FC00000), 0.0f, 0.0f, 0.0f) : q;
+      if (bad && stats) atomicAdd(stats + 2, 1ull);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBS) void k_table_build(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ sigma, const double* __restrict__ coef64,
@@ -615,7 +706,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
     const tpe_table* __restrict__ tables, const float* __restrict__ cells,
     const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
     double* __restrict__ out_x, tpe_best* __restrict__ partial,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, int n_tiles, int n_jobs) {
   __shared__ MixLds s_mix;
   // per wave: 4 DMA slabs of 64 x 16 B, the gather's LDS image; also the
   // sampler's staging buffer before scoring
@@ -623,15 +714,27 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   __shared__ BestT red[kBS / kWave];
   __shared__ int nred[kBS / kWave];
   static_assert(kTR * kWave * sizeof(float) <= kWave * kChunks * sizeof(float4), "staging alias");
-  const tpe_job J = jobs[blockIdx.y];
-  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-  const int64_t base0 = (int64_t)blockIdx.x * kTiles * kTile;
+  // XCD-aware work order: consecutive blocks land on consecutive XCDs (block
+  // b on XCD b % 8), so block b takes work item (b % 8) * per + b / 8 of the
+  // (job, tile) list -- each XCD sweeps one contiguous eighth of it and its
+  // L2 holds the cell tables of ~1/8 of the labels instead of all of them
+  int job, bx;
+  {
+    const int64_t W = (int64_t)n_tiles * n_jobs, per = (W + 7) / 8;
+    const int64_t w = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (w >= W) return;  // padding block (the grid is 8 * per)
+    job = (int)(w / n_tiles);
+    bx = (int)(w - (int64_t)job * n_tiles);
+  }
+  const tpe_job J = jobs[job];
+  tpe_best* P = partial + (int64_t)job * n_tiles + bx;
+  const int64_t base0 = (int64_t)bx * kTiles * kTile;
   if (base0 >= J.n_cand) {
     if (threadIdx.x == 0) *P = empty_best();
     return;
   }
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
-  const tpe_table Tb = tables[blockIdx.y];
+  const tpe_table Tb = tables[job];
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
   const bool log_in = INJ && lgmm, exp_out = !INJ && lgmm;
@@ -814,6 +917,135 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
 }
 
+// Fast path for sampled candidates (the suggest path: no per-candidate
+// log-densities asked for).  Same draws as k_score_table (draw32_pairs), same
+// cell index; the score comes from the cell's 16-B cubic (k_table_score):
+// one global_load_dwordx4 per candidate instead of a 64-B gather, and three
+// FMAs instead of two degree-8 polynomials and two logs.  Loads run four
+// candidates ahead.  Candidates on a flagged score cell (or off the grid)
+// take the two-polynomial cell, then the exact log-sum-exp, after the loop.
+// out_score / out_x (nullable, tests): per-candidate score and value.
+__global__ __launch_bounds__(kBS) void k_score_table_fast(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ wcdf, const float4* __restrict__ coef32,
+    const tpe_table* __restrict__ tables, const float* __restrict__ cells,
+    double* __restrict__ out_score, double* __restrict__ out_x, tpe_best* __restrict__ partial,
+    unsigned long long* __restrict__ stats, int n_tiles, int n_jobs) {
+  __shared__ MixLds s_mix;
+  __shared__ float s_stage[(kBS / kWave) * kTR * kWave];  // retry staging, then fallback stash
+  __shared__ BestT red[kBS / kWave];
+  __shared__ int nred[kBS / kWave];
+  int job, bx;
+  {  // XCD-aware work order (see k_score_table)
+    const int64_t W = (int64_t)n_tiles * n_jobs, per = (W + 7) / 8;
+    const int64_t w = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (w >= W) return;
+    job = (int)(w / n_tiles);
+    bx = (int)(w - (int64_t)job * n_tiles);
+  }
+  const tpe_job J = jobs[job];
+  tpe_best* P = partial + (int64_t)job * n_tiles + bx;
+  const int64_t base = (int64_t)bx * kTile;
+  if (base >= J.n_cand) {
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
+  }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const tpe_table Tb = tables[job];
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  const float g0 = (float)Tb.origin, inv_w = Tb.inv_w, inv_h = Tb.inv_h, h32 = (float)Tb.h;
+  const int nb = Tb.nb;
+  const char* region = reinterpret_cast<const char*>(cells) + J.tbl_off * kSlotB;
+  const float4* sc = score_cells_of(region, J.tbl_cap);
+  const int lane = lane_id();
+  float* stage = s_stage + (threadIdx.x / kWave) * (kTR * kWave);
+  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
+  const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
+  const int nvalid = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
+  float x[kTR];  // candidates in the scoring coordinate y (log x for LGMM1)
+  draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nvalid, lo_on, hi_on, (float)J.low,
+                    (float)J.high, false, stage, x);
+  auto cell_of = [&](float y) __attribute__((always_inline)) -> int {
+    const float t = (y - g0) * inv_w;
+    const int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
+    return min(c, nb - 1);
+  };
+  float bs = -INFINITY, by = 0.0f;
+  int br = -1;
+  uint32_t fb = 0;  // candidates the score cells do not cover
+  float4 q[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) q[r] = sc[cell_of(x[r])];
+#pragma unroll
+  for (int r = 0; r < kTR; ++r) {
+    const float y = x[r];
+    const int c = cell_of(y);
+    const float4 k = q[r & 3];
+    if (r + 4 < kTR) q[r & 3] = sc[cell_of(x[r + 4])];
+    const float u = (y - cell_centre(g0, h32, c)) * inv_h;
+    const float s = fmaf(fmaf(fmaf(k.w, u, k.z), u, k.y), u, k.x);
+    const bool ok = (s == s) && (fabsf(u) <= kULim);
+    const bool valid = r < nvalid;
+    fb |= (valid && !ok) ? (1u << r) : 0u;
+    if (valid && ok) {
+      // finite scores: strict > keeps the first of equal scores (np.argmax)
+      const bool take = s > bs;
+      bs = take ? s : bs;
+      by = take ? y : by;
+      br = take ? r : br;
+      if (out_score) out_score[J.out_off + t0 + r] = (double)s;
+    }
+    if (out_x && valid) out_x[J.out_off + t0 + r] = (double)(lgmm ? __expf(y) : y);
+  }
+  int n_fb = 0;
+  if (__any(fb != 0)) {
+    // fallback: the two-polynomial cell, else the exact fp32 log-sum-exp;
+    // the lane's candidates wait in its own column of the wave's stage
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < kTR; ++r)
+      if (fb & (1u << r)) stage[r * kWave + lane] = x[r];
+    __builtin_amdgcn_wave_barrier();
+    const f4* cell4 = reinterpret_cast<const f4*>(region);
+    while (fb) {
+      const int r = __builtin_ctz(fb);
+      fb &= fb - 1;
+      const float y = stage[r * kWave + lane];
+      const int c = cell_of(y);
+      const float u = (y - cell_centre(g0, h32, c)) * inv_h;
+      const f4 q0 = cell4[4 * c], q1 = cell4[4 * c + 1], q2 = cell4[4 * c + 2],
+               q3 = cell4[4 * c + 3];
+      float pb, pa, s;
+      horner9x2(q0, q1, q2, q3, u, pb, pa);
+      if ((q3.w == q3.w) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f)) {
+        s = q3.w + (__builtin_amdgcn_logf(pb) - __builtin_amdgcn_logf(pa)) * kLn2T;
+      } else {
+        s = lse_exact32(coef32 + SB.comp_off, SB, y) - lse_exact32(coef32 + SA.comp_off, SA, y);
+      }
+      if (out_score) out_score[J.out_off + t0 + r] = (double)s;
+      const bool na = s != s, nbn = bs != bs;
+      const bool take =
+          (br < 0) || (na ? (!nbn || r < br) : (!nbn && (s > bs || (s == bs && r < br))));
+      if (take) {
+        bs = s;
+        br = r;
+        by = y;
+      }
+      ++n_fb;
+    }
+  }
+  BestT run{0.0, -1, 0.0};
+  if (br >= 0) run = BestT{(double)bs, J.cand_base + t0 + br, (double)(lgmm ? __expf(by) : by)};
+  const BestT best = block_best<kBS>(run, red);
+  if (stats) {
+    const int ne = block_sum<kBS, int>(n_fb, nred);
+    if (threadIdx.x == 0 && ne) atomicAdd(stats, (unsigned long long)ne);
+  }
+  if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
+}
+
 __global__ __launch_bounds__(kBS) void k_reduce_t(const tpe_job* __restrict__ jobs,
                                                   const tpe_best* __restrict__ partial,
                                                   int64_t nper, tpe_best* __restrict__ best) {
@@ -890,6 +1122,12 @@ extern "C" int tpe_table_build(const tpe_job* jobs, const tpe_job* host_jobs, in
   hipLaunchKernelGGL(k_table_build, dim3(kBuildBlocks, n_jobs), dim3(kBS), 0, st, jobs, segs,
                      sigma, coef64, reach_hi, reach_lo, wide_idx, tables, cells,
                      (unsigned long long*)stats);
+  int64_t cap = 1;
+  for (int i = 0; i < n_jobs; ++i) cap = std::max(cap, host_jobs[i].tbl_cap);
+  const int64_t sblocks =
+      std::min<int64_t>(kScoreBlocks, (cap + kScoreCellsPerBlock - 1) / kScoreCellsPerBlock);
+  hipLaunchKernelGGL(k_table_score, dim3((unsigned)sblocks, n_jobs), dim3(kBS), 0, st, jobs, tables,
+                     cells, (unsigned long long*)stats);
   return check_launch("tpe_table_build");
 }
 
@@ -917,20 +1155,68 @@ extern "C" int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, in
     return TPE_E_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((unsigned)gx, (unsigned)n_jobs);
+  // one block per (job, tile) work item, padded to a multiple of the 8 XCDs
+  // (the kernel maps blocks to work items XCD by XCD)
+  const int64_t per = (gx * n_jobs + 7) / 8;
+  if (gx > INT32_MAX || 8 * per > INT32_MAX) {
+    set_error("tpe_score_table: %lld work items", (long long)(gx * n_jobs));
+    return TPE_E_UNSUPPORTED;
+  }
+  const dim3 grid((unsigned)(8 * per));
   const float4* c = reinterpret_cast<const float4*>(coef32);
   unsigned long long* s = (unsigned long long*)stats;
   if (inj)
     hipLaunchKernelGGL(k_score_table<true>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
-                       c, tables, cells, cand, out_bl, out_al, out_x, partial, s);
+                       c, tables, cells, cand, out_bl, out_al, out_x, partial, s, (int)gx,
+                       n_jobs);
   else
 #ifndef TPE_DIAG_EXTRA_LDS  // diagnostic builds: dynamic LDS padding to lower occupancy
 #define TPE_DIAG_EXTRA_LDS 0
 #endif
     hipLaunchKernelGGL(k_score_table<false>, grid, dim3(kBS), TPE_DIAG_EXTRA_LDS, st, jobs, segs, mu, sigma, wcdf,
-                       c, tables, cells, cand, out_bl, out_al, out_x, partial, s);
+                       c, tables, cells, cand, out_bl, out_al, out_x, partial, s, (int)gx,
+                       n_jobs);
   hipLaunchKernelGGL(k_reduce_t, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
   return check_launch("tpe_score_table");
+}
+
+extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                    const tpe_seg* segs, const double* mu, const double* sigma,
+                                    const double* wcdf, const float* coef32,
+                                    const tpe_table* tables, const float* cells,
+                                    double* out_score, double* out_x, tpe_best* partial,
+                                    int64_t n_partial, tpe_best* best, uint64_t* stats,
+                                    void* stream) {
+  bool inj = false;
+  if (!check_table_jobs("tpe_score_table_fast", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (inj) {
+    set_error("tpe_score_table_fast: sampled jobs only (injected candidates: tpe_score_table)");
+    return TPE_E_ARG;
+  }
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !coef32 || !tables || !cells || !partial ||
+      !best) {
+    set_error("tpe_score_table_fast: null pointer");
+    return TPE_E_ARG;
+  }
+  int64_t gx = 1;
+  for (int i = 0; i < n_jobs; ++i) gx = std::max(gx, (host_jobs[i].n_cand + kTile - 1) / kTile);
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_score_table_fast: partial workspace %lld < %lld", (long long)n_partial,
+              (long long)(gx * n_jobs));
+    return TPE_E_ARG;
+  }
+  const int64_t per = (gx * n_jobs + 7) / 8;
+  if (gx > INT32_MAX || 8 * per > INT32_MAX) {
+    set_error("tpe_score_table_fast: %lld work items", (long long)(gx * n_jobs));
+    return TPE_E_UNSUPPORTED;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_score_table_fast, dim3((unsigned)(8 * per)), dim3(kBS), 0, st, jobs, segs,
+                     mu, sigma, wcdf, reinterpret_cast<const float4*>(coef32), tables, cells,
+                     out_score, out_x, partial, (unsigned long long*)stats, (int)gx, n_jobs);
+  hipLaunchKernelGGL(k_reduce_t, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
+  return check_launch("tpe_score_table_fast");
 }
 
 extern "C" int64_t tpe_table_partials(const tpe_job* host_jobs, int n_jobs) {

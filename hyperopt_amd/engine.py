@@ -6,8 +6,11 @@ space (all labels, for a flat space) and runs, on the current torch stream:
 
     tpe_parzen_fit        adaptive_parzen_normal for every below/above set
     tpe_cat_posterior     randint / categorical pseudocount posteriors
-    tpe_table_build       fp32: per-cell Taylor expansions of both mixtures
-    tpe_score_table       fp32: sample + cell lookup + 2 polynomials + argmax
+    tpe_table_build       fp32: per-cell Taylor expansions of both mixtures and a
+                          cubic of the score per cell
+    tpe_score_table_fast  fp32: sample + score cubic lookup + argmax (suggest path)
+    tpe_score_table       fp32: sample/read + cell lookup + 2 polynomials + argmax
+                          (injected candidates, per-candidate log-densities)
     tpe_score_continuous  unquantized labels: sample + GMM1/LGMM1_lpdf + argmax
     tpe_lattice_*         quantized labels: sample -> distinct values -> score
     tpe_score_categorical categorical labels: sample + lookup + argmax
@@ -232,6 +235,10 @@ class Engine:
         # table build only); "1": join at the end of the level
         self.side_stream = os.environ.get("TPE_SIDE_STREAM", "0")
         self._side = None
+        # sampled table jobs without per-candidate outputs: "cubic" scores
+        # each candidate by its cell's score cubic (tpe_score_table_fast);
+        # "poly" evaluates both cell polynomials (tpe_score_table)
+        self.table_scorer = os.environ.get("TPE_TABLE_SCORER", "cubic")
 
     # -- memory --------------------------------------------------------------
     def _buf(self, name, nbytes):
@@ -352,7 +359,8 @@ class Engine:
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
             outputs=False, stream=None, timers=None, sample_only=False,
             pruned=True, scorer=None, posteriors=False, history=None, rows=None,
-            is_below=None, histories=None, timer_groups=None) -> List[LabelResult]:
+            is_below=None, histories=None, timer_groups=None,
+            table_scores=False) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``;
         ``timer_groups`` (optional set) limits them to those groups (each event
@@ -411,6 +419,8 @@ class Engine:
         if history is not None and histories is not None:
             raise ValueError("give either history or histories")
         hist_mode = history is not None or histories is not None
+        if table_scores:  # the fast table path's per-candidate scores (test hook)
+            outputs = False
         pkey = self._plan_key(works, prior_weight, lf, precision, scorer, outputs, sample_only,
                               hist_mode, histories is not None)
         cached = self._plans.get(pkey) if pkey is not None else None
@@ -664,7 +674,7 @@ class Engine:
         o_fb = pack.add(fb_jobs) if fb_jobs.size else None
         o_cand = pack.add(cand_pool)
         # one result block, zeroed by the upload and read back with one copy:
-        # [0,16) error bits, [16,32) table stats, [32,40) sorted-path pair
+        # [0,16) error bits, [16,40) table stats, [40,48) sorted-path pair
         # count, [64,...) tpe_best per job
         JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
         n_jobs = len(order)
@@ -673,7 +683,7 @@ class Engine:
         d_segs = base + o_segs if o_segs is not None else None
         d_csegs = base + o_csegs if o_csegs is not None else None
         d_res = base + o_res
-        d_err, d_stats, d_pairs, d_best = d_res, d_res + 16, d_res + 32, d_res + 64
+        d_err, d_stats, d_pairs, d_best = d_res, d_res + 16, d_res + 40, d_res + 64
         # every workspace pointer before the first launch: the launches then
         # follow each other without host work in between
         d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
@@ -741,9 +751,13 @@ class Engine:
         _hmark('jobs')
         d_cand = base + o_cand
         d_bl = d_al = d_x = None
+        d_sc = None
         if outputs:
             d_bl = self._buf("out_bl", 8 * max(out_off, 1))
             d_al = self._buf("out_al", 8 * max(out_off, 1))
+            d_x = self._buf("out_x", 8 * max(out_off, 1))
+        elif table_scores:
+            d_sc = self._buf("out_sc", 8 * max(out_off, 1))
             d_x = self._buf("out_x", 8 * max(out_off, 1))
 
         _hmark('fit')
@@ -830,9 +844,15 @@ class Engine:
                     stream.wait_event(ev)
                     joined = True
                 e0 = tick("table")
-                L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32, d_tab,
-                                            d_cells, d_cand, d_bl, d_al, d_x, d_part, npart, db,
-                                            d_stats, sp), "tpe_score_table")
+                if outputs or inj(ids[0]) or self.table_scorer == "poly":
+                    L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32,
+                                                d_tab, d_cells, d_cand, d_bl, d_al, d_x, d_part,
+                                                npart, db, d_stats, sp), "tpe_score_table")
+                else:  # the suggest path: one score cubic per candidate
+                    L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
+                                                     d_c32, d_tab, d_cells, d_sc, d_x, d_part,
+                                                     npart, db, d_stats, sp),
+                            "tpe_score_table_fast")
                 table_calls.append(nj)
             elif kind == "lat":
                 d_slot = self._buf("lat_slot", 8 * lat_off)
@@ -882,15 +902,19 @@ class Engine:
             err = int(res_h[:4].view(np.int32)[0])
             self.last_pairs = None
             if any(k == "sorted" and ids for k, ids in groups):
-                self.last_pairs = int(res_h[32:40].view(np.int64)[0])
+                self.last_pairs = int(res_h[40:48].view(np.int64)[0])
             self.last_table_stats = None
             if table_calls:
-                st = res_h[16:32].view(np.int64).tolist()
-                self.last_table_stats = {"exact_candidates": st[0], "failed_cells": st[1]}
+                st = res_h[16:40].view(np.int64).tolist()
+                self.last_table_stats = {"exact_candidates": st[0], "failed_cells": st[1],
+                                         "failed_score_cells": st[2]}
             outs = None
             if outputs:
                 outs = [self._bufs[k][:8 * max(out_off, 1)].to("cpu").numpy().view(np.float64)
                         for k in ("out_bl", "out_al", "out_x")]
+            elif table_scores:
+                outs = [self._bufs[k][:8 * max(out_off, 1)].to("cpu").numpy().view(np.float64)
+                        for k in ("out_sc", "out_x")]
         if err & 1:
             raise ValueError("negative arg to lognormal_cdf")  # tpe.py:196-197
         if err & 2:
@@ -910,6 +934,10 @@ class Engine:
                 r.below_llik = outs[0][o:o + n].copy()
                 r.above_llik = outs[1][o:o + n].copy()
                 r.cand = outs[2][o:o + n].copy()
+            elif table_scores and i in cont and modes[i] == "table":
+                o, n = int(jobs[pos]["out_off"]), int(jobs[pos]["n_cand"])
+                r.extra["score"] = outs[0][o:o + n].copy()
+                r.cand = outs[1][o:o + n].copy()
             results[i] = r
         _hmark("results")
         return results

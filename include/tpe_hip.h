@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 6
+#define TPE_ABI_VERSION 7
 
 enum {
   TPE_OK = 0,
@@ -248,21 +248,31 @@ int tpe_score_sorted(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
  * Same quantity as tpe_score_continuous(precision=32): per candidate the log
  * densities of both mixtures (GMM1_lpdf / LGMM1_lpdf, tpe.py:117-180,
  * 265-307) and the fused argmax (broadcast_best, tpe.py:649-658).  The
- * candidate coordinate range is cut into nb cells of half-width h; on every
- * cell each mixture sum_j exp(l_j(y)) is expanded around the cell centre
- * y0 as exp(m) * sum_{n<12} P_n u^n, u = (y - y0)/h, built in fp64 from
- * every component that can reach 2^-36 of the sum on that cell
- * (tpe_table_build).  Each component's factor exp(A u + B u^2) is expanded
- * only where 9|A| + 65|B| <= 5.8, which bounds the truncation error of the
- * degree-8 series by 1.0e-6 relative (Cauchy estimate).
+ * candidate coordinate range is cut into nb cells of half-width h.  On every
+ * cell each mixture sum_j exp(l_j(y)) is expanded around the cell centre y0
+ * as exp(m) * sum_{n<9} P_n u^n, u = (y - y0)/h: a degree-8 polynomial whose
+ * P_0..P_5 are stored in fp32 and P_6..P_8 in fp16 (tpe_table_build).  Each
+ * component's factor exp(A u + B u^2) is expanded only where 9|A| + 65|B| <=
+ * 5.8, which bounds the relative error of the stored, fp32-evaluated
+ * polynomial by 1.0e-6 (truncation 4.3e-7 + fp32/fp16 storage 1.4e-7 + fp16
+ * tail evaluation 4.4e-7; DESIGN.md section 3.1, tools/table_bounds.py);
+ * components whose largest term on the whole range is below e^-25 / M of the
+ * prior component's smallest term are left out (< 1.4e-11 of the sum).
+ * From those two polynomials the build also fits, per cell, a cubic of the
+ * score f(u) = (m_b - m_a) + log P_b(u) - log P_a(u) at four Chebyshev nodes
+ * of [-1.05, 1.05], rounds it to fp32 and checks it against f at 12 more
+ * points: a cell whose error exceeds 1e-6 + 2^-22 |f| is flagged.
  * A candidate whose cell fails the bound, or that lies outside the grid, is
  * scored by the exact fp32 log-sum-exp over all components instead.
  * tables: one tpe_table per job (device); cells: byte pool, 128 B per cell
  * slot: job j's region starts at 128 * job.tbl_off and holds tbl_cap 64-B
- * cells, then tbl_cap (m_below, m_above) fp32 pairs; reach_hi / reach_lo: fp64 per-component
- * workspace (size of the mixture pool); wide_idx: int32, same size.
- * stats (nullable, 2 x u64): [0] candidates scored by the exact fallback,
- * [1] cells that failed the bound. */
+ * cells, then tbl_cap (m_below, m_above) fp32 pairs, then (at the next 16-B
+ * boundary) tbl_cap 16-B score cubics {c0, c1, c2, c3} (c0 NaN: flagged);
+ * reach_hi / reach_lo: fp64 per-component workspace (size of the mixture
+ * pool); wide_idx: int32, same size.
+ * stats (nullable, 3 x u64): [0] candidates scored by a fallback (exact
+ * log-sum-exp; for tpe_score_table_fast also the two-polynomial cell),
+ * [1] cells that failed the bound, [2] score cubics that failed their check. */
 typedef struct tpe_table {
   double lo, hi;        /* candidate coordinate range (x, or log x for LGMM1) */
   double h_below, h_above; /* largest admissible half-width per mixture       */
@@ -293,6 +303,18 @@ int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                     const float* cells, const double* cand, double* out_bl, double* out_al,
                     double* out_x, tpe_best* partial, int64_t n_partial, tpe_best* best,
                     uint64_t* stats, void* stream);
+/* The suggest path (sampled jobs only): the same draws and argmax as
+ * tpe_score_table, each candidate scored by its cell's score cubic -- one
+ * 16-B load and three FMAs -- or, on a flagged cubic, by the two-polynomial
+ * cell, then the exact log-sum-exp.  out_score / out_x (nullable): the
+ * per-candidate score (below - above log-density) and value at job.out_off.
+ * Partial workspace: tpe_table_partials(). */
+int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                         const tpe_seg* segs, const double* mu, const double* sigma,
+                         const double* wcdf, const float* coef32, const tpe_table* tables,
+                         const float* cells, double* out_score, double* out_x,
+                         tpe_best* partial, int64_t n_partial, tpe_best* best, uint64_t* stats,
+                         void* stream);
 
 /* ---- quantized labels: lattice path ---------------------------------------
  * Candidates of a quantized label take values k*q (np.round(x/q)*q,

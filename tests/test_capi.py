@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 6
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 7
     sizes = (ctypes.c_int32 * 7)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 7) == 7
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -68,6 +68,12 @@ def test_argument_errors_are_reported():
     rc = lib.tpe_score_table(None, hp_, 1, *([None] * 12), 0, None, None, None)
     assert rc == -1 and b"no cell table" in lib.tpe_last_error()
     jobs["tbl_cap"] = 64
+    jobs["flags"] = L.F_INJECTED
+    rc = lib.tpe_score_table_fast(None, hp_, 1, *([None] * 10), 0, None, None, None)
+    assert rc == -1 and b"sampled jobs only" in lib.tpe_last_error()
+    jobs["flags"] = 0
+    rc = lib.tpe_score_table_fast(None, hp_, 1, *([None] * 10), 0, None, None, None)
+    assert rc == -1 and b"null pointer" in lib.tpe_last_error()
     rc = lib.tpe_table_build(None, hp_, 1, None, None, None, None, 8, *([None] * 8))
     assert rc == -1 and b"null pointer" in lib.tpe_last_error()
     assert lib.tpe_table_scratch_bytes(3, 1000) > 0 and lib.tpe_table_scratch_bytes(-1, 5) == -1

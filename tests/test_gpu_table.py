@@ -181,3 +181,42 @@ def test_table_winner_at_c3_size_vs_fp64_exact(engine, kind, args, gen, seed):
     ref = _oracle(w, cand=cand[pick])
     np.testing.assert_allclose(ref["below_llik"] - ref["above_llik"], s64[pick], rtol=1e-6,
                                atol=1e-9)
+
+
+@pytest.mark.parametrize("kind,args", CONT)
+@pytest.mark.parametrize("n_hist", [3, 40, 2000, 10000])
+def test_fast_table_scores_vs_oracle(engine, kind, args, n_hist):
+    """The suggest path (tpe_score_table_fast: one score cubic per cell):
+    per-candidate scores of its own Philox candidates vs the oracle's
+    below - above log-density at the same values (fp32 bound of north_star,
+    rtol/atol 1e-4), the same candidates as the two-polynomial kernel, and a
+    winner whose exact score is the two-polynomial winner's within fp32."""
+    from hyperopt_amd.engine import LabelWork
+    rng = np.random.RandomState(n_hist + 71)
+    gen = _mixture_case(rng, kind, args, 1, n_hist, 1)
+    obs = gen.obs_above
+    losses = rng.normal(size=n_hist)
+    below, above = O.ap_split_trials(np.arange(n_hist), obs, np.arange(n_hist), losses, 0.25)
+    n = 1 << 16
+    w = LabelWork(kind, kind, args, below, above, n_cand=n, key=515151 + n_hist)
+    fast, = engine.run([w], precision=32, table_scores=True)
+    st = engine.last_table_stats
+    assert st["exact_candidates"] <= n // 1000, st
+    score = fast.extra["score"]
+    poly, = engine.run([w], precision=32, outputs=True, scorer="table")
+    np.testing.assert_array_equal(fast.cand, poly.cand)  # same Philox draws
+    pick = np.random.RandomState(1).choice(n, 3000, replace=False)
+    ref = _oracle(w, cand=fast.cand[pick])
+    s_ref = ref["below_llik"] - ref["above_llik"]
+    np.testing.assert_allclose(score[pick], s_ref, rtol=RTOL, atol=ATOL)
+    # against the two-polynomial scores: the cubic adds ~1e-6 at most
+    s_poly = poly.below_llik - poly.above_llik
+    np.testing.assert_allclose(score, s_poly, rtol=2e-5, atol=2e-5)
+    assert fast.index == int(np.argmax(score))
+    assert fast.value == fast.cand[fast.index] and fast.n_scored == n
+    if fast.index != poly.index:
+        w2 = LabelWork(kind, kind, args, below, above,
+                       cand=np.array([fast.cand[fast.index], poly.cand[poly.index]]))
+        r, = engine.run([w2], precision=64, outputs=True)
+        s = r.below_llik - r.above_llik
+        assert abs(s[0] - s[1]) <= 1e-4 * max(1.0, abs(s[1])), (s, fast, poly)
