@@ -4,15 +4,19 @@
 Workload (BASELINE.json configs[2]): a 50-dim mixed space
 (10 x uniform(-5,5), 10 x loguniform(-5,0), 10 x quniform(0,100,1),
 10 x normal(0,2), 10 x choice(8)), a 10k-trial history drawn from the prior
-(seed 0) with N(0,1) losses (seed 1), and 2^22 EI candidates per label per
-GPU.  One step = one full suggest level on the device path: the below/above
-split of the resident columnar history, the Parzen fit of all 100 mixtures,
-sampling 50 x 2^22 candidates from the below posteriors, scoring each under
-both posteriors, and the per-label argmax (plus the cross-GPU max-loc combine
-when N > 1).  Scaling is weak: every rank scores 2^22 candidates per label
-(its own global index range), the job total grows with N.
+(seed 0) with N(0,1) losses (seed 1), and 2^22 EI candidates per label.  One
+step = one full suggest level on the device path: the below/above split of the
+resident columnar history, the Parzen fit of all mixtures, sampling 50 x 2^22
+candidates from the below posteriors, scoring each under both posteriors, and
+the per-label argmax (plus the cross-GPU max-loc combine when N > 1).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Scaling (``--scaling``): "strong" (default) keeps the job at 2^22 candidates
+per label and splits it over the N ranks with hyperopt_amd.dist.plan_units
+(whole labels per rank when labels >= ranks, the reference's label
+independence, tpe.py:697-746); "weak" gives every rank 2^22 candidates per
+label of its own global index range.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
 
 Prints ONE JSON line on rank 0.
 """
@@ -35,7 +39,7 @@ T_HIST = 10_000
 N_CAND = 1 << 22
 FP32_PEAK_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 FLOPS_PER_PAIR = 9  # unquantized GMM1/LGMM1 pair
-OPS_PER_TABLE_CAND = 97  # cell-table scorer (degree-8 cells), per candidate
+OPS_PER_TABLE_CAND = 56  # fast table scorer (score cubic per cell), per candidate
 DIRECT_PAIR_CEILING = 9.81e12  # pairs/s of the exp-bound direct loop (profiles/r01_valu_microbench.txt)
 
 
@@ -91,17 +95,23 @@ def below_rows(losses, gamma=0.25):
     return np.sort(_smallest_rows(losses, n_below))
 
 
-def history_works(space, mat, hist, rows_b, step, n_cand, cand_base):
+def history_works(space, mat, hist, rows_b, step, n_cand, cand_base, units=None, n_total=0):
     """LabelWork list for the device-resident history: only the (small) below
-    sets are read on the host; the above sets are gathered on the GPU."""
+    sets are read on the host; the above sets are gathered on the GPU.
+    ``units`` (label position, start, count): this rank's share of the level
+    (hyperopt_amd.dist.plan_units); default every label, n_cand candidates
+    from cand_base."""
     from hyperopt_amd.engine import LabelWork
     below = mat[rows_b]
     n_above = (hist.n_active - hist.active_host[rows_b].sum(0)).tolist()
     keys = label_keys(0, step, [lab for lab, _, _ in space])
-    return [LabelWork(label=lab, kind=kind, args=a, obs_below=below[:, j], obs_above=None,
-                      n_cand=n_cand, key=keys[j], cand_base=cand_base, col=j,
-                      n_above=n_above[j])
-            for j, (lab, kind, a) in enumerate(space)]
+    if units is None:
+        units = [(j, 0, n_cand) for j in range(len(space))]
+    return [LabelWork(label=space[j][0], kind=space[j][1], args=space[j][2],
+                      obs_below=below[:, j], obs_above=None, n_cand=count, key=keys[j],
+                      cand_base=cand_base + start, col=j, n_above=n_above[j],
+                      n_total=n_total or n_cand)
+            for j, start, count in units]
 
 
 def label_key(seed, step, lab):
@@ -124,34 +134,76 @@ def make_works(space, splits, step, n_cand, cand_base):
                       cand_base=cand_base) for lab, kind, a in space]
 
 
-def cpu_baseline(space, vals, losses, seconds_hint=True):
-    """The oracle (numpy restatement of tpe.suggest's per-label pipeline) on a
-    bounded sample (~10 s): one label of each kind, 20480 candidates each, same 10k
-    history.  Test infrastructure only -- never on the product path."""
+def _cpu_label(task):
+    """One label of the oracle pipeline (fit + sample + score + argmax);
+    returns the candidates it scored.  Module-level so that spawned
+    multiprocessing workers can import it."""
     from oracle import tpe_oracle as O
+    kind, a, below, above, n, seed = task
+    rng = np.random.RandomState(seed)
+    if kind == "randint":
+        pb = O.randint_posterior(below, 1.0, a[0])
+        cand = rng.choice(a[0], size=n, p=pb)
+        O.categorical_label_scores(kind, a, below, above, cand)
+        return n
+    fam, pmu, psig, tf, low, high, q = O.posterior_spec(kind, a)
+    post_b = O.adaptive_parzen_normal(tf(below), 1.0, pmu, psig)
+    samp = O.gmm1_sample if fam == "GMM1" else O.lgmm1_sample
+    cand = samp(*post_b, low=low, high=high, q=q, rng=rng, size=n)
+    with np.errstate(all="ignore"):
+        O.continuous_label_scores(kind, a, below, above, cand)
+    return n
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(space, vals, losses, n=20480, workers=16):
+    """The oracle (numpy restatement of tpe.suggest's per-label pipeline,
+    /root/reference/hyperopt/tpe.py:837-964) on a bounded sample of C3 --
+    test infrastructure only, never on the product path.  Two variants
+    (BASELINE.md "CPU-baseline plan"): one process over one label of each kind
+    (numpy elementwise code is single-threaded), and label-parallel
+    multiprocessing, one label per worker over min(16, cpu_count) spawned
+    workers (the box's CPU share), timed after the workers have started."""
+    import multiprocessing as mp
     sp = split(vals, losses)
-    picks = [s for s in space if s[0] in ("u0", "lu0", "qu0", "n0", "c0")]
-    n = 20480
-    rng = np.random.RandomState(5)
+    by_kind = {}
+    for lab, kind, a in space:
+        by_kind.setdefault(kind, []).append((lab, kind, a))
+    picks = [v[0] for v in by_kind.values()]
     t0 = time.perf_counter()
-    for lab, kind, a in picks:
-        below, above = sp[lab]
-        if kind == "randint":
-            pb = O.randint_posterior(below, 1.0, a[0])
-            cand = rng.choice(a[0], size=n, p=pb)
-            O.categorical_label_scores(kind, a, below, above, cand)
-            continue
-        fam, pmu, psig, tf, low, high, q = O.posterior_spec(kind, a)
-        post_b = O.adaptive_parzen_normal(tf(below), 1.0, pmu, psig)
-        samp = O.gmm1_sample if fam == "GMM1" else O.lgmm1_sample
-        cand = samp(*post_b, low=low, high=high, q=q, rng=rng, size=n)
-        with np.errstate(all="ignore"):
-            O.continuous_label_scores(kind, a, below, above, cand)
-    dt = time.perf_counter() - t0
-    return {"value": len(picks) * n / dt, "unit": "EI candidates/s", "cores": 1, "kind": "port",
+    done = sum(_cpu_label((kind, a, sp[lab][0], sp[lab][1], n, 5)) for lab, kind, a in picks)
+    dt1 = time.perf_counter() - t0
+    ncpu = os.cpu_count() or 1
+    nw = max(1, min(workers, ncpu))
+    order = [s for group in zip(*by_kind.values()) for s in group][:nw]  # kinds interleaved
+    tasks = [(kind, a, sp[lab][0], sp[lab][1], n, 5 + i) for i, (lab, kind, a) in enumerate(order)]
+    multi = None
+    try:
+        with mp.get_context("spawn").Pool(nw) as pool:
+            pool.map(_cpu_label, [(t[0], t[1], t[2], t[3], 64, 0) for t in tasks])  # warm-up
+            t0 = time.perf_counter()
+            done_m = sum(pool.map(_cpu_label, tasks, chunksize=1))
+            dtm = time.perf_counter() - t0
+        multi = {"value": done_m / dtm, "cores": nw, "seconds": dtm,
+                 "sample": "%d labels (kinds interleaved), one per worker, %d candidates each"
+                           % (len(tasks), n)}
+    except Exception as e:  # report, do not fail the bench line
+        multi = {"error": repr(e)}
+    return {"value": done / dt1, "unit": "EI candidates/s", "cores": 1, "kind": "port",
             "sample": "oracle/tpe_oracle.py numpy pipeline (fit+sample+score+argmax), 5 labels "
                       "(uniform, loguniform, quniform, normal, choice8) x %d candidates, 10k-trial "
-                      "history, %.2f s on %s" % (n, dt, platform.processor() or platform.machine())}
+                      "history, %.2f s" % (n, dt1),
+            "cpu_model": _cpu_model(), "os_cpu_count": ncpu,
+            "label_parallel": multi}
 
 
 def readme_suggest_p50():
@@ -234,6 +286,27 @@ def dropin_suggest_p50(space, vals, losses, n_cand, calls=20, warmup=3):
                       % (losses.size, int(round(math.log2(n_cand))))}
 
 
+def valu_issue(prof, n_launch_cand):
+    """VALU-issue roofline of the dominant kernel from its PMC pass
+    (profiles/traffic.json, tools/make_traffic.py): wave-level VALU
+    instructions per candidate (one lane's worth), measured cycles per VALU
+    instruction (SQ_ACTIVE_INST_VALU x 4 / SQ_INSTS_VALU), and the fraction of
+    the plain-VALU issue rate the kernel reaches: the time its instructions
+    would take at 2 cycles each (v_fma_f32 wave64 on a SIMD-32,
+    MI355X_MICROARCH.md) on all 1024 SIMDs, over its measured duration."""
+    insts = prof.get("valu_insts_per_launch")
+    cand = prof.get("candidates_per_launch") or n_launch_cand
+    if not insts or not cand:
+        return None
+    out = {"insts_per_candidate": insts * 64.0 / cand}
+    if prof.get("active_inst_valu"):
+        out["cycles_per_inst"] = prof["active_inst_valu"] * 4.0 / insts
+    if prof.get("grbm_gui_active"):
+        out["issue_frac"] = 2.0 * insts / 1024.0 / (prof["grbm_gui_active"] / 8.0)
+    out["source"] = prof.get("source")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,7 +314,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", type=int, default=32)
     ap.add_argument("--n-cand", type=int, default=N_CAND)
+    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
+                    help="strong: 2^22 candidates per label in total, split over the ranks by "
+                         "dist.plan_units; weak: 2^22 per label per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the fp64 line and the drop-in / README suggest timings")
     ap.add_argument("--upload-history", action="store_true",
                     help="pack and upload the observation lists every step instead of gathering "
                          "them from the HBM-resident history")
@@ -256,9 +334,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU (ranks
+    # share cuda:0; the winners are combined on the host) -- never for numbers
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from hyperopt_amd.engine import DeviceHistory, Engine
     from hyperopt_amd import dist as hdist
 
@@ -267,27 +353,40 @@ def main():
     vals, losses = c3_history(space)
     eng = Engine()
     n_cand = args.n_cand
-    cand_base = rank * n_cand
+    strong = args.scaling == "strong"
+    if strong:  # this rank's units of the level (whole labels at 50 labels >= ranks)
+        units = hdist.plan_units([k for _, k, _ in space], n_cand, world)[rank]
+        cand_base = 0
+    else:  # every label, 2^22 candidates of this rank's own global range
+        units = [(j, 0, n_cand) for j in range(len(space))]
+        cand_base = rank * n_cand
     # the history is resident in HBM before timing starts (appended once, as
     # trials would be); each step uploads only the below-row flags
     mat = c3_matrix(space, vals)
     hist = DeviceHistory(eng, len(space), cap=T_HIST)
     hist.append(mat)
 
-    def step(k, timers=None, timer_groups=None):
+    def step(k, timers=None, timer_groups=None, precision=None):
+        prec = precision or args.precision
         if args.upload_history:
             works = make_works(space, split(vals, losses), k, n_cand, cand_base)
-            res = eng.run(works, precision=args.precision, timers=timers, scorer=scorer,
+            works = [works[j] for j, _, _ in units]
+            for w, (_, start, count) in zip(works, units):
+                w.n_cand, w.cand_base, w.n_total = count, cand_base + start, n_cand
+            res = eng.run(works, precision=prec, timers=timers, scorer=scorer,
                           timer_groups=timer_groups)
         else:
             rb = below_rows(losses)
             isb = np.zeros(T_HIST, np.uint8)
             isb[rb] = 1
-            works = history_works(space, mat, hist, rb, k, n_cand, cand_base)
-            res = eng.run(works, precision=args.precision, timers=timers, scorer=scorer,
+            works = history_works(space, mat, hist, rb, k, n_cand, cand_base, units, n_cand)
+            res = eng.run(works, precision=prec, timers=timers, scorer=scorer,
                           history=hist, is_below=isb, timer_groups=timer_groups)
         if world > 1:
-            hdist.allreduce_best(res)
+            if strong:  # label-sharded level: every rank learns every label's winner
+                hdist.gather_best(len(space), [(u[0], r) for u, r in zip(units, res)])
+            else:
+                hdist.allreduce_best(res)
         return works, res
 
     for k in range(args.warmup):
@@ -317,28 +416,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel: unquantized continuous scoring of the 30 continuous labels
+    # dominant kernel: unquantized continuous scoring of this rank's continuous labels
     cont = [w for w in works if w.kind in ("uniform", "loguniform", "normal", "lognormal")]
-    dense_pairs = sum(n_cand * (w.obs_below.size + 1 + (w.n_above if w.obs_above is None
-                                                        else w.obs_above.size) + 1)
+    dense_pairs = sum(w.n_cand * (w.obs_below.size + 1 + (w.n_above if w.obs_above is None
+                                                          else w.obs_above.size) + 1)
                       for w in cont)
-    n_cont = n_cand * len(cont)
+    n_cont = sum(w.n_cand for w in cont)
     kname = {"cont": "k_score32 (tpe_score_continuous)",
              "sorted": "k_score_sorted (tpe_score_sorted)",
-             "table": "k_score_table (tpe_score_table)"}[group]
+             "table": "k_score_table_fast (tpe_score_table_fast)"}[group]
     kms = [e0.elapsed_time(e1) for e0, e1 in timers.get(group, [])]
     avg_ms = float(np.mean(kms)) if kms else float("nan")
     sec = avg_ms * 1e-3
     if group == "table":
-        # algorithmic operations per candidate of the
-        # cell-table scorer (sample + cell lookup + two degree-8 polynomials)
+        # builder-defined operations per candidate of the
+        # fast table scorer (sample + cell lookup + score cubic + argmax)
         ops = OPS_PER_TABLE_CAND * n_cont
         work = {"ops_per_candidate": OPS_PER_TABLE_CAND, "candidates_per_launch": n_cont}
     else:
         exec_pairs = dense_pairs if group == "cont" else (eng.last_pairs or dense_pairs)
         ops = exec_pairs * FLOPS_PER_PAIR
         work = {"flops_per_pair": FLOPS_PER_PAIR, "evaluated_pairs_per_launch": exec_pairs}
-    achieved = ops / sec / 1e12
+    achieved = ops / sec / 1e12 if sec > 0 else float("nan")
     all_timers = {}
     for k in range(3):
         step(args.warmup + args.steps + k, all_timers)
@@ -346,9 +445,10 @@ def main():
     group_ms = {k: round(float(np.mean([a.elapsed_time(b) for a, b in v])), 4)
                 for k, v in all_timers.items()}
 
-    total_cand = len(space) * n_cand * world * args.steps
+    per_rank = sum(c for _, _, c in units)
+    total_cand = (len(space) * n_cand if strong else per_rank * world) * args.steps
     value = total_cand / elapsed
-    # per-launch HBM bytes / VALU busy of the dominant kernel, from the PMC
+    # per-launch HBM bytes / VALU figures of the dominant kernel, from the PMC
     # passes of tools/profile_round.sh (tools/make_traffic.py)
     traffic, prof = None, {}
     tfile = os.path.join(HERE, "profiles", "traffic.json")
@@ -359,16 +459,18 @@ def main():
         else:
             prof = {}
     roofline = {"bound": "valu", "kernel": kname, "achieved": achieved,
-                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s (builder-defined ops per candidate, DESIGN.md 3.1)",
                 "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
                 "algorithmic_ops_per_launch": ops, "avg_launch_ms": avg_ms,
                 "dense_pairs_per_launch": dense_pairs,
-                "dense_equivalent_pairs_per_s": dense_pairs / sec,
+                "dense_equivalent_pairs_per_s": dense_pairs / sec if sec > 0 else None,
                 "direct_pair_ceiling_per_s": DIRECT_PAIR_CEILING,
-                "valu_busy": prof.get("valu_busy"), "traffic_source": prof.get("source")}
+                "valu_busy": prof.get("valu_busy"), "traffic_source": prof.get("source"),
+                "valu_issue": valu_issue(prof, n_cont) if prof else None}
     roofline.update(work)
     if group == "table":
-        roofline["l2_gather_bytes_per_launch"] = 64 * n_cont  # one 64-B cell per candidate
+        roofline["l2_gather_bytes_per_launch"] = 16 * n_cont  # one 16-B score cubic per candidate
         roofline["build_ms"] = group_ms.get("table_build")
     line = {
         "metric": "EI candidates scored/sec (50-dim, 10k trials)",
@@ -380,19 +482,34 @@ def main():
         "ms_per_step": elapsed / args.steps * 1e3,
         "suggest_p50_ms": float(np.median(step_times)) * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32" if args.precision == 32 else "f64",
         "data": "synthetic: prior draws (seed 0), N(0,1) losses (seed 1), Philox candidates",
         "config": {"workload": "C3: 50-dim mixed (10x uniform/loguniform/quniform/normal/"
-                               "choice8), 10k-trial history, 2^%d EI candidates per label per GPU"
-                               % int(round(math.log2(n_cand))),
+                               "choice8), 10k-trial history, 2^%d EI candidates per label%s"
+                               % (int(round(math.log2(n_cand))),
+                                  "" if strong else " per GPU"),
                    "labels": len(space), "history": T_HIST, "candidates_per_label": n_cand,
-                   "parallelism": "candidate-sharded x%d, RCCL max-loc combine" % world},
+                   "parallelism": ("label-sharded x%d (dist.plan_units), RCCL all-gather + "
+                                   "device max-loc" % world) if strong else
+                                  ("candidate-sharded x%d, RCCL max-loc combine" % world),
+                   "rank0_units": len(units)},
         "roofline": roofline,
         "group_ms": group_ms,
     }
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_extras:
+        if args.precision == 32:  # the fp64 parity mode's throughput on the same workload
+            step(0, precision=64)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(2):
+                step(1000 + k, precision=64)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 2
+            line["fp64"] = {"value": len(space) * n_cand / dt, "ms_per_step": dt * 1e3,
+                            "steps": 2, "dtype": "f64",
+                            "note": "exact dense fp64 scoring (k_score64) of every label"}
         line["dropin_suggest"] = dropin_suggest_p50(space, vals, losses, n_cand)
         line["readme_suggest"] = readme_suggest_p50()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -841,7 +841,11 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
           continue;
         }
         const uint32_t rel = (uint32_t)(t0 + r - base);
+#ifdef TPE_DIAG_NO_MARK  // diagnostic builds only: slots computed, not marked
+        if (rel == 0xFFFFFFFFu) lfirst[slot] = rel;
+#else
         if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
+#endif
       }
     } else {
 #pragma unroll
