@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kBS) void k_score32(
       x[r] = li < J.n_cand ? (float)cand[J.cand_off + li] : 1.0f;
     }
   } else {
-    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
+    const Mix M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);
 #pragma unroll
     for (int r = 0; r < kR32; ++r) {
       const int64_t li = base + r * kBS + threadIdx.x;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kBS) void k_score64(
       x[r] = li < J.n_cand ? cand[J.cand_off + li] : 1.0;
     }
   } else {
-    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
+    const Mix M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);
 #pragma unroll
     for (int r = 0; r < kR64; ++r) {
       const int64_t li = base + r * kBS + threadIdx.x;
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(kBS) void k_sort_count(
   const int64_t base = (int64_t)blockIdx.x * kSortPer;
   if (base >= J.n_cand) return;
   for (int i = threadIdx.x; i < kNB; i += kBS) h[i] = 0u;
-  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_mix);
+  const Mix M = stage_mix(J, segs[J.below], wcdf, mu, sigma, s_mix);
   __syncthreads();
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
@@ -766,12 +766,24 @@ __global__ __launch_bounds__(kBS) void k_score_sorted(
 // ---------------------------------------------------------------------------
 // quantized labels
 // ---------------------------------------------------------------------------
+// POW2: every job draws in fp32 (TPE_F_DRAW32) with q a power of two and at
+// most kLatLds lattice slots (C3's quniform labels) -- slots come from rintf
+// in fp32 and the kernel carries no fp64 slot code (fewer registers); the
+// general instantiation handles the rest.  lfirst is dynamic LDS sized by the
+// host to the largest lattice of the launch (up to kLatLds slots).
+__host__ __device__ __forceinline__ bool lattice_pow2(const tpe_job& j) {
+  int qe;
+  return (j.flags & TPE_F_DRAW32) && frexp(j.q, &qe) == 0.5 && qe > -100 && qe < 100 &&
+         j.lat_n <= kLatLds;
+}
+
+template <bool POW2>
 __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
     int32_t* __restrict__ err, int n_tiles, int n_jobs) {
-  __shared__ uint32_t lfirst[kLatLds];
+  extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
   __shared__ float s_stage[kLatR * kBS];
   // XCD-aware work order (as k_score_table): each XCD sweeps a contiguous
@@ -792,87 +804,91 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   // beyond go to the global marks directly, each read before its atomic
   const int n_loc = (int)min((int64_t)kLatLds, J.lat_n);
   for (int s = threadIdx.x; s < n_loc; s += kBS) lfirst[s] = 0xFFFFFFFFu;
-  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
+  const Mix M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);
   __syncthreads();
-  // np.round(x / q) (tpe.py:106) without a division per draw: t = x * (1/q) is
-  // within 3.4e-16 |t| of fl(x / q), so rint(t) == rint(fl(x / q)) unless
-  // fl(x / q) sits that close to a half-integer -- those few redo the division
-  const double inv_q = 1.0 / J.q;
-  auto mark = [&](double v, int64_t li) {
-    const double t = v * inv_q;
-    double k = rint(t);
-    if (fabs(fabs(t - k) - 0.5) <= 8e-16 * fabs(t)) k = rint(v / J.q);
-    const int64_t slot = (int64_t)k - J.lat_kmin;
-    if (slot < 0 || slot >= J.lat_n) {
-      atomicOr(err, 2);
-      return;
-    }
-    if (slot < n_loc) {
-      // most draws land on slots already holding a smaller index: a plain
-      // read first keeps the atomics (and their same-address serialisation) rare
-      const uint32_t rel = (uint32_t)(li - base);
-      if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
-    } else {
-      unsigned long long* dst = &slot_first[J.lat_off + slot];
-      const unsigned long long g = (unsigned long long)(J.cand_base + li);
-      if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
-    }
-  };
-  if (J.flags & TPE_F_DRAW32) {
-    // kLatR consecutive candidates per thread, pair-shared Philox draws
+  if constexpr (POW2) {
+    // kLatR consecutive candidates per thread (draw32_pairs); q a power of two:
+    // x * (1/q) is exact in fp32, so rintf gives np.round(x / q) (tpe.py:106)
+    // exactly and the slot needs no fp64 work
     const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
     const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
     float x[kLatR];
     draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
                         (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
                         x);
-    int qe;
-    if (frexp(J.q, &qe) == 0.5 && qe > -100 && qe < 100 && J.lat_n <= kLatLds) {
-      // q a power of two: x * (1/q) is exact in fp32, so rintf gives np.round(x / q)
-      // exactly and the slot needs no fp64 work
-      const float inv_q32 = (float)inv_q;
+    const float inv_q32 = (float)(1.0 / J.q);
+    const int kmin = (int)J.lat_kmin, nl = (int)J.lat_n;
 #pragma unroll
-      for (int r = 0; r < kLatR; ++r) {
-        if (r >= nv) continue;
-        const float t = rintf(x[r] * inv_q32);
-        const int64_t slot = (fabsf(t) < 2147483648.0f) ? (int64_t)t - J.lat_kmin : -1;
-        if (slot < 0 || slot >= J.lat_n) {
-          atomicOr(err, 2);
-          continue;
-        }
-        const uint32_t rel = (uint32_t)(t0 + r - base);
-#ifdef TPE_DIAG_NO_MARK  // diagnostic builds only: slots computed, not marked
-        if (rel == 0xFFFFFFFFu) lfirst[slot] = rel;
-#else
-        if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
-#endif
+    for (int r = 0; r < kLatR; ++r) {
+      if (r >= nv) continue;
+      const float t = rintf(x[r] * inv_q32);
+      const int slot = (fabsf(t) < 2147483648.0f) ? (int)t - kmin : -1;
+      if (slot < 0 || slot >= nl) {
+        atomicOr(err, 2);
+        continue;
       }
-    } else {
+      // most draws land on slots already holding a smaller index: a plain read
+      // first keeps the atomics (and their same-address serialisation) rare
+      const uint32_t rel = (uint32_t)(t0 + r - base);
+#ifdef TPE_DIAG_NO_MARK  // diagnostic builds only: slots computed, not marked
+      if (rel == 0xFFFFFFFFu) lfirst[slot] = rel;
+#else
+      if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
+#endif
+    }
+  } else {
+    // np.round(x / q) (tpe.py:106) without a division per draw: t = x * (1/q) is
+    // within 3.4e-16 |t| of fl(x / q), so rint(t) == rint(fl(x / q)) unless
+    // fl(x / q) sits that close to a half-integer -- those few redo the division
+    const double inv_q = 1.0 / J.q;
+    auto mark = [&](double v, int64_t li) {
+      const double t = v * inv_q;
+      double k = rint(t);
+      if (fabs(fabs(t - k) - 0.5) <= 8e-16 * fabs(t)) k = rint(v / J.q);
+      const int64_t slot = (int64_t)k - J.lat_kmin;
+      if (slot < 0 || slot >= J.lat_n) {
+        atomicOr(err, 2);
+        return;
+      }
+      if (slot < n_loc) {
+        const uint32_t rel = (uint32_t)(li - base);
+        if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
+      } else {
+        unsigned long long* dst = &slot_first[J.lat_off + slot];
+        const unsigned long long g = (unsigned long long)(J.cand_base + li);
+        if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
+      }
+    };
+    if (J.flags & TPE_F_DRAW32) {
+      const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
+      const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
+      float x[kLatR];
+      draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
+                          (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
+                          x);
 #pragma unroll
       for (int r = 0; r < kLatR; ++r)
         if (r < nv) mark((double)x[r], t0 + r);
-    }
-  } else {
-    for (int r = 0; r < kLatR; ++r) {
-      const int64_t li = base + r * kBS + threadIdx.x;
-      if (li >= J.n_cand) break;
-      double v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
-      if (lgmm) v = exp(v);
-      mark(v, li);
+    } else {
+      for (int r = 0; r < kLatR; ++r) {
+        const int64_t li = base + r * kBS + threadIdx.x;
+        if (li >= J.n_cand) break;
+        double v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+        if (lgmm) v = exp(v);
+        mark(v, li);
+      }
     }
   }
-  {
-    __syncthreads();
-    // blocks run roughly in index order, so the global slot mostly holds a
-    // smaller index already: an agent-scope load first keeps the (cross-XCD)
-    // atomics to the blocks that improve a slot
-    for (int s = threadIdx.x; s < n_loc; s += kBS) {
-      const uint32_t f = lfirst[s];
-      if (f == 0xFFFFFFFFu) continue;
-      unsigned long long* dst = &slot_first[J.lat_off + s];
-      const unsigned long long g = (unsigned long long)(J.cand_base + base + f);
-      if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
-    }
+  __syncthreads();
+  // blocks run roughly in index order, so the global slot mostly holds a
+  // smaller index already: an agent-scope load first keeps the (cross-XCD)
+  // atomics to the blocks that improve a slot
+  for (int s = threadIdx.x; s < n_loc; s += kBS) {
+    const uint32_t f = lfirst[s];
+    if (f == 0xFFFFFFFFu) continue;
+    unsigned long long* dst = &slot_first[J.lat_off + s];
+    const unsigned long long g = (unsigned long long)(J.cand_base + base + f);
+    if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
   }
 }
 
@@ -1177,7 +1193,7 @@ __global__ __launch_bounds__(kBS) void k_sample(const tpe_job* __restrict__ jobs
   const tpe_job J = jobs[blockIdx.y];
   const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
   if (base >= J.n_cand) return;
-  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_mix);
+  const Mix M = stage_mix(J, segs[J.below], wcdf, mu, sigma, s_mix);
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
   if (sizeof(T) == 4) {
@@ -1349,8 +1365,21 @@ extern "C" int tpe_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
     set_error("tpe_lattice_sample: %lld work items", (long long)(gx * n_jobs));
     return TPE_E_UNSUPPORTED;
   }
-  hipLaunchKernelGGL(k_lattice_sample, dim3((unsigned)(8 * per)), dim3(kBS), 0, st, jobs, segs,
-                     mu, sigma, wcdf, (unsigned long long*)slot_first, err, (int)gx, n_jobs);
+  bool pow2 = true;
+  int64_t n_loc = 1;
+  for (int i = 0; i < n_jobs; ++i) {
+    pow2 = pow2 && lattice_pow2(host_jobs[i]);
+    n_loc = std::max(n_loc, std::min((int64_t)kLatLds, host_jobs[i].lat_n));
+  }
+  const size_t lds = (size_t)n_loc * sizeof(uint32_t);
+  if (pow2)
+    hipLaunchKernelGGL(k_lattice_sample<true>, dim3((unsigned)(8 * per)), dim3(kBS), lds, st, jobs,
+                       segs, mu, sigma, wcdf, (unsigned long long*)slot_first, err, (int)gx,
+                       n_jobs);
+  else
+    hipLaunchKernelGGL(k_lattice_sample<false>, dim3((unsigned)(8 * per)), dim3(kBS), lds, st,
+                       jobs, segs, mu, sigma, wcdf, (unsigned long long*)slot_first, err, (int)gx,
+                       n_jobs);
   return check_launch("tpe_lattice_sample");
 }
 

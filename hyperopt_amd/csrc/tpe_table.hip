@@ -752,7 +752,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   const bool outs = out_bl || out_al || out_x;
   Mix M{};
 #ifndef TPE_DIAG_SKIP_SAMPLE
-  if (!INJ) M = stage_mix(SB, wcdf, mu, sigma, s_mix);  // once per block
+  if (!INJ) M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);  // once per block
 #endif
   BestT run{0.0, -1, 0.0};
   int n_exact = 0;
@@ -961,7 +961,7 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   const float4* sc = score_cells_of(region, J.tbl_cap);
   const int lane = lane_id();
   float* stage = s_stage + (threadIdx.x / kWave) * (kTR * kWave);
-  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
+  const Mix M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);
   const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
   const int nvalid = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
   float x[kTR];  // candidates in the scoring coordinate y (log x for LGMM1)
