@@ -38,8 +38,6 @@ struct Mix {  // sampler view of the below mixture (LDS or global)
   const uint32_t* thr;  // staged: component k takes words < thr[k] (fp32 draws)
   const uint2* gd;      // staged: guide entry of bucket b (see stage_mix)
   const float4* cw;     // staged: {mu, sigma, bits of thr[k-1], 1 / (thr[k] - thr[k-1])}
-  const double* tc;     // staged, bounded jobs: cumulative w_k * (mass of k inside the bounds)
-  const double2* tp;    // staged, bounded jobs: {Phi(a'), +-(Phi(b') - Phi(a'))} (see stage_mix)
   int n;
 };
 
@@ -48,8 +46,6 @@ struct MixLds {  // LDS image of a below mixture of <= kStage components
   uint32_t thr[kStage];
   float4 cw[kStage];
   uint2 gd[kGuide];
-  double tc[kStage];
-  double2 tp[kStage];
 };
 
 // stage the below mixture for sampling; returns the view (call by all threads).
@@ -62,21 +58,12 @@ struct MixLds {  // LDS image of a below mixture of <= kStage components
 // inside the bucket (multi), where the walk over thr[] finishes the search.
 // cw[k] also carries component k's word interval [thr[k-1], thr[k]) so the
 // fp32 sampler can read the word's position inside it (comp_res).
-// Bounded jobs also get the truncated mixture the reference's rejection loop
-// accepts from (tpe.py:97-102): component k with probability proportional to
-// w_k * m_k, m_k = its mass inside [low, high), then N(mu_k, sigma_k)
-// truncated to the bounds by inverse CDF.  With a = (low - mu)/sigma and
-// b = (high - mu)/sigma, a component whose interval lies above its mean is
-// mirrored (a' = -b, b' = -a, stored as a negative mass) so that Phi(a') <=
-// 1/2 is formed by erfc without cancellation.
-__device__ __forceinline__ Mix stage_mix(const tpe_job& J, const tpe_seg& S, const double* wcdf,
-                                         const double* mu, const double* sigma, MixLds& L) {
+__device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, const double* mu,
+                                         const double* sigma, MixLds& L) {
   const int n = S.n_obs + 1;
   if (n > kStage)
     return Mix{wcdf + S.comp_off, mu + S.comp_off, sigma + S.comp_off, nullptr, nullptr,
-               nullptr, nullptr, nullptr, n};
-  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
-  const bool bounded = lo_on || hi_on;
+               nullptr, n};
   const double total = wcdf[S.comp_off + n - 1];
   for (int k = threadIdx.x; k < n; k += kBS) {
     const double c = wcdf[S.comp_off + k], m = mu[S.comp_off + k], g = sigma[S.comp_off + k];
@@ -103,34 +90,9 @@ __device__ __forceinline__ Mix stage_mix(const tpe_job& J, const tpe_seg& S, con
     const uint32_t lo = k ? L.thr[k - 1] : 0u, width = L.thr[k] - lo;
     L.cw[k] = make_float4((float)L.mu[k], (float)L.sg[k], __uint_as_float(lo),
                           width ? 1.0f / (float)width : 0.0f);
-    if (bounded) {
-      const double sgk = L.sg[k] > 0.0 ? L.sg[k] : kEps;
-      double a = lo_on ? (J.low - L.mu[k]) / sgk : -INFINITY;
-      double b = hi_on ? (J.high - L.mu[k]) / sgk : INFINITY;
-      const bool flip = a > 0.0;
-      if (flip) {
-        const double t = a;
-        a = -b;
-        b = -t;
-      }
-      const double pa = 0.5 * erfc(-a / kSqrt2), pb = 0.5 * erfc(-b / kSqrt2);
-      const double m = fmax(pb - pa, 0.0);
-      L.tp[k] = make_double2(pa, flip ? -m : m);
-      L.tc[k] = (L.cdf[k] - (k ? L.cdf[k - 1] : 0.0)) * m;  // w_k m_k, summed below
-    }
   }
   __syncthreads();
-  if (bounded && threadIdx.x == 0) {
-    double acc = 0.0;
-    for (int k = 0; k < n; ++k) {
-      acc += L.tc[k];
-      L.tc[k] = acc;
-    }
-  }
-  if (bounded) __syncthreads();
-  const bool usable = bounded && L.tc[n - 1] > 0.0;
-  return Mix{L.cdf, L.mu, L.sg, L.thr, L.gd, L.cw, usable ? L.tc : nullptr,
-             usable ? L.tp : nullptr, n};
+  return Mix{L.cdf, L.mu, L.sg, L.thr, L.gd, L.cw, n};
 }
 
 // One draw from the (possibly truncated) below mixture: returns the value in
@@ -255,8 +217,7 @@ __device__ __forceinline__ float attempt32_first(const Mix& M, uint64_t key, int
   return second ? fmaf(sgb, z1, mub) : fmaf(sga, z0, mua);
 }
 
-// attempt a >= 1 of candidate g: one Philox call of the retry stream (only
-// for mixtures staged without truncation data: more than kStage components)
+// attempt a >= 1 of candidate g: one Philox call of the retry stream
 __device__ __forceinline__ float attempt32_retry(const Mix& M, uint64_t key, int64_t g,
                                                  uint32_t a) {
   const U4 r = draw_words(key, g, a, kStreamRetry);
@@ -265,53 +226,6 @@ __device__ __forceinline__ float attempt32_retry(const Mix& M, uint64_t key, int
   float z0, z1;
   bm_pair(u01_f32(r.y), u01_f32(r.z), z0, z1);
   return fmaf(sg, z0, mu);
-}
-
-// Standard normal quantile z with Phi(z) = p for p in (0, 1/2] given as the
-// fp32 lower-tail probability (Acklam's rational approximation, relative
-// error 1.2e-9 in exact arithmetic; evaluated in fp32, so about the fp32
-// Box-Muller normals' own precision).  Returns z <= 0.
-__device__ __forceinline__ float norm_quantile_lower(float p) {
-  if (p > 0.02425f) {  // central region
-    const float q = p - 0.5f, r = q * q;
-    const float num = (((((-3.969683028665376e+01f * r + 2.209460984245205e+02f) * r -
-                          2.759285104469687e+02f) * r + 1.383577518672690e+02f) * r -
-                        3.066479806614716e+01f) * r + 2.506628277459239e+00f) * q;
-    const float den = (((((-5.447609879822406e+01f * r + 1.615858368580409e+02f) * r -
-                          1.556989798598866e+02f) * r + 6.680131188771972e+01f) * r -
-                        1.328068155288572e+01f) * r + 1.0f);
-    return num / den;
-  }
-  const float q = __builtin_sqrtf(-2.0f * __logf(fmaxf(p, 1e-38f)));
-  return (((((-7.784894002430293e-03f * q - 3.223964580411365e-01f) * q -
-             2.400758277161838e+00f) * q - 2.549732539343734e+00f) * q +
-           4.374664141464968e+00f) * q + 2.938163982698783e+00f) /
-         ((((7.784695709041462e-03f * q + 3.224671290700398e-01f) * q +
-            2.445134137142996e+00f) * q + 3.754408661907416e+00f) * q + 1.0f);
-}
-
-// A candidate whose attempt 0 fell outside the bounds is redrawn ONCE from the
-// truncated mixture itself (stage_mix): attempt 0 accepted is distributed as
-// the truncated mixture, and so is this draw, so the candidate is -- exactly
-// the distribution of the reference's rejection loop, with no loop.  One
-// Philox call of the retry stream at counter (g, 1): word x picks the
-// component by the truncated weights, words (y, z) give a 53-bit uniform u;
-// p = Phi(a') + u (Phi(b') - Phi(a')) is formed in fp64 and the quantile of
-// the smaller of p and 1 - p is taken (fp32), so neither tail loses precision.
-__device__ __forceinline__ float draw32_truncated(const Mix& M, uint64_t key, int64_t g,
-                                                  bool lo_on, bool hi_on, float lo, float hi) {
-  const U4 r = draw_words(key, g, 1u, kStreamRetry);
-  const double u = (double)r.x * 0x1.0p-32 * M.tc[M.n - 1];
-  const int k = upper_bound(M.tc, M.n, u);  // first k with tc[k] > u: mass > 0
-  const double2 t = M.tp[k];
-  const double p = t.x + u01_f64(r.y, r.z) * fabs(t.y);
-  const double pc = 1.0 - p;
-  float z = p <= 0.5 ? norm_quantile_lower((float)p) : -norm_quantile_lower((float)pc);
-  if (t.y < 0.0) z = -z;
-  float y = fmaf((float)M.sg[k], z, (float)M.mu[k]);
-  if (lo_on && y < lo) y = lo;
-  if (hi_on && !(y < hi)) y = nextafterf(hi, -INFINITY);
-  return y;
 }
 
 __device__ __forceinline__ bool accept32(float y, bool lo_on, bool hi_on, float lo, float hi) {
@@ -329,7 +243,6 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
                                         bool hi_on, float lo, float hi) {
   float y = attempt32_first(M, key, g);
   if (accept32(y, lo_on, hi_on, lo, hi)) return y;
-  if (M.tc) return draw32_truncated(M, key, g, lo_on, hi_on, lo, hi);
   for (uint32_t a = 1; a < kMaxAttempts; ++a) {
     y = attempt32_retry(M, key, g, a);
     if (accept32(y, lo_on, hi_on, lo, hi)) return y;
@@ -344,18 +257,26 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
 // start inside a call (g0 not a multiple of 4 -- only at a shard boundary;
 // g0 is cand_base + a multiple of R, so the test is job-uniform) draws
 // attempt 0 one candidate at a time in a rolled loop through `wstage`, which
-// keeps the register footprint of the aligned loop.  Bounded labels then
-// redraw their rejected candidates from the truncated mixture, one per
-// rejection (draw32_truncated; mixtures staged without truncation data retry
-// attempt by attempt, each lane walking its own queue); redrawn values come
-// back through `wstage`, the calling wave's own R*64 floats of LDS (slot r
-// of lane l at r*64 + l).
+// keeps the register footprint of the aligned loop.
+// Bounded labels then retry their rejected candidates (attempts 1, 2, ... of
+// the retry stream, as draw32).  ~7% of C3's bounded draws are rejected, so a
+// wave holds ~70 of them but its busiest lane ~4: the wave's rejections are
+// listed in `wlist` (kRetryList entries per wave, a prefix sum of the lanes'
+// counts places them) and worked off 64 at a time, one per lane, so the wave
+// waits ~2 retry steps instead of its busiest lane's ~4; rejections past the
+// list (a rare wave) retry in their own lane.  Retried values come back
+// through `wstage`, the wave's R*64 floats of LDS (slot r of lane l at
+// r*64 + l).
+constexpr int kRetryList = 256;  // listed rejections per wave (uint16 entries)
+
 template <int R>
 __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t g0, int n,
                                              bool lo_on, bool hi_on, float lo, float hi,
-                                             bool to_x, float* wstage, float (&x)[R]) {
+                                             bool to_x, float* wstage, uint16_t* wlist,
+                                             float (&x)[R]) {
   static_assert(R % 4 == 0 && R <= 32, "quads, one mask bit per candidate");
-  float* st = wstage + lane_id();
+  const int lane = lane_id();
+  float* st = wstage + lane;
   if ((g0 & 3) == 0) {
 #pragma unroll
     for (int q = 0; q < R / 4; ++q)
@@ -377,30 +298,49 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
     if (rej & (1u << r)) x[r] = clamp32(x[r], lo_on, hi_on, lo, hi);
   rej = 0;
 #endif
+  auto retry = [&](int64_t g) __attribute__((always_inline)) -> float {
+    for (uint32_t a = 1;; ++a) {
+      const float y = attempt32_retry(M, key, g, a);
+      if (accept32(y, lo_on, hi_on, lo, hi)) return y;
+      if (a + 1 >= kMaxAttempts) return clamp32(y, lo_on, hi_on, lo, hi);
+    }
+  };
   if (__any(rej != 0)) {
-    uint32_t todo = rej, att = 1;
-    if (M.tc) {  // block-uniform: one truncated redraw per rejected candidate
-      while (todo) {
-        const int r = __builtin_ctz(todo);
-        todo &= todo - 1;
-        st[r * kWave] = draw32_truncated(M, key, g0 + r, lo_on, hi_on, lo, hi);
-      }
+    // list the wave's rejections: exclusive prefix of the lanes' counts
+    const int cnt = __popc(rej);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int o = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += o;
     }
-    while (__any(todo != 0)) {
-      if (todo) {
-        const int r = __builtin_ctz(todo);
-        float y = attempt32_retry(M, key, g0 + r, att);
-        const bool ok = accept32(y, lo_on, hi_on, lo, hi);
-        if (ok || att + 1 >= kMaxAttempts) {
-          if (!ok) y = clamp32(y, lo_on, hi_on, lo, hi);
-          st[r * kWave] = y;
-          todo &= todo - 1;
-          att = 1;
-        } else {
-          ++att;
-        }
-      }
+    const int total = min(__shfl(incl, kWave - 1, kWave), kRetryList);
+    int pos = incl - cnt;
+    uint32_t left = 0;  // this lane's rejections past the list
+    for (uint32_t m = rej; m; m &= m - 1) {
+      const int r = __builtin_ctz(m);
+      if (pos < kRetryList)
+        wlist[pos] = (uint16_t)((lane << 5) | r);
+      else
+        left |= 1u << r;
+      ++pos;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int b = 0; b < total; b += kWave) {
+      const int e = b + lane;
+      const int ent = e < total ? (int)wlist[e] : 0;
+      const int owner = ent >> 5, r = ent & 31;
+      const int64_t go = __shfl(g0, owner, kWave);  // every lane takes part
+      if (e < total) wstage[r * kWave + owner] = retry(go + r);
+    }
+    while (left) {
+      const int r = __builtin_ctz(left);
+      left &= left - 1;
+      st[r * kWave] = retry(g0 + r);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < R; ++r)
       if (rej & (1u << r)) x[r] = st[r * kWave];

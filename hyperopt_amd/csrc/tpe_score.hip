@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kBS) void k_score32(
       x[r] = li < J.n_cand ? (float)cand[J.cand_off + li] : 1.0f;
     }
   } else {
-    const Mix M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
 #pragma unroll
     for (int r = 0; r < kR32; ++r) {
       const int64_t li = base + r * kBS + threadIdx.x;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kBS) void k_score64(
       x[r] = li < J.n_cand ? cand[J.cand_off + li] : 1.0;
     }
   } else {
-    const Mix M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
 #pragma unroll
     for (int r = 0; r < kR64; ++r) {
       const int64_t li = base + r * kBS + threadIdx.x;
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(kBS) void k_sort_count(
   const int64_t base = (int64_t)blockIdx.x * kSortPer;
   if (base >= J.n_cand) return;
   for (int i = threadIdx.x; i < kNB; i += kBS) h[i] = 0u;
-  const Mix M = stage_mix(J, segs[J.below], wcdf, mu, sigma, s_mix);
+  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_mix);
   __syncthreads();
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
@@ -786,6 +786,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
   __shared__ float s_stage[kLatR * kBS];
+  __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   // XCD-aware work order (as k_score_table): each XCD sweeps a contiguous
   // eighth of the (job, tile) list, so a job's first-index atomics stay in
   // few XCDs' L2s
@@ -804,7 +805,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   // beyond go to the global marks directly, each read before its atomic
   const int n_loc = (int)min((int64_t)kLatLds, J.lat_n);
   for (int s = threadIdx.x; s < n_loc; s += kBS) lfirst[s] = 0xFFFFFFFFu;
-  const Mix M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);
+  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
   __syncthreads();
   if constexpr (POW2) {
     // kLatR consecutive candidates per thread (draw32_pairs); q a power of two:
@@ -814,7 +815,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
     float x[kLatR];
     draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
+                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList,
                         x);
     const float inv_q32 = (float)(1.0 / J.q);
     const int kmin = (int)J.lat_kmin, nl = (int)J.lat_n;
@@ -864,7 +865,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
       const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
       float x[kLatR];
       draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                          (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
+                          (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList,
                           x);
 #pragma unroll
       for (int r = 0; r < kLatR; ++r)
@@ -1190,10 +1191,11 @@ __global__ __launch_bounds__(kBS) void k_sample(const tpe_job* __restrict__ jobs
                                                 double* __restrict__ out_x) {
   __shared__ MixLds s_mix;
   __shared__ float s_stage[kLatR * kBS];
+  __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   const tpe_job J = jobs[blockIdx.y];
   const int64_t base = (int64_t)blockIdx.x * (kBS * kLatR);
   if (base >= J.n_cand) return;
-  const Mix M = stage_mix(J, segs[J.below], wcdf, mu, sigma, s_mix);
+  const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_mix);
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
   if (sizeof(T) == 4) {
@@ -1204,7 +1206,7 @@ __global__ __launch_bounds__(kBS) void k_sample(const tpe_job* __restrict__ jobs
     const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
     float x[kLatR];
     draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), x);
+                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList, x);
 #pragma unroll
     for (int r = 0; r < kLatR; ++r) {
       if (r >= nv) continue;

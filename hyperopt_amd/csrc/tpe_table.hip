@@ -711,6 +711,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   // per wave: 4 DMA slabs of 64 x 16 B, the gather's LDS image; also the
   // sampler's staging buffer before scoring
   __shared__ float4 s_rows[(kBS / kWave) * kWave * kChunks];
+  __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   __shared__ BestT red[kBS / kWave];
   __shared__ int nred[kBS / kWave];
   static_assert(kTR * kWave * sizeof(float) <= kWave * kChunks * sizeof(float4), "staging alias");
@@ -752,7 +753,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   const bool outs = out_bl || out_al || out_x;
   Mix M{};
 #ifndef TPE_DIAG_SKIP_SAMPLE
-  if (!INJ) M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);  // once per block
+  if (!INJ) M = stage_mix(SB, wcdf, mu, sigma, s_mix);  // once per block
 #endif
   BestT run{0.0, -1, 0.0};
   int n_exact = 0;
@@ -779,7 +780,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
 #else
       const int nv = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
       draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                        (float)J.high, false, reinterpret_cast<float*>(rows), x);
+                        (float)J.high, false, reinterpret_cast<float*>(rows), s_list + (threadIdx.x / kWave) * kRetryList, x);
 #endif
     }
     // per-thread argmax in fp32 over the thread's candidates r = 0..kTR-1
@@ -934,6 +935,7 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
     unsigned long long* __restrict__ stats, int n_tiles, int n_jobs) {
   __shared__ MixLds s_mix;
   __shared__ float s_stage[(kBS / kWave) * kTR * kWave];  // retry staging, then fallback stash
+  __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   __shared__ BestT red[kBS / kWave];
   __shared__ int nred[kBS / kWave];
   int job, bx;
@@ -961,12 +963,12 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   const float4* sc = score_cells_of(region, J.tbl_cap);
   const int lane = lane_id();
   float* stage = s_stage + (threadIdx.x / kWave) * (kTR * kWave);
-  const Mix M = stage_mix(J, SB, wcdf, mu, sigma, s_mix);
+  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
   const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
   const int nvalid = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
   float x[kTR];  // candidates in the scoring coordinate y (log x for LGMM1)
   draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nvalid, lo_on, hi_on, (float)J.low,
-                    (float)J.high, false, stage, x);
+                    (float)J.high, false, stage, s_list + (threadIdx.x / kWave) * kRetryList, x);
   auto cell_of = [&](float y) __attribute__((always_inline)) -> int {
     const float t = (y - g0) * inv_w;
     const int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
