@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32 = 1, 2, 4, 8, 16
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -51,6 +51,10 @@ HISTORY_DTYPE = np.dtype([
     ("rows_off", "<i8"), ("isb_off", "<i8")], align=True)
 BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
                        ("n_scored", "<i8")], align=True)
+PRIOR_DTYPE = np.dtype([("kind", "<i4"), ("n_cat", "<i4"), ("a", "<f8"), ("b", "<f8"),
+                        ("q", "<f8"), ("p_off", "<i8"), ("key", "<u8")], align=True)
+PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
+    PRIOR_CATEGORICAL = range(6)
 
 
 class TpeHipError(RuntimeError):
@@ -91,6 +95,7 @@ _SIGNATURES = {
     "tpe_score_categorical": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P]),
     "tpe_sample": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P]),
     "tpe_best_combine": (_I, [_P, _I, _I, _P, _P]),
+    "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
     "tpe_last_error": (ctypes.c_char_p, []),
     "tpe_abi_version": (_I, []),
     "tpe_struct_sizes": (_I, [_P, _I]),
@@ -116,10 +121,11 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    sizes = (ctypes.c_int32 * 7)()
-    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 7)
+    sizes = (ctypes.c_int32 * 8)()
+    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 8)
     want = (SEG_DTYPE.itemsize, CAT_SEG_DTYPE.itemsize, JOB_DTYPE.itemsize, BEST_DTYPE.itemsize,
-            TABLE_DTYPE.itemsize, GATHER_DTYPE.itemsize, HISTORY_DTYPE.itemsize)
+            TABLE_DTYPE.itemsize, GATHER_DTYPE.itemsize, HISTORY_DTYPE.itemsize,
+            PRIOR_DTYPE.itemsize)
     if lib.tpe_abi_version() != ABI_VERSION:
         raise ImportError("hyperopt_amd: libtpe_hip.so ABI %d, expected %d (rebuild with make)"
                           % (lib.tpe_abi_version(), ABI_VERSION))

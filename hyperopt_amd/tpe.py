@@ -6,7 +6,8 @@
 Same signature, defaults, startup rule, history rules and returned document
 as the reference (hyperopt/tpe.py:837-964):
   * per-tid best loss, ``from_tid`` aliasing, None -> +inf (tpe.py:874-896);
-  * fewer than ``n_startup_jobs`` distinct tids -> rand.suggest (tpe.py:909-911);
+  * fewer than ``n_startup_jobs`` distinct tids -> random search from the
+    priors, drawn on the GPU (rand.suggest_device; tpe.py:909-911);
   * the below set is the best min(ceil(gamma*sqrt(T)), 25) tids (tpe.py:637);
   * every live label gets ``n_EI_candidates`` candidates drawn from its below
     posterior, scored by l(x)/g(x), and the argmax is kept (tpe.py:649-658);
@@ -312,8 +313,8 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
                 hist.tids.size, len(trials), np.nanmin(hist.losses)))
         else:
             logger.info("TPE using 0 trials")
-    if hist.tids.size < n_startup_jobs:
-        return rand.suggest(new_ids, domain, trials, seed)
+    if hist.tids.size < n_startup_jobs:  # tpe.py:909-911, prior draws on the GPU
+        return rand.suggest_device(new_ids, domain, trials, seed)
 
     first_new_id = new_ids[0]
     isb, isa = split_masks(hist, gamma)
@@ -395,7 +396,7 @@ def suggest_many(requests, shard_studies=False):
         labels = list(rq.domain.params)
         hist = collect_history(rq.trials, labels)
         if hist.tids.size < kw["n_startup_jobs"]:
-            out[qi] = rand.suggest(rq.new_ids, rq.domain, rq.trials, rq.seed)
+            out[qi] = rand.suggest_device(rq.new_ids, rq.domain, rq.trials, rq.seed)
             continue
         isb, isa = split_masks(hist, kw["gamma"])
         n_ei = max(int(kw["n_EI_candidates"]), 0)

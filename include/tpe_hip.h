@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 7
+#define TPE_ABI_VERSION 8
 
 enum {
   TPE_OK = 0,
@@ -356,6 +356,28 @@ int tpe_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                const tpe_seg* segs, const double* mu, const double* sigma,
                const double* wcdf, int precision, double* out_x, void* stream);
 
+/* ---- prior draws (startup phase: rand.suggest, hyperopt/rand.py:15-27) ----
+ * Replaces the prior samplers of pyll/stochastic.py:36-158: n draws of every
+ * prior, draw i of prior j at out[j * n + i], a function of (key, base + i)
+ * only (Philox4x32-10).  kind: TPE_PRIOR_*; a, b = low, high (uniform,
+ * loguniform in log space, randint: [low, high)) or mu, sigma (normal,
+ * lognormal in log space); q > 0 quantizes as np.round(x / q) * q;
+ * categorical: n_cat probabilities at p + p_off (need not be normalised).
+ * Values are fp64 (category / randint values as whole numbers). */
+enum {
+  TPE_PRIOR_UNIFORM = 0, TPE_PRIOR_LOGUNIFORM = 1, TPE_PRIOR_NORMAL = 2,
+  TPE_PRIOR_LOGNORMAL = 3, TPE_PRIOR_RANDINT = 4, TPE_PRIOR_CATEGORICAL = 5
+};
+typedef struct tpe_prior {
+  int32_t kind;
+  int32_t n_cat;        /* categorical: number of categories                 */
+  double a, b, q;
+  int64_t p_off;        /* categorical: first probability in `p`             */
+  uint64_t key;         /* Philox key (seed mixed with the label)            */
+} tpe_prior;
+int tpe_prior_sample(const tpe_prior* priors, const tpe_prior* host_priors, int n_priors,
+                     const double* p, int64_t n, int64_t base, double* out, void* stream);
+
 /* ---- argmax combine: n_sets tpe_best arrays of n_labels each (e.g. one per
  * rank after an all-gather) -> n_labels winners, same tie rules. ------------ */
 int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* out,
@@ -364,7 +386,7 @@ int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* o
 const char* tpe_last_error(void);
 int tpe_abi_version(void);
 /* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table, tpe_gather,
- * tpe_history) to out[0..n); returns 7 */
+ * tpe_history, tpe_prior) to out[0..n); returns 8 */
 int tpe_struct_sizes(int32_t* out, int n);
 
 #ifdef __cplusplus

@@ -30,12 +30,13 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 7
-    sizes = (ctypes.c_int32 * 7)()
-    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 7) == 7
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 8
+    sizes = (ctypes.c_int32 * 8)()
+    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 8) == 8
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
                             L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize, L.TABLE_DTYPE.itemsize,
-                            L.GATHER_DTYPE.itemsize, L.HISTORY_DTYPE.itemsize)
+                            L.GATHER_DTYPE.itemsize, L.HISTORY_DTYPE.itemsize,
+                            L.PRIOR_DTYPE.itemsize)
 
 
 def test_argument_errors_are_reported():
@@ -81,6 +82,17 @@ def test_argument_errors_are_reported():
     rc = lib.tpe_table_build(None, hp_, 1, None, None, None, None, 8, *([None] * 8))
     assert rc == -1 and b"not an unquantized" in lib.tpe_last_error()
     assert lib.tpe_best_combine(None, 0, 1, None, None) == -1
+    pri = np.zeros(1, L.PRIOR_DTYPE)
+    pri["kind"] = 9
+    pp = pri.ctypes.data_as(ctypes.c_void_p)
+    assert lib.tpe_prior_sample(None, pp, 1, None, 4, 0, None, None) == -1
+    assert b"kind 9" in lib.tpe_last_error()
+    pri["kind"], pri["a"], pri["b"] = L.PRIOR_RANDINT, 3.0, 3.0
+    assert lib.tpe_prior_sample(None, pp, 1, None, 4, 0, None, None) == -1
+    assert b"high <= low" in lib.tpe_last_error()
+    pri["kind"] = L.PRIOR_CATEGORICAL
+    assert lib.tpe_prior_sample(None, pp, 1, None, 4, 0, None, None) == -1
+    assert lib.tpe_prior_sample(None, None, 0, None, 4, 0, None, None) == 0
     g = np.zeros(1, L.GATHER_DTYPE)
     g["to_int"] = 1
     gp = g.ctypes.data_as(ctypes.c_void_p)

@@ -184,7 +184,8 @@ def test_startup_delegates_to_rand():
     dom = Domain(passthrough, space)
     trials = Trials()
     docs = tpe.suggest([0], dom, trials, 7)
-    assert docs[0]["misc"]["vals"]["x"][0] == rand.suggest([0], dom, trials, 7)[0]["misc"]["vals"]["x"][0]
+    assert docs[0]["misc"]["vals"]["x"][0] == \
+        rand.suggest_device([0], dom, trials, 7)[0]["misc"]["vals"]["x"][0]
 
 
 def test_large_candidate_count_fp32_and_fp64_agree():
