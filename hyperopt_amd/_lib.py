@@ -83,6 +83,9 @@ _SIGNATURES = {
                              _P, _P, _P]),
     "tpe_score_table_fast": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P,
                                   _P, _P]),
+    "tpe_pruned64_partials": (_I64, [_P, _I]),
+    "tpe_score_pruned64": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P,
+                                _P, _P, _P, _I64, _P, _P]),
     "tpe_score_partials": (_I64, [_P, _I]),
     "tpe_score_continuous": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P,
                                   _P, _I64, _P, _P]),

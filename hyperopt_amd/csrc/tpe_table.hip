@@ -64,6 +64,8 @@ constexpr int kChunks = 4;           // 16-B chunks of a cell the scorer reads
 constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
 constexpr double kTauExtra = 25.0;   // exclusion margin (nats) on top of log(M)
 constexpr double kDrawZ = 5.8;       // |z| of an fp32 Box-Muller draw is < 5.77
+constexpr double kDrawZ64 = 8.7;     // |z| of an fp64 Box-Muller draw (53-bit uniforms) is < 8.6
+constexpr double kTauExact = 40.0;   // margin of the pruned exact fp64 scorer: e^-40 < 5e-18
 constexpr float kULim = 1.05f;       // |u| accepted by the scorer (fp32 cell-centre rounding)
 #ifndef TPE_TR
 #define TPE_TR 16
@@ -127,17 +129,21 @@ constexpr int kPlanStride = 4;  // per tile: {max reach_hi, min reach_lo, #wide,
 // candidate: mu +- 5.8 sigma per component, clipped to the bounds) and the
 // global lower bound T of a term that can matter (the prior's smallest term
 // over the range, minus log(M) + kTauExtra); identical in every block
+// draw_z: |z| bound of the sampler's normals (kDrawZ for fp32 draws, kDrawZ64
+// for fp64 ones); tau: the exclusion margin (kTauExtra for the table,
+// kTauExact for the pruned exact fp64 scorer)
 __device__ __forceinline__ void plan_range(const tpe_job& J, const tpe_seg& SB, const tpe_seg& S,
                                            const double* __restrict__ mu,
                                            const double* __restrict__ sigma,
                                            const double* __restrict__ coef64, double* red,
-                                           double& a, double& b, double& T) {
+                                           double draw_z, double tau, double& a, double& b,
+                                           double& T) {
   a = INFINITY;
   b = -INFINITY;
   for (int k = threadIdx.x; k < SB.n_obs + 1; k += kBS) {
     const double m = mu[SB.comp_off + k], sg = sigma[SB.comp_off + k];
-    a = fmin(a, m - kDrawZ * sg);
-    b = fmax(b, m + kDrawZ * sg);
+    a = fmin(a, m - draw_z * sg);
+    b = fmax(b, m + draw_z * sg);
   }
   a = -block_max<kBS, double>(-a, red);
   b = block_max<kBS, double>(b, red);
@@ -154,7 +160,7 @@ __device__ __forceinline__ void plan_range(const tpe_job& J, const tpe_seg& SB, 
   }
   const double4 cp = ld4(coef64, S.comp_off + S.prior_pos);
   const double far = fmax(fabs(a - cp.x), fabs(b - cp.x)) * cp.y;
-  T = cp.z - 0.5 * far * far - (log((double)(S.n_obs + 1)) + kTauExtra);
+  T = cp.z - 0.5 * far * far - (log((double)(S.n_obs + 1)) + tau);
 }
 
 // wide components (the prior, and any with sigma >= prior_sigma / 4) are not
@@ -182,7 +188,8 @@ __global__ __launch_bounds__(kBS) void k_table_plan1(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ coef64, double* __restrict__ reach_hi,
-    double* __restrict__ reach_lo, double* __restrict__ part, tpe_table* __restrict__ tables) {
+    double* __restrict__ reach_lo, double* __restrict__ part, tpe_table* __restrict__ tables,
+    double draw_z, double tau) {
   __shared__ double red[kBS / kWave];
   __shared__ double scan_d[kBS / kWave];
   const int job = blockIdx.y >> 1, half = blockIdx.y & 1;
@@ -192,7 +199,7 @@ __global__ __launch_bounds__(kBS) void k_table_plan1(
   const int nc = S.n_obs + 1;
   if ((int)blockIdx.x * kBS >= nc) return;  // block-uniform
   double a, b, T;
-  plan_range(J, SB, S, mu, sigma, coef64, red, a, b, T);
+  plan_range(J, SB, S, mu, sigma, coef64, red, draw_z, tau, a, b, T);
   const int k = blockIdx.x * kBS + threadIdx.x;
   bool wide = true;
   double hr = -INFINITY, lr = INFINITY, hk = INFINITY;
@@ -1048,6 +1055,105 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
 }
 
+// ---------------------------------------------------------------------------
+// exact fp64 scoring with component pruning (the parity mode at large M)
+// ---------------------------------------------------------------------------
+// The plan (k_table_plan1/2 with margin kTauExact) gives every mixture a
+// floor T: a component whose term stays below T over the whole candidate
+// range can add at most e^-40 of the prior component's term, itself a lower
+// bound of the sum (exactly the table's exclusion rule with a wider margin),
+// and reach windows over the sorted means.  A candidate sums, in fp64 with
+// the online log-sum-exp of k_score64, the components of its reach window
+// plus the wide list -- ~2 sigma_min / (range / M) components instead of M --
+// and every component when it lies off the planned range.
+constexpr int kR64P = 4;  // candidates per thread
+
+__device__ __forceinline__ double lse64_pruned(const tpe_seg& S, const double* __restrict__ coef64,
+                                               const double* __restrict__ rh,
+                                               const double* __restrict__ rl,
+                                               const int32_t* __restrict__ wide, int n_wide,
+                                               double lo, double hi, double y) {
+  const int nc = S.n_obs + 1;
+  const int64_t off = S.comp_off;
+  double m = -INFINITY, s = 0.0;
+  auto add = [&](const double4 c) __attribute__((always_inline)) {
+    const double t = (y - c.x) * c.y;
+    const double v = -0.5 * (t * t) + c.z;
+    // one exp per pair on every lane (as k_score64): same values as
+    // s*exp(m-v)+1 (new max) / s+exp(v-m), NaN included
+    const bool up = v > m;
+    const double e = exp(up ? m - v : v - m);
+    s = up ? s * e + 1.0 : s + e;
+    m = up ? v : m;
+  };
+  if (y >= lo && y <= hi) {
+    const int k_lo = first_ge(rh + off, nc, y);
+    const int k_hi = last_le(rl + off, nc, y);
+    for (int k = k_lo; k <= k_hi; ++k) {
+      const double4 c = ld4(coef64, off + k);
+      if (!is_wide(S, k, c.y)) add(c);
+    }
+    for (int i = 0; i < n_wide; ++i) add(ld4(coef64, off + wide[off + i]));
+  } else {
+    for (int k = 0; k < nc; ++k) add(ld4(coef64, off + k));
+  }
+  return log(s) + m;
+}
+
+template <bool INJ>
+__global__ __launch_bounds__(kBS) void k_score_pruned64(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const double* __restrict__ wcdf, const double* __restrict__ coef64,
+    const double* __restrict__ reach_hi, const double* __restrict__ reach_lo,
+    const int32_t* __restrict__ wide_idx, const tpe_table* __restrict__ tables,
+    const double* __restrict__ cand, double* __restrict__ out_bl, double* __restrict__ out_al,
+    double* __restrict__ out_x, tpe_best* __restrict__ partial) {
+  __shared__ MixLds s_mix;
+  __shared__ BestT red[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (kBS * kR64P);
+  if (base >= J.n_cand) {
+    if (threadIdx.x == 0) *P = empty_best();
+    return;
+  }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const tpe_table Tb = tables[blockIdx.y];
+  const bool lgmm = J.family == TPE_LGMM1;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  Mix M{};
+  if (!INJ) M = stage_mix(SB, wcdf, mu, sigma, s_mix);
+  BestT b{0.0, -1, 0.0};
+  for (int r = 0; r < kR64P; ++r) {
+    const int64_t li = base + r * kBS + threadIdx.x;
+    if (li >= J.n_cand) break;
+    double x;
+    if (INJ) {
+      x = cand[J.cand_off + li];
+    } else {
+      x = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+      if (lgmm) x = exp(x);
+    }
+    const double y = lgmm ? log(x) : x;
+    double bl = lse64_pruned(SB, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below, Tb.lo,
+                             Tb.hi, y);
+    double al = lse64_pruned(SA, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above, Tb.lo,
+                             Tb.hi, y);
+    if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
+      bl -= y;
+      al -= y;
+    }
+    const int64_t o = J.out_off + li;
+    if (out_bl) out_bl[o] = bl;
+    if (out_al) out_al[o] = al;
+    if (out_x) out_x[o] = x;
+    best_update(b, bl - al, J.cand_base + li, x);
+  }
+  b = block_best<kBS>(b, red);
+  if (threadIdx.x == 0) *P = tpe_best{b.score, b.index, b.value, 0};
+}
+
 __global__ __launch_bounds__(kBS) void k_reduce_t(const tpe_job* __restrict__ jobs,
                                                   const tpe_best* __restrict__ partial,
                                                   int64_t nper, tpe_best* __restrict__ best) {
@@ -1118,7 +1224,7 @@ extern "C" int tpe_table_build(const tpe_job* jobs, const tpe_job* host_jobs, in
   hipStream_t st = (hipStream_t)stream;
   const dim3 pg((max_comp + kBS - 1) / kBS, 2 * n_jobs);
   hipLaunchKernelGGL(k_table_plan1, pg, dim3(kBS), 0, st, jobs, segs, mu, sigma, coef64, reach_hi,
-                     reach_lo, scratch, tables);
+                     reach_lo, scratch, tables, kDrawZ, kTauExtra);
   hipLaunchKernelGGL(k_table_plan2, pg, dim3(kBS), 0, st, jobs, segs, mu, sigma, coef64, reach_hi,
                      reach_lo, wide_idx, scratch, tables);
   hipLaunchKernelGGL(k_table_build, dim3(kBuildBlocks, n_jobs), dim3(kBS), 0, st, jobs, segs,
@@ -1219,6 +1325,70 @@ extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_job
                      out_score, out_x, partial, (unsigned long long*)stats, (int)gx, n_jobs);
   hipLaunchKernelGGL(k_reduce_t, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
   return check_launch("tpe_score_table_fast");
+}
+
+extern "C" int64_t tpe_pruned64_partials(const tpe_job* host_jobs, int n_jobs) {
+  int64_t gx = 1;
+  for (int i = 0; i < n_jobs; ++i)
+    gx = std::max(gx, (host_jobs[i].n_cand + kBS * kR64P - 1) / (kBS * kR64P));
+  return gx * n_jobs;
+}
+
+extern "C" int tpe_score_pruned64(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                  const tpe_seg* segs, const double* mu, const double* sigma,
+                                  const double* wcdf, const double* coef64, int max_comp,
+                                  double* reach_hi, double* reach_lo, int32_t* wide_idx,
+                                  double* scratch, tpe_table* tables, const double* cand,
+                                  double* out_bl, double* out_al, double* out_x,
+                                  tpe_best* partial, int64_t n_partial, tpe_best* best,
+                                  void* stream) {
+  if (n_jobs < 0 || n_jobs > 32767 || (n_jobs > 0 && !host_jobs)) {
+    set_error("tpe_score_pruned64: bad job list (n_jobs=%d)", n_jobs);
+    return TPE_E_ARG;
+  }
+  bool inj = false;
+  for (int i = 0; i < n_jobs; ++i) {
+    const tpe_job& j = host_jobs[i];
+    if (j.family == TPE_CAT || (j.flags & TPE_F_QUANT) || j.n_cand < 0) {
+      set_error("tpe_score_pruned64: job %d is not an unquantized GMM1/LGMM1 job", i);
+      return TPE_E_ARG;
+    }
+    const bool ji = (j.flags & TPE_F_INJECTED) != 0;
+    if (i > 0 && ji != inj) {
+      set_error("tpe_score_pruned64: mixed injected / sampled jobs in one call");
+      return TPE_E_ARG;
+    }
+    inj = ji;
+  }
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !coef64 || !reach_hi || !reach_lo ||
+      !wide_idx || !scratch || !tables || !partial || !best || (inj && !cand) || max_comp < 1) {
+    set_error("tpe_score_pruned64: null pointer or max_comp < 1");
+    return TPE_E_ARG;
+  }
+  const int64_t gx = tpe_pruned64_partials(host_jobs, n_jobs) / n_jobs;
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_score_pruned64: partial workspace %lld < %lld", (long long)n_partial,
+              (long long)(gx * n_jobs));
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 pg((max_comp + kBS - 1) / kBS, 2 * n_jobs);
+  hipLaunchKernelGGL(k_table_plan1, pg, dim3(kBS), 0, st, jobs, segs, mu, sigma, coef64, reach_hi,
+                     reach_lo, scratch, tables, kDrawZ64, kTauExact);
+  hipLaunchKernelGGL(k_table_plan2, pg, dim3(kBS), 0, st, jobs, segs, mu, sigma, coef64, reach_hi,
+                     reach_lo, wide_idx, scratch, tables);
+  const dim3 grid((unsigned)gx, (unsigned)n_jobs);
+  if (inj)
+    hipLaunchKernelGGL(k_score_pruned64<true>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma, wcdf,
+                       coef64, reach_hi, reach_lo, wide_idx, tables, cand, out_bl, out_al, out_x,
+                       partial);
+  else
+    hipLaunchKernelGGL(k_score_pruned64<false>, grid, dim3(kBS), 0, st, jobs, segs, mu, sigma,
+                       wcdf, coef64, reach_hi, reach_lo, wide_idx, tables, cand, out_bl, out_al,
+                       out_x, partial);
+  hipLaunchKernelGGL(k_reduce_t, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
+  return check_launch("tpe_score_pruned64");
 }
 
 extern "C" int64_t tpe_table_partials(const tpe_job* host_jobs, int n_jobs) {

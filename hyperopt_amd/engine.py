@@ -40,6 +40,7 @@ DRAW32_MAX_SLOT = 1 << 12  # fp32 lattice draws only while |k| <= 2^12
 LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense fallback
 TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
+PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
 SORTED_MIN_CAND = 1 << 12  # auto scorer: sorted/pruned path from this many (below: dense)
 SCORERS = ("auto", "dense", "sorted", "table")
 SIDE_KINDS = ("lat", "qfb", "qinj", "cat")  # groups scored on the side stream
@@ -239,6 +240,10 @@ class Engine:
         # each candidate by its cell's score cubic (tpe_score_table_fast);
         # "poly" evaluates both cell polynomials (tpe_score_table)
         self.table_scorer = os.environ.get("TPE_TABLE_SCORER", "cubic")
+        # fp64 continuous labels: "auto" prunes components (tpe_score_pruned64)
+        # once the above mixture has PRUNED64_MIN_COMP components, "dense"
+        # always sums every component (tpe_score_continuous), "pruned" always prunes
+        self.exact64 = os.environ.get("TPE_EXACT64", "auto")
 
     # -- memory --------------------------------------------------------------
     def _buf(self, name, nbytes):
@@ -531,8 +536,13 @@ class Engine:
                     else:
                         lat_ranges[i] = (kmin, kmax - kmin + 1)
             def cont_mode(i):
-                if precision != 32 or sample_only:
+                if sample_only:
                     return "cont"
+                if precision != 32:
+                    w = works[i]
+                    m = int(w.n_above) if w.obs_above is None else np.size(w.obs_above)
+                    return "pruned64" if (self.exact64 == "pruned" or (
+                        self.exact64 == "auto" and m >= PRUNED64_MIN_COMP)) else "cont"
                 n = int(np.asarray(works[i].cand).size) if inj(i) else \
                     int(works[i].n_total or works[i].n_cand)
                 mode = scorer
@@ -551,6 +561,8 @@ class Engine:
                 ("cont", [i for i in cont if inj(i) and modes[i] == "cont"]),
                 ("cont", [i for i in cont if not inj(i) and modes[i] == "cont"]),
                 ("sorted", [i for i in cont if modes[i] == "sorted"]),
+                ("pruned64", [i for i in cont if inj(i) and modes[i] == "pruned64"]),
+                ("pruned64", [i for i in cont if not inj(i) and modes[i] == "pruned64"]),
                 ("table", [i for i in cont if inj(i) and modes[i] == "table"]),
                 ("table", [i for i in cont if not inj(i) and modes[i] == "table"]),
                 ("lat", [i for i in quant if i in lat_ranges]),
@@ -617,6 +629,8 @@ class Engine:
                     tbl_off += TABLE_CAP
                     if inj(i):
                         J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P)
+                elif modes[i] == "pruned64" and inj(i):
+                    J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P, fp32=False)
                 elif modes[i] == "sorted":
                     J["bin_lo"][pos], J["bin_hi"][pos] = _support(w, P)
                     J["sort_off"][pos], J["cnt_off"][pos] = sort_off, cnt_off
@@ -854,6 +868,19 @@ class Engine:
                                                      npart, db, d_stats, sp),
                             "tpe_score_table_fast")
                 table_calls.append(nj)
+            elif kind == "pruned64":
+                npart = lib.tpe_pruned64_partials(hjp, nj)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
+                d_rh = self._buf("reach_hi", 8 * n_comp)
+                d_rl = self._buf("reach_lo", 8 * n_comp)
+                d_wide = self._buf("wide_idx", 4 * n_comp)
+                max_comp = max_obs + 1
+                d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
+                L.check(lib.tpe_score_pruned64(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c64,
+                                               max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab, d_cand,
+                                               d_bl, d_al, d_x, d_part, npart, db, sp),
+                        "tpe_score_pruned64")
             elif kind == "lat":
                 d_slot = self._buf("lat_slot", 8 * lat_off)
                 d_vals = self._buf("lat_vals", 8 * lat_off)
@@ -997,13 +1024,14 @@ def _support(w: LabelWork, P):
     return float(pts.min()) - 9.0 * P["prior_sigma"], float(pts.max()) + 9.0 * P["prior_sigma"]
 
 
-def _injected_range(w: LabelWork, P):
+def _injected_range(w: LabelWork, P, fp32=True):
     """Scoring-coordinate range of injected candidates (finite ones; the table
-    grid covers it, anything outside is scored exactly)."""
+    grid covers it, anything outside is scored exactly).  fp32: the log of an
+    LGMM1 candidate as the fp32 scorer forms it."""
     c = np.asarray(w.cand, dtype=np.float64).reshape(-1)
     if P["family"] == L.LGMM1:
         with np.errstate(all="ignore"):
-            c = np.log(c.astype(np.float32)).astype(np.float64)
+            c = np.log(c.astype(np.float32)).astype(np.float64) if fp32 else np.log(c)
     c = c[np.isfinite(c)]
     if c.size == 0:
         return P["prior_mu"], P["prior_mu"]

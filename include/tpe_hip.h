@@ -316,6 +316,25 @@ int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_jobs, int n_jo
                          tpe_best* partial, int64_t n_partial, tpe_best* best, uint64_t* stats,
                          void* stream);
 
+/* ---- continuous candidates, exact fp64 with pruning (parity mode) ----------
+ * Same results as tpe_score_continuous(precision=64) up to fp64 rounding: the
+ * plan of tpe_table_build (with an e^-40 exclusion margin and the fp64
+ * sampler's |z| < 8.7 range) finds, per mixture, the components whose term
+ * can reach e^-40 of the sum somewhere on the candidate range, with reach
+ * windows over the sorted means; each candidate sums its window plus the
+ * wide components in fp64 (every component when it lies off the range), so
+ * the work per candidate follows the components near it, not M.  Workspaces
+ * as tpe_table_build (reach_hi / reach_lo / wide_idx / scratch / tables);
+ * partial: tpe_pruned64_partials() entries.  out_* as tpe_score_continuous. */
+int64_t tpe_pruned64_partials(const tpe_job* host_jobs, int n_jobs);
+int tpe_score_pruned64(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                       const tpe_seg* segs, const double* mu, const double* sigma,
+                       const double* wcdf, const double* coef64, int max_comp,
+                       double* reach_hi, double* reach_lo, int32_t* wide_idx, double* scratch,
+                       tpe_table* tables, const double* cand, double* out_bl, double* out_al,
+                       double* out_x, tpe_best* partial, int64_t n_partial, tpe_best* best,
+                       void* stream);
+
 /* ---- quantized labels: lattice path ---------------------------------------
  * Candidates of a quantized label take values k*q (np.round(x/q)*q,
  * tpe.py:106, 256); equal values have equal scores, so every distinct value
