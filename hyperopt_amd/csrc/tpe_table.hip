@@ -1066,38 +1066,108 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
 // the online log-sum-exp of k_score64, the components of its reach window
 // plus the wide list -- ~2 sigma_min / (range / M) components instead of M --
 // and every component when it lies off the planned range.
-constexpr int kR64P = 4;  // candidates per thread
+//
+// Coherence: a block sorts its kP64N candidates by coordinate in LDS (bitonic)
+// and each wave scores runs of 64 consecutive ones, looping over the union of
+// its lanes' windows with wave-uniform (scalar) component loads; a lane adds
+// only the components of its own window, so a candidate's sum -- terms, order
+// and offset -- is a function of its coordinate alone, whatever its
+// neighbours.  The offset is the mixture's largest log-coefficient (every
+// term <= 1, one exp per pair); a sum below 2^-900 (or a candidate off the
+// range, or NaN) is redone with the online log-sum-exp over all components.
+constexpr int kR64P = 4;                 // candidates per thread
+constexpr int kP64N = kBS * kR64P;       // candidates per block (sorted together)
 
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off, kWave));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// largest log-coefficient of mixture S (every thread gets it)
+__device__ __forceinline__ double lc_max(const tpe_seg& S, const double* __restrict__ coef64,
+                                         double* red) {
+  double m = -INFINITY;
+  for (int k = threadIdx.x; k < S.n_obs + 1; k += kBS) m = fmax(m, coef64[4 * (S.comp_off + k) + 2]);
+  return block_max<kBS, double>(m, red);
+}
+
+// log of mixture S at y for lane-active candidates (see above); call by the
+// whole wave
 __device__ __forceinline__ double lse64_pruned(const tpe_seg& S, const double* __restrict__ coef64,
                                                const double* __restrict__ rh,
                                                const double* __restrict__ rl,
                                                const int32_t* __restrict__ wide, int n_wide,
-                                               double lo, double hi, double y) {
+                                               double m, bool act, bool inr, double y) {
   const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
-  double m = -INFINITY, s = 0.0;
-  auto add = [&](const double4 c) __attribute__((always_inline)) {
+  int k_lo = nc, k_hi = -1;
+  if (act && inr) {
+    k_lo = first_ge(rh + off, nc, y);
+    k_hi = last_le(rl + off, nc, y);
+  }
+  const int ulo = wave_min_i(k_lo), uhi = wave_max_i(k_hi);
+  double s = 0.0;
+  for (int k = ulo; k <= uhi; ++k) {
+    const double4 c = ld4(coef64, off + k);
+    if (is_wide(S, k, c.y)) continue;
     const double t = (y - c.x) * c.y;
-    const double v = -0.5 * (t * t) + c.z;
+    const double e = exp(fma(-0.5 * t, t, c.z - m));
+    s += (k >= k_lo && k <= k_hi) ? e : 0.0;
+  }
+  if (__any(act && inr)) {
+    for (int i = 0; i < n_wide; ++i) {
+      const double4 c = ld4(coef64, off + wide[off + i]);
+      const double t = (y - c.x) * c.y;
+      s += exp(fma(-0.5 * t, t, c.z - m));
+    }
+  }
+  double r = log(s) + m;
+  const bool slow = act && !(inr && s >= 0x1p-900);
+  if (__any(slow)) {
     // one exp per pair on every lane (as k_score64): same values as
     // s*exp(m-v)+1 (new max) / s+exp(v-m), NaN included
-    const bool up = v > m;
-    const double e = exp(up ? m - v : v - m);
-    s = up ? s * e + 1.0 : s + e;
-    m = up ? v : m;
-  };
-  if (y >= lo && y <= hi) {
-    const int k_lo = first_ge(rh + off, nc, y);
-    const int k_hi = last_le(rl + off, nc, y);
-    for (int k = k_lo; k <= k_hi; ++k) {
+    double mo = -INFINITY, so = 0.0;
+    for (int k = 0; k < nc; ++k) {
       const double4 c = ld4(coef64, off + k);
-      if (!is_wide(S, k, c.y)) add(c);
+      const double t = (y - c.x) * c.y;
+      const double v = -0.5 * (t * t) + c.z;
+      const bool up = v > mo;
+      const double e = exp(up ? mo - v : v - mo);
+      so = up ? so * e + 1.0 : so + e;
+      mo = up ? v : mo;
     }
-    for (int i = 0; i < n_wide; ++i) add(ld4(coef64, off + wide[off + i]));
-  } else {
-    for (int k = 0; k < nc; ++k) add(ld4(coef64, off + k));
+    if (slow) r = log(so) + mo;
   }
-  return log(s) + m;
+  return r;
+}
+
+// ascending bitonic sort of kP64N (key, index) pairs in LDS, ties by index
+__device__ __forceinline__ void sort_block(double* key, uint16_t* idx) {
+  for (int k = 2; k <= kP64N; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (int h = 0; h < kP64N / 2 / kBS; ++h) {
+        const int p = h * kBS + threadIdx.x;
+        const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), l = i + j;
+        const double a = key[i], b = key[l];
+        const uint16_t ia = idx[i], ib = idx[l];
+        const bool gt = a > b || (!(a < b) && ia > ib);
+        if (gt == ((i & k) == 0)) {
+          key[i] = b;
+          key[l] = a;
+          idx[i] = ib;
+          idx[l] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
 }
 
 template <bool INJ>
@@ -1111,39 +1181,61 @@ __global__ __launch_bounds__(kBS) void k_score_pruned64(
     double* __restrict__ out_x, tpe_best* __restrict__ partial) {
   __shared__ MixLds s_mix;
   __shared__ BestT red[kBS / kWave];
+  __shared__ double dred[kBS / kWave];
+  __shared__ double s_key[kP64N], s_x[kP64N];
+  __shared__ uint16_t s_idx[kP64N];
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * (kBS * kR64P);
+  const int64_t base = (int64_t)blockIdx.x * kP64N;
   if (base >= J.n_cand) {
     if (threadIdx.x == 0) *P = empty_best();
     return;
   }
+  const int n_here = (int)min((int64_t)kP64N, J.n_cand - base);
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const tpe_table Tb = tables[blockIdx.y];
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
   Mix M{};
   if (!INJ) M = stage_mix(SB, wcdf, mu, sigma, s_mix);
-  BestT b{0.0, -1, 0.0};
   for (int r = 0; r < kR64P; ++r) {
-    const int64_t li = base + r * kBS + threadIdx.x;
-    if (li >= J.n_cand) break;
-    double x;
-    if (INJ) {
-      x = cand[J.cand_off + li];
-    } else {
-      x = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
-      if (lgmm) x = exp(x);
+    const int i = r * kBS + threadIdx.x;
+    double x = 0.0, y = INFINITY;
+    if (i < n_here) {
+      const int64_t li = base + i;
+      if (INJ) {
+        x = cand[J.cand_off + li];
+      } else {
+        x = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+        if (lgmm) x = exp(x);
+      }
+      y = lgmm ? log(x) : x;
     }
-    const double y = lgmm ? log(x) : x;
-    double bl = lse64_pruned(SB, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below, Tb.lo,
-                             Tb.hi, y);
-    double al = lse64_pruned(SA, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above, Tb.lo,
-                             Tb.hi, y);
+    s_key[i] = y;
+    s_x[i] = x;
+    s_idx[i] = (uint16_t)i;
+  }
+  const double mb = lc_max(SB, coef64, dred), ma = lc_max(SA, coef64, dred);
+  __syncthreads();
+  sort_block(s_key, s_idx);
+  BestT b{0.0, -1, 0.0};
+  const int wid = threadIdx.x / kWave;
+  for (int r = 0; r < kR64P; ++r) {
+    const int p = (wid * kR64P + r) * kWave + lane_id();
+    const int i = s_idx[p];
+    const bool act = i < n_here;
+    const double y = s_key[p], x = s_x[i];
+    const bool inr = y >= Tb.lo && y <= Tb.hi;
+    double bl = lse64_pruned(SB, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below, mb, act,
+                             inr, y);
+    double al = lse64_pruned(SA, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above, ma, act,
+                             inr, y);
+    if (!act) continue;
     if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
       bl -= y;
       al -= y;
     }
+    const int64_t li = base + i;
     const int64_t o = J.out_off + li;
     if (out_bl) out_bl[o] = bl;
     if (out_al) out_al[o] = al;

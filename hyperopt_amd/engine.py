@@ -75,6 +75,40 @@ class LabelWork:
     n_total: int = 0
 
 
+class WorkBatch(object):
+    """The labels of many studies for one Engine.run, as columns -- the
+    batched-suggest fast path (tpe.suggest_many).  ``key`` names the
+    structure (hashable; equal keys must mean equal kinds, prior arguments,
+    candidate counts, history columns and slots, lattice ranges, in order),
+    the arrays carry the per-call values in work order, and ``materialize()``
+    returns the equivalent LabelWork list, used when the structure is new.
+    Requires ``histories``; Engine.run then returns a BatchResult."""
+    __slots__ = ("key", "n_below", "n_above", "keys", "cand_base", "materialize")
+
+    def __init__(self, key, n_below, n_above, keys, cand_base, materialize):
+        self.key = key
+        self.n_below = np.asarray(n_below, np.int64)
+        self.n_above = np.asarray(n_above, np.int64)
+        self.keys = np.asarray(keys, np.uint64)
+        self.cand_base = np.asarray(cand_base, np.int64)
+        self.materialize = materialize
+
+    def __len__(self):
+        return self.keys.size
+
+
+@dataclass
+class BatchResult:
+    """Engine.run's result for a WorkBatch: one entry per work, in work order."""
+    index: np.ndarray
+    value: np.ndarray
+    score: np.ndarray
+    n_scored: np.ndarray
+
+    def __len__(self):
+        return self.index.size
+
+
 @dataclass(slots=True)
 class LabelResult:
     label: str
@@ -315,18 +349,30 @@ class Engine:
             (g["col"], g["below"], g["dst_off"], g["offset"], g["count"], g["to_int"],
              g["hist"]) = (np.array(c) for c in zip(*gathers))
         return dict(cont=cont, quant=quant, cat=cat, fit_ids=fit_ids, params=params,
+                    fit_idx=np.asarray(fit_ids, np.int64), cat_idx=np.asarray(cat, np.int64),
+                    order_idx=np.asarray(order, np.int64),
                     segs=segs.copy(), csegs=csegs.copy(), p_pool=p_pool.copy(),
                     cat_meta=cat_meta, lat_ranges=lat_ranges, fallback=fallback, modes=modes,
                     groups=groups, order=order, g=g, jobs=jobs.copy(), fb_slice=fb_slice,
                     counts=(out_off, lat_off, qfb_off, sort_off, cnt_off, tbl_off))
 
-    def _plan_fast(self, P, works):
+    @staticmethod
+    def _columns(works):
+        """(n_below, n_above, keys, cand_base) per work of a history-mode list."""
+        n = len(works)
+        return (np.fromiter((np.size(w.obs_below) for w in works), np.int64, n),
+                np.fromiter((w.n_above for w in works), np.int64, n),
+                np.fromiter((int(w.key) & 0xFFFFFFFFFFFFFFFF for w in works), np.uint64, n),
+                np.fromiter((w.cand_base for w in works), np.int64, n))
+
+    def _plan_fast(self, P, nb, na):
         fit_ids, cat = P["fit_ids"], P["cat"]
         nf = len(fit_ids)
         segs = P["segs"].copy()
         sizes = np.empty(2 * nf, np.int64)
-        sizes[0::2] = [np.size(works[i].obs_below) for i in fit_ids]
-        sizes[1::2] = [works[i].n_above for i in fit_ids]
+        fi = P["fit_idx"]
+        sizes[0::2] = nb[fi]
+        sizes[1::2] = na[fi]
         ends = np.cumsum(sizes)
         obs_off = ends - sizes
         segs["obs_off"], segs["n_obs"] = obs_off, sizes
@@ -336,8 +382,9 @@ class Engine:
         max_obs = int(sizes.max()) if nf else 0
         csegs = P["csegs"].copy()
         csizes = np.empty(2 * len(cat), np.int64)
-        csizes[0::2] = [np.size(works[i].obs_below) for i in cat]
-        csizes[1::2] = [works[i].n_above for i in cat]
+        ci = P["cat_idx"]
+        csizes[0::2] = nb[ci]
+        csizes[1::2] = na[ci]
         cends = np.cumsum(csizes)
         coff = cends - csizes
         csegs["obs_off"], csegs["n_obs"] = coff, csizes
@@ -350,11 +397,11 @@ class Engine:
                 P["cat_meta"], cobs_off, P["lat_ranges"], P["fallback"], P["modes"],
                 P["groups"], P["order"], g_arr)
 
-    def _jobs_fast(self, P, works):
-        order = P["order"]
+    def _jobs_fast(self, P, keys, cand_base):
+        oi = P["order_idx"]
         jobs = P["jobs"].copy()
-        jobs["key"] = [int(works[i].key) & 0xFFFFFFFFFFFFFFFF for i in order]
-        jobs["cand_base"] = [works[i].cand_base for i in order]
+        jobs["key"] = keys[oi]
+        jobs["cand_base"] = cand_base[oi]
         a, b = P["fb_slice"]
         fb_jobs = jobs[a:b].copy()
         fb_jobs["out_off"] = fb_jobs["cand_off"]
@@ -426,15 +473,34 @@ class Engine:
         hist_mode = history is not None or histories is not None
         if table_scores:  # the fast table path's per-candidate scores (test hook)
             outputs = False
-        pkey = self._plan_key(works, prior_weight, lf, precision, scorer, outputs, sample_only,
-                              hist_mode, histories is not None)
-        cached = self._plans.get(pkey) if pkey is not None else None
+        batch = works if isinstance(works, WorkBatch) else None
+        if batch is not None:
+            if histories is None or outputs or sample_only or posteriors or table_scores:
+                raise ValueError("a WorkBatch runs with histories= and no output hooks")
+            pkey = ("batch", batch.key, float(prior_weight), int(lf), int(precision), scorer)
+            cached = self._plans.get(pkey)
+            if cached is None:
+                works = batch.materialize()
+                if len(works) != len(batch):
+                    raise ValueError("WorkBatch.materialize() gave %d works for %d rows"
+                                     % (len(works), len(batch)))
+            elif len(self._plans) > 64:
+                self._plans.clear()
+        else:
+            pkey = self._plan_key(works, prior_weight, lf, precision, scorer, outputs,
+                                  sample_only, hist_mode, histories is not None)
+            cached = self._plans.get(pkey) if pkey is not None else None
         pack = _Pack()
         if cached is not None:
+            cols = (batch.n_below, batch.n_above, batch.keys, batch.cand_base) \
+                if batch is not None else self._columns(works)
             (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp, max_obs,
              csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes, groups,
-             order, g_arr) = self._plan_fast(cached, works)
-            inj = lambda i: works[i].cand is not None  # noqa: E731
+             order, g_arr) = self._plan_fast(cached, cols[0], cols[1])
+            if batch is not None:
+                inj = lambda i: False  # noqa: E731
+            else:
+                inj = lambda i: works[i].cand is not None  # noqa: E731
         else:
             cont, quant, cat = [], [], []
             for i, w in enumerate(works):
@@ -574,7 +640,7 @@ class Engine:
             order = [i for _, ids in groups for i in ids]
         if cached is not None:
             (jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off, sort_off, cnt_off,
-             tbl_off) = self._jobs_fast(cached, works)
+             tbl_off) = self._jobs_fast(cached, cols[2], cols[3])
         else:
             nj_all = len(order)
             jobs = np.zeros(nj_all, L.JOB_DTYPE)
@@ -950,6 +1016,13 @@ class Engine:
             raise L.TpeHipError("history gather: observation counts do not match the "
                                 "segment sizes given by the host")
         _hmark('readback')
+        if batch is not None:
+            n = len(batch)
+            by = np.empty(n, L.BEST_DTYPE)
+            by[np.asarray(order, np.int64)] = best_h[:n]
+            _hmark("results")
+            return BatchResult(by["index"].copy(), by["value"].copy(), by["score"].copy(),
+                               by["n_scored"].copy())
         results = [None] * len(works)
         b_idx, b_val = best_h["index"].tolist(), best_h["value"].tolist()
         b_sc, b_ns = best_h["score"].tolist(), best_h["n_scored"].tolist()

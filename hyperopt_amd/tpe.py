@@ -27,6 +27,7 @@ all-gather + device max-loc (hyperopt_amd/dist.py).
 from __future__ import annotations
 
 import functools
+import itertools
 import logging
 import os
 import time
@@ -36,7 +37,7 @@ import numpy as np
 from . import dist as hdist
 from . import rand
 from .base import doc_loss
-from .engine import DEFAULT_LF, Engine, LabelWork
+from .engine import DEFAULT_LF, Engine, LabelWork, WorkBatch, _lattice_range, _params
 
 logger = logging.getLogger(__name__)
 
@@ -281,7 +282,7 @@ class LevelInputs(object):
         below_pos = np.flatnonzero(isb)
         crow = below_pos if hist.rows is None else hist.rows[below_pos]
         self.vb, self.ab = c.vals[crow], c.active[crow]
-        nb = self.ab.sum(0)
+        self.nb = nb = self.ab.sum(0)
         if T - below_pos.size == int(np.count_nonzero(isa)):  # every other row is above
             self.n_above = hist.label_counts() - nb
         else:
@@ -367,6 +368,128 @@ class SuggestRequest(object):
         self.kwargs = kwargs
 
 
+_SPACE_IDS = {}   # (label, kind, args) tuple of a space -> small int
+_LEVELS = {}      # (space id, level labels) -> _Level
+_LEVEL_IDS = itertools.count()  # never reused: level ids are part of engine plan keys
+
+
+def _space_sig(domain):
+    """Small int naming a space's (label, kind, prior arguments) list, cached
+    on the domain; None when a prior argument is unhashable."""
+    d = domain.__dict__
+    if "_tpe_space_id" not in d:
+        sig = tuple((lab, domain.specs[lab].kind, domain.specs[lab].args) for lab in domain.params)
+        try:
+            sid = _SPACE_IDS.get(sig)
+            if sid is None:
+                sid = _SPACE_IDS[sig] = len(_SPACE_IDS)
+        except TypeError:
+            sid = None
+        domain._tpe_space_id = sid
+    return d["_tpe_space_id"]
+
+
+class _Level(object):
+    """What a level of a space needs per call, computed once: label columns,
+    FNV hashes (label_keys without the per-label Python), and the unbounded
+    quantized labels whose lattice range follows the below set."""
+
+    def __init__(self, lid, domain, level):
+        self.id = lid
+        labels = list(domain.params)
+        self.js = np.array([labels.index(lab) for lab in level], np.int64)
+        self.h = np.fromiter((_label_hash(lab) for lab in level), np.uint64, len(level))
+        self.lat = []
+        for i, lab in enumerate(level):
+            spec = domain.specs[lab]
+            if spec.kind in ("qnormal", "qlognormal"):
+                self.lat.append((i, lab, spec))
+
+
+def _level_info(domain, level):
+    k = (_space_sig(domain), tuple(level))
+    lv = _LEVELS.get(k)
+    if lv is None:
+        if len(_LEVELS) > 4096:
+            _LEVELS.clear()
+        lv = _LEVELS[k] = _Level(next(_LEVEL_IDS), domain, level)
+    return lv
+
+
+def _run_columnar(eng, items, pw, lf, prec):
+    """One engine launch for a batch of studies' levels as a WorkBatch: the
+    per-label work is a few array operations per study (counts from the
+    LevelInputs, keys from cached hashes); LabelWork objects are only built
+    the first time a batch structure is seen.  Returns the winners' values
+    per item."""
+    hists, struct, nb, na, hh, ss, cb, sizes = [], [], [], [], [], [], [], []
+    for st, level in items:
+        obs = st["obs"]
+        rk = obs.run_kwargs
+        hists.append((rk["history"], rk["rows"], rk["is_below"]))
+        lv = _level_info(st["rq"].domain, level)
+        lat = ()
+        if lv.lat:
+            lat = tuple(_lattice_range(obs.work(lab, spec, int(lv.js[i])),
+                                       _params(spec.kind, spec.args)) for i, lab, spec in lv.lat)
+        struct.append((lv.id, st["count"], st["n_ei"], lat))
+        nb.append(obs.nb[lv.js])
+        na.append(obs.n_above[lv.js])
+        hh.append(lv.h)
+        ss.append(_mix64((int(st["rq"].seed) * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF))
+        cb.append(st["start"])
+        sizes.append(len(level))
+    sizes = np.asarray(sizes, np.int64)
+    with np.errstate(over="ignore"):
+        keys = _mix64_np(np.concatenate(hh) ^ np.repeat(np.asarray(ss, np.uint64), sizes))
+
+    def materialize():
+        out = []
+        for h, (st, level) in enumerate(items):
+            specs, col = st["rq"].domain.specs, st["col"]
+            for lab, k in zip(level, label_keys(st["rq"].seed, level)):
+                w = st["obs"].work(lab, specs[lab], col[lab], n_cand=st["count"], key=k,
+                                   cand_base=st["start"], n_total=st["n_ei"])
+                w.hist = h
+                out.append(w)
+        return out
+    batch = WorkBatch(tuple(struct), np.concatenate(nb), np.concatenate(na), keys,
+                      np.repeat(np.asarray(cb, np.int64), sizes), materialize)
+    res = eng.run(batch, prior_weight=pw, lf=lf, precision=prec, histories=hists)
+    vals = res.value.tolist()
+    out, a = [], 0
+    for n in sizes.tolist():
+        out.append(vals[a:a + n])
+        a += n
+    return out
+
+
+def _run_works(eng, items, pw, lf, prec, dev, combine):
+    """The general path: one LabelWork per label (host lists or histories),
+    winners combined across ranks when the candidates are sharded."""
+    works, kw_run, hists = [], {}, []
+    for h, (st, level) in enumerate(items):
+        specs, col = st["rq"].domain.specs, st["col"]
+        for lab, k in zip(level, label_keys(st["rq"].seed, level)):
+            w = st["obs"].work(lab, specs[lab], col[lab], n_cand=st["count"], key=k,
+                               cand_base=st["start"], n_total=st["n_ei"])
+            w.hist = h
+            works.append(w)
+        if dev:  # one history per study of the batch
+            rk = st["obs"].run_kwargs
+            hists.append((rk["history"], rk["rows"], rk["is_below"]))
+    if dev:
+        kw_run["histories"] = hists
+    res = eng.run(works, prior_weight=pw, lf=lf, precision=prec, **kw_run)
+    if combine:
+        hdist.allreduce_best(res)
+    out, a = [], 0
+    for _, level in items:
+        out.append([r.value for r in res[a:a + len(level)]])
+        a += len(level)
+    return out
+
+
 def suggest_many(requests, shard_studies=False):
     """Batched suggest over many independent studies.
 
@@ -408,8 +531,9 @@ def suggest_many(requests, shard_studies=False):
                            col={lab: j for j, lab in enumerate(labels)}, walk={}, stored={},
                            live=[], start=start, count=count, n_ei=n_ei, done=n_ei == 0,
                            prec=_precision(kw["precision"], n_ei, hist.tids.size)))
+    columnar = ws == 1 or shard_studies  # no cross-rank combine of the winners
     while True:
-        batches = {}  # (prior_weight, lf, precision, device) -> [(state, label, work)]
+        batches = {}  # (prior_weight, lf, precision, device) -> [(state, level)]
         for st in states:
             if st["done"]:
                 continue
@@ -421,32 +545,19 @@ def suggest_many(requests, shard_studies=False):
                 continue
             key = (st["kw"]["prior_weight"], st["kw"]["linear_forgetting"], st["prec"],
                    st["obs"].device)
-            for lab, k in zip(level, label_keys(st["rq"].seed, level)):
-                spec = st["rq"].domain.specs[lab]
-                j = st["col"][lab]
-                w = st["obs"].work(lab, spec, j, n_cand=st["count"], key=k,
-                                   cand_base=st["start"], n_total=st["n_ei"])
-                batches.setdefault(key, []).append((st, lab, w))
+            batches.setdefault(key, []).append((st, level))
         if not batches:
             break
         for (pw, lf, prec, dev), items in batches.items():
-            kw_run = {}
-            if dev:  # one history per study of the batch
-                slot, hists = {}, []
-                for st, _, w in items:
-                    h = slot.get(st["qi"])
-                    if h is None:
-                        h = slot[st["qi"]] = len(hists)
-                        rk = st["obs"].run_kwargs
-                        hists.append((rk["history"], rk["rows"], rk["is_below"]))
-                    w.hist = h
-                kw_run["histories"] = hists
-            res = eng.run([w for _, _, w in items], prior_weight=pw, lf=lf, precision=prec,
-                          **kw_run)
-            if ws > 1 and not shard_studies:
-                hdist.allreduce_best(res)
-            for (st, lab, _), r in zip(items, res):
-                st["walk"][lab], st["stored"][lab] = _decode(st["rq"].domain.specs[lab], r.value)
+            if dev and columnar and all(_space_sig(st["rq"].domain) is not None
+                                        for st, _ in items):
+                values = _run_columnar(eng, items, pw, lf, prec)
+            else:
+                values = _run_works(eng, items, pw, lf, prec, dev, ws > 1 and not shard_studies)
+            for (st, level), vals in zip(items, values):
+                specs, walk, stored = st["rq"].domain.specs, st["walk"], st["stored"]
+                for lab, v in zip(level, vals):
+                    walk[lab], stored[lab] = _decode(specs[lab], v)
     for st in states:
         rq, live = st["rq"], set(st["live"])
         tid = rq.new_ids[0]
