@@ -262,6 +262,8 @@ class Engine:
         self._plans = {}  # level structure -> static descriptor arrays (_plan_record)
         self._retired = []
         self._pinned = {}
+        self._res_pin = None   # pinned result block of a deferred (WorkBatch) run
+        self._inflight = None  # that run's _Pending until collected
         self.host_marks = None  # set to a list to record host-side phase times (diagnostic)
         # quantized / categorical scoring runs on a second stream, concurrently
         # with the cell-table path (the two share no buffers); TPE_SIDE_STREAM=0
@@ -412,7 +414,7 @@ class Engine:
             outputs=False, stream=None, timers=None, sample_only=False,
             pruned=True, scorer=None, posteriors=False, history=None, rows=None,
             is_below=None, histories=None, timer_groups=None,
-            table_scores=False) -> List[LabelResult]:
+            table_scores=False, defer=False) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``;
         ``timer_groups`` (optional set) limits them to those groups (each event
@@ -436,9 +438,16 @@ class Engine:
         gathered on the device (tpe_gather_obs) instead of being uploaded.
         ``histories``: a list of (DeviceHistory, rows or None, is_below) for
         batches of independent studies; each work names its history by
-        ``hist`` (one tpe_gather_obs_multi launch gathers every list)."""
+        ``hist`` (one tpe_gather_obs_multi launch gathers every list).
+        ``works`` may be a WorkBatch (with ``histories``): the result is a
+        BatchResult, and with ``defer`` a _Pending whose ``result()`` waits
+        for it -- the readback is queued behind the launches and the call
+        returns at once, so the host can prepare the next batch while this one
+        runs (the next run on this engine first collects it)."""
         if not works:
             return []
+        if self._inflight is not None:  # its pinned buffers are about to be reused
+            self._inflight.result()
         if sample_only:
             outputs = True
         if scorer is None:
@@ -446,7 +455,7 @@ class Engine:
         if scorer not in SCORERS:
             raise ValueError("scorer must be one of %s, got %r" % (SCORERS, scorer))
         torch = self.torch
-        self._retired.clear()  # every earlier run ended with a synchronising readback
+        self._retired.clear()  # every earlier run ended with a synchronising readback / collect
         hp = self.host_marks  # diagnostic: list of (name, perf_counter) or None
 
         def _hmark(name):
@@ -988,6 +997,19 @@ class Engine:
             ev.record(side)
             stream.wait_event(ev)
         _hmark('score launches')
+        if batch is not None:  # queued readback into pinned memory (see _Pending)
+            nbytes = 64 + n_jobs * BS
+            pin = self._res_pin
+            if pin is None or pin.numel() < nbytes:
+                pin = self._res_pin = torch.empty(_align(int(nbytes * 1.25)), dtype=torch.uint8,
+                                                  pin_memory=True)
+            with torch.cuda.stream(stream):
+                pin[:nbytes].copy_(self._bufs["stage"][o_res:o_res + nbytes], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            p = self._inflight = _Pending(self, ev, pin, nbytes, np.asarray(order, np.int64),
+                                          bool(table_calls))
+            return p if defer else p.result()
         # ---- results (one device->host copy; syncs the stream) --------------------
         with torch.cuda.stream(stream):
             res_h = self._bufs["stage"][o_res:o_res + 64 + n_jobs * BS].to("cpu").numpy()
@@ -1008,21 +1030,8 @@ class Engine:
             elif table_scores:
                 outs = [self._bufs[k][:8 * max(out_off, 1)].to("cpu").numpy().view(np.float64)
                         for k in ("out_sc", "out_x")]
-        if err & 1:
-            raise ValueError("negative arg to lognormal_cdf")  # tpe.py:196-197
-        if err & 2:
-            raise L.TpeHipError("lattice slot out of range (internal error)")
-        if err & 4:
-            raise L.TpeHipError("history gather: observation counts do not match the "
-                                "segment sizes given by the host")
+        _raise_errors(err)
         _hmark('readback')
-        if batch is not None:
-            n = len(batch)
-            by = np.empty(n, L.BEST_DTYPE)
-            by[np.asarray(order, np.int64)] = best_h[:n]
-            _hmark("results")
-            return BatchResult(by["index"].copy(), by["value"].copy(), by["score"].copy(),
-                               by["n_scored"].copy())
         results = [None] * len(works)
         b_idx, b_val = best_h["index"].tolist(), best_h["value"].tolist()
         b_sc, b_ns = best_h["score"].tolist(), best_h["n_scored"].tolist()
@@ -1078,6 +1087,51 @@ class Engine:
                 post[name] = host["p"][a:a + n].copy()
             results[i].extra = post
         return results
+
+
+class _Pending(object):
+    """A WorkBatch run whose result block is being copied back (Engine.run
+    with defer=True).  ``result()`` waits for it once, checks the error bits
+    and returns the BatchResult (cached)."""
+
+    def __init__(self, eng, event, pin, nbytes, order, table):
+        self.eng, self.event, self.pin, self.nbytes = eng, event, pin, nbytes
+        self.order, self.table = order, table
+        self._res = None
+
+    def result(self):
+        if self._res is not None:
+            return self._res
+        self.event.synchronize()
+        eng = self.eng
+        if eng._inflight is self:
+            eng._inflight = None
+        res_h = self.pin[:self.nbytes].numpy().copy()
+        err = int(res_h[:4].view(np.int32)[0])
+        eng.last_pairs = None
+        eng.last_table_stats = None
+        if self.table:
+            st = res_h[16:40].view(np.int64).tolist()
+            eng.last_table_stats = {"exact_candidates": st[0], "failed_cells": st[1],
+                                    "failed_score_cells": st[2]}
+        _raise_errors(err)
+        best_h = res_h[64:].view(L.BEST_DTYPE)
+        n = self.order.size
+        by = np.empty(n, L.BEST_DTYPE)
+        by[self.order] = best_h[:n]
+        self._res = BatchResult(by["index"].copy(), by["value"].copy(), by["score"].copy(),
+                                by["n_scored"].copy())
+        return self._res
+
+
+def _raise_errors(err):
+    if err & 1:
+        raise ValueError("negative arg to lognormal_cdf")  # tpe.py:196-197
+    if err & 2:
+        raise L.TpeHipError("lattice slot out of range (internal error)")
+    if err & 4:
+        raise L.TpeHipError("history gather: observation counts do not match the "
+                            "segment sizes given by the host")
 
 
 def _slice_of(groups, g):

@@ -50,15 +50,19 @@ _default_linear_forgetting = DEFAULT_LF
 
 _engines = {}
 USE_DEVICE_HISTORY = True  # gather observation lists from the HBM mirror (LevelInputs)
+SUGGEST_MANY_CHUNKS = 4       # suggest_many: studies per launch = max(MIN_CHUNK, n / CHUNKS)
+SUGGEST_MANY_MIN_CHUNK = 64   # (env HYPEROPT_AMD_CHUNK overrides)
 
 
-def engine():
-    """The Engine of the current device (created on first use)."""
+def engine(slot=0):
+    """The Engine of the current device (created on first use); ``slot`` 1 is a
+    second engine with its own buffers, which suggest_many alternates with the
+    first so one batch can run while the next is prepared."""
     import torch
     dev = torch.cuda.current_device()
-    eng = _engines.get(dev)
+    eng = _engines.get((dev, slot))
     if eng is None:
-        eng = _engines[dev] = Engine(torch.device("cuda", dev))
+        eng = _engines[(dev, slot)] = Engine(torch.device("cuda", dev))
     return eng
 
 
@@ -416,7 +420,7 @@ def _level_info(domain, level):
     return lv
 
 
-def _run_columnar(eng, items, pw, lf, prec):
+def _run_columnar(eng, items, pw, lf, prec, defer=False):
     """One engine launch for a batch of studies' levels as a WorkBatch: the
     per-label work is a few array operations per study (counts from the
     LevelInputs, keys from cached hashes); LabelWork objects are only built
@@ -455,7 +459,9 @@ def _run_columnar(eng, items, pw, lf, prec):
         return out
     batch = WorkBatch(tuple(struct), np.concatenate(nb), np.concatenate(na), keys,
                       np.repeat(np.asarray(cb, np.int64), sizes), materialize)
-    res = eng.run(batch, prior_weight=pw, lf=lf, precision=prec, histories=hists)
+    res = eng.run(batch, prior_weight=pw, lf=lf, precision=prec, histories=hists, defer=defer)
+    if defer:
+        return res
     vals = res.value.tolist()
     out, a = [], 0
     for n in sizes.tolist():
@@ -507,11 +513,16 @@ def suggest_many(requests, shard_studies=False):
     """
     rank, ws = hdist.world()
     out = [None] * len(requests)
+    todo = [(qi, rq) for qi, rq in enumerate(requests)
+            if not (shard_studies and ws > 1 and qi % ws != rank)]
+    columnar = ws == 1 or shard_studies  # no cross-rank combine of the winners
+    chunk = int(os.environ.get("HYPEROPT_AMD_CHUNK", "0")) or \
+        max(SUGGEST_MANY_MIN_CHUNK, -(-len(todo) // SUGGEST_MANY_CHUNKS))
     states = []
-    eng = None
-    for qi, rq in enumerate(requests):
-        if shard_studies and ws > 1 and qi % ws != rank:
-            continue
+    pend = []  # launched batches not yet decoded: (items, values or _Pending)
+    turn = itertools.count()
+
+    def make_state(qi, rq):
         kw = dict(prior_weight=_default_prior_weight, n_startup_jobs=_default_n_startup_jobs,
                   n_EI_candidates=_default_n_EI_candidates, gamma=_default_gamma,
                   linear_forgetting=_default_linear_forgetting, precision=None)
@@ -520,44 +531,71 @@ def suggest_many(requests, shard_studies=False):
         hist = collect_history(rq.trials, labels)
         if hist.tids.size < kw["n_startup_jobs"]:
             out[qi] = rand.suggest_device(rq.new_ids, rq.domain, rq.trials, rq.seed)
-            continue
+            return None
         isb, isa = split_masks(hist, kw["gamma"])
         n_ei = max(int(kw["n_EI_candidates"]), 0)
         start, count = (0, n_ei) if (shard_studies or ws == 1) else hdist.shard(n_ei, rank, ws)
-        if eng is None and n_ei > 0:
-            eng = engine()
-        states.append(dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist,
-                           obs=LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY),
-                           col={lab: j for j, lab in enumerate(labels)}, walk={}, stored={},
-                           live=[], start=start, count=count, n_ei=n_ei, done=n_ei == 0,
-                           prec=_precision(kw["precision"], n_ei, hist.tids.size)))
-    columnar = ws == 1 or shard_studies  # no cross-rank combine of the winners
+        return dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist,
+                    obs=LevelInputs(hist, isb, isa, engine() if n_ei > 0 else None,
+                                    device=USE_DEVICE_HISTORY),
+                    col={lab: j for j, lab in enumerate(labels)}, walk={}, stored={},
+                    live=[], start=start, count=count, n_ei=n_ei, done=n_ei == 0,
+                    prec=_precision(kw["precision"], n_ei, hist.tids.size))
+
+    def finish(items, values):
+        if not isinstance(values, list):
+            r = values.result().value.tolist()
+            values, a = [], 0
+            for _, level in items:
+                values.append(r[a:a + len(level)])
+                a += len(level)
+        for (st, level), vals in zip(items, values):
+            specs, walk, stored = st["rq"].domain.specs, st["walk"], st["stored"]
+            for lab, v in zip(level, vals):
+                walk[lab], stored[lab] = _decode(specs[lab], v)
+
+    # Level by level; within a level the studies go in chunks, each chunk's
+    # batches launched without waiting (Engine.run defer=True, two engines
+    # taking turns), so the host prepares chunk c+1 while chunk c runs.
+    first = True
     while True:
-        batches = {}  # (prior_weight, lf, precision, device) -> [(state, level)]
-        for st in states:
-            if st["done"]:
-                continue
-            live = st["rq"].domain.reachable(st["walk"])
-            st["live"] = live
-            level = [lab for lab in live if lab not in st["walk"]]
-            if not level:
-                st["done"] = True
-                continue
-            key = (st["kw"]["prior_weight"], st["kw"]["linear_forgetting"], st["prec"],
-                   st["obs"].device)
-            batches.setdefault(key, []).append((st, level))
-        if not batches:
+        src = todo if first else [st for st in states if not st["done"]]
+        if not src:
             break
-        for (pw, lf, prec, dev), items in batches.items():
-            if dev and columnar and all(_space_sig(st["rq"].domain) is not None
-                                        for st, _ in items):
-                values = _run_columnar(eng, items, pw, lf, prec)
+        for c0 in range(0, len(src), chunk):
+            if first:
+                sts = [st for st in (make_state(qi, rq) for qi, rq in src[c0:c0 + chunk])
+                       if st is not None]
+                states.extend(sts)
             else:
-                values = _run_works(eng, items, pw, lf, prec, dev, ws > 1 and not shard_studies)
-            for (st, level), vals in zip(items, values):
-                specs, walk, stored = st["rq"].domain.specs, st["walk"], st["stored"]
-                for lab, v in zip(level, vals):
-                    walk[lab], stored[lab] = _decode(specs[lab], v)
+                sts = src[c0:c0 + chunk]
+            batches = {}  # (prior_weight, lf, precision, device) -> [(state, level)]
+            for st in sts:
+                if st["done"]:
+                    continue
+                live = st["rq"].domain.reachable(st["walk"])
+                st["live"] = live
+                level = [lab for lab in live if lab not in st["walk"]]
+                if not level:
+                    st["done"] = True
+                    continue
+                key = (st["kw"]["prior_weight"], st["kw"]["linear_forgetting"], st["prec"],
+                       st["obs"].device)
+                batches.setdefault(key, []).append((st, level))
+            for (pw, lf, prec, dev), items in batches.items():
+                if dev and columnar and all(_space_sig(st["rq"].domain) is not None
+                                            for st, _ in items):
+                    eng = engine(next(turn) % 2)
+                    values = _run_columnar(eng, items, pw, lf, prec, defer=True)
+                else:
+                    values = _run_works(engine(), items, pw, lf, prec, dev,
+                                        ws > 1 and not shard_studies)
+                pend.append((items, values))
+                while len(pend) > 1:
+                    finish(*pend.pop(0))
+        while pend:
+            finish(*pend.pop(0))
+        first = False
     for st in states:
         rq, live = st["rq"], set(st["live"])
         tid = rq.new_ids[0]

@@ -86,3 +86,30 @@ def test_c4_study_vs_oracle_on_injected(studies, s):
                                            err_msg=w.label)
         s_ref = ref["below_llik"] - ref["above_llik"]
         assert r.index == int(np.argmax(s_ref)), (w.label, r.index, int(np.argmax(s_ref)))
+
+
+@pytest.mark.parametrize("chunk", ["3", "0"])
+def test_suggest_many_chunked_mixed_spaces(monkeypatch, chunk):
+    """Pipelined chunks (two engines, deferred readback) over studies of
+    different spaces -- nested choices (several levels), a 50-dim mixed space,
+    the README space -- one of them still in its startup phase: each study's
+    suggestion equals its own tpe.suggest."""
+    from hyperopt_amd import hp, tpe
+    from hyperopt_amd.base import Domain
+    from tests.golden import spaces
+    from tools import scale_configs as S
+    monkeypatch.setenv("HYPEROPT_AMD_CHUNK", chunk)
+    makers = [spaces.nested, spaces.mixed_50d, spaces.readme, spaces.many_dists]
+    doms, trs = [], []
+    for s in range(11):
+        d = Domain(lambda p: 0.0, makers[s % len(makers)](hp))
+        doms.append(d)
+        trs.append(S.prior_trials(d, 10 if s == 5 else 300 + 37 * s, s))
+    reqs = [tpe.SuggestRequest([10_000 + s], d, t, 77 + s,
+                               n_EI_candidates=512)
+            for s, (d, t) in enumerate(zip(doms, trs))]
+    many = tpe.suggest_many(reqs)
+    for s, (rq, m) in enumerate(zip(reqs, many)):
+        one = tpe.suggest(rq.new_ids, rq.domain, rq.trials, rq.seed, n_EI_candidates=512,
+                          verbose=False)
+        assert m[0]["misc"]["vals"] == one[0]["misc"]["vals"], s
