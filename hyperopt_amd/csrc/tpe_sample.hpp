@@ -56,8 +56,9 @@ struct MixLds {  // LDS image of a below mixture of <= kStage components
 // Entry gd[b] = {thr[g], g | step << 8 | multi << 9}: step = (g < n-1), and
 // the component is g + step * (w >= thr[g]) unless a second threshold falls
 // inside the bucket (multi), where the walk over thr[] finishes the search.
-// cw[k] also carries component k's word interval [thr[k-1], thr[k]) so the
-// fp32 sampler can read the word's position inside it (comp_res).
+// cw[k] also carries the end thr[k] and inverse width of component k's word
+// interval [thr[k-1], thr[k]) so the fp32 sampler can read the word's
+// position inside it (comp_res).
 __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, const double* mu,
                                          const double* sigma, MixLds& L) {
   const int n = S.n_obs + 1;
@@ -88,7 +89,7 @@ __device__ __forceinline__ Mix stage_mix(const tpe_seg& S, const double* wcdf, c
   }
   for (int k = threadIdx.x; k < n; k += kBS) {
     const uint32_t lo = k ? L.thr[k - 1] : 0u, width = L.thr[k] - lo;
-    L.cw[k] = make_float4((float)L.mu[k], (float)L.sg[k], __uint_as_float(lo),
+    L.cw[k] = make_float4((float)L.mu[k], (float)L.sg[k], __uint_as_float(L.thr[k]),
                           width ? 1.0f / (float)width : 0.0f);
   }
   __syncthreads();
@@ -122,10 +123,10 @@ __device__ __forceinline__ double draw64(const Mix& M, uint64_t key, int64_t g, 
 // residuals of words 0 / 1 give radius / angle of the pair (4m, 4m+1) (cos ->
 // 4m, sin -> 4m+1), words 2 / 3 those of (4m+2, 4m+3).  Four candidates per
 // call, so the sampler spends half as many Philox rounds (quarter-rate
-// v_mad_u64_u32) per candidate as a pair-per-call scheme.  Retries (attempt
-// a >= 1, bounded labels) take one call per candidate at counter (g, a) in a
-// stream of their own.  Candidate g's value depends on g alone, whichever
-// kernel draws it.
+// v_mad_u64_u32) per candidate as a pair-per-call scheme.  Retries (bounded
+// labels) take four attempts per call at counter (g, c) in a stream of their
+// own (retry32).  Candidate g's value depends on g alone, whichever kernel
+// draws it.
 __device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
   if (M.thr) {  // block-uniform: staged mixture, one guide entry (+ rare walk)
     const uint2 e = M.gd[word >> 24];
@@ -138,43 +139,51 @@ __device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
   return upper_bound(M.cdf, M.n, u);
 }
 
-// component (mu, sigma) of `word` and the word's residual uniform in [0, 1)
-// (clamped below 1, so 1 - res >= 2^-24 and a Box-Muller radius stays < 5.77)
+// component (mu, sigma) of `word` and the word's upper residual t in (0, 1]:
+// the distance from the word to the top of its component's interval, over the
+// interval's width -- uniform on the interval's grid whatever the component,
+// and never 0, so Box-Muller takes log(t) directly (no 1 - u, no clamp).
+// The staged test is per word on purpose: splitting the samplers into staged
+// and global instantiations lets the scheduler hoist the four words' LDS
+// reads and costs ~35 VGPRs, which lost more (occupancy) than the branches.
 __device__ __forceinline__ void comp_res(const Mix& M, uint32_t word, float& mu, float& sg,
                                          float& res) {
 #ifdef TPE_DIAG_NO_COMP  // diagnostic builds only (tools/diag_variants.sh)
   const float4 c = M.cw ? M.cw[word & 7] : make_float4(0.0f, 1.0f, 0.0f, 0x1.0p-32f);
   mu = c.x;
   sg = c.y;
-  res = (float)word * 0x1.0p-32f;
+  res = (float)(~word) * 0x1.0p-32f + 0x1.0p-32f;
 #else
   if (M.cw) {
     const float4 c = M.cw[comp_of(M, word)];
     mu = c.x;
     sg = c.y;
-    res = (float)(word - __float_as_uint(c.z)) * c.w;
+    res = (float)(__float_as_uint(c.z) - word) * c.w;  // c.z: the interval's end
   } else {
     const double total = M.cdf[M.n - 1];
     const double u = (double)word * 0x1.0p-32 * total;
     const int k = upper_bound(M.cdf, M.n, u);
     const double lo = k ? M.cdf[k - 1] : 0.0, wk = M.cdf[k] - lo;
-    res = wk > 0.0 ? (float)((u - lo) / wk) : 0.0f;
+    res = wk > 0.0 ? (float)((M.cdf[k] - u) / wk) : 1.0f;
     mu = (float)M.mu[k];
     sg = (float)M.sg[k];
   }
 #endif
-  res = fminf(res, 0x1.fffffep-1f);
 }
 
-// Box-Muller pair from two residual uniforms: radius from ra, angle from rb
-__device__ __forceinline__ void bm_pair(float ra, float rb, float& z0, float& z1) {
+// Box-Muller pair from two upper residuals: radius from ta (clamped to
+// >= 2^-24, so the radius stays < 5.77), angle from tb (in turns)
+__device__ __forceinline__ void bm_pair(float ta, float tb, float& z0, float& z1) {
 #ifdef TPE_DIAG_NO_BM
-  z0 = ra - 0.5f;
-  z1 = rb - 0.5f;
+  z0 = ta - 0.5f;
+  z1 = tb - 0.5f;
 #else
-  const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(1.0f - ra));
-  z0 = r * __builtin_amdgcn_cosf(rb);
-  z1 = r * __builtin_amdgcn_sinf(rb);
+  // v_sqrt_f32 (1 ulp) without the correctly-rounded expansion: the argument
+  // is 0 or a normal number in [2.4e-7, 33.3]
+  const float r =
+      __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(fmaxf(ta, 0x1.0p-24f)));
+  z0 = r * __builtin_amdgcn_cosf(tb);
+  z1 = r * __builtin_amdgcn_sinf(tb);
 #endif
 }
 
@@ -217,17 +226,6 @@ __device__ __forceinline__ float attempt32_first(const Mix& M, uint64_t key, int
   return second ? fmaf(sgb, z1, mub) : fmaf(sga, z0, mua);
 }
 
-// attempt a >= 1 of candidate g: one Philox call of the retry stream
-__device__ __forceinline__ float attempt32_retry(const Mix& M, uint64_t key, int64_t g,
-                                                 uint32_t a) {
-  const U4 r = draw_words(key, g, a, kStreamRetry);
-  float mu, sg, res;
-  comp_res(M, r.x, mu, sg, res);
-  float z0, z1;
-  bm_pair(u01_f32(r.y), u01_f32(r.z), z0, z1);
-  return fmaf(sg, z0, mu);
-}
-
 __device__ __forceinline__ bool accept32(float y, bool lo_on, bool hi_on, float lo, float hi) {
   return (!lo_on || lo <= y) && (!hi_on || y < hi);
 }
@@ -239,15 +237,44 @@ __device__ __forceinline__ float clamp32(float y, bool lo_on, bool hi_on, float 
   return y;
 }
 
-__device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, bool lo_on,
-                                        bool hi_on, float lo, float hi) {
-  float y = attempt32_first(M, key, g);
-  if (accept32(y, lo_on, hi_on, lo, hi)) return y;
-  for (uint32_t a = 1; a < kMaxAttempts; ++a) {
-    y = attempt32_retry(M, key, g, a);
-    if (accept32(y, lo_on, hi_on, lo, hi)) return y;
+// Retries of candidate g (bounded labels, attempt 0 rejected): call c >= 1
+// of the retry stream, at counter (g, c), gives attempts 4c-3 .. 4c the way a
+// quad gives attempt 0 of four candidates (each word a component and a
+// residual, the residual pairs Box-Muller); the first accepted one is the
+// draw.  Four attempts per call: at C3's ~7% rejection a rejected candidate
+// almost never needs a second call, so a wave's retry pass is one call deep
+// instead of the longest of its lanes' geometric runs.  After kMaxRetryCalls
+// calls (acceptance below ~1e-77) the last attempt is clamped.
+constexpr uint32_t kMaxRetryCalls = kMaxAttempts / 4;
+
+__device__ __forceinline__ float retry32(const Mix& M, uint64_t key, int64_t g, bool lo_on,
+                                         bool hi_on, float lo, float hi) {
+  float y = 0.0f;
+  for (uint32_t c = 1; c <= kMaxRetryCalls; ++c) {
+    const U4 r = draw_words(key, g, c, kStreamRetry);
+    float mu0, sg0, r0, mu1, sg1, r1, mu2, sg2, r2, mu3, sg3, r3;
+    comp_res(M, r.x, mu0, sg0, r0);
+    comp_res(M, r.y, mu1, sg1, r1);
+    comp_res(M, r.z, mu2, sg2, r2);
+    comp_res(M, r.w, mu3, sg3, r3);
+    float z0, z1, z2, z3;
+    bm_pair(r0, r1, z0, z1);
+    bm_pair(r2, r3, z2, z3);
+    const float y0 = fmaf(sg0, z0, mu0), y1 = fmaf(sg1, z1, mu1);
+    const float y2 = fmaf(sg2, z2, mu2), y3 = fmaf(sg3, z3, mu3);
+    const bool a0 = accept32(y0, lo_on, hi_on, lo, hi), a1 = accept32(y1, lo_on, hi_on, lo, hi);
+    const bool a2 = accept32(y2, lo_on, hi_on, lo, hi);
+    y = a0 ? y0 : (a1 ? y1 : (a2 ? y2 : y3));
+    if (a0 || a1 || a2 || accept32(y3, lo_on, hi_on, lo, hi)) return y;
   }
   return clamp32(y, lo_on, hi_on, lo, hi);
+}
+
+__device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, bool lo_on,
+                                        bool hi_on, float lo, float hi) {
+  const float y = attempt32_first(M, key, g);
+  if (accept32(y, lo_on, hi_on, lo, hi)) return y;
+  return retry32(M, key, g, lo_on, hi_on, lo, hi);
 }
 
 // R consecutive candidates g0 .. g0+R-1 per thread, n of them valid, each
@@ -258,13 +285,13 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
 // g0 is cand_base + a multiple of R, so the test is job-uniform) draws
 // attempt 0 one candidate at a time in a rolled loop through `wstage`, which
 // keeps the register footprint of the aligned loop.
-// Bounded labels then retry their rejected candidates (attempts 1, 2, ... of
-// the retry stream, as draw32).  ~7% of C3's bounded draws are rejected, so a
-// wave holds ~70 of them but its busiest lane ~4: the wave's rejections are
-// listed in `wlist` (kRetryList entries per wave, a prefix sum of the lanes'
-// counts places them) and worked off 64 at a time, one per lane, so the wave
-// waits ~2 retry steps instead of its busiest lane's ~4; rejections past the
-// list (a rare wave) retry in their own lane.  Retried values come back
+// Bounded labels then retry their rejected candidates (retry32, as draw32).
+// ~7% of C3's bounded draws are rejected, so a wave holds ~70 of them but its
+// busiest lane ~4: the wave's rejections are listed in `wlist` (kRetryList
+// entries per wave, a prefix sum of the lanes' counts places them) and worked
+// off 64 at a time, one per lane, so the wave waits ~2 retry calls instead of
+// its busiest lane's ~4; rejections past the list (a rare wave) retry in
+// their own lane.  Retried values come back
 // through `wstage`, the wave's R*64 floats of LDS (slot r of lane l at
 // r*64 + l).
 constexpr int kRetryList = 256;  // listed rejections per wave (uint16 entries)
@@ -299,11 +326,7 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
   rej = 0;
 #endif
   auto retry = [&](int64_t g) __attribute__((always_inline)) -> float {
-    for (uint32_t a = 1;; ++a) {
-      const float y = attempt32_retry(M, key, g, a);
-      if (accept32(y, lo_on, hi_on, lo, hi)) return y;
-      if (a + 1 >= kMaxAttempts) return clamp32(y, lo_on, hi_on, lo, hi);
-    }
+    return retry32(M, key, g, lo_on, hi_on, lo, hi);
   };
   if (__any(rej != 0)) {
     // list the wave's rejections: exclusive prefix of the lanes' counts

@@ -37,7 +37,10 @@ constexpr int kR32 = 8;
 constexpr int kR64 = 4;
 constexpr int kTile32 = 1024;  // float4 components per tile (16 KB)
 constexpr int kTile64 = 512;   // double4 components per tile (16 KB)
-constexpr int kLatR = 16;      // lattice sampler: candidates per thread
+#ifndef TPE_LATR
+#define TPE_LATR 16
+#endif
+constexpr int kLatR = TPE_LATR;  // lattice sampler: candidates per thread
 constexpr int kLatLds = 4096;  // lattice slots deduplicated in LDS per block
 constexpr float kFastFloor = -100.0f;            // log2 units below the mixture max
 constexpr float kLn2f = 0.6931471805599453f;
@@ -884,6 +887,9 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   // blocks run roughly in index order, so the global slot mostly holds a
   // smaller index already: an agent-scope load first keeps the (cross-XCD)
   // atomics to the blocks that improve a slot
+#ifdef TPE_DIAG_NO_FLUSH  // diagnostic builds only: block results dropped
+  if (n_loc > 0x7FFFFFF0)
+#endif
   for (int s = threadIdx.x; s < n_loc; s += kBS) {
     const uint32_t f = lfirst[s];
     if (f == 0xFFFFFFFFu) continue;

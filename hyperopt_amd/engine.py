@@ -358,6 +358,15 @@ class Engine:
                     groups=groups, order=order, g=g, jobs=jobs.copy(), fb_slice=fb_slice,
                     counts=(out_off, lat_off, qfb_off, sort_off, cnt_off, tbl_off))
 
+    def _big64(self, precision, n_above):
+        """The per-call input of the scorer choice that a plan records: at fp64,
+        which labels' above mixtures reach PRUNED64_MIN_COMP (pruned vs dense
+        exact scorer) -- part of the plan key, so a cached plan never scores a
+        label with the other kernel than an uncached run would."""
+        if precision == 32 or self.exact64 != "auto":
+            return self.exact64
+        return np.packbits(np.asarray(n_above) >= PRUNED64_MIN_COMP).tobytes()
+
     @staticmethod
     def _columns(works):
         """(n_below, n_above, keys, cand_base) per work of a history-mode list."""
@@ -486,7 +495,8 @@ class Engine:
         if batch is not None:
             if histories is None or outputs or sample_only or posteriors or table_scores:
                 raise ValueError("a WorkBatch runs with histories= and no output hooks")
-            pkey = ("batch", batch.key, float(prior_weight), int(lf), int(precision), scorer)
+            pkey = ("batch", batch.key, float(prior_weight), int(lf), int(precision), scorer,
+                    self._big64(precision, batch.n_above))
             cached = self._plans.get(pkey)
             if cached is None:
                 works = batch.materialize()
@@ -498,6 +508,10 @@ class Engine:
         else:
             pkey = self._plan_key(works, prior_weight, lf, precision, scorer, outputs,
                                   sample_only, hist_mode, histories is not None)
+            if pkey is not None:
+                pkey += (self._big64(precision, np.fromiter(
+                    (w.n_above if w.obs_above is None else np.size(w.obs_above) for w in works),
+                    np.int64, len(works))),)
             cached = self._plans.get(pkey) if pkey is not None else None
         pack = _Pack()
         if cached is not None:

@@ -65,3 +65,24 @@ def test_pruned_equals_dense_sampled(engine, kind, args):
     np.testing.assert_allclose(p.below_llik, d.below_llik, rtol=1e-13, atol=1e-13)
     np.testing.assert_allclose(p.above_llik, d.above_llik, rtol=1e-13, atol=1e-13)
     assert (p.index, p.value, p.n_scored) == (d.index, d.value, d.n_scored)
+
+
+def test_plan_cache_follows_scorer_choice():
+    """A plan recorded while a label's above mixture was small (dense exact
+    scorer) is not reused once it reaches PRUNED64_MIN_COMP: the cached run
+    equals an uncached run (history mode caches plans, upload mode does not)."""
+    from hyperopt_amd.engine import PRUNED64_MIN_COMP, DeviceHistory, Engine
+    from tests import test_gpu_history as H
+    eng = Engine()
+    for T in (40, 3000):
+        assert (T - 2 >= PRUNED64_MIN_COMP) == (T == 3000)
+        mat, active, losses = H._history(T, T, 0.0)
+        rows = np.arange(T)
+        up, _ = H._works(mat, active, losses, rows)
+        hist = DeviceHistory(eng, len(H.SPACE), cap=64)
+        hist.append(mat, active)
+        hw, isb = H._works(mat, active, losses, rows, hist=hist)
+        r_up = eng.run(up, precision=64)
+        r_h = eng.run(hw, precision=64, history=hist, is_below=isb)
+        for a, b in zip(r_up, r_h):
+            assert (a.index, a.value, a.score) == (b.index, b.value, b.score), (T, a, b)
