@@ -102,15 +102,13 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
   auto fold = [&]() {
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
-      // 16 reads in flight per batch: the chain of adds, not LDS latency,
-      // sets the pace
       int j = 0;
-      for (; j + 16 <= filled; j += 16) {
-        double v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = list[j + u];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) cnt = __dadd_rn(cnt, v[u]);
+      for (; j + 4 <= filled; j += 4) {
+        const double a = list[j], b = list[j + 1], c = list[j + 2], d = list[j + 3];
+        cnt = __dadd_rn(cnt, a);
+        cnt = __dadd_rn(cnt, b);
+        cnt = __dadd_rn(cnt, c);
+        cnt = __dadd_rn(cnt, d);
       }
       for (; j < filled; ++j) cnt = __dadd_rn(cnt, list[j]);
     }

@@ -99,39 +99,21 @@ __device__ __forceinline__ int count_le(const uint64_t* a, int n, uint64_t key) 
   return lo;
 }
 
-// K1: transform + tile sort.  Bitonic over the 2048 (key, index) pairs of a
-// tile with the pairs in registers: element i = 8 t + r of thread t.  Stages
-// with j < 8 exchange inside a thread, 8 <= j < 512 across the lanes of a wave
-// (__shfl_xor by j / 8), and only the three stages with j >= 512 go through
-// LDS -- one block per tile runs latency-bound (few waves per CU), so the
-// barrier-per-stage LDS network it replaces spent ~50 us per tile waiting.
-constexpr int kSortPer = kSortTile / kFitBS;  // elements per thread (8)
-
-__device__ __forceinline__ bool key_gt(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
-  return (ka > kb) || (ka == kb && ia > ib);
-}
-
+// K1: transform + tile sort
 __global__ __launch_bounds__(kFitBS) void k_fit_tilesort(const double* __restrict__ obs,
                                                          const tpe_seg* __restrict__ segs,
                                                          FitScratch sc) {
-  static_assert(kSortPer == 8 && kSortTile == 2048, "8 elements per thread, 2048 per tile");
   __shared__ uint64_t skey[kSortTile];
-  __shared__ uint32_t sidx[kSortTile];
+  __shared__ uint16_t sidx[kSortTile];
   const tpe_seg& S = segs[blockIdx.y];
   const int n = S.n_obs;
   const int t0 = blockIdx.x * kSortTile;
   if (t0 >= n) return;  // block-uniform
   const int m = min(kSortTile, n - t0);
+  int N = 2;
+  while (N < m) N <<= 1;
   const int64_t ooff = S.obs_off;
-  const int tid = threadIdx.x;
-  uint64_t K[kSortPer];
-  uint32_t I[kSortPer];
-  // coalesced load (element e = it * 256 + tid), transform, then through LDS
-  // into the blocked register layout (element 8 t + r)
-#pragma unroll
-  for (int it = 0; it < kSortPer; ++it) {
-    const int e = it * kFitBS + tid;
-    uint64_t key = ~0ull;
+  for (int e = threadIdx.x; e < N; e += kFitBS) {
     if (e < m) {
       double v = obs[ooff + t0 + e];
       if (S.transform == TPE_OBS_LOG) {
@@ -140,117 +122,36 @@ __global__ __launch_bounds__(kFitBS) void k_fit_tilesort(const double* __restric
         v = log(v);
       }
       sc.xf[ooff + t0 + e] = v;
-      key = order_key(v);
+      skey[e] = order_key(v);
+      sidx[e] = (uint16_t)e;
+    } else {
+      skey[e] = ~0ull;
+      sidx[e] = 0xFFFF;
     }
-    skey[e] = key;
   }
   __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kSortPer; ++r) {
-    K[r] = skey[kSortPer * tid + r];
-    I[r] = (uint32_t)(kSortPer * tid + r);
-  }
-  for (int k = 2; k <= kSortTile; k <<= 1) {
+  for (int k = 2; k <= N; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j < kSortPer) {  // inside the thread
-#pragma unroll
-        for (int r = 0; r < kSortPer; ++r) {
-          if (r & j) continue;
-          const int i = kSortPer * tid + r;
-          const bool up = (i & k) == 0;
-          const int l = r | j;
-          if (key_gt(K[r], I[r], K[l], I[l]) == up) {
-            const uint64_t tk = K[r];
-            K[r] = K[l];
-            K[l] = tk;
-            const uint32_t ti = I[r];
-            I[r] = I[l];
-            I[l] = ti;
-          }
-        }
-      } else if (j < kSortPer * kWave) {  // across the lanes of the wave
-        const int lm = j / kSortPer;
-        const bool lower = (tid & lm) == 0;
-#pragma unroll
-        for (int r = 0; r < kSortPer; ++r) {
-          const int i = kSortPer * tid + r;
-          const bool up = (i & k) == 0;
-          const uint32_t klo = __shfl_xor((uint32_t)K[r], lm, kWave);
-          const uint32_t khi = __shfl_xor((uint32_t)(K[r] >> 32), lm, kWave);
-          const uint64_t ko = ((uint64_t)khi << 32) | klo;
-          const uint32_t io = __shfl_xor(I[r], lm, kWave);
-          // the lower element keeps the smaller pair when ascending
-          const bool take = lower == up ? key_gt(K[r], I[r], ko, io) : key_gt(ko, io, K[r], I[r]);
-          if (take) {
-            K[r] = ko;
-            I[r] = io;
-          }
-        }
-      } else {  // across waves, through LDS
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < kSortPer; ++r) {
-          skey[kSortPer * tid + r] = K[r];
-          sidx[kSortPer * tid + r] = I[r];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < kSortPer; ++r) {
-          const int i = kSortPer * tid + r, o = i ^ j;
-          const bool up = (i & k) == 0, lower = i < o;
-          const uint64_t ko = skey[o];
-          const uint32_t io = sidx[o];
-          const bool take = lower == up ? key_gt(K[r], I[r], ko, io) : key_gt(ko, io, K[r], I[r]);
-          if (take) {
-            K[r] = ko;
-            I[r] = io;
-          }
+      for (int e = threadIdx.x; e < N / 2; e += kFitBS) {
+        const int i = ((e & ~(j - 1)) << 1) | (e & (j - 1));
+        const int l = i + j;
+        const uint64_t ka = skey[i], kb = skey[l];
+        const uint16_t ia = sidx[i], ib = sidx[l];
+        const bool gt = (ka > kb) || (ka == kb && ia > ib);
+        if (gt == ((i & k) == 0)) {
+          skey[i] = kb;
+          skey[l] = ka;
+          sidx[i] = ib;
+          sidx[l] = ia;
         }
       }
+      __syncthreads();
     }
   }
-#pragma unroll
-  for (int r = 0; r < kSortPer; ++r) {
-    const int e = kSortPer * tid + r;
-    if (e < m) {
-      sc.key[ooff + t0 + e] = K[r];
-      sc.perm[ooff + t0 + e] = t0 + (int32_t)I[r];
-    }
+  for (int e = threadIdx.x; e < m; e += kFitBS) {
+    sc.key[ooff + t0 + e] = skey[e];
+    sc.perm[ooff + t0 + e] = t0 + sidx[e];
   }
-}
-
-// Entries of the sorted tiles other than `own` that precede key kq in the
-// stable order: tiles before `own` count keys <= kq, the others keys < kq
-// (own = -1: keys < kq everywhere).  The binary searches of eight tiles run
-// in lockstep, so their dependent global loads overlap instead of chaining
-// tile after tile.
-__device__ __forceinline__ int count_in_tiles(const uint64_t* key, int n, int nt, int own,
-                                              uint64_t kq) {
-  constexpr int kLanes = 8;
-  int total = 0;
-  for (int tb = 0; tb < nt; tb += kLanes) {
-    int lo[kLanes], hi[kLanes];
-#pragma unroll
-    for (int b = 0; b < kLanes; ++b) {
-      const int tt = tb + b;
-      lo[b] = 0;
-      hi[b] = (tt < nt && tt != own) ? min(kSortTile, n - tt * kSortTile) : 0;
-    }
-#pragma unroll
-    for (int step = 0; step < 12; ++step) {  // 2^12 > kSortTile
-#pragma unroll
-      for (int b = 0; b < kLanes; ++b) {
-        if (lo[b] < hi[b]) {
-          const int tt = tb + b, mid = (lo[b] + hi[b]) >> 1;
-          const uint64_t v = key[tt * kSortTile + mid];
-          if (tt < own ? v <= kq : v < kq) lo[b] = mid + 1; else hi[b] = mid;
-        }
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < kLanes; ++b) total += lo[b];
-  }
-  return total;
 }
 
 // K2: stable ranks, prior insertion, mu and LF weights in sorted order
@@ -267,14 +168,22 @@ __global__ __launch_bounds__(kFitBS) void k_fit_rank(tpe_seg* __restrict__ segs,
   const uint64_t* key = sc.key + ooff;
   int prior_pos = 0;
   if (n >= 2) {
-    prior_pos = count_in_tiles(key, n, nt, -1, order_key(pmu));
+    const uint64_t kp = order_key(pmu);
+    for (int t = 0; t < nt; ++t)
+      prior_pos += count_lt(key + t * kSortTile, min(kSortTile, n - t * kSortTile), kp);
   } else if (n == 1) {
     prior_pos = (pmu < sc.xf[ooff]) ? 0 : 1;  // tpe.py:414-421
   }
   if (q < n) {
     const int t = q / kSortTile, p = q - t * kSortTile;
     const uint64_t kq = key[q];
-    const int rank = p + count_in_tiles(key, n, nt, t, kq);
+    int rank = p;
+    for (int tt = 0; tt < nt; ++tt) {
+      if (tt == t) continue;
+      const int mm = min(kSortTile, n - tt * kSortTile);
+      rank += (tt < t) ? count_le(key + tt * kSortTile, mm, kq)
+                       : count_lt(key + tt * kSortTile, mm, kq);
+    }
     const int gi = sc.perm[ooff + q];
     const int pos = rank + (rank >= prior_pos ? 1 : 0);
     mu[coff + pos] = sc.xf[ooff + gi];
