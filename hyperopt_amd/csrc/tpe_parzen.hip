@@ -99,8 +99,11 @@ __device__ __forceinline__ int count_le(const uint64_t* a, int n, uint64_t key) 
   return lo;
 }
 
-// K1: transform + tile sort
-__global__ __launch_bounds__(kFitBS) void k_fit_tilesort(const double* __restrict__ obs,
+// K1: transform + tile sort, one 1024-thread block per 2048-observation tile
+// (a pair per thread per bitonic stage: the sort is barrier/latency-bound, so
+// more waves per tile, not fewer instructions, is what shortens it)
+constexpr int kSortBS = 1024;
+__global__ __launch_bounds__(kSortBS) void k_fit_tilesort(const double* __restrict__ obs,
                                                          const tpe_seg* __restrict__ segs,
                                                          FitScratch sc) {
   __shared__ uint64_t skey[kSortTile];
@@ -113,7 +116,7 @@ __global__ __launch_bounds__(kFitBS) void k_fit_tilesort(const double* __restric
   int N = 2;
   while (N < m) N <<= 1;
   const int64_t ooff = S.obs_off;
-  for (int e = threadIdx.x; e < N; e += kFitBS) {
+  for (int e = threadIdx.x; e < N; e += kSortBS) {
     if (e < m) {
       double v = obs[ooff + t0 + e];
       if (S.transform == TPE_OBS_LOG) {
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(kFitBS) void k_fit_tilesort(const double* __restric
   __syncthreads();
   for (int k = 2; k <= N; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int e = threadIdx.x; e < N / 2; e += kFitBS) {
+      for (int e = threadIdx.x; e < N / 2; e += kSortBS) {
         const int i = ((e & ~(j - 1)) << 1) | (e & (j - 1));
         const int l = i + j;
         const uint64_t ka = skey[i], kb = skey[l];
@@ -148,16 +151,23 @@ __global__ __launch_bounds__(kFitBS) void k_fit_tilesort(const double* __restric
       __syncthreads();
     }
   }
-  for (int e = threadIdx.x; e < m; e += kFitBS) {
+  for (int e = threadIdx.x; e < m; e += kSortBS) {
     sc.key[ooff + t0 + e] = skey[e];
     sc.perm[ooff + t0 + e] = t0 + sidx[e];
   }
 }
 
-// K2: stable ranks, prior insertion, mu and LF weights in sorted order
+// K2: stable ranks, prior insertion, mu and LF weights in sorted order.
+// LDS: the segment's sorted tiles are first copied into LDS (segments of up
+// to kRankLds observations -- every C3/C4 history), so the ~4 x 11 dependent
+// probes of a rank hit LDS instead of L2.
+constexpr int kRankLds = 12288;  // keys staged per block (96 KB)
+
+template <bool LDS>
 __global__ __launch_bounds__(kFitBS) void k_fit_rank(tpe_seg* __restrict__ segs, FitScratch sc,
                                                      double* __restrict__ w,
                                                      double* __restrict__ mu) {
+  extern __shared__ uint64_t s_keys[];
   tpe_seg* S = segs + blockIdx.y;
   const int n = S->n_obs;
   const int q = blockIdx.x * kFitBS + threadIdx.x;
@@ -166,24 +176,53 @@ __global__ __launch_bounds__(kFitBS) void k_fit_rank(tpe_seg* __restrict__ segs,
   const double pmu = S->prior_mu;
   const int nt = (n + kSortTile - 1) / kSortTile;
   const uint64_t* key = sc.key + ooff;
-  int prior_pos = 0;
-  if (n >= 2) {
-    const uint64_t kp = order_key(pmu);
-    for (int t = 0; t < nt; ++t)
-      prior_pos += count_lt(key + t * kSortTile, min(kSortTile, n - t * kSortTile), kp);
-  } else if (n == 1) {
-    prior_pos = (pmu < sc.xf[ooff]) ? 0 : 1;  // tpe.py:414-421
-  }
-  if (q < n) {
-    const int t = q / kSortTile, p = q - t * kSortTile;
-    const uint64_t kq = key[q];
-    int rank = p;
-    for (int tt = 0; tt < nt; ++tt) {
-      if (tt == t) continue;
-      const int mm = min(kSortTile, n - tt * kSortTile);
-      rank += (tt < t) ? count_le(key + tt * kSortTile, mm, kq)
-                       : count_lt(key + tt * kSortTile, mm, kq);
+  if constexpr (LDS) {
+    // eight loads in flight per thread, then the stores
+    for (int e0 = 0; e0 < n; e0 += 8 * kFitBS) {
+      uint64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * kFitBS + threadIdx.x;
+        v[u] = e < n ? key[e] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * kFitBS + threadIdx.x;
+        if (e < n) s_keys[e] = v[u];
+      }
     }
+    __syncthreads();
+    key = s_keys;
+  }
+  // the prior's insertion point (keys < prior) and this observation's stable
+  // rank, searched together tile by tile (two independent chains per step)
+  const bool two = n >= 2;
+  const uint64_t kp = two ? order_key(pmu) : 0ull;
+  const int t = q / kSortTile, p = q - t * kSortTile;
+  const bool mine = q < n;
+  const uint64_t kq = mine ? key[q] : 0ull;
+  int prior_pos = 0, rank = p;
+  for (int tt = 0; tt < nt; ++tt) {
+    const uint64_t* a = key + tt * kSortTile;
+    const int mm = min(kSortTile, n - tt * kSortTile);
+    const bool search = mine && tt != t, le = tt < t;
+    int plo = 0, phi = two ? mm : 0, rlo = 0, rhi = search ? mm : 0;
+    while (plo < phi || rlo < rhi) {
+      if (plo < phi) {
+        const int mid = (plo + phi) >> 1;
+        if (a[mid] < kp) plo = mid + 1; else phi = mid;
+      }
+      if (rlo < rhi) {
+        const int mid = (rlo + rhi) >> 1;
+        const uint64_t v = a[mid];
+        if (le ? v <= kq : v < kq) rlo = mid + 1; else rhi = mid;
+      }
+    }
+    prior_pos += plo;
+    rank += rlo;
+  }
+  if (n == 1) prior_pos = (pmu < sc.xf[ooff]) ? 0 : 1;  // tpe.py:414-421
+  if (mine) {
     const int gi = sc.perm[ooff + q];
     const int pos = rank + (rank >= prior_pos ? 1 : 0);
     mu[coff + pos] = sc.xf[ooff + gi];
@@ -491,10 +530,18 @@ extern "C" int tpe_parzen_fit(const double* obs, void* scratch, tpe_seg* segs, i
   const FitScratch sc = carve(scratch, n_seg, max_obs, n_obs_total);
   if (max_obs > 0) {
     const int gs = (max_obs + kSortTile - 1) / kSortTile;
-    hipLaunchKernelGGL(k_fit_tilesort, dim3(gs, n_seg), dim3(kFitBS), 0, st, obs, segs, sc);
+    hipLaunchKernelGGL(k_fit_tilesort, dim3(gs, n_seg), dim3(kSortBS), 0, st, obs, segs, sc);
   }
   const int gr = (std::max(max_obs, 1) + kFitBS - 1) / kFitBS;
-  hipLaunchKernelGGL(k_fit_rank, dim3(gr, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu);
+  // staged ranks need > 64 KB of dynamic LDS: opt in once (gfx950 has 160 KB)
+  static const bool rank_lds = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&k_fit_rank<true>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 8 * kRankLds) == hipSuccess;
+  if (rank_lds && max_obs <= kRankLds)
+    hipLaunchKernelGGL(k_fit_rank<true>, dim3(gr, n_seg), dim3(kFitBS),
+                       (size_t)8 * std::max(max_obs, 1), st, segs, sc, w, mu);
+  else
+    hipLaunchKernelGGL(k_fit_rank<false>, dim3(gr, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu);
   const int gc = (int)comp_tiles(max_obs);
   hipLaunchKernelGGL(k_fit_comp, dim3(gc, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu, sigma);
   hipLaunchKernelGGL(k_fit_coef, dim3(gc, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu, sigma,

@@ -62,7 +62,10 @@ constexpr int kCellF = 16;           // floats per cell (64 B: four 16-B chunks)
 constexpr int kSlotB = 128;          // bytes per cell slot of a job's region (cells + m pairs)
 constexpr int kChunks = 4;           // 16-B chunks of a cell the scorer reads
 constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
-constexpr double kTauExtra = 25.0;   // exclusion margin (nats) on top of log(M)
+#ifndef TPE_TAU_TABLE
+#define TPE_TAU_TABLE 25.0
+#endif
+constexpr double kTauExtra = TPE_TAU_TABLE;  // exclusion margin (nats) on top of log(M)
 constexpr double kDrawZ = 5.8;       // |z| of an fp32 Box-Muller draw is < 5.77
 constexpr double kDrawZ64 = 8.7;     // |z| of an fp64 Box-Muller draw (53-bit uniforms) is < 8.6
 constexpr double kTauExact = 40.0;   // margin of the pruned exact fp64 scorer: e^-40 < 5e-18
