@@ -75,24 +75,46 @@ constexpr int kCatWaves = kCatBS / kWave;
 // Weighted counts, one wave per (segment, category): np.bincount's sum
 // (pyll/base.py:1053-1060) adds the LF weights of a category's observations
 // sequentially in observation order, so the fp64 chain itself cannot be
-// split.  The wave scans 64 observations per step (weights computed in
-// parallel), ballots the matches, and walks the set bits in lane order:
-// each match's weight comes over by v_readlane into an add on the wave-uniform
-// running count -- the only serial work is one fp64 add per match, with no
-// LDS round trip in the chain.
+// split.  The wave scans 64 observations per step, ballots the matches, and
+// every matching lane writes its weight (computed in parallel) into the
+// wave's LDS list at its rank; when the list fills, lane 0 folds it into the
+// running count in list order -- the only serial work left is one fp64 add
+// per match.
+constexpr int kCatList = 512;  // weights buffered per wave before a fold
+
 __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict__ obs,
                                                        const tpe_cat_seg* __restrict__ segs,
                                                        double* __restrict__ p) {
+  __shared__ double s_list[kCatWaves][kCatList];
   const tpe_cat_seg& S = segs[blockIdx.y];
   const int k = blockIdx.x * kCatWaves + threadIdx.x / kWave;
   if (k >= S.n_cat) return;  // wave-uniform
+  double* list = s_list[threadIdx.x / kWave];
   const int n = S.n_obs, lane = lane_id();
   // linear-forgetting ramp (np.linspace(1/N, 1, N-LF), tpe.py:380-392)
   const bool ramp = S.lf > 0 && S.lf < n;
   const int64_t num = n - S.lf;
   const double start = 1.0 / (double)n;
   const double step = (ramp && num > 1) ? (1.0 - start) / (double)(num - 1) : 0.0;
+  const uint64_t lt = (1ull << lane) - 1ull;
   double cnt = 0.0;
+  int filled = 0;
+  auto fold = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      int j = 0;
+      for (; j + 4 <= filled; j += 4) {
+        const double a = list[j], b = list[j + 1], c = list[j + 2], d = list[j + 3];
+        cnt = __dadd_rn(cnt, a);
+        cnt = __dadd_rn(cnt, b);
+        cnt = __dadd_rn(cnt, c);
+        cnt = __dadd_rn(cnt, d);
+      }
+      for (; j < filled; ++j) cnt = __dadd_rn(cnt, list[j]);
+    }
+    filled = 0;
+    __builtin_amdgcn_wave_barrier();
+  };
   constexpr int kDepth = 32;  // tiles of 64 observations in flight per step (latency-bound scan)
   for (int t0 = 0; t0 < n; t0 += kDepth * kWave) {
     int64_t cur[kDepth];
@@ -103,26 +125,24 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
     }
 #pragma unroll
     for (int b = 0; b < kDepth; ++b) {
-      uint64_t m = __ballot(cur[b] == (int64_t)k);
+      const bool hit = cur[b] == (int64_t)k;
+      const uint64_t m = __ballot(hit);
       if (m == 0) continue;  // wave-uniform
-      const int64_t i = t0 + b * kWave + lane;
-      double wt = 1.0;
-      if (ramp && i < num) {
-        if (num == 1) wt = start;
-        else if (i == num - 1) wt = 1.0;
-        else wt = __dadd_rn(__dmul_rn((double)i, step), start);
+      if (filled + kWave > kCatList) fold();
+      if (hit) {
+        const int64_t i = t0 + b * kWave + lane;
+        double wt = 1.0;
+        if (ramp && i < num) {
+          if (num == 1) wt = start;
+          else if (i == num - 1) wt = 1.0;
+          else wt = __dadd_rn(__dmul_rn((double)i, step), start);
+        }
+        list[filled + __popcll(m & lt)] = wt;
       }
-      const uint64_t wb = __builtin_bit_cast(uint64_t, wt);
-      const int lo32 = (int)(uint32_t)wb, hi32 = (int)(uint32_t)(wb >> 32);
-      while (m) {  // wave-uniform loop over the matching lanes, in lane order
-        const int l = __builtin_ctzll(m);
-        m &= m - 1;
-        const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi32, l) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane(lo32, l);
-        cnt = __dadd_rn(cnt, __builtin_bit_cast(double, v));
-      }
+      filled += __popcll(m);
     }
   }
+  fold();
   if (lane == 0) {
     double pseudo;
     if (S.mode == 0) {
