@@ -265,12 +265,13 @@ class Engine:
         self._res_pin = None   # pinned result block of a deferred (WorkBatch) run
         self._inflight = None  # that run's _Pending until collected
         self.host_marks = None  # set to a list to record host-side phase times (diagnostic)
-        # quantized / categorical scoring runs on a second stream, concurrently
-        # with the cell-table path (the two share no buffers); TPE_SIDE_STREAM=0
-        # puts everything on the caller's stream (diagnostic)
-        # "2": the table scorer waits for the side stream (side work overlaps the
-        # table build only); "1": join at the end of the level
-        self.side_stream = os.environ.get("TPE_SIDE_STREAM", "0")
+        # categorical posteriors and quantized / categorical scoring run on a
+        # second stream, concurrently with the continuous fit and the
+        # cell-table path (they share no buffers): -7% per level on one GPU,
+        # -11% at an 8-way label share (tools/rank_share.py).
+        # "1": join at the end of the level; "2": the table scorer waits for
+        # the side stream; "0": everything on the caller's stream
+        self.side_stream = os.environ.get("TPE_SIDE_STREAM", "1")
         self._side = None
         # sampled table jobs without per-candidate outputs: "cubic" scores
         # each candidate by its cell's score cubic (tpe_score_table_fast);
@@ -831,6 +832,19 @@ class Engine:
             d_obs, d_cobs = base + o_obs, base + o_cobs
 
         _hmark('upload+gather')
+        # side stream (TPE_SIDE_STREAM != "0"): quantized and categorical work
+        # overlaps the continuous pipeline; the categorical posterior starts on
+        # it as soon as the lists are gathered (it needs nothing else)
+        side = None
+        if self.side_stream != "0" and not sample_only and not posteriors and any(
+                ids for k, ids in groups if k in SIDE_KINDS):
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            side = self._side
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            side.wait_event(ev)
+        side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
         # ---- posterior fit ------------------------------------------------------
         if fit_ids:
             e0 = tick("fit")
@@ -839,12 +853,12 @@ class Engine:
                                        d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
             tock("fit", e0)
         if cat:
-            e0 = tick("cat_fit")
+            e0 = tick("cat_fit", side)
             d_p = base + o_p  # the posterior is formed in place in the staged pool
             L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
-                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, sp),
-                    "tpe_cat_posterior")
-            tock("cat_fit", e0)
+                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
+                                          side_p), "tpe_cat_posterior")
+            tock("cat_fit", e0, side)
 
         if posteriors:
             return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
@@ -867,16 +881,10 @@ class Engine:
         # ---- scoring, one call per group ----------------------------------------
         # quantized and categorical groups go to the side stream (after the job
         # table has landed); continuous groups stay on `stream`
-        side = None
-        if self.side_stream != "0" and not sample_only and any(
-                ids for k, ids in groups if k in SIDE_KINDS):
-            if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
-            side = self._side
+        if side is not None:  # quantized groups need the continuous fit
             ev = torch.cuda.Event()
             ev.record(stream)
             side.wait_event(ev)
-        side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
         table_calls = []
         g_order = list(range(len(groups)))
         if side is not None:  # side groups launched first
