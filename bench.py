@@ -509,7 +509,9 @@ def main():
             dt = (time.perf_counter() - t0) / 2
             line["fp64"] = {"value": len(space) * n_cand / dt, "ms_per_step": dt * 1e3,
                             "steps": 2, "dtype": "f64",
-                            "note": "exact dense fp64 scoring (k_score64) of every label"}
+                            "note": "exact fp64 scoring of every label: component-pruned "
+                                    "k_score_pruned64 for the 10k-component above mixtures "
+                                    "(e^-40 margin), dense k_score64 for smaller ones"}
         line["dropin_suggest"] = dropin_suggest_p50(space, vals, losses, n_cand)
         line["readme_suggest"] = readme_suggest_p50()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

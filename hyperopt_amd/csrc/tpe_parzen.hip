@@ -159,8 +159,10 @@ __global__ __launch_bounds__(kSortBS) void k_fit_tilesort(const double* __restri
 
 // K2: stable ranks, prior insertion, mu and LF weights in sorted order.
 // LDS: the segment's sorted tiles are first copied into LDS (segments of up
-// to kRankLds observations -- every C3/C4 history), so the ~4 x 11 dependent
-// probes of a rank hit LDS instead of L2.
+// to kRankLds observations, launches of up to 1024 blocks), so the ~4 x 11
+// dependent probes of a rank hit LDS instead of L2: 23 -> 16 us at an 8-way
+// label share, but 31 -> 57 us for a whole C3 level (4000 blocks each
+// copying 80 KB), hence the block-count gate at the launch.
 constexpr int kRankLds = 12288;  // keys staged per block (96 KB)
 
 template <bool LDS>
@@ -537,7 +539,10 @@ extern "C" int tpe_parzen_fit(const double* obs, void* scratch, tpe_seg* segs, i
   static const bool rank_lds = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&k_fit_rank<true>),
       hipFuncAttributeMaxDynamicSharedMemorySize, 8 * kRankLds) == hipSuccess;
-  if (rank_lds && max_obs <= kRankLds)
+  // staging costs every block a copy of its segment's keys: it pays while
+  // the launch leaves the GPU half-idle (a rank's share of labels), not when
+  // thousands of blocks already hide the L2 latency (a whole C3 level)
+  if (rank_lds && max_obs <= kRankLds && (int64_t)gr * n_seg <= 1024)
     hipLaunchKernelGGL(k_fit_rank<true>, dim3(gr, n_seg), dim3(kFitBS),
                        (size_t)8 * std::max(max_obs, 1), st, segs, sc, w, mu);
   else

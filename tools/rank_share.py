@@ -53,6 +53,17 @@ def main(worlds, only=None):
                 t0 = time.perf_counter()
                 step(10 + k)
                 ts.append(time.perf_counter() - t0)
+            marks, phases, names = [], [], []
+            for k in range(5):  # host phases (Engine.host_marks)
+                eng.host_marks = []
+                step(50 + k)
+                m = dict(eng.host_marks)
+                marks.append((m["score launches"] - m["start"], m["readback"] - m["score launches"]))
+                hm = eng.host_marks
+                phases.append([b[1] - a[1] for a, b in zip(hm[:-1], hm[1:])])
+                names = [b[0] for b in hm[1:]]
+            eng.host_marks = None
+            host = np.median(np.array(marks), axis=0) * 1e3
             timers = {}
             for k in range(3):
                 step(100 + k, timers)
@@ -60,6 +71,9 @@ def main(worlds, only=None):
             g = {a: round(float(np.mean([e0.elapsed_time(e1) for e0, e1 in v])), 4)
                  for a, v in timers.items()}
             ranks.append({"rank": r, "labels": len(units), "ms": round(float(np.median(ts)) * 1e3, 4),
+                          "host_launch_ms": round(float(host[0]), 4),
+                          "wait_ms": round(float(host[1]), 4),
+                          "phases_us": dict(zip(names, np.round(np.median(np.array(phases), axis=0) * 1e6, 1).tolist())),
                           "group_ms": g, "gpu_ms": round(sum(g.values()), 4)})
         worst = max(x["ms"] for x in ranks)
         if only:
@@ -68,7 +82,10 @@ def main(worlds, only=None):
         out[N] = {"max_rank_ms": worst, "ranks": ranks}
         print(json.dumps({"N": N, "max_rank_ms": worst,
                           "per_rank_ms": [x["ms"] for x in ranks],
+                          "host_launch_ms": [x["host_launch_ms"] for x in ranks],
+                          "wait_ms": [x["wait_ms"] for x in ranks],
                           "per_rank_gpu_ms": [x["gpu_ms"] for x in ranks]}), flush=True)
+        print(json.dumps({"N": N, "rank0_phases_us": ranks[0]["phases_us"]}), flush=True)
     base = out[1]["max_rank_ms"]
     for N in worlds:
         print(json.dumps({"N": N, "projected_speedup_no_collective": round(base / out[N]["max_rank_ms"], 2)}))
