@@ -479,6 +479,14 @@ class Trials(object):
                     show_progressbar=show_progressbar, early_stop_fn=early_stop_fn)
 
     # -- columnar history for the suggest path --------------------------------------
+    def invalidate_loss_cache(self):
+        """Forget the cached losses of finished trials (Columnar.losses): call
+        after editing the ``result`` of a document that was already DONE, so
+        the next suggest re-reads every loss (the reference re-reads them on
+        every suggest, tpe.py:880-882)."""
+        for col in getattr(self, "_columnar", {}).values():
+            col.n_final = 0
+
     def columnar(self, labels):
         key = tuple(labels)
         cache = getattr(self, "_columnar", None)

@@ -162,3 +162,21 @@ def test_loss_cache_follows_finishing_documents():
     docs[3]["result"], docs[3]["state"] = {"status": "ok", "loss": 5.0}, 2
     _check(t)
     assert t.columnar(LABELS).n_final == 5
+
+
+def test_invalidate_loss_cache_rereads_edited_results():
+    """Finished documents' losses are cached (Columnar.losses); editing one and
+    calling Trials.invalidate_loss_cache() makes the next history read it
+    again, as the reference does on every suggest (tpe.py:880-882)."""
+    rng = np.random.RandomState(5)
+    t = _random_trials(rng, 40)
+    h0 = tpe.collect_history(t, LABELS)
+    doc = t.trials[7]
+    old = float(doc["result"]["loss"])
+    doc["result"]["loss"] = old - 100.0
+    assert tpe.collect_history(t, LABELS).losses[7] == h0.losses[7] == old  # cached
+    t.invalidate_loss_cache()
+    h1 = tpe.collect_history(t, LABELS)
+    assert h1.losses[7] == old - 100.0
+    _, ref_losses, _ = _reference_rule(t)
+    np.testing.assert_array_equal(h1.losses, ref_losses)
