@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32 = 1, 2, 4, 8, 16
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -98,6 +98,7 @@ _SIGNATURES = {
     "tpe_score_categorical": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P]),
     "tpe_sample": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P]),
     "tpe_best_combine": (_I, [_P, _I, _I, _P, _P]),
+    "tpe_maxloc_allreduce": (_I, [_P, _P, _P, _I, _P, _P]),
     "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
     "tpe_last_error": (ctypes.c_char_p, []),
     "tpe_abi_version": (_I, []),

@@ -1,0 +1,87 @@
+// tpe_dist.hip -- the cross-GPU argmax of a suggest level over RCCL.
+//
+// SURVEY §8(b)'s max-loc all-reduce: every rank holds one tpe_best record per
+// label of the level (an empty record -- index -1 -- for labels it did not
+// score); the records are all-gathered over the caller's RCCL communicator
+// (xGMI inside a node) and folded on the device by tpe_best_combine with
+// np.argmax's rules (tpe.py:650-658: first maximum, NaN wins), so every rank
+// ends with the same per-label winners.  This is what hyperopt_amd/dist.py
+// does through torch.distributed; the entry point lets a host without torch
+// (cgo / JNI / N-API bindings of this ABI) do the same with its own
+// communicator.
+//
+// RCCL is bound at the first call by dlopen("librccl.so.1"): a process that
+// already holds an RCCL (torch's bundled one, or the host's) gets that copy,
+// so the communicator and the collective come from the same library; the
+// shared object itself carries no link-time RCCL dependency.
+#include <dlfcn.h>
+#include <mutex>
+#include <rccl/rccl.h>
+
+#include "tpe_common.hpp"
+
+extern "C" int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* out,
+                                void* stream);
+
+namespace tpe {
+namespace {
+typedef ncclResult_t (*AllGatherFn)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                                    hipStream_t);
+typedef ncclResult_t (*CommCountFn)(const ncclComm_t, int*);
+typedef const char* (*ErrorStringFn)(ncclResult_t);
+
+struct Rccl {
+  AllGatherFn all_gather = nullptr;
+  CommCountFn comm_count = nullptr;
+  ErrorStringFn error_string = nullptr;
+  bool ok = false;
+};
+
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW);
+    if (!h) return;
+    r.all_gather = reinterpret_cast<AllGatherFn>(dlsym(h, "ncclAllGather"));
+    r.comm_count = reinterpret_cast<CommCountFn>(dlsym(h, "ncclCommCount"));
+    r.error_string = reinterpret_cast<ErrorStringFn>(dlsym(h, "ncclGetErrorString"));
+    r.ok = r.all_gather && r.comm_count;
+  });
+  return r;
+}
+}  // namespace
+}  // namespace tpe
+
+using namespace tpe;
+
+extern "C" int tpe_maxloc_allreduce(const tpe_best* local, tpe_best* gathered, tpe_best* out,
+                                    int n_labels, void* comm, void* stream) {
+  if (n_labels < 0 || (n_labels > 0 && (!local || !gathered || !out || !comm))) {
+    set_error("tpe_maxloc_allreduce: bad arguments (n_labels=%d)", n_labels);
+    return TPE_E_ARG;
+  }
+  if (n_labels == 0) return TPE_OK;
+  const Rccl& r = rccl();
+  if (!r.ok) {
+    set_error("tpe_maxloc_allreduce: librccl.so.1 not loadable (%s)", dlerror());
+    return TPE_E_UNSUPPORTED;
+  }
+  int world = 0;
+  ncclResult_t e = r.comm_count(static_cast<ncclComm_t>(comm), &world);
+  if (e != ncclSuccess || world < 1) {
+    set_error("tpe_maxloc_allreduce: ncclCommCount: %s",
+              r.error_string ? r.error_string(e) : "error");
+    return TPE_E_ARG;
+  }
+  e = r.all_gather(local, gathered, (size_t)n_labels * sizeof(tpe_best), ncclUint8,
+                   static_cast<ncclComm_t>(comm), static_cast<hipStream_t>(stream));
+  if (e != ncclSuccess) {
+    set_error("tpe_maxloc_allreduce: ncclAllGather: %s",
+              r.error_string ? r.error_string(e) : "error");
+    return TPE_E_LAUNCH;
+  }
+  return tpe_best_combine(gathered, world, n_labels, out, stream);
+}

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 8
+#define TPE_ABI_VERSION 9
 
 enum {
   TPE_OK = 0,
@@ -401,6 +401,15 @@ int tpe_prior_sample(const tpe_prior* priors, const tpe_prior* host_priors, int 
  * rank after an all-gather) -> n_labels winners, same tie rules. ------------ */
 int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* out,
                      void* stream);
+
+/* ---- cross-GPU max-loc (replaces the argmax of tpe.py:650-658
+ * across ranks): all-gather of every rank's n_labels records over the caller's
+ * RCCL communicator `comm` (an ncclComm_t; librccl.so.1 is bound at the first
+ * call), then tpe_best_combine of the world's sets into `out`.  `local`: this
+ * rank's records (index -1 where it scored nothing); `gathered`: device
+ * scratch of world * n_labels records.  Asynchronous on `stream`. */
+int tpe_maxloc_allreduce(const tpe_best* local, tpe_best* gathered, tpe_best* out, int n_labels,
+                         void* comm, void* stream);
 
 const char* tpe_last_error(void);
 int tpe_abi_version(void);

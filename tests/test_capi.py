@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 8
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 9
     sizes = (ctypes.c_int32 * 8)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 8) == 8
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -82,6 +82,9 @@ def test_argument_errors_are_reported():
     rc = lib.tpe_table_build(None, hp_, 1, None, None, None, None, 8, *([None] * 8))
     assert rc == -1 and b"not an unquantized" in lib.tpe_last_error()
     assert lib.tpe_best_combine(None, 0, 1, None, None) == -1
+    assert lib.tpe_maxloc_allreduce(None, None, None, 3, None, None) == -1
+    assert b"tpe_maxloc_allreduce" in lib.tpe_last_error()
+    assert lib.tpe_maxloc_allreduce(None, None, None, 0, None, None) == 0
     pri = np.zeros(1, L.PRIOR_DTYPE)
     pri["kind"] = 9
     pp = pri.ctypes.data_as(ctypes.c_void_p)
