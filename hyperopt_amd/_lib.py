@@ -106,6 +106,36 @@ _SIGNATURES = {
 }
 
 _lib = None
+_hip = None
+
+H2D, D2H = 1, 2  # hipMemcpyKind
+EVENT_NO_TIMING = 0x2  # hipEventDisableTiming
+
+
+def hip():
+    """The HIP runtime the library is bound to (torch's libamdhip64.so.7),
+    for the few stream-ordered runtime calls the engine makes per level
+    (async copies, events, stream waits) without torch's per-call overhead."""
+    global _hip
+    if _hip is None:
+        load()
+        h = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
+        for name, args in (("hipMemcpyAsync", [_P, _P, ctypes.c_size_t, _I, _P]),
+                           ("hipEventCreateWithFlags", [ctypes.POINTER(_P), ctypes.c_uint]),
+                           ("hipEventRecord", [_P, _P]),
+                           ("hipStreamWaitEvent", [_P, _P, ctypes.c_uint]),
+                           ("hipEventSynchronize", [_P]),
+                           ("hipStreamSynchronize", [_P])):
+            fn = getattr(h, name)
+            fn.restype = _I
+            fn.argtypes = args
+        _hip = h
+    return _hip
+
+
+def hip_check(rc, what):
+    if rc != 0:
+        raise TpeHipError("%s: hipError %d" % (what, rc))
 
 
 def load():

@@ -262,8 +262,10 @@ class Engine:
         self._plans = {}  # level structure -> static descriptor arrays (_plan_record)
         self._retired = []
         self._pinned = {}
-        self._res_pin = None   # pinned result block of a deferred (WorkBatch) run
-        self._inflight = None  # that run's _Pending until collected
+        self._res_pin = None   # pinned result block of a level's readback
+        self._inflight = None  # a deferred (WorkBatch) run's _Pending until collected
+        self._events = {}      # reusable HIP events (no timing) by name
+        self._hip = L.hip()
         self.host_marks = None  # set to a list to record host-side phase times (diagnostic)
         # categorical posteriors and quantized / categorical scoring run on a
         # second stream, concurrently with the continuous fit and the
@@ -294,6 +296,28 @@ class Engine:
             self._bufs[name] = t
         return t.data_ptr()
 
+    def _event(self, name):
+        e = self._events.get(name)
+        if e is None:
+            h = ctypes.c_void_p()
+            L.hip_check(self._hip.hipEventCreateWithFlags(ctypes.byref(h), L.EVENT_NO_TIMING),
+                        "hipEventCreateWithFlags")
+            e = self._events[name] = h
+        return e
+
+    def _order(self, name, src, dst):
+        """`dst` waits for the work queued so far on `src` (raw stream handles)."""
+        e = self._event(name)
+        L.hip_check(self._hip.hipEventRecord(e, src), "hipEventRecord")
+        L.hip_check(self._hip.hipStreamWaitEvent(dst, e, 0), "hipStreamWaitEvent")
+
+    def _res_pinned(self, nbytes):
+        pin = self._res_pin
+        if pin is None or pin.numel() < nbytes:
+            pin = self._res_pin = self.torch.empty(_align(int(nbytes * 1.25)),
+                                                   dtype=self.torch.uint8, pin_memory=True)
+        return pin
+
     def _upload(self, pack, stream, slot=0):
         """One host->device copy of ``pack`` through pinned buffer / device
         staging area ``slot`` (a level uploads twice: descriptors for the fit,
@@ -309,9 +333,8 @@ class Engine:
             host[off:off + arr.nbytes] = arr.reshape(-1).view(np.uint8)
         name = "stage" if slot == 0 else "stage%d" % slot
         dev = self._buf(name, pack.size)
-        dst = self._bufs[name]
-        with torch.cuda.stream(stream):
-            dst[:pack.size].copy_(pinned[:pack.size], non_blocking=True)
+        L.hip_check(self._hip.hipMemcpyAsync(dev, pinned.data_ptr(), pack.size, L.H2D,
+                                             stream.cuda_stream), "hipMemcpyAsync")
         return dev
 
     # -- level plans -----------------------------------------------------------
@@ -841,10 +864,9 @@ class Engine:
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
             side = self._side
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            side.wait_event(ev)
         side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
+        if side is not None:
+            self._order("gathered", sp, side_p)
         # ---- posterior fit ------------------------------------------------------
         if fit_ids:
             e0 = tick("fit")
@@ -882,10 +904,9 @@ class Engine:
         # quantized and categorical groups go to the side stream (after the job
         # table has landed); continuous groups stay on `stream`
         if side is not None:  # quantized groups need the continuous fit
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            side.wait_event(ev)
+            self._order("fitted", sp, side_p)
         table_calls = []
+        jobs_ptr = jobs.__array_interface__["data"][0]
         g_order = list(range(len(groups)))
         if side is not None:  # side groups launched first
             g_order.sort(key=lambda g: groups[g][0] not in SIDE_KINDS)
@@ -904,7 +925,7 @@ class Engine:
                 continue
             a, b = _slice_of(groups, g)
             hj = jobs[a:b]
-            hjp = hj.ctypes.data_as(ctypes.c_void_p)
+            hjp = jobs_ptr + a * JS  # host copy of the slice (plain int: no ctypes object)
             dj = base + o_jobs + a * JS
             db = d_best + a * BS
             nj = b - a
@@ -950,9 +971,7 @@ class Engine:
                                             sp), "tpe_table_build")
                 tock("table_build", e0)
                 if not joined and self.side_stream == "2":
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    stream.wait_event(ev)
+                    self._order("joined", side_p, sp)
                     joined = True
                 e0 = tick("table")
                 if outputs or inj(ids[0]) or self.table_scorer == "poly":
@@ -1015,27 +1034,23 @@ class Engine:
             tock(kind, e0, kst)
 
         if not joined:  # join before the readback
-            ev = torch.cuda.Event()
-            ev.record(side)
-            stream.wait_event(ev)
+            self._order("joined", side_p, sp)
         _hmark('score launches')
-        if batch is not None:  # queued readback into pinned memory (see _Pending)
-            nbytes = 64 + n_jobs * BS
-            pin = self._res_pin
-            if pin is None or pin.numel() < nbytes:
-                pin = self._res_pin = torch.empty(_align(int(nbytes * 1.25)), dtype=torch.uint8,
-                                                  pin_memory=True)
-            with torch.cuda.stream(stream):
-                pin[:nbytes].copy_(self._bufs["stage"][o_res:o_res + nbytes], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
+        # ---- results: one device->host copy of the result block into pinned memory
+        nbytes = 64 + n_jobs * BS
+        pin = self._res_pinned(nbytes)
+        L.hip_check(self._hip.hipMemcpyAsync(pin.data_ptr(), d_res, nbytes, L.D2H, sp),
+                    "hipMemcpyAsync")
+        if batch is not None:  # queued readback (see _Pending)
+            ev = self._event("result")
+            L.hip_check(self._hip.hipEventRecord(ev, sp), "hipEventRecord")
             p = self._inflight = _Pending(self, ev, pin, nbytes, np.asarray(order, np.int64),
                                           bool(table_calls))
             return p if defer else p.result()
-        # ---- results (one device->host copy; syncs the stream) --------------------
+        L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
+        res_h = pin[:nbytes].numpy().copy()
+        best_h = res_h[64:].view(L.BEST_DTYPE)
         with torch.cuda.stream(stream):
-            res_h = self._bufs["stage"][o_res:o_res + 64 + n_jobs * BS].to("cpu").numpy()
-            best_h = res_h[64:].view(L.BEST_DTYPE)
             err = int(res_h[:4].view(np.int32)[0])
             self.last_pairs = None
             if any(k == "sorted" and ids for k, ids in groups):
@@ -1124,7 +1139,7 @@ class _Pending(object):
     def result(self):
         if self._res is not None:
             return self._res
-        self.event.synchronize()
+        L.hip_check(self.eng._hip.hipEventSynchronize(self.event), "hipEventSynchronize")
         eng = self.eng
         if eng._inflight is self:
             eng._inflight = None
