@@ -450,19 +450,9 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   // per-component tests in fp32; each lane keeps its own scale m_l (raised
   // only when a term would exceed e^8 of it) and the lanes are merged at the
   // end.  The next item's coefficients are loaded before this item's work.
-  // Components at the bandwidth floor (sigma = prior_sigma / min(100, M+1),
-  // tpe.py:455 -- the bulk of a large mixture) share B = -h^2 inv^2 / 2, so
-  // exp(A u + B u^2) = exp(B u^2) exp(A u) and their part of the cell is
-  // exp(B u^2) sum_m (u^m / m!) M_m with power sums M_m = sum_j e_j A_j^m:
-  // 8 multiplies and 9 adds per component instead of the 24-op recurrence.
-  // The product with exp(B u^2)'s series is formed once per lane at the end
-  // (same degree-8 truncation, so the same coefficients up to rounding);
-  // every other component takes the recurrence.
-  float P[kP], Mp[kP];
+  float P[kP];
 #pragma unroll
-  for (int n = 0; n < kP; ++n) P[n] = Mp[n] = 0.0f;
-  const double inv_ref =
-      1.0 / fmax(S.prior_sigma / fmin(100.0, 1.0 + (double)(S.n_obs + 1)), kEps);
+  for (int n = 0; n < kP; ++n) P[n] = 0.0f;
   double ml = -INFINITY;
   bool bad = false;
   const float hf = (float)h, Tf = (float)T;
@@ -485,59 +475,25 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
       if (v > ml + 8.0) {  // new scale: rescale this lane's partial sums
         const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - v));
 #pragma unroll
-        for (int n = 0; n < kP; ++n) {
-          P[n] *= r;
-          Mp[n] *= r;
-        }
+        for (int n = 0; n < kP; ++n) P[n] *= r;
         ml = v;
       }
       const float hi2 = hf * inv * inv;
       const float Af = -dyf * hi2, B2 = -hf * hi2;  // A and 2B
       bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > kRhoLim * (1.0 + 1e-5));
       const float e = __expf((float)(v - ml));
-      if (c.y == inv_ref) {  // floor bandwidth: power sums
-        float pw = e;
-        Mp[0] += pw;
+      float cm = 0.0f, cc = e;  // e * c_n
+      P[0] += e;
 #pragma unroll
-        for (int n = 1; n < kP; ++n) {
-          pw *= Af;
-          Mp[n] += pw;
-        }
-      } else {
-        float cm = 0.0f, cc = e;  // e * c_n
-        P[0] += e;
-#pragma unroll
-        for (int n = 0; n + 1 < kP; ++n) {
-          const float cnx = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
-          P[n + 1] += cnx;
-          cm = cc;
-          cc = cnx;
-        }
+      for (int n = 0; n + 1 < kP; ++n) {
+        const float cnx = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
+        P[n + 1] += cnx;
+        cm = cc;
+        cc = cnx;
       }
     }
     k = kn;
     c = cn;
-  }
-  {
-    // P_n += sum_{2k+m=n} (B^k / k!) (M_m / m!), B = -h^2 inv_ref^2 / 2
-    const float hir = hf * (float)inv_ref;
-    const float B = -0.5f * hir * hir;
-    float bk[kP / 2 + 1];
-    bk[0] = 1.0f;
-#pragma unroll
-    for (int k = 1; k <= kP / 2; ++k) bk[k] = bk[k - 1] * B * (1.0f / (float)k);
-    float mf[kP];
-    float fact = 1.0f;
-#pragma unroll
-    for (int m = 0; m < kP; ++m) {
-      if (m > 0) fact *= 1.0f / (float)m;
-      mf[m] = Mp[m] * fact;
-    }
-#pragma unroll
-    for (int n = 0; n < kP; ++n) {
-#pragma unroll
-      for (int k = 0; 2 * k <= n; ++k) P[n] = fmaf(bk[k], mf[n - 2 * k], P[n]);
-    }
   }
   const double m0 = wave_max_dpp(ml);
   {
