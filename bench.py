@@ -114,6 +114,21 @@ def history_works(space, mat, hist, rows_b, step, n_cand, cand_base, units=None,
             for j, start, count in units]
 
 
+def history_batch(space, mat, hist, rows_b, step, n_cand, cand_base, units, n_total):
+    """The same level as history_works, as an engine.WorkBatch (the columnar
+    form tpe.suggest uses): counts and keys as arrays, LabelWork objects only
+    when the engine first sees the structure."""
+    from hyperopt_amd.engine import WorkBatch
+    nb = hist.active_host[rows_b].sum(0)
+    na = hist.n_active - nb
+    keys = np.asarray(label_keys(0, step, [lab for lab, _, _ in space]), np.uint64)
+    j = np.fromiter((u[0] for u in units), np.int64, len(units))
+    return WorkBatch(("bench-c3", tuple(units), n_total), nb[j], na[j], keys[j],
+                     [cand_base + u[1] for u in units],
+                     lambda: history_works(space, mat, hist, rows_b, step, n_cand, cand_base,
+                                           units, n_total))
+
+
 def label_key(seed, step, lab):
     """Philox key of (seed, step, label): the drop-in's key rule (tpe.label_key)
     with the step folded into the seed."""
@@ -345,7 +360,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    from hyperopt_amd.engine import DeviceHistory, Engine
+    from hyperopt_amd.engine import DeviceHistory, Engine, LabelResult
     from hyperopt_amd import dist as hdist
 
     scorer = "dense" if args.dense else args.scorer
@@ -379,9 +394,12 @@ def main():
             rb = below_rows(losses)
             isb = np.zeros(T_HIST, np.uint8)
             isb[rb] = 1
-            works = history_works(space, mat, hist, rb, k, n_cand, cand_base, units, n_cand)
-            res = eng.run(works, precision=prec, timers=timers, scorer=scorer,
-                          history=hist, is_below=isb, timer_groups=timer_groups)
+            works = history_batch(space, mat, hist, rb, k, n_cand, cand_base, units, n_cand)
+            r = eng.run(works, precision=prec, timers=timers, scorer=scorer,
+                        history=hist, is_below=isb, timer_groups=timer_groups)
+            res = [LabelResult(space[u[0]][0], ix, v, sc, ns) for u, ix, v, sc, ns in
+                   zip(units, r.index.tolist(), r.value.tolist(), r.score.tolist(),
+                       r.n_scored.tolist())]
         if world > 1:
             if strong:  # label-sharded level: every rank learns every label's winner
                 hdist.gather_best(len(space), [(u[0], r) for u, r in zip(units, res)])
@@ -417,6 +435,8 @@ def main():
         elapsed = float(t.item())
 
     # dominant kernel: unquantized continuous scoring of this rank's continuous labels
+    if not isinstance(works, list):
+        works = works.materialize()
     cont = [w for w in works if w.kind in ("uniform", "loguniform", "normal", "lognormal")]
     dense_pairs = sum(w.n_cand * (w.obs_below.size + 1 + (w.n_above if w.obs_above is None
                                                           else w.obs_above.size) + 1)

@@ -82,7 +82,7 @@ class WorkBatch(object):
     candidate counts, history columns and slots, lattice ranges, in order),
     the arrays carry the per-call values in work order, and ``materialize()``
     returns the equivalent LabelWork list, used when the structure is new.
-    Requires ``histories``; Engine.run then returns a BatchResult."""
+    Requires ``history`` or ``histories``; Engine.run then returns a BatchResult."""
     __slots__ = ("key", "n_below", "n_above", "keys", "cand_base", "materialize")
 
     def __init__(self, key, n_below, n_above, keys, cand_base, materialize):
@@ -517,10 +517,10 @@ class Engine:
             outputs = False
         batch = works if isinstance(works, WorkBatch) else None
         if batch is not None:
-            if histories is None or outputs or sample_only or posteriors or table_scores:
-                raise ValueError("a WorkBatch runs with histories= and no output hooks")
+            if not hist_mode or outputs or sample_only or posteriors or table_scores:
+                raise ValueError("a WorkBatch runs with history= / histories= and no output hooks")
             pkey = ("batch", batch.key, float(prior_weight), int(lf), int(precision), scorer,
-                    self._big64(precision, batch.n_above))
+                    histories is not None, self._big64(precision, batch.n_above))
             cached = self._plans.get(pkey)
             if cached is None:
                 works = batch.materialize()

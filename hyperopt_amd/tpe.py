@@ -37,7 +37,8 @@ import numpy as np
 from . import dist as hdist
 from . import rand
 from .base import doc_loss
-from .engine import DEFAULT_LF, Engine, LabelWork, WorkBatch, _lattice_range, _params
+from .engine import (DEFAULT_LF, Engine, LabelResult, LabelWork, WorkBatch, _lattice_range,
+                     _params)
 
 logger = logging.getLogger(__name__)
 
@@ -338,16 +339,20 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
             level = [lab for lab in live if lab not in walk]
             if not level:
                 break
-            keys = label_keys(seed, level)
             # under torch.distributed this rank scores its units of the level
             # (whole labels, or candidate ranges when labels < ranks) and the
             # winners are combined across ranks (hyperopt_amd/dist.py)
             units = hdist.plan_units([domain.specs[lab].kind for lab in level], n_ei, ws)[rank]
-            works = [obs.work(level[i], domain.specs[level[i]], col[level[i]], n_cand=count,
-                              key=keys[i], cand_base=start, n_total=n_ei)
-                     for i, start, count in units]
-            res = eng.run(works, prior_weight=prior_weight, lf=linear_forgetting,
-                          precision=prec, **obs.run_kwargs)
+            if obs.device and _space_sig(domain) is not None:
+                res = _level_batch(eng, domain, obs, level, units, seed, n_ei, col,
+                                   prior_weight, linear_forgetting, prec)
+            else:
+                keys = label_keys(seed, level)
+                works = [obs.work(level[i], domain.specs[level[i]], col[level[i]], n_cand=count,
+                                  key=keys[i], cand_base=start, n_total=n_ei)
+                         for i, start, count in units]
+                res = eng.run(works, prior_weight=prior_weight, lf=linear_forgetting,
+                              precision=prec, **obs.run_kwargs)
             if ws > 1:
                 best = hdist.gather_best(len(level), [(u[0], r) for u, r in zip(units, res)])
                 values = [b[2] for b in best]
@@ -418,6 +423,35 @@ def _level_info(domain, level):
             _LEVELS.clear()
         lv = _LEVELS[k] = _Level(next(_LEVEL_IDS), domain, level)
     return lv
+
+
+def _level_batch(eng, domain, obs, level, units, seed, n_ei, col, pw, lf, prec):
+    """One study's level (this rank's units of it) as a WorkBatch on the
+    device history: counts from the split, keys from the cached label hashes,
+    a structure key of a few small ints -- LabelWork objects only the first
+    time the structure is seen.  Returns one LabelResult per unit."""
+    lv = _level_info(domain, level)
+    idx = np.fromiter((u[0] for u in units), np.int64, len(units))
+    js = lv.js[idx]
+    lat = ()
+    if lv.lat:
+        lat = tuple(_lattice_range(obs.work(lab, spec, int(lv.js[i])),
+                                   _params(spec.kind, spec.args)) for i, lab, spec in lv.lat)
+    s = np.uint64(_mix64((int(seed) * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF))
+    with np.errstate(over="ignore"):
+        keys = _mix64_np(lv.h[idx] ^ s)
+
+    def materialize():
+        specs = domain.specs
+        return [obs.work(level[i], specs[level[i]], col[level[i]], n_cand=count,
+                         key=int(k), cand_base=start, n_total=n_ei)
+                for (i, start, count), k in zip(units, keys.tolist())]
+    batch = WorkBatch(("suggest", lv.id, tuple(units), n_ei, lat), obs.nb[js], obs.n_above[js],
+                      keys, [u[1] for u in units], materialize)
+    r = eng.run(batch, prior_weight=pw, lf=lf, precision=prec, **obs.run_kwargs)
+    return [LabelResult(level[u[0]], ix, v, sc, ns) for u, ix, v, sc, ns in
+            zip(units, r.index.tolist(), r.value.tolist(), r.score.tolist(),
+                r.n_scored.tolist())]
 
 
 def _run_columnar(eng, items, pw, lf, prec, defer=False):

@@ -43,7 +43,7 @@ def main(worlds, only=None):
             if only and r != only[1]:
                 continue
             def step(k, timers=None):
-                works = bench.history_works(space, mat, hist, rb, k, n, 0, units, n)
+                works = bench.history_batch(space, mat, hist, rb, k, n, 0, units, n)
                 return eng.run(works, precision=32, history=hist, is_below=isb, timers=timers)
             for k in range(3):
                 step(k)
@@ -57,8 +57,9 @@ def main(worlds, only=None):
             for k in range(5):  # host phases (Engine.host_marks)
                 eng.host_marks = []
                 step(50 + k)
+                eng.host_marks.append(("returned", time.perf_counter()))
                 m = dict(eng.host_marks)
-                marks.append((m["score launches"] - m["start"], m["readback"] - m["score launches"]))
+                marks.append((m["score launches"] - m["start"], m["returned"] - m["score launches"]))
                 hm = eng.host_marks
                 phases.append([b[1] - a[1] for a, b in zip(hm[:-1], hm[1:])])
                 names = [b[0] for b in hm[1:]]
