@@ -17,8 +17,16 @@ namespace tpe {
 namespace {
 constexpr int kGBS = 1024;
 constexpr int kGWaves = kGBS / kWave;
+constexpr int kGT = 16;                 // 1024-row tiles per pass (16 384 rows)
+constexpr int kGSlots = kGT * kGWaves;  // (tile, wave) counts scanned per pass
 
-// compacts one descriptor's rows (block-wide, in position order)
+// Compacts one descriptor's rows (block-wide, in position order).  A pass
+// covers kGT tiles: every thread first loads its kGT rows' flags and values
+// (the global loads of the whole pass in flight at once -- the kernel is
+// latency-bound, one block per descriptor), the waves' per-tile counts go to
+// LDS, one block-wide exclusive scan over the (tile, wave) slots gives every
+// wave its offsets, then the writes: three barriers per pass instead of three
+// per tile.
 __device__ __forceinline__ void gather_one(const double* __restrict__ V,
                                            const uint8_t* __restrict__ A,
                                            const int32_t* __restrict__ rows, int64_t n_rows,
@@ -28,37 +36,61 @@ __device__ __forceinline__ void gather_one(const double* __restrict__ V,
                                            int* wsum, int64_t& carry_s) {
   const uint8_t side = G.below ? 1 : 0;
   const int lane = lane_id(), wid = threadIdx.x / kWave;
+  const uint64_t lt = (1ull << lane) - 1ull;
   if (threadIdx.x == 0) carry_s = 0;
-  __syncthreads();
-  for (int64_t t0 = 0; t0 < n_rows; t0 += kGBS) {
-    const int64_t i = t0 + threadIdx.x;
-    bool take = false;
-    int64_t r = 0;
-    if (i < n_rows) {
-      r = rows ? (int64_t)rows[i] : i;
-      take = A[r] && (is_below[i] == side);
+  for (int64_t p0 = 0; p0 < n_rows; p0 += (int64_t)kGT * kGBS) {
+    bool take[kGT];
+    double v[kGT];
+#pragma unroll
+    for (int t = 0; t < kGT; ++t) {
+      const int64_t i = p0 + (int64_t)t * kGBS + threadIdx.x;
+      take[t] = false;
+      v[t] = 0.0;
+      if (i < n_rows) {
+        const int64_t r = rows ? (int64_t)rows[i] : i;
+        take[t] = A[r] && (is_below[i] == side);
+        if (take[t]) v[t] = V[r];
+      }
     }
-    const uint64_t bal = __ballot(take);
-    const int before = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[wid] = __popcll(bal);
+    int before[kGT];
+#pragma unroll
+    for (int t = 0; t < kGT; ++t) {
+      const uint64_t bal = __ballot(take[t]);
+      before[t] = __popcll(bal & lt);
+      if (lane == 0) wsum[t * kGWaves + wid] = __popcll(bal);
+    }
     __syncthreads();
-    int64_t pos = carry_s;
-    int tile = 0;
-    for (int q = 0; q < kGWaves; ++q) {
-      const int c = wsum[q];
-      if (q < wid) pos += c;
-      tile += c;
+    // exclusive scan of the kGSlots counts (slot order = tile-major, then
+    // wave = row order), one slot per thread
+    int c = threadIdx.x < kGSlots ? wsum[threadIdx.x] : 0;
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int o = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += o;
     }
-    pos += before;
-    if (take && pos < G.count) {
-      const double v = V[r];
-      if (G.to_int)
-        out_i[G.dst_off + pos] = (int64_t)v - G.offset;
-      else
-        out_f[G.dst_off + pos] = v;
+    __syncthreads();
+    if (threadIdx.x < kGSlots && lane == kWave - 1) wsum[kGSlots + wid] = incl;  // wave totals
+    __syncthreads();
+    int wave_base = 0;
+    for (int q = 0; q < wid && q < kGSlots / kWave; ++q) wave_base += wsum[kGSlots + q];
+    const int64_t carry = carry_s;
+    if (threadIdx.x < kGSlots) wsum[threadIdx.x] = wave_base + incl - c;  // exclusive
+    int total = 0;
+    for (int q = 0; q < kGSlots / kWave; ++q) total += wsum[kGSlots + q];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kGT; ++t) {
+      const int64_t pos = carry + wsum[t * kGWaves + wid] + before[t];
+      if (take[t] && pos < G.count) {
+        if (G.to_int)
+          out_i[G.dst_off + pos] = (int64_t)v[t] - G.offset;
+        else
+          out_f[G.dst_off + pos] = v[t];
+      }
     }
     __syncthreads();  // everyone has read carry_s / wsum
-    if (threadIdx.x == 0) carry_s += tile;
+    if (threadIdx.x == 0) carry_s = carry + total;
     __syncthreads();
   }
   if (threadIdx.x == 0 && carry_s != G.count && err) atomicOr(err, 4);
@@ -73,9 +105,11 @@ __global__ __launch_bounds__(kGBS) void k_gather_obs(const double* __restrict__ 
                                                      double* __restrict__ out_f,
                                                      int64_t* __restrict__ out_i,
                                                      int32_t* __restrict__ err) {
-  __shared__ int wsum[kGWaves];
+  __shared__ int wsum[kGSlots + kGSlots / kWave];
   __shared__ int64_t carry_s;
   const tpe_gather G = gs[blockIdx.x];
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
   gather_one(vals + (int64_t)G.col * ld, active + (int64_t)G.col * ld, rows, n_rows, is_below, G,
              out_f, out_i, err, wsum, carry_s);
 }
@@ -87,9 +121,11 @@ __global__ __launch_bounds__(kGBS) void k_gather_obs_multi(const tpe_history* __
                                                            double* __restrict__ out_f,
                                                            int64_t* __restrict__ out_i,
                                                            int32_t* __restrict__ err) {
-  __shared__ int wsum[kGWaves];
+  __shared__ int wsum[kGSlots + kGSlots / kWave];
   __shared__ int64_t carry_s;
   const tpe_gather G = gs[blockIdx.x];
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
   const tpe_history H = hs[G.hist];
   const int32_t* rows =
       H.rows_off >= 0 ? reinterpret_cast<const int32_t*>(aux + H.rows_off) : nullptr;
