@@ -1365,7 +1365,9 @@ extern "C" int tpe_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
     end = std::max(end, j.lat_off + j.lat_n);
   }
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(slot_first, 0xFF, (size_t)end * sizeof(uint64_t), st) != hipSuccess)
+  bool ready = true;
+  for (int i = 0; i < n_jobs; ++i) ready = ready && (host_jobs[i].flags & TPE_F_LATTICE_READY);
+  if (!ready && hipMemsetAsync(slot_first, 0xFF, (size_t)end * sizeof(uint64_t), st) != hipSuccess)
     return check_launch("tpe_lattice_sample memset");
   const int64_t gx = max_blocks(host_jobs, n_jobs, (int64_t)kBS * kLatR, -1);
   const int64_t per = (gx * n_jobs + 7) / 8;
@@ -1401,9 +1403,13 @@ extern "C" int tpe_lattice_compact(const tpe_job* jobs, const tpe_job* host_jobs
     return TPE_E_ARG;
   }
   int64_t maxn = 1;
-  for (int i = 0; i < n_jobs; ++i) maxn = std::max(maxn, host_jobs[i].lat_n);
+  bool ready = true;
+  for (int i = 0; i < n_jobs; ++i) {
+    maxn = std::max(maxn, host_jobs[i].lat_n);
+    ready = ready && (host_jobs[i].flags & TPE_F_LATTICE_READY);
+  }
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(counts, 0, (size_t)n_jobs * sizeof(int64_t), st) != hipSuccess)
+  if (!ready && hipMemsetAsync(counts, 0, (size_t)n_jobs * sizeof(int64_t), st) != hipSuccess)
     return check_launch("tpe_lattice_compact memset");
   hipLaunchKernelGGL(k_lattice_compact, dim3((unsigned)((maxn + kBS - 1) / kBS), (unsigned)n_jobs),
                      dim3(kBS), 0, st, jobs, (const unsigned long long*)slot_first, vals, firsts,

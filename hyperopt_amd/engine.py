@@ -38,6 +38,7 @@ EPS = 1e-12  # tpe.py:32
 DEFAULT_LF = 25  # tpe.py:36
 DRAW32_MAX_SLOT = 1 << 12  # fp32 lattice draws only while |k| <= 2^12
 LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense fallback
+LAT_PACK_MAX = 1 << 16  # lattice slots of a level initialised through the upload (else memset)
 TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
@@ -295,6 +296,13 @@ class Engine:
                                  device=self.device)
             self._bufs[name] = t
         return t.data_ptr()
+
+    def _ones(self, n):
+        """n all-ones uint64 words (cached)."""
+        a = self.__dict__.get("_ones_arr")
+        if a is None or a.size < n:
+            a = self._ones_arr = np.full(max(n, 1024), np.uint64(0xFFFFFFFFFFFFFFFF))
+        return a[:n]
 
     def _event(self, name):
         e = self._events.get(name)
@@ -733,6 +741,7 @@ class Engine:
                         J["lat_off"][pos], J["lat_kmin"][pos], J["lat_n"][pos] = lat_off, kmin, nk
                         if precision == 32 and max(abs(kmin), abs(kmin + nk - 1)) <= DRAW32_MAX_SLOT:
                             flags |= L.F_DRAW32
+                        flags |= L.F_LATTICE_READY  # cleared below for a large level
                         lat_off += nk
                     elif i in fallback:
                         J["cand_off"][pos] = qfb_off
@@ -751,6 +760,8 @@ class Engine:
                     cnt_off += lib.tpe_sort_layout(n, ctypes.byref(slots))
                     sort_off += slots.value
                 J["flags"][pos] = flags
+            if lat_off > LAT_PACK_MAX:  # the slots are set by the library's memset instead
+                J["flags"] &= ~L.F_LATTICE_READY
             for name, col in J.items():
                 jobs[name] = col
             cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
@@ -797,6 +808,14 @@ class Engine:
         else:
             o_obs = pack.add(obs_pool)
             o_cobs = pack.add(cobs_pool)
+        # lattice first-index slots (all-ones) and compaction counts (zero) ride
+        # in the upload when the level is small (TPE_F_LATTICE_READY): no memsets
+        lat_g = _slice_of(groups, [k for k, _ in groups].index("lat"))
+        lat_ready = lat_g[1] > lat_g[0] and bool(
+            np.all(jobs["flags"][lat_g[0]:lat_g[1]] & L.F_LATTICE_READY))
+        if lat_ready:
+            o_slot = pack.add(self._ones(lat_off))
+            o_lcnt = pack.add(np.zeros(lat_g[1] - lat_g[0], np.int64))
         o_jobs = pack.add(jobs) if jobs.size else None
         o_fb = pack.add(fb_jobs) if fb_jobs.size else None
         o_cand = pack.add(cand_pool)
@@ -998,10 +1017,13 @@ class Engine:
                                                d_bl, d_al, d_x, d_part, npart, db, sp),
                         "tpe_score_pruned64")
             elif kind == "lat":
-                d_slot = self._buf("lat_slot", 8 * lat_off)
                 d_vals = self._buf("lat_vals", 8 * lat_off)
                 d_first = self._buf("lat_first", 8 * lat_off)
-                d_cnt = self._buf("lat_cnt", 8 * nj)
+                if lat_ready:
+                    d_slot, d_cnt = base + o_slot, base + o_lcnt
+                else:
+                    d_slot = self._buf("lat_slot", 8 * lat_off)
+                    d_cnt = self._buf("lat_cnt", 8 * nj)
                 L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_slot,
                                                d_err, ks), "tpe_lattice_sample")
                 L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt, ks),

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 9
+#define TPE_ABI_VERSION 10
 
 enum {
   TPE_OK = 0,
@@ -49,9 +49,15 @@ enum {
   TPE_F_HIGH = 2,       /* upper bound present                               */
   TPE_F_QUANT = 4,      /* quantized (q is not None)                         */
   TPE_F_INJECTED = 8,   /* candidates read from `cand` instead of sampled    */
-  TPE_F_DRAW32 = 16     /* sampled quantized job: draw in fp32 (set only when
+  TPE_F_DRAW32 = 16,    /* sampled quantized job: draw in fp32 (set only when
                            every lattice index |k| <= 2^12, so fp32 resolves a
                            slot to < 2^-11 of q)                              */
+  TPE_F_LATTICE_READY = 32 /* lattice job: the caller has already set its
+                           slot_first region [lat_off, lat_off + lat_n) to
+                           all-ones and its `counts` entry to 0 (e.g. in the
+                           level's upload); when every job of a
+                           tpe_lattice_sample / tpe_lattice_compact call has
+                           it, those calls skip their memsets               */
 };
 
 /*
