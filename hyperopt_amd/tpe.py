@@ -27,6 +27,7 @@ all-gather + device max-loc (hyperopt_amd/dist.py).
 from __future__ import annotations
 
 import functools
+import gc
 import itertools
 import logging
 import os
@@ -531,6 +532,20 @@ def _run_works(eng, items, pw, lf, prec, dev, combine):
 
 
 def suggest_many(requests, shard_studies=False):
+    """Batched suggest over many independent studies; see _suggest_many.  The
+    cyclic garbage collector is paused for the call: a batch allocates a few
+    objects per label and study, and with many studies' trial documents alive
+    a full collection triggered mid-call scans them all (tens of ms)."""
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        return _suggest_many(requests, shard_studies)
+    finally:
+        if enabled:
+            gc.enable()
+
+
+def _suggest_many(requests, shard_studies=False):
     """Batched suggest over many independent studies.
 
     Every study runs tpe.suggest's exact logic, but the labels of all studies
