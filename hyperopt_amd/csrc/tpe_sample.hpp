@@ -294,22 +294,13 @@ __device__ __forceinline__ float draw32(const Mix& M, uint64_t key, int64_t g, b
 // their own lane.  Retried values come back
 // through `wstage`, the wave's R*64 floats of LDS (slot r of lane l at
 // r*64 + l).
-// POOL (kernels whose every thread calls draw32_pairs for one job per block):
-// the block's four wave lists are worked off together -- entry e of the
-// concatenated lists by thread e mod 256 -- so a block holding ~290
-// rejections spends five wave-rounds on them instead of eight (each wave's
-// ~72 would need two rounds of 64 on its own); the block synchronises twice.
 constexpr int kRetryList = 256;  // listed rejections per wave (uint16 entries)
-struct RetryPool {
-  int cnt[kBS / kWave];
-  int64_t g0[kBS];
-};
 
-template <int R, bool POOL = false>
+template <int R>
 __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t g0, int n,
                                              bool lo_on, bool hi_on, float lo, float hi,
                                              bool to_x, float* wstage, uint16_t* wlist,
-                                             float (&x)[R], RetryPool* pool = nullptr) {
+                                             float (&x)[R]) {
   static_assert(R % 4 == 0 && R <= 32, "quads, one mask bit per candidate");
   const int lane = lane_id();
   float* st = wstage + lane;
@@ -337,59 +328,7 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
   auto retry = [&](int64_t g) __attribute__((always_inline)) -> float {
     return retry32(M, key, g, lo_on, hi_on, lo, hi);
   };
-  if constexpr (POOL) {
-    if (lo_on || hi_on) {  // job-uniform, so block-uniform: every thread reaches the barriers
-      const int wid = threadIdx.x / kWave;
-      uint16_t* lists = wlist - wid * kRetryList;
-      float* stages = wstage - wid * (R * kWave);
-      const int cnt = __popc(rej);
-      int incl = cnt;
-#pragma unroll
-      for (int off = 1; off < kWave; off <<= 1) {
-        const int o = __shfl_up(incl, off, kWave);
-        if (lane >= off) incl += o;
-      }
-      int pos = incl - cnt;
-      uint32_t left = 0;
-      for (uint32_t m = rej; m; m &= m - 1) {
-        const int r = __builtin_ctz(m);
-        if (pos < kRetryList)
-          wlist[pos] = (uint16_t)((lane << 5) | r);
-        else
-          left |= 1u << r;
-        ++pos;
-      }
-      if (lane == kWave - 1) pool->cnt[wid] = min(incl, kRetryList);
-      pool->g0[threadIdx.x] = g0;
-      __syncthreads();
-      int off[kBS / kWave], total = 0;
-#pragma unroll
-      for (int w = 0; w < kBS / kWave; ++w) {
-        off[w] = total;
-        total += pool->cnt[w];
-      }
-      for (int b = 0; b < total; b += kBS) {
-        const int e = b + (int)threadIdx.x;
-        if (e < total) {
-          int w = 0;
-#pragma unroll
-          for (int q = 1; q < kBS / kWave; ++q) w += e >= off[q] ? 1 : 0;
-          const int ent = lists[w * kRetryList + (e - off[w])];
-          const int owner = ent >> 5, r = ent & 31;
-          stages[w * (R * kWave) + r * kWave + owner] = retry(pool->g0[w * kWave + owner] + r);
-        }
-      }
-      while (left) {
-        const int r = __builtin_ctz(left);
-        left &= left - 1;
-        st[r * kWave] = retry(g0 + r);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (rej & (1u << r)) x[r] = st[r * kWave];
-    }
-  } else if (__any(rej != 0)) {
+  if (__any(rej != 0)) {
     // list the wave's rejections: exclusive prefix of the lanes' counts
     const int cnt = __popc(rej);
     int incl = cnt;

@@ -790,7 +790,6 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   __shared__ MixLds s_mix;
   __shared__ float s_stage[kLatR * kBS];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
-  __shared__ RetryPool s_pool;
   // XCD-aware work order (as k_score_table): each XCD sweeps a contiguous
   // eighth of the (job, tile) list, so a job's first-index atomics stay in
   // few XCDs' L2s
@@ -818,16 +817,9 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
     const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
     float x[kLatR];
-#ifdef TPE_NO_RETRY_POOL  // diagnostic: per-wave retry lists
     draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
-                        s_list + (threadIdx.x / kWave) * kRetryList, x);
-#else
-    draw32_pairs<kLatR, true>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                              (float)J.high, lgmm,
-                              s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
-                              s_list + (threadIdx.x / kWave) * kRetryList, x, &s_pool);
-#endif
+                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList,
+                        x);
     const float inv_q32 = (float)(1.0 / J.q);
     const int kmin = (int)J.lat_kmin, nl = (int)J.lat_n;
 #pragma unroll

@@ -977,15 +977,8 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
   const int nvalid = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
   float x[kTR];  // candidates in the scoring coordinate y (log x for LGMM1)
-#ifdef TPE_NO_RETRY_POOL  // diagnostic: per-wave retry lists
   draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nvalid, lo_on, hi_on, (float)J.low,
                     (float)J.high, false, stage, s_list + (threadIdx.x / kWave) * kRetryList, x);
-#else
-  __shared__ RetryPool s_pool;
-  draw32_pairs<kTR, true>(M, J.key, J.cand_base + t0, nvalid, lo_on, hi_on, (float)J.low,
-                          (float)J.high, false, stage, s_list + (threadIdx.x / kWave) * kRetryList,
-                          x, &s_pool);
-#endif
   auto cell_of = [&](float y) __attribute__((always_inline)) -> int {
     const float t = (y - g0) * inv_w;
     const int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
