@@ -110,6 +110,8 @@ _hip = None
 
 H2D, D2H = 1, 2  # hipMemcpyKind
 EVENT_NO_TIMING = 0x2  # hipEventDisableTiming
+CAPTURE_RELAXED = 2  # hipStreamCaptureModeRelaxed
+CAPTURE_SET_DEPENDENCIES = 1  # hipStreamSetCaptureDependencies
 
 
 def hip():
@@ -125,7 +127,26 @@ def hip():
                            ("hipEventRecord", [_P, _P]),
                            ("hipStreamWaitEvent", [_P, _P, ctypes.c_uint]),
                            ("hipEventSynchronize", [_P]),
-                           ("hipStreamSynchronize", [_P])):
+                           ("hipStreamSynchronize", [_P]),
+                           # level graphs (Engine.run): capture once, replay per call
+                           ("hipGetLastError", []),
+                           ("hipEventElapsedTime", [ctypes.POINTER(ctypes.c_float), _P, _P]),
+                           ("hipEventDestroy", [_P]),
+                           ("hipStreamBeginCapture", [_P, _I]),
+                           ("hipStreamEndCapture", [_P, ctypes.POINTER(_P)]),
+                           ("hipGraphInstantiate", [ctypes.POINTER(_P), _P, _P, _P,
+                                                    ctypes.c_size_t]),
+                           ("hipGraphLaunch", [_P, _P]),
+                           ("hipStreamGetCaptureInfo_v2",
+                            [_P, ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_ulonglong),
+                             ctypes.POINTER(_P), ctypes.POINTER(ctypes.POINTER(_P)),
+                             ctypes.POINTER(ctypes.c_size_t)]),
+                           ("hipGraphAddEventRecordNode",
+                            [ctypes.POINTER(_P), _P, ctypes.POINTER(_P), ctypes.c_size_t, _P]),
+                           ("hipStreamUpdateCaptureDependencies",
+                            [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.c_uint]),
+                           ("hipGraphExecDestroy", [_P]),
+                           ("hipGraphDestroy", [_P])):
             fn = getattr(h, name)
             fn.restype = _I
             fn.argtypes = args

@@ -284,6 +284,20 @@ class Engine:
         # once the above mixture has PRUNED64_MIN_COMP components, "dense"
         # always sums every component (tpe_score_continuous), "pruned" always prunes
         self.exact64 = os.environ.get("TPE_EXACT64", "auto")
+        # level graphs (opt-in, TPE_GRAPHS=1): a level whose launch sequence
+        # (kernels, grids, workspace pointers, every scalar argument) repeats
+        # the previous call's is captured into a hipGraph once and replayed
+        # with one hipGraphLaunch (the per-call inputs -- split flags, counts,
+        # Philox keys -- arrive through the level's upload, outside the graph).
+        # Off by default: on ROCm 7 a replayed C3 level is slower than the
+        # eager launches (1.21 vs 1.13 ms on one stream, 1.33 vs 1.06 ms with
+        # the side stream)
+        self.graphs = os.environ.get("TPE_GRAPHS", "0") == "1"
+        self._graphs = {}       # launch key -> _LevelGraph
+        self._last_gkey = None  # launch key of the previous eager level
+        self._gen = 0           # bumped whenever a workspace buffer is (re)allocated
+        self._own = None        # the engine's own stream (capture needs a non-null stream)
+        self.graph_stats = {"captured": 0, "replayed": 0, "eager": 0}
 
     # -- memory --------------------------------------------------------------
     def _buf(self, name, nbytes):
@@ -295,7 +309,13 @@ class Engine:
             t = self.torch.empty(_align(int(nbytes * 1.25)), dtype=self.torch.uint8,
                                  device=self.device)
             self._bufs[name] = t
+            self._gen += 1  # captured graphs hold the old pointers
         return t.data_ptr()
+
+    def _drop_graphs(self):
+        for g in self._graphs.values():
+            g.destroy(self._hip)
+        self._graphs.clear()
 
     def _ones(self, n):
         """n all-ones uint64 words (cached)."""
@@ -504,16 +524,6 @@ class Engine:
                 hp.append((name, time.perf_counter()))
         _hmark("start")
 
-        def tick(name, on=None):
-            if timers is None or (timer_groups is not None and name not in timer_groups):
-                return None
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(stream if on is None else on)
-            return e
-
-        def tock(name, e0, on=None):
-            if e0 is not None:
-                timers.setdefault(name, []).append((e0, tick(name, on)))
         lib = self.lib
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
@@ -545,6 +555,19 @@ class Engine:
                     (w.n_above if w.obs_above is None else np.size(w.obs_above) for w in works),
                     np.int64, len(works))),)
             cached = self._plans.get(pkey) if pkey is not None else None
+        # graph-eligible levels run on the engine's own stream (ordered after
+        # the caller's): stream capture is not allowed on the null stream
+        graph_ok = self.graphs and pkey is not None and not (
+            outputs or sample_only or posteriors or table_scores)
+        caller_p = None
+        if graph_ok:
+            if self._own is None:
+                self._own = torch.cuda.Stream(self.device)
+            if self._own.cuda_stream != stream.cuda_stream:
+                caller_p = sp
+                stream = self._own
+                sp = ctypes.c_void_p(stream.cuda_stream)
+                self._order("enter", caller_p, sp)
         pack = _Pack()
         if cached is not None:
             cols = (batch.n_below, batch.n_above, batch.keys, batch.cand_base) \
@@ -852,224 +875,297 @@ class Engine:
         if cat:
             d_logp = self._buf("cat_logp", 8 * p_pool.size)
             d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
-        if hist_mode:
-            d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
-            d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
-            e0 = tick("gather")
-            if histories is None:
-                L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
-                                           history.ld,
-                                           base + o_rows if o_rows is not None else None,
-                                           n_rows, base + o_isb, base + o_g,
-                                           g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr),
-                                           d_obs, d_cobs, d_err, sp), "tpe_gather_obs")
-            else:
-                L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
-                                                 len(h_arr), base, base + o_g,
-                                                 g_arr.ctypes.data_as(ctypes.c_void_p),
-                                                 len(g_arr), d_obs, d_cobs, d_err, sp),
-                        "tpe_gather_obs_multi")
-            tock("gather", e0)
-        else:
-            d_obs, d_cobs = base + o_obs, base + o_cobs
-
-        _hmark('upload+gather')
-        # side stream (TPE_SIDE_STREAM != "0"): quantized and categorical work
-        # overlaps the continuous pipeline; the categorical posterior starts on
-        # it as soon as the lists are gathered (it needs nothing else)
-        side = None
-        if self.side_stream != "0" and not sample_only and not posteriors and any(
-                ids for k, ids in groups if k in SIDE_KINDS):
-            if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
-            side = self._side
-        side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
-        if side is not None:
-            self._order("gathered", sp, side_p)
-        # ---- posterior fit ------------------------------------------------------
-        if fit_ids:
-            e0 = tick("fit")
-            L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
-                                       n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
-                                       d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
-            tock("fit", e0)
-        if cat:
-            e0 = tick("cat_fit", side)
-            d_p = base + o_p  # the posterior is formed in place in the staged pool
-            L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
-                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
-                                          side_p), "tpe_cat_posterior")
-            tock("cat_fit", e0, side)
-
-        if posteriors:
-            return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
-                                         d_segs, stream, o_p)
-
         self.last_plan = (segs, csegs, g_arr if hist_mode else None, jobs, cached is not None)
-        _hmark('jobs')
-        d_cand = base + o_cand
-        d_bl = d_al = d_x = None
-        d_sc = None
-        if outputs:
-            d_bl = self._buf("out_bl", 8 * max(out_off, 1))
-            d_al = self._buf("out_al", 8 * max(out_off, 1))
-            d_x = self._buf("out_x", 8 * max(out_off, 1))
-        elif table_scores:
-            d_sc = self._buf("out_sc", 8 * max(out_off, 1))
-            d_x = self._buf("out_x", 8 * max(out_off, 1))
 
-        _hmark('fit')
-        # ---- scoring, one call per group ----------------------------------------
-        # quantized and categorical groups go to the side stream (after the job
-        # table has landed); continuous groups stay on `stream`
-        if side is not None:  # quantized groups need the continuous fit
-            self._order("fitted", sp, side_p)
-        table_calls = []
-        jobs_ptr = jobs.__array_interface__["data"][0]
-        g_order = list(range(len(groups)))
-        if side is not None:  # side groups launched first
-            g_order.sort(key=lambda g: groups[g][0] not in SIDE_KINDS)
-        joined = side is None
-        for g in g_order:
-            kind, ids = groups[g]
-            if not ids:
-                continue
-            if sample_only:
-                if kind in ("cont", "lat", "qfb"):
-                    a, b = _slice_of(groups, g)
-                    hj = jobs[a:b]
-                    L.check(lib.tpe_sample(base + o_jobs + a * L.JOB_DTYPE.itemsize,
-                                           hj.ctypes.data_as(ctypes.c_void_p), b - a, d_segs,
-                                           d_mu, d_sig, d_cdf, precision, d_x, sp), "tpe_sample")
-                continue
-            a, b = _slice_of(groups, g)
-            hj = jobs[a:b]
-            hjp = jobs_ptr + a * JS  # host copy of the slice (plain int: no ctypes object)
-            dj = base + o_jobs + a * JS
-            db = d_best + a * BS
-            nj = b - a
-            on_side = side is not None and kind in SIDE_KINDS
-            ks = side_p if on_side else sp
-            kst = side if on_side else None
-            pname = "partial_side" if on_side else "partial"
-            e0 = tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst)
-            if kind == "cont":
-                npart = lib.tpe_score_partials(hjp, nj)
-                d_part = self._buf("partial", 32 * max(npart, 1))
-                L.check(lib.tpe_score_continuous(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
-                                                 d_c64, d_c32, d_cand, precision, d_bl, d_al, d_x,
-                                                 d_part, npart, db, sp), "tpe_score_continuous")
-            elif kind == "sorted":
-                npart = lib.tpe_score_partials(hjp, nj) * 2
-                d_part = self._buf("partial", 32 * max(npart, 1))
-                d_cnt = self._buf("sort_cnt", 8 * max(cnt_off, 1))
-                d_gen = self._buf("sort_gen", 4 * max(sort_off, 1))
-                d_sx = self._buf("sort_x", 4 * max(sort_off, 1))
-                d_si = self._buf("sort_i", 4 * max(sort_off, 1))
-                L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
-                                                d_gen, d_sx, d_si, sp), "tpe_sort_candidates")
-                tock("sort", e0)
-                e0 = tick("sorted")
-                L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,
-                                             d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
-                        "tpe_score_sorted")
-            elif kind == "table":
-                npart = lib.tpe_table_partials(hjp, nj)
-                d_part = self._buf("partial", 32 * max(npart, 1))
-                d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
-                d_cells = self._buf("cells", 128 * int(hj["tbl_off"].max() + TABLE_CAP
-                                                       - hj["tbl_off"].min()))
-                d_cells -= 128 * int(hj["tbl_off"].min())
-                d_rh = self._buf("reach_hi", 8 * n_comp)
-                d_rl = self._buf("reach_lo", 8 * n_comp)
-                d_wide = self._buf("wide_idx", 4 * n_comp)
-                max_comp = max_obs + 1
-                d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
-                L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64, max_comp,
-                                            d_rh, d_rl, d_wide, d_tsc, d_tab, d_cells, d_stats,
-                                            sp), "tpe_table_build")
-                tock("table_build", e0)
-                if not joined and self.side_stream == "2":
-                    self._order("joined", side_p, sp)
-                    joined = True
-                e0 = tick("table")
-                if outputs or inj(ids[0]) or self.table_scorer == "poly":
-                    L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32,
-                                                d_tab, d_cells, d_cand, d_bl, d_al, d_x, d_part,
-                                                npart, db, d_stats, sp), "tpe_score_table")
-                else:  # the suggest path: one score cubic per candidate
-                    L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
-                                                     d_c32, d_tab, d_cells, d_sc, d_x, d_part,
-                                                     npart, db, d_stats, sp),
-                            "tpe_score_table_fast")
-                table_calls.append(nj)
-            elif kind == "pruned64":
-                npart = lib.tpe_pruned64_partials(hjp, nj)
-                d_part = self._buf("partial", 32 * max(npart, 1))
-                d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
-                d_rh = self._buf("reach_hi", 8 * n_comp)
-                d_rl = self._buf("reach_lo", 8 * n_comp)
-                d_wide = self._buf("wide_idx", 4 * n_comp)
-                max_comp = max_obs + 1
-                d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
-                L.check(lib.tpe_score_pruned64(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c64,
-                                               max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab, d_cand,
-                                               d_bl, d_al, d_x, d_part, npart, db, sp),
-                        "tpe_score_pruned64")
-            elif kind == "lat":
-                d_vals = self._buf("lat_vals", 8 * lat_off)
-                d_first = self._buf("lat_first", 8 * lat_off)
-                if lat_ready:
-                    d_slot, d_cnt = base + o_slot, base + o_lcnt
-                else:
-                    d_slot = self._buf("lat_slot", 8 * lat_off)
-                    d_cnt = self._buf("lat_cnt", 8 * nj)
-                L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_slot,
-                                               d_err, ks), "tpe_lattice_sample")
-                L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt, ks),
-                        "tpe_lattice_compact")
-                max_vals = int(hj["lat_n"].max())
-                npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                d_part = self._buf(pname, 32 * max(npart, 1))
-                L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_vals,
-                                                d_first, d_cnt, max_vals, None, None, d_part,
-                                                npart, db, d_err, ks), "tpe_score_quantized")
-            elif kind in ("qfb", "qinj"):
-                vals = d_cand
-                if kind == "qfb":
-                    vals = self._buf("q_cand", 8 * max(qfb_off, 1))
-                    L.check(lib.tpe_sample(base + o_fb, fb_jobs.ctypes.data_as(ctypes.c_void_p),
-                                           nj, d_segs, d_mu, d_sig, d_cdf, 64, vals, ks),
-                            "tpe_sample")
-                max_vals = int(hj["n_cand"].max())
-                npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                d_part = self._buf(pname, 32 * max(npart, 1))
-                L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, vals, None,
-                                                None, max_vals, d_bl, d_al, d_part, npart, db,
-                                                d_err, ks), "tpe_score_quantized")
+        # ---- the level's launches (eager, captured into a graph, or replayed) ----
+        # Every argument below is a workspace pointer (unchanged while _gen is),
+        # an offset into the staged pack, or a size covered by the launch key;
+        # the values that change from call to call live in the uploaded pack.
+        gkey = None
+        if graph_ok:
+            gkey = (pkey, self._gen, tuple(off for off, _ in pack.parts), n_obs_total, max_obs,
+                    cobs_off, lat_off,
+                    (history.vals.data_ptr(), history.active.data_ptr(), history.ld, n_rows)
+                    if history is not None else None,
+                    self.side_stream, self.table_scorer, self.exact64,
+                    None if timers is None else
+                    (None if timer_groups is None else frozenset(timer_groups)))
+        cap = None  # _LevelGraph being captured (tick/tock then record graph nodes)
+
+        def tick(name, on=None):
+            if timers is None or (timer_groups is not None and name not in timer_groups):
+                return None
+            if cap is not None:
+                return cap.record(self._hip, stream if on is None else on)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream if on is None else on)
+            return e
+
+        def tock(name, e0, on=None):
+            if e0 is None:
+                return
+            if cap is not None:
+                cap.timed.append((name, e0, tick(name, on)))
             else:
-                npart = lib.tpe_categorical_partials(hjp, nj)
-                d_part = self._buf(pname, 32 * max(npart, 1))
-                L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf, d_cand,
-                                                  d_bl, d_al, d_x, d_part, npart, db, ks),
-                        "tpe_score_categorical")
-            tock(kind, e0, kst)
+                timers.setdefault(name, []).append((e0, tick(name, on)))
 
-        if not joined:  # join before the readback
-            self._order("joined", side_p, sp)
+        def launch_level():
+            if hist_mode:
+                d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
+                d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
+                e0 = tick("gather")
+                if histories is None:
+                    L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
+                                               history.ld,
+                                               base + o_rows if o_rows is not None else None,
+                                               n_rows, base + o_isb, base + o_g,
+                                               g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr),
+                                               d_obs, d_cobs, d_err, sp), "tpe_gather_obs")
+                else:
+                    L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
+                                                     len(h_arr), base, base + o_g,
+                                                     g_arr.ctypes.data_as(ctypes.c_void_p),
+                                                     len(g_arr), d_obs, d_cobs, d_err, sp),
+                            "tpe_gather_obs_multi")
+                tock("gather", e0)
+            else:
+                d_obs, d_cobs = base + o_obs, base + o_cobs
+
+            _hmark('upload+gather')
+            # side stream (TPE_SIDE_STREAM != "0"): quantized and categorical work
+            # overlaps the continuous pipeline; the categorical posterior starts on
+            # it as soon as the lists are gathered (it needs nothing else)
+            side = None
+            if self.side_stream != "0" and not sample_only and not posteriors and any(
+                    ids for k, ids in groups if k in SIDE_KINDS):
+                if self._side is None:
+                    self._side = torch.cuda.Stream(self.device)
+                side = self._side
+            side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
+            if side is not None:
+                self._order("gathered", sp, side_p)
+            # ---- posterior fit ------------------------------------------------------
+            if fit_ids:
+                e0 = tick("fit")
+                L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
+                                           n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
+                                           d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
+                tock("fit", e0)
+            if cat:
+                e0 = tick("cat_fit", side)
+                d_p = base + o_p  # the posterior is formed in place in the staged pool
+                L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
+                                              int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
+                                              side_p), "tpe_cat_posterior")
+                tock("cat_fit", e0, side)
+
+            if posteriors:
+                return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
+                                             d_segs, stream, o_p), True
+
+            _hmark('jobs')
+            d_cand = base + o_cand
+            d_bl = d_al = d_x = None
+            d_sc = None
+            if outputs:
+                d_bl = self._buf("out_bl", 8 * max(out_off, 1))
+                d_al = self._buf("out_al", 8 * max(out_off, 1))
+                d_x = self._buf("out_x", 8 * max(out_off, 1))
+            elif table_scores:
+                d_sc = self._buf("out_sc", 8 * max(out_off, 1))
+                d_x = self._buf("out_x", 8 * max(out_off, 1))
+
+            _hmark('fit')
+            # ---- scoring, one call per group ----------------------------------------
+            # quantized and categorical groups go to the side stream (after the job
+            # table has landed); continuous groups stay on `stream`
+            if side is not None:  # quantized groups need the continuous fit
+                self._order("fitted", sp, side_p)
+            table_calls = []
+            jobs_ptr = jobs.__array_interface__["data"][0]
+            g_order = list(range(len(groups)))
+            if side is not None:  # side groups launched first
+                g_order.sort(key=lambda g: groups[g][0] not in SIDE_KINDS)
+            joined = side is None
+            for g in g_order:
+                kind, ids = groups[g]
+                if not ids:
+                    continue
+                if sample_only:
+                    if kind in ("cont", "lat", "qfb"):
+                        a, b = _slice_of(groups, g)
+                        hj = jobs[a:b]
+                        L.check(lib.tpe_sample(base + o_jobs + a * L.JOB_DTYPE.itemsize,
+                                               hj.ctypes.data_as(ctypes.c_void_p), b - a, d_segs,
+                                               d_mu, d_sig, d_cdf, precision, d_x, sp), "tpe_sample")
+                    continue
+                a, b = _slice_of(groups, g)
+                hj = jobs[a:b]
+                hjp = jobs_ptr + a * JS  # host copy of the slice (plain int: no ctypes object)
+                dj = base + o_jobs + a * JS
+                db = d_best + a * BS
+                nj = b - a
+                on_side = side is not None and kind in SIDE_KINDS
+                ks = side_p if on_side else sp
+                kst = side if on_side else None
+                pname = "partial_side" if on_side else "partial"
+                e0 = tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst)
+                if kind == "cont":
+                    npart = lib.tpe_score_partials(hjp, nj)
+                    d_part = self._buf("partial", 32 * max(npart, 1))
+                    L.check(lib.tpe_score_continuous(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
+                                                     d_c64, d_c32, d_cand, precision, d_bl, d_al, d_x,
+                                                     d_part, npart, db, sp), "tpe_score_continuous")
+                elif kind == "sorted":
+                    npart = lib.tpe_score_partials(hjp, nj) * 2
+                    d_part = self._buf("partial", 32 * max(npart, 1))
+                    d_cnt = self._buf("sort_cnt", 8 * max(cnt_off, 1))
+                    d_gen = self._buf("sort_gen", 4 * max(sort_off, 1))
+                    d_sx = self._buf("sort_x", 4 * max(sort_off, 1))
+                    d_si = self._buf("sort_i", 4 * max(sort_off, 1))
+                    L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
+                                                    d_gen, d_sx, d_si, sp), "tpe_sort_candidates")
+                    tock("sort", e0)
+                    e0 = tick("sorted")
+                    L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,
+                                                 d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
+                            "tpe_score_sorted")
+                elif kind == "table":
+                    npart = lib.tpe_table_partials(hjp, nj)
+                    d_part = self._buf("partial", 32 * max(npart, 1))
+                    d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
+                    d_cells = self._buf("cells", 128 * int(hj["tbl_off"].max() + TABLE_CAP
+                                                           - hj["tbl_off"].min()))
+                    d_cells -= 128 * int(hj["tbl_off"].min())
+                    d_rh = self._buf("reach_hi", 8 * n_comp)
+                    d_rl = self._buf("reach_lo", 8 * n_comp)
+                    d_wide = self._buf("wide_idx", 4 * n_comp)
+                    max_comp = max_obs + 1
+                    d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
+                    L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64, max_comp,
+                                                d_rh, d_rl, d_wide, d_tsc, d_tab, d_cells, d_stats,
+                                                sp), "tpe_table_build")
+                    tock("table_build", e0)
+                    if not joined and self.side_stream == "2":
+                        self._order("joined", side_p, sp)
+                        joined = True
+                    e0 = tick("table")
+                    if outputs or inj(ids[0]) or self.table_scorer == "poly":
+                        L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32,
+                                                    d_tab, d_cells, d_cand, d_bl, d_al, d_x, d_part,
+                                                    npart, db, d_stats, sp), "tpe_score_table")
+                    else:  # the suggest path: one score cubic per candidate
+                        L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
+                                                         d_c32, d_tab, d_cells, d_sc, d_x, d_part,
+                                                         npart, db, d_stats, sp),
+                                "tpe_score_table_fast")
+                    table_calls.append(nj)
+                elif kind == "pruned64":
+                    npart = lib.tpe_pruned64_partials(hjp, nj)
+                    d_part = self._buf("partial", 32 * max(npart, 1))
+                    d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
+                    d_rh = self._buf("reach_hi", 8 * n_comp)
+                    d_rl = self._buf("reach_lo", 8 * n_comp)
+                    d_wide = self._buf("wide_idx", 4 * n_comp)
+                    max_comp = max_obs + 1
+                    d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
+                    L.check(lib.tpe_score_pruned64(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c64,
+                                                   max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab, d_cand,
+                                                   d_bl, d_al, d_x, d_part, npart, db, sp),
+                            "tpe_score_pruned64")
+                elif kind == "lat":
+                    d_vals = self._buf("lat_vals", 8 * lat_off)
+                    d_first = self._buf("lat_first", 8 * lat_off)
+                    if lat_ready:
+                        d_slot, d_cnt = base + o_slot, base + o_lcnt
+                    else:
+                        d_slot = self._buf("lat_slot", 8 * lat_off)
+                        d_cnt = self._buf("lat_cnt", 8 * nj)
+                    L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_slot,
+                                                   d_err, ks), "tpe_lattice_sample")
+                    L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt, ks),
+                            "tpe_lattice_compact")
+                    max_vals = int(hj["lat_n"].max())
+                    npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+                    d_part = self._buf(pname, 32 * max(npart, 1))
+                    L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_vals,
+                                                    d_first, d_cnt, max_vals, None, None, d_part,
+                                                    npart, db, d_err, ks), "tpe_score_quantized")
+                elif kind in ("qfb", "qinj"):
+                    vals = d_cand
+                    if kind == "qfb":
+                        vals = self._buf("q_cand", 8 * max(qfb_off, 1))
+                        L.check(lib.tpe_sample(base + o_fb, fb_jobs.ctypes.data_as(ctypes.c_void_p),
+                                               nj, d_segs, d_mu, d_sig, d_cdf, 64, vals, ks),
+                                "tpe_sample")
+                    max_vals = int(hj["n_cand"].max())
+                    npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+                    d_part = self._buf(pname, 32 * max(npart, 1))
+                    L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, vals, None,
+                                                    None, max_vals, d_bl, d_al, d_part, npart, db,
+                                                    d_err, ks), "tpe_score_quantized")
+                else:
+                    npart = lib.tpe_categorical_partials(hjp, nj)
+                    d_part = self._buf(pname, 32 * max(npart, 1))
+                    L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf, d_cand,
+                                                      d_bl, d_al, d_x, d_part, npart, db, ks),
+                            "tpe_score_categorical")
+                tock(kind, e0, kst)
+
+            if not joined:  # join before the readback
+                self._order("joined", side_p, sp)
+            return table_calls, False
+
+        graph = self._graphs.get(gkey) if gkey is not None else None
+        if graph is None and gkey is not None and gkey == self._last_gkey:
+            # the second call in a row with this launch key: capture it
+            cap = _LevelGraph()
+            try:
+                graph = cap.capture(self, sp, launch_level)
+            except L.TpeHipError:  # capture unsupported here: eager from now on
+                self.graphs = False
+                self._drop_graphs()
+                graph = None
+            finally:
+                cap = None
+            if graph is not None and graph.gen == self._gen:
+                if len(self._graphs) >= 8 or any(g.gen != self._gen for g in self._graphs.values()):
+                    self._drop_graphs()
+                self._graphs[gkey] = graph
+                self.graph_stats["captured"] += 1
+            elif graph is not None:  # a buffer grew during the capture: not replayable
+                graph.destroy(self._hip)
+                graph = None
+        if graph is not None:
+            L.hip_check(self._hip.hipGraphLaunch(graph.exec, sp), "hipGraphLaunch")
+            self.graph_stats["replayed"] += 1
+            table_calls = graph.table_calls
+        else:
+            table_calls, post = launch_level()
+            if post:
+                return table_calls
+            self._last_gkey = gkey
+            self.graph_stats["eager"] += 1
         _hmark('score launches')
         # ---- results: one device->host copy of the result block into pinned memory
         nbytes = 64 + n_jobs * BS
         pin = self._res_pinned(nbytes)
         L.hip_check(self._hip.hipMemcpyAsync(pin.data_ptr(), d_res, nbytes, L.D2H, sp),
                     "hipMemcpyAsync")
+        after = None
+        if graph is not None and graph.timed and timers is not None:
+            after = functools.partial(graph.read_timers, self._hip, timers)
         if batch is not None:  # queued readback (see _Pending)
             ev = self._event("result")
             L.hip_check(self._hip.hipEventRecord(ev, sp), "hipEventRecord")
+            if caller_p is not None:  # the caller's later work follows this level
+                L.hip_check(self._hip.hipStreamWaitEvent(caller_p, ev, 0), "hipStreamWaitEvent")
             p = self._inflight = _Pending(self, ev, pin, nbytes, np.asarray(order, np.int64),
-                                          bool(table_calls))
+                                          bool(table_calls), after)
             return p if defer else p.result()
         L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
+        if after is not None:
+            after()
         res_h = pin[:nbytes].numpy().copy()
         best_h = res_h[64:].view(L.BEST_DTYPE)
         with torch.cuda.stream(stream):
@@ -1153,15 +1249,18 @@ class _Pending(object):
     with defer=True).  ``result()`` waits for it once, checks the error bits
     and returns the BatchResult (cached)."""
 
-    def __init__(self, eng, event, pin, nbytes, order, table):
+    def __init__(self, eng, event, pin, nbytes, order, table, after=None):
         self.eng, self.event, self.pin, self.nbytes = eng, event, pin, nbytes
-        self.order, self.table = order, table
+        self.order, self.table, self.after = order, table, after
         self._res = None
 
     def result(self):
         if self._res is not None:
             return self._res
         L.hip_check(self.eng._hip.hipEventSynchronize(self.event), "hipEventSynchronize")
+        if self.after is not None:
+            self.after()
+            self.after = None
         eng = self.eng
         if eng._inflight is self:
             eng._inflight = None
@@ -1181,6 +1280,102 @@ class _Pending(object):
         self._res = BatchResult(by["index"].copy(), by["value"].copy(), by["score"].copy(),
                                 by["n_scored"].copy())
         return self._res
+
+
+class _Timed(object):
+    """A kernel-group duration read from a replayed level graph's event
+    nodes, in the shape of Engine.run's (start, end) timer pairs:
+    ``pair[0].elapsed_time(pair[1])`` gives milliseconds."""
+    __slots__ = ("ms",)
+
+    def __init__(self, ms):
+        self.ms = ms
+
+    def elapsed_time(self, _end):
+        return self.ms
+
+
+class _LevelGraph(object):
+    """One level's launch sequence captured into a hipGraph (Engine.run).
+
+    Captured from the launches of a level whose launch key repeats (the
+    kernels, grids, workspace pointers and scalar arguments are then equal),
+    replayed by one hipGraphLaunch after the level's upload.  Timer groups
+    become external event-record nodes; their durations are read after the
+    level's readback (``read_timers``)."""
+    __slots__ = ("exec", "graph", "gen", "table_calls", "timed", "events")
+
+    def __init__(self):
+        self.exec = self.graph = None
+        self.gen = -1
+        self.table_calls = []
+        self.timed = []   # (group, start event, end event) recorded by graph nodes
+        self.events = []
+
+    def record(self, hip, stream):
+        """A timing event recorded by a node of the graph being captured on
+        `stream`: the node is added to the capture's graph after the stream's
+        current dependencies and becomes the stream's only dependency (HIP
+        captures a plain hipEventRecord as an ordering edge only, and refuses
+        hipEventRecordExternal during capture)."""
+        h = ctypes.c_void_p()
+        L.hip_check(hip.hipEventCreateWithFlags(ctypes.byref(h), 0), "hipEventCreateWithFlags")
+        self.events.append(h)
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        status, cid, graph = ctypes.c_int(), ctypes.c_ulonglong(), ctypes.c_void_p()
+        deps, n_deps = ctypes.POINTER(ctypes.c_void_p)(), ctypes.c_size_t()
+        L.hip_check(hip.hipStreamGetCaptureInfo_v2(sp, ctypes.byref(status), ctypes.byref(cid),
+                                                   ctypes.byref(graph), ctypes.byref(deps),
+                                                   ctypes.byref(n_deps)),
+                    "hipStreamGetCaptureInfo_v2")
+        node = ctypes.c_void_p()
+        L.hip_check(hip.hipGraphAddEventRecordNode(ctypes.byref(node), graph, deps, n_deps.value,
+                                                   h), "hipGraphAddEventRecordNode")
+        L.hip_check(hip.hipStreamUpdateCaptureDependencies(sp, ctypes.byref(node), 1,
+                                                           L.CAPTURE_SET_DEPENDENCIES),
+                    "hipStreamUpdateCaptureDependencies")
+        return h
+
+    def capture(self, eng, sp, launch):
+        hip = eng._hip
+        gen0 = eng._gen
+        L.hip_check(hip.hipStreamBeginCapture(sp, L.CAPTURE_RELAXED), "hipStreamBeginCapture")
+        g = ctypes.c_void_p()
+        try:
+            self.table_calls, _ = launch()
+        except BaseException:
+            hip.hipStreamEndCapture(sp, ctypes.byref(g))
+            if g.value:
+                hip.hipGraphDestroy(g)
+            hip.hipGetLastError()  # the failed capture's status is not the next launch's
+            self.destroy(hip)
+            raise
+        L.hip_check(hip.hipStreamEndCapture(sp, ctypes.byref(g)), "hipStreamEndCapture")
+        self.graph = g
+        e = ctypes.c_void_p()
+        rc = hip.hipGraphInstantiate(ctypes.byref(e), g, None, None, 0)
+        if rc != 0:
+            self.destroy(hip)
+            L.hip_check(rc, "hipGraphInstantiate")
+        self.exec = e
+        self.gen = gen0 if eng._gen == gen0 else -1
+        return self
+
+    def read_timers(self, hip, timers):
+        ms = ctypes.c_float()
+        for name, e0, e1 in self.timed:
+            L.hip_check(hip.hipEventElapsedTime(ctypes.byref(ms), e0, e1), "hipEventElapsedTime")
+            timers.setdefault(name, []).append((_Timed(ms.value), None))
+
+    def destroy(self, hip):
+        if self.exec is not None:
+            hip.hipGraphExecDestroy(self.exec)
+        if self.graph is not None:
+            hip.hipGraphDestroy(self.graph)
+        for h in self.events:
+            hip.hipEventDestroy(h)
+        self.exec = self.graph = None
+        self.events = []
 
 
 def _raise_errors(err):

@@ -1,0 +1,143 @@
+"""Level graphs (Engine.run, opt-in TPE_GRAPHS=1): a level whose launch key repeats is
+captured into a hipGraph on its second call and replayed afterwards.
+
+The per-call inputs (split flags, observation counts, Philox keys) travel in
+the level's upload, outside the graph, so a replayed level must give exactly
+what an eager engine gives on the same inputs: every label's winner index,
+value, score and n_scored, byte for byte, for every prior kind and scorer
+path.  A changed history (new counts), a grown workspace buffer or another
+structure must never replay a stale graph.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SPACE = [("u", "uniform", (-5.0, 5.0)), ("lu", "loguniform", (-5.0, 0.0)),
+         ("q", "quniform", (0.0, 20.0, 1.0)), ("n", "normal", (0.0, 2.0)),
+         ("qn", "qnormal", (0.0, 3.0, 0.5)), ("ln", "lognormal", (0.0, 1.0)),
+         ("c", "randint", (6,)), ("r", "randint", (3, 11)),
+         ("k", "categorical", ((0.1, 0.2, 0.3, 0.4),))]
+
+
+def _history(T, seed):
+    rng = np.random.RandomState(seed)
+    cols = [rng.uniform(-5, 5, T), np.exp(rng.uniform(-5, 0, T)),
+            np.round(rng.uniform(0, 20, T)), rng.normal(0, 2, T),
+            np.round(rng.normal(0, 3, T) / 0.5) * 0.5, np.exp(rng.normal(0, 1, T)),
+            rng.randint(0, 6, T).astype(float), rng.randint(3, 11, T).astype(float),
+            rng.randint(0, 4, T).astype(float)]
+    mat = np.stack(cols, axis=1)
+    active = rng.uniform(size=mat.shape) >= 0.1
+    return mat, active, rng.normal(size=T)
+
+
+def _works(mat, active, losses, T, step, n_cand):
+    from hyperopt_amd.engine import LabelWork
+    n_below = min(int(np.ceil(0.25 * np.sqrt(T))), 25)
+    isb = np.zeros(T, np.uint8)
+    isb[np.argsort(losses[:T], kind="stable")[:n_below]] = 1
+    works = []
+    for j, (lab, kind, a) in enumerate(SPACE):
+        act = active[:T, j]
+        below = mat[:T, j][act & (isb == 1)]
+        n_above = int((act & (isb == 0)).sum())
+        works.append(LabelWork(lab, kind, a, below, None, n_cand=n_cand,
+                               key=7919 * step + 31 * j + 5, cand_base=0, col=j,
+                               n_above=n_above))
+    return works, isb
+
+
+def _rows(res):
+    return [(r.label, r.index, r.value, r.score, r.n_scored) for r in res]
+
+
+def _pair():
+    from hyperopt_amd.engine import DeviceHistory, Engine
+    eager, graph = Engine(), Engine()
+    eager.graphs, graph.graphs = False, True
+    return eager, graph, DeviceHistory
+
+
+@pytest.mark.parametrize("n_cand", [24, 1 << 18])
+def test_replayed_level_equals_eager(n_cand):
+    eager, graph, DeviceHistory = _pair()
+    mat, active, losses = _history(3000, 11)
+    he = DeviceHistory(eager, len(SPACE), cap=4096)
+    hg = DeviceHistory(graph, len(SPACE), cap=4096)
+    for h in (he, hg):
+        h.append(mat, active)
+    for step in range(6):  # new Philox keys every call, same counts: graph hits
+        works, isb = _works(mat, active, losses, 3000, step, n_cand)
+        a = eager.run(works, history=he, is_below=isb)
+        b = graph.run(works, history=hg, is_below=isb)
+        assert _rows(a) == _rows(b), step
+    st = graph.graph_stats
+    # the first call sizes the workspace, a call whose key repeats the previous
+    # one's is captured, every later call replays
+    assert st["captured"] == 1 and st["replayed"] >= 4 and st["eager"] + st["replayed"] == 6, st
+    # the winners moved with the keys (the replay did not reuse old inputs)
+    idx = set()
+    for s in (10, 11):
+        works, isb = _works(mat, active, losses, 3000, s, n_cand)
+        idx.add(tuple(r[1] for r in _rows(graph.run(works, history=hg, is_below=isb))))
+    assert len(idx) == 2
+
+
+def test_growing_history_never_replays_stale_graph():
+    eager, graph, DeviceHistory = _pair()
+    mat, active, losses = _history(2400, 5)
+    he = DeviceHistory(eager, len(SPACE), cap=512)
+    hg = DeviceHistory(graph, len(SPACE), cap=512)
+    T = 400
+    for h in (he, hg):
+        h.append(mat[:T], active[:T])
+    for step in range(8):
+        works, isb = _works(mat, active, losses, T, step, 1 << 16)
+        for _ in range(3):  # three calls per history size: capture, then replay
+            a = eager.run(works, history=he, is_below=isb)
+            b = graph.run(works, history=hg, is_below=isb)
+            assert _rows(a) == _rows(b), (step, T)
+        # more trials (the history buffers grow past their capacity too)
+        for h in (he, hg):
+            h.append(mat[T:T + 250], active[T:T + 250])
+        T += 250
+    st = graph.graph_stats
+    assert st["captured"] >= 4 and st["replayed"] >= 4, st
+
+
+def test_other_structure_between_replays():
+    """A larger level in between grows the workspace (new pointers): the
+    first structure's graph is dropped and re-captured, never replayed stale."""
+    eager, graph, DeviceHistory = _pair()
+    mat, active, losses = _history(3000, 2)
+    he = DeviceHistory(eager, len(SPACE), cap=4096)
+    hg = DeviceHistory(graph, len(SPACE), cap=4096)
+    for h in (he, hg):
+        h.append(mat, active)
+    for step, n_cand in enumerate([1 << 14, 1 << 14, 1 << 14, 1 << 20, 1 << 20, 1 << 14,
+                                   1 << 14, 1 << 14]):
+        works, isb = _works(mat, active, losses, 3000, step, n_cand)
+        a = eager.run(works, history=he, is_below=isb)
+        b = graph.run(works, history=hg, is_below=isb)
+        assert _rows(a) == _rows(b), step
+
+
+def test_timers_from_graph_nodes():
+    """Timer groups inside a replayed graph are external event-record nodes:
+    their durations are read after the level and look like kernel times."""
+    _, graph, DeviceHistory = _pair()
+    mat, active, losses = _history(3000, 4)
+    hg = DeviceHistory(graph, len(SPACE), cap=4096)
+    hg.append(mat, active)
+    timers = {}
+    for step in range(5):
+        works, isb = _works(mat, active, losses, 3000, step, 1 << 20)
+        graph.run(works, history=hg, is_below=isb, timers=timers, timer_groups={"table"})
+    st = graph.graph_stats
+    assert st["replayed"] >= 3 and st["eager"] + st["replayed"] == 5, st
+    ms = [a.elapsed_time(b) for a, b in timers["table"]]
+    assert len(ms) == 5
+    assert all(0.0 < m < 50.0 for m in ms), ms
+    # replayed durations agree with the eager ones (same kernel, same work)
+    assert max(ms[-3:]) < 3.0 * min(ms[:2]) + 0.05
