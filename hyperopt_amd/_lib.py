@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -53,6 +53,16 @@ BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
                        ("n_scored", "<i8")], align=True)
 PRIOR_DTYPE = np.dtype([("kind", "<i4"), ("n_cat", "<i4"), ("a", "<f8"), ("b", "<f8"),
                         ("q", "<f8"), ("p_off", "<i8"), ("key", "<u8")], align=True)
+OP_ARGS = 23
+OP_DTYPE = np.dtype([("code", "<i4"), ("n_args", "<i4"), ("a", "<i8", (OP_ARGS,))], align=True)
+# tpe_run_ops record codes (tpe_hip.h TPE_OP_*): entry point -> code
+OP_CODES = {name: i + 1 for i, name in enumerate((
+    "tpe_gather_obs", "tpe_gather_obs_multi", "tpe_parzen_fit", "tpe_cat_posterior",
+    "tpe_table_build", "tpe_score_table", "tpe_score_table_fast", "tpe_score_pruned64",
+    "tpe_score_continuous", "tpe_sort_candidates", "tpe_score_sorted", "tpe_lattice_sample",
+    "tpe_lattice_compact", "tpe_score_quantized", "tpe_score_categorical", "tpe_sample"))}
+OP_EVENT_RECORD, OP_STREAM_WAIT, OP_MEMCPY, OP_STREAM_SYNC = range(len(OP_CODES) + 1,
+                                                                  len(OP_CODES) + 5)
 PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
     PRIOR_CATEGORICAL = range(6)
 
@@ -100,6 +110,7 @@ _SIGNATURES = {
     "tpe_best_combine": (_I, [_P, _I, _I, _P, _P]),
     "tpe_maxloc_allreduce": (_I, [_P, _P, _P, _I, _P, _P]),
     "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
+    "tpe_run_ops": (_I, [_P, _I, ctypes.POINTER(_I)]),
     "tpe_last_error": (ctypes.c_char_p, []),
     "tpe_abi_version": (_I, []),
     "tpe_struct_sizes": (_I, [_P, _I]),
@@ -176,11 +187,11 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    sizes = (ctypes.c_int32 * 8)()
-    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 8)
+    sizes = (ctypes.c_int32 * 9)()
+    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 9)
     want = (SEG_DTYPE.itemsize, CAT_SEG_DTYPE.itemsize, JOB_DTYPE.itemsize, BEST_DTYPE.itemsize,
             TABLE_DTYPE.itemsize, GATHER_DTYPE.itemsize, HISTORY_DTYPE.itemsize,
-            PRIOR_DTYPE.itemsize)
+            PRIOR_DTYPE.itemsize, OP_DTYPE.itemsize)
     if lib.tpe_abi_version() != ABI_VERSION:
         raise ImportError("hyperopt_amd: libtpe_hip.so ABI %d, expected %d (rebuild with make)"
                           % (lib.tpe_abi_version(), ABI_VERSION))

@@ -1,0 +1,128 @@
+// tpe_ops.hip -- the level launcher (tpe_run_ops, include/tpe_hip.h).
+//
+// A suggest level is ~20 stream operations (history gather, Parzen fit,
+// categorical posteriors, table build, scoring launches, side-stream
+// fork/join, upload and readback).  Issued one ctypes call at a time they
+// cost ~8 us of host time each -- at a one-eighth label share on 8 GPUs that
+// host time, not the GPU, sets the level's length.
+// Here the binding hands over the whole level as an array of records and the
+// calls are made from C++: each record names an entry point of this library
+// and carries its arguments as 64-bit words, converted back to the entry
+// point's parameter types by the call adapter below (the prototypes in
+// tpe_hip.h drive the conversion, so a record can only call a function with
+// exactly its declared arity).
+#include <cstddef>
+#include <cstdint>
+#include <type_traits>
+#include <utility>
+
+#include "tpe_common.hpp"
+
+namespace tpe {
+namespace {
+
+// one argument word, convertible to any pointer or integer parameter type
+struct Word {
+  int64_t v;
+  template <class T>
+  operator T*() const {
+    return reinterpret_cast<T*>(static_cast<intptr_t>(v));
+  }
+  template <class T, class = std::enable_if_t<std::is_integral<T>::value>>
+  operator T() const {
+    return static_cast<T>(v);
+  }
+};
+
+template <class R, class... Ps, size_t... I>
+R invoke(R (*f)(Ps...), const int64_t* a, std::index_sequence<I...>) {
+  return f(Word{a[I]}...);
+}
+
+// calls f with the record's words; TPE_E_ARG when the record's arity differs
+template <class R, class... Ps>
+int call(R (*f)(Ps...), const tpe_op& op, const char* name) {
+  if (op.n_args != (int)sizeof...(Ps)) {
+    set_error("tpe_run_ops: %s takes %d arguments, record has %d", name, (int)sizeof...(Ps),
+              op.n_args);
+    return TPE_E_ARG;
+  }
+  return (int)invoke(f, op.a, std::index_sequence_for<Ps...>{});
+}
+
+void* ptr(int64_t v) { return reinterpret_cast<void*>(static_cast<intptr_t>(v)); }
+
+int runtime(hipError_t e, const char* what) {
+  if (e == hipSuccess) return TPE_OK;
+  set_error("tpe_run_ops: %s: %s", what, hipGetErrorString(e));
+  return TPE_E_LAUNCH;
+}
+
+int run_one(const tpe_op& op) {
+#define TPE_CALL(CODE, FN) \
+  case CODE:               \
+    return call(&FN, op, #FN)
+  switch (op.code) {
+    TPE_CALL(TPE_OP_GATHER_OBS, tpe_gather_obs);
+    TPE_CALL(TPE_OP_GATHER_OBS_MULTI, tpe_gather_obs_multi);
+    TPE_CALL(TPE_OP_PARZEN_FIT, tpe_parzen_fit);
+    TPE_CALL(TPE_OP_CAT_POSTERIOR, tpe_cat_posterior);
+    TPE_CALL(TPE_OP_TABLE_BUILD, tpe_table_build);
+    TPE_CALL(TPE_OP_SCORE_TABLE, tpe_score_table);
+    TPE_CALL(TPE_OP_SCORE_TABLE_FAST, tpe_score_table_fast);
+    TPE_CALL(TPE_OP_SCORE_PRUNED64, tpe_score_pruned64);
+    TPE_CALL(TPE_OP_SCORE_CONTINUOUS, tpe_score_continuous);
+    TPE_CALL(TPE_OP_SORT_CANDIDATES, tpe_sort_candidates);
+    TPE_CALL(TPE_OP_SCORE_SORTED, tpe_score_sorted);
+    TPE_CALL(TPE_OP_LATTICE_SAMPLE, tpe_lattice_sample);
+    TPE_CALL(TPE_OP_LATTICE_COMPACT, tpe_lattice_compact);
+    TPE_CALL(TPE_OP_SCORE_QUANTIZED, tpe_score_quantized);
+    TPE_CALL(TPE_OP_SCORE_CATEGORICAL, tpe_score_categorical);
+    TPE_CALL(TPE_OP_SAMPLE, tpe_sample);
+#undef TPE_CALL
+    case TPE_OP_EVENT_RECORD:
+      return runtime(hipEventRecord((hipEvent_t)ptr(op.a[0]),
+                                    (hipStream_t)ptr(op.a[1])),
+                     "hipEventRecord");
+    case TPE_OP_STREAM_WAIT:
+      return runtime(hipStreamWaitEvent((hipStream_t)ptr(op.a[0]),
+                                        (hipEvent_t)ptr(op.a[1]), 0),
+                     "hipStreamWaitEvent");
+    case TPE_OP_MEMCPY:
+      if (op.a[3] != hipMemcpyHostToDevice && op.a[3] != hipMemcpyDeviceToHost &&
+          op.a[3] != hipMemcpyDeviceToDevice) {
+        set_error("tpe_run_ops: memcpy kind %lld", (long long)op.a[3]);
+        return TPE_E_ARG;
+      }
+      return runtime(hipMemcpyAsync(ptr(op.a[0]),
+                                    ptr(op.a[1]), (size_t)op.a[2],
+                                    (hipMemcpyKind)op.a[3],
+                                    (hipStream_t)ptr(op.a[4])),
+                     "hipMemcpyAsync");
+    case TPE_OP_STREAM_SYNC:
+      return runtime(hipStreamSynchronize((hipStream_t)ptr(op.a[0])),
+                     "hipStreamSynchronize");
+    default:
+      set_error("tpe_run_ops: unknown op code %d", op.code);
+      return TPE_E_ARG;
+  }
+}
+
+}  // namespace
+}  // namespace tpe
+
+extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
+  if (failed_op) *failed_op = -1;
+  if (n_ops < 0 || (n_ops > 0 && !ops)) {
+    tpe::set_error("tpe_run_ops: n_ops=%d", n_ops);
+    return TPE_E_ARG;
+  }
+  for (int i = 0; i < n_ops; ++i) {
+    const int rc = tpe::run_one(ops[i]);
+    if (rc != TPE_OK) {
+      if (failed_op) *failed_op = i;
+      return rc;
+    }
+  }
+  return TPE_OK;
+}

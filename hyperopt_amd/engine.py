@@ -298,6 +298,14 @@ class Engine:
         self._gen = 0           # bumped whenever a workspace buffer is (re)allocated
         self._own = None        # the engine's own stream (capture needs a non-null stream)
         self.graph_stats = {"captured": 0, "replayed": 0, "eager": 0}
+        # native level launcher (default; TPE_NATIVE_LAUNCH=0: one ctypes call
+        # per entry point): a level whose launch key repeats the previous
+        # call's is recorded once as tpe_run_ops records -- upload, every
+        # launch, stream fork/join, readback and the final synchronise -- and
+        # re-issued with one C call per level (hyperopt_amd/csrc/tpe_ops.hip)
+        self.native = os.environ.get("TPE_NATIVE_LAUNCH", "1") != "0"
+        self._oplists = {}      # launch key -> _OpList
+        self._oplist_once = None
 
     # -- memory --------------------------------------------------------------
     def _buf(self, name, nbytes):
@@ -311,6 +319,11 @@ class Engine:
             self._bufs[name] = t
             self._gen += 1  # captured graphs hold the old pointers
         return t.data_ptr()
+
+    def _drop_oplists(self):
+        for o in self._oplists.values():
+            o.destroy(self._hip)
+        self._oplists.clear()
 
     def _drop_graphs(self):
         for g in self._graphs.values():
@@ -344,25 +357,30 @@ class Engine:
         if pin is None or pin.numel() < nbytes:
             pin = self._res_pin = self.torch.empty(_align(int(nbytes * 1.25)),
                                                    dtype=self.torch.uint8, pin_memory=True)
+            self._gen += 1
         return pin
 
-    def _upload(self, pack, stream, slot=0):
+    def _upload(self, pack, stream, slot=0, copy=True):
         """One host->device copy of ``pack`` through pinned buffer / device
         staging area ``slot`` (a level uploads twice: descriptors for the fit,
-        then the job table, each into its own slot)."""
+        then the job table, each into its own slot).  ``copy=False``: stage
+        only; the copy (``self._staged`` = dst, src, bytes) is issued later."""
         torch = self.torch
         pinned = self._pinned.get(slot)
         if pinned is None or pinned.numel() < pack.size:
             pinned = torch.empty(_align(int(pack.size * 1.25) + 1), dtype=torch.uint8,
                                  pin_memory=True)
             self._pinned[slot] = pinned
+            self._gen += 1
         host = pinned.numpy()
         for off, arr in pack.parts:
             host[off:off + arr.nbytes] = arr.reshape(-1).view(np.uint8)
         name = "stage" if slot == 0 else "stage%d" % slot
         dev = self._buf(name, pack.size)
-        L.hip_check(self._hip.hipMemcpyAsync(dev, pinned.data_ptr(), pack.size, L.H2D,
-                                             stream.cuda_stream), "hipMemcpyAsync")
+        self._staged = (dev, pinned.data_ptr(), pack.size)
+        if copy:
+            L.hip_check(self._hip.hipMemcpyAsync(dev, pinned.data_ptr(), pack.size, L.H2D,
+                                                 stream.cuda_stream), "hipMemcpyAsync")
         return dev
 
     # -- level plans -----------------------------------------------------------
@@ -848,7 +866,9 @@ class Engine:
         JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
         n_jobs = len(order)
         o_res = pack.add(np.zeros(64 + n_jobs * BS, np.uint8))
-        base = self._upload(pack, stream)
+        native_ok = self.native and not self.graphs and pkey is not None and not (
+            outputs or sample_only or posteriors or table_scores)
+        base = self._upload(pack, stream, copy=not native_ok)
         d_segs = base + o_segs if o_segs is not None else None
         d_csegs = base + o_csegs if o_csegs is not None else None
         d_res = base + o_res
@@ -882,15 +902,15 @@ class Engine:
         # an offset into the staged pack, or a size covered by the launch key;
         # the values that change from call to call live in the uploaded pack.
         gkey = None
-        if graph_ok:
+        if graph_ok or native_ok:
             gkey = (pkey, self._gen, tuple(off for off, _ in pack.parts), n_obs_total, max_obs,
                     cobs_off, lat_off,
                     (history.vals.data_ptr(), history.active.data_ptr(), history.ld, n_rows)
                     if history is not None else None,
                     self.side_stream, self.table_scorer, self.exact64,
-                    None if timers is None else
-                    (None if timer_groups is None else frozenset(timer_groups)))
-        cap = None  # _LevelGraph being captured (tick/tock then record graph nodes)
+                    "off" if timers is None else
+                    ("all" if timer_groups is None else frozenset(timer_groups)))
+        cap = None  # _LevelGraph being captured / _OpList being recorded (tick/tock follow it)
 
         def tick(name, on=None):
             if timers is None or (timer_groups is not None and name not in timer_groups):
@@ -909,7 +929,13 @@ class Engine:
             else:
                 timers.setdefault(name, []).append((e0, tick(name, on)))
 
-        def launch_level():
+        def stream_order(name, src, dst):
+            if isinstance(cap, _OpList):
+                cap.order(self._event(name), src, dst)
+            else:
+                self._order(name, src, dst)
+
+        def launch_level(lib=lib):
             if hist_mode:
                 d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
                 d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
@@ -943,7 +969,7 @@ class Engine:
                 side = self._side
             side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
             if side is not None:
-                self._order("gathered", sp, side_p)
+                stream_order("gathered", sp, side_p)
             # ---- posterior fit ------------------------------------------------------
             if fit_ids:
                 e0 = tick("fit")
@@ -980,7 +1006,7 @@ class Engine:
             # quantized and categorical groups go to the side stream (after the job
             # table has landed); continuous groups stay on `stream`
             if side is not None:  # quantized groups need the continuous fit
-                self._order("fitted", sp, side_p)
+                stream_order("fitted", sp, side_p)
             table_calls = []
             jobs_ptr = jobs.__array_interface__["data"][0]
             g_order = list(range(len(groups)))
@@ -1047,7 +1073,7 @@ class Engine:
                                                 sp), "tpe_table_build")
                     tock("table_build", e0)
                     if not joined and self.side_stream == "2":
-                        self._order("joined", side_p, sp)
+                        stream_order("joined", side_p, sp)
                         joined = True
                     e0 = tick("table")
                     if outputs or inj(ids[0]) or self.table_scorer == "poly":
@@ -1113,11 +1139,48 @@ class Engine:
                 tock(kind, e0, kst)
 
             if not joined:  # join before the readback
-                self._order("joined", side_p, sp)
+                stream_order("joined", side_p, sp)
             return table_calls, False
 
-        graph = self._graphs.get(gkey) if gkey is not None else None
-        if graph is None and gkey is not None and gkey == self._last_gkey:
+        nbytes = 64 + n_jobs * BS  # the result block read back at the end
+        ops = None
+        if native_ok:
+            ops = self._oplists.get(gkey)
+            if ops is None and gkey == self._last_gkey:
+                # the second call in a row with this launch key: record the
+                # level's stream work once, re-issue it from C on later calls
+                gen0 = self._gen
+                rec = _OpList(self.lib)
+                dst, src, nb = self._staged
+                rec.add(L.OP_MEMCPY, dst, src, nb, L.H2D, sp)
+                cap = rec
+                try:
+                    rec.table_calls, _ = launch_level(rec)
+                finally:
+                    cap = None
+                pin = self._res_pinned(nbytes)
+                rec.add(L.OP_MEMCPY, pin.data_ptr(), d_res, nbytes, L.D2H, sp)
+                if batch is not None:
+                    rec.add(L.OP_EVENT_RECORD, self._event("result"), sp)
+                else:
+                    rec.add(L.OP_STREAM_SYNC, sp)
+                rec.finish((jobs, fb_jobs, g_arr if hist_mode else None,
+                            h_arr if histories is not None else None))
+                if self._gen == gen0:  # every recorded pointer is still the live one
+                    if len(self._oplists) >= 16 or any(
+                            k[1] != gen0 for k in self._oplists):
+                        self._drop_oplists()
+                    self._oplists[gkey] = rec
+                else:
+                    if self._oplist_once is not None:
+                        self._oplist_once.destroy(self._hip)
+                    self._oplist_once = rec  # this call's only (its events freed later)
+                ops = rec
+            if ops is None:  # eager: the deferred upload first
+                dst, src, nb = self._staged
+                L.hip_check(self._hip.hipMemcpyAsync(dst, src, nb, L.H2D, sp), "hipMemcpyAsync")
+        graph = self._graphs.get(gkey) if (gkey is not None and graph_ok) else None
+        if graph is None and graph_ok and gkey == self._last_gkey:
             # the second call in a row with this launch key: capture it
             cap = _LevelGraph()
             try:
@@ -1136,7 +1199,15 @@ class Engine:
             elif graph is not None:  # a buffer grew during the capture: not replayable
                 graph.destroy(self._hip)
                 graph = None
-        if graph is not None:
+        if ops is not None:
+            failed = ctypes.c_int(-1)
+            rc = self.lib.tpe_run_ops(ops.ptr, ops.n, ctypes.byref(failed))
+            if rc != 0:
+                raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
+                    rc, failed.value, self.lib.tpe_last_error().decode(errors="replace")))
+            self.graph_stats["native"] = self.graph_stats.get("native", 0) + 1
+            table_calls = ops.table_calls
+        elif graph is not None:
             L.hip_check(self._hip.hipGraphLaunch(graph.exec, sp), "hipGraphLaunch")
             self.graph_stats["replayed"] += 1
             table_calls = graph.table_calls
@@ -1148,22 +1219,26 @@ class Engine:
             self.graph_stats["eager"] += 1
         _hmark('score launches')
         # ---- results: one device->host copy of the result block into pinned memory
-        nbytes = 64 + n_jobs * BS
+        # (issued by the records themselves on the native path)
         pin = self._res_pinned(nbytes)
-        L.hip_check(self._hip.hipMemcpyAsync(pin.data_ptr(), d_res, nbytes, L.D2H, sp),
-                    "hipMemcpyAsync")
+        if ops is None:
+            L.hip_check(self._hip.hipMemcpyAsync(pin.data_ptr(), d_res, nbytes, L.D2H, sp),
+                        "hipMemcpyAsync")
         after = None
-        if graph is not None and graph.timed and timers is not None:
-            after = functools.partial(graph.read_timers, self._hip, timers)
+        timed = ops if ops is not None else graph
+        if timed is not None and timed.timed and timers is not None:
+            after = functools.partial(timed.read_timers, self._hip, timers)
         if batch is not None:  # queued readback (see _Pending)
             ev = self._event("result")
-            L.hip_check(self._hip.hipEventRecord(ev, sp), "hipEventRecord")
+            if ops is None:
+                L.hip_check(self._hip.hipEventRecord(ev, sp), "hipEventRecord")
             if caller_p is not None:  # the caller's later work follows this level
                 L.hip_check(self._hip.hipStreamWaitEvent(caller_p, ev, 0), "hipStreamWaitEvent")
             p = self._inflight = _Pending(self, ev, pin, nbytes, np.asarray(order, np.int64),
                                           bool(table_calls), after)
             return p if defer else p.result()
-        L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
+        if ops is None:
+            L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
         if after is not None:
             after()
         res_h = pin[:nbytes].numpy().copy()
@@ -1295,7 +1370,87 @@ class _Timed(object):
         return self.ms
 
 
-class _LevelGraph(object):
+def _word(a):
+    """A tpe_run_ops argument word: pointers / handles as addresses, ints by value."""
+    if a is None:
+        return 0
+    if isinstance(a, ctypes.c_void_p):
+        return a.value or 0
+    return int(a)
+
+
+class _Timing(object):
+    """Timing events owned by a recorded / captured level (tick/tock groups)."""
+
+    def read_timers(self, hip, timers):
+        ms = ctypes.c_float()
+        for name, e0, e1 in self.timed:
+            L.hip_check(hip.hipEventElapsedTime(ctypes.byref(ms), e0, e1), "hipEventElapsedTime")
+            timers.setdefault(name, []).append((_Timed(ms.value), None))
+
+    def _new_event(self, hip):
+        h = ctypes.c_void_p()
+        L.hip_check(hip.hipEventCreateWithFlags(ctypes.byref(h), 0), "hipEventCreateWithFlags")
+        self.events.append(h)
+        return h
+
+
+class _OpList(_Timing):
+    """One level's stream work as tpe_run_ops records (Engine.run, native
+    launcher).  Stands in for the library while the level is recorded: the
+    entry points named in L.OP_CODES append a record (their ctypes-level
+    arguments, as words) and return 0; size queries go to the library.
+    ``keep`` holds the host arrays the records point to (host job slices,
+    gather / history tables) for as long as the records live."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        self.rows = []
+        self.timed = []
+        self.events = []
+        self.table_calls = []
+        self.keep = self.arr = None
+        self.ptr = self.n = 0
+
+    def __getattr__(self, name):
+        code = L.OP_CODES.get(name)
+        if code is None:
+            return getattr(self.lib, name)
+
+        def record(*args):
+            self.rows.append((code, args))
+            return 0
+        return record
+
+    def add(self, code, *args):
+        self.rows.append((code, args))
+
+    def order(self, ev, src, dst):
+        self.add(L.OP_EVENT_RECORD, ev, src)
+        self.add(L.OP_STREAM_WAIT, dst, ev)
+
+    def record(self, hip, stream):
+        h = self._new_event(hip)
+        self.add(L.OP_EVENT_RECORD, h, stream.cuda_stream)
+        return h
+
+    def finish(self, keep):
+        arr = np.zeros(len(self.rows), L.OP_DTYPE)
+        for i, (code, args) in enumerate(self.rows):
+            if len(args) > L.OP_ARGS:
+                raise ValueError("op %d has %d arguments" % (code, len(args)))
+            arr["code"][i], arr["n_args"][i] = code, len(args)
+            arr["a"][i, :len(args)] = [_word(a) for a in args]
+        self.arr, self.keep, self.rows = arr, keep, None
+        self.ptr, self.n = arr.ctypes.data, len(arr)
+
+    def destroy(self, hip):
+        for h in self.events:
+            hip.hipEventDestroy(h)
+        self.events = []
+
+
+class _LevelGraph(_Timing):
     """One level's launch sequence captured into a hipGraph (Engine.run).
 
     Captured from the launches of a level whose launch key repeats (the
@@ -1318,9 +1473,7 @@ class _LevelGraph(object):
         current dependencies and becomes the stream's only dependency (HIP
         captures a plain hipEventRecord as an ordering edge only, and refuses
         hipEventRecordExternal during capture)."""
-        h = ctypes.c_void_p()
-        L.hip_check(hip.hipEventCreateWithFlags(ctypes.byref(h), 0), "hipEventCreateWithFlags")
-        self.events.append(h)
+        h = self._new_event(hip)
         sp = ctypes.c_void_p(stream.cuda_stream)
         status, cid, graph = ctypes.c_int(), ctypes.c_ulonglong(), ctypes.c_void_p()
         deps, n_deps = ctypes.POINTER(ctypes.c_void_p)(), ctypes.c_size_t()
@@ -1360,12 +1513,6 @@ class _LevelGraph(object):
         self.exec = e
         self.gen = gen0 if eng._gen == gen0 else -1
         return self
-
-    def read_timers(self, hip, timers):
-        ms = ctypes.c_float()
-        for name, e0, e1 in self.timed:
-            L.hip_check(hip.hipEventElapsedTime(ctypes.byref(ms), e0, e1), "hipEventElapsedTime")
-            timers.setdefault(name, []).append((_Timed(ms.value), None))
 
     def destroy(self, hip):
         if self.exec is not None:

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 10
+#define TPE_ABI_VERSION 11
 
 enum {
   TPE_OK = 0,
@@ -417,10 +417,53 @@ int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* o
 int tpe_maxloc_allreduce(const tpe_best* local, tpe_best* gathered, tpe_best* out, int n_labels,
                          void* comm, void* stream);
 
+/* ---- level launcher: a whole suggest level's stream work in one host call.
+ * `ops` (host) is a list of records, each naming one of the entry points above
+ * (or a runtime step) by `code` and carrying that call's arguments, in
+ * declaration order, as 64-bit words (pointers and handles as addresses,
+ * int / int64_t by value).  tpe_run_ops issues them in order and stops at the
+ * first failing record (its index in *failed_op, -1 when all succeeded).  A
+ * binding that replays the same level (same kernels, grids, workspace) keeps
+ * its record array and re-issues it with one call: the per-call inputs live
+ * in the device buffers the records point to (the level's upload).  This is
+ * the host-side counterpart of a hipGraph; on ROCm 7 re-issuing the launches
+ * is faster than replaying a captured graph. ---------- */
+enum {
+  TPE_OP_GATHER_OBS = 1,       /* tpe_gather_obs                             */
+  TPE_OP_GATHER_OBS_MULTI,     /* tpe_gather_obs_multi                       */
+  TPE_OP_PARZEN_FIT,           /* tpe_parzen_fit                             */
+  TPE_OP_CAT_POSTERIOR,        /* tpe_cat_posterior                          */
+  TPE_OP_TABLE_BUILD,          /* tpe_table_build                            */
+  TPE_OP_SCORE_TABLE,          /* tpe_score_table                            */
+  TPE_OP_SCORE_TABLE_FAST,     /* tpe_score_table_fast                       */
+  TPE_OP_SCORE_PRUNED64,       /* tpe_score_pruned64                         */
+  TPE_OP_SCORE_CONTINUOUS,     /* tpe_score_continuous                       */
+  TPE_OP_SORT_CANDIDATES,      /* tpe_sort_candidates                        */
+  TPE_OP_SCORE_SORTED,         /* tpe_score_sorted                           */
+  TPE_OP_LATTICE_SAMPLE,       /* tpe_lattice_sample                         */
+  TPE_OP_LATTICE_COMPACT,      /* tpe_lattice_compact                        */
+  TPE_OP_SCORE_QUANTIZED,      /* tpe_score_quantized                        */
+  TPE_OP_SCORE_CATEGORICAL,    /* tpe_score_categorical                      */
+  TPE_OP_SAMPLE,               /* tpe_sample                                 */
+  TPE_OP_EVENT_RECORD,         /* hipEventRecord(a[0] event, a[1] stream)    */
+  TPE_OP_STREAM_WAIT,          /* hipStreamWaitEvent(a[0] stream, a[1] event) */
+  TPE_OP_MEMCPY,               /* hipMemcpyAsync(a[0] dst, a[1] src, a[2] bytes,
+                                  a[3] hipMemcpyKind, a[4] stream)           */
+  TPE_OP_STREAM_SYNC,          /* hipStreamSynchronize(a[0] stream)          */
+  TPE_OP_COUNT
+};
+#define TPE_OP_ARGS 23
+typedef struct tpe_op {
+  int32_t code;
+  int32_t n_args;               /* must equal the entry point's parameter count */
+  int64_t a[TPE_OP_ARGS];
+} tpe_op;                       /* 192 bytes */
+int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op);
+
 const char* tpe_last_error(void);
 int tpe_abi_version(void);
 /* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table, tpe_gather,
- * tpe_history, tpe_prior) to out[0..n); returns 8 */
+ * tpe_history, tpe_prior, tpe_op) to out[0..n); returns 9 */
 int tpe_struct_sizes(int32_t* out, int n);
 
 #ifdef __cplusplus

@@ -30,13 +30,51 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 10
-    sizes = (ctypes.c_int32 * 8)()
-    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 8) == 8
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 11
+    sizes = (ctypes.c_int32 * 9)()
+    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 9) == 9
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
                             L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize, L.TABLE_DTYPE.itemsize,
                             L.GATHER_DTYPE.itemsize, L.HISTORY_DTYPE.itemsize,
-                            L.PRIOR_DTYPE.itemsize)
+                            L.PRIOR_DTYPE.itemsize, L.OP_DTYPE.itemsize)
+    assert L.OP_DTYPE.itemsize == 192
+
+
+def _ops(*records):
+    ops = np.zeros(len(records), L.OP_DTYPE)
+    for i, (code, args) in enumerate(records):
+        ops[i]["code"], ops[i]["n_args"] = code, len(args)
+        ops[i]["a"][:len(args)] = [0 if a is None else a for a in args]
+    return ops
+
+
+def test_run_ops_records():
+    """tpe_run_ops (the level launcher): records reach the named entry point
+    with their words as its arguments; arity, code and argument errors stop
+    the list at the failing record.  Only calls that need no GPU here."""
+    lib = L.load()
+    failed = ctypes.c_int(7)
+    assert lib.tpe_run_ops(None, 0, ctypes.byref(failed)) == 0 and failed.value == -1
+    # every record code's arity is its entry point's parameter count
+    for name, code in L.OP_CODES.items():
+        assert code == list(L.OP_CODES).index(name) + 1
+        assert name in L._SIGNATURES
+    fit = L.OP_CODES["tpe_parzen_fit"]
+    nfit = len(L._SIGNATURES["tpe_parzen_fit"][1])
+    ok = (fit, [0] * nfit)  # n_seg = 0: nothing to do
+    bad_n = (fit, [0, 0, 0, -1] + [0] * (nfit - 4))  # n_seg = -1
+    ops = _ops(ok, ok, bad_n, ok)
+    rc = lib.tpe_run_ops(ops.ctypes.data_as(ctypes.c_void_p), len(ops), ctypes.byref(failed))
+    assert rc == -1 and failed.value == 2 and b"tpe_parzen_fit" in lib.tpe_last_error()
+    ops = _ops(ok, (fit, [0] * (nfit - 1)))
+    rc = lib.tpe_run_ops(ops.ctypes.data_as(ctypes.c_void_p), len(ops), ctypes.byref(failed))
+    assert rc == -1 and failed.value == 1 and b"arguments" in lib.tpe_last_error()
+    ops = _ops((99, []))
+    rc = lib.tpe_run_ops(ops.ctypes.data_as(ctypes.c_void_p), 1, ctypes.byref(failed))
+    assert rc == -1 and failed.value == 0 and b"unknown op" in lib.tpe_last_error()
+    ops = _ops((L.OP_MEMCPY, [0, 0, 0, 77, 0]))
+    rc = lib.tpe_run_ops(ops.ctypes.data_as(ctypes.c_void_p), 1, ctypes.byref(failed))
+    assert rc == -1 and b"memcpy kind" in lib.tpe_last_error()
 
 
 def test_argument_errors_are_reported():

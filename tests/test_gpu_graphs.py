@@ -1,5 +1,7 @@
-"""Level graphs (Engine.run, opt-in TPE_GRAPHS=1): a level whose launch key repeats is
-captured into a hipGraph on its second call and replayed afterwards.
+"""Replayed levels (Engine.run): a level whose launch key repeats is
+recorded on its second call and replayed afterwards -- by the native level
+launcher (default: tpe_run_ops records, csrc/tpe_ops.hip) or as a captured
+hipGraph (opt-in TPE_GRAPHS=1).
 
 The per-call inputs (split flags, observation counts, Philox keys) travel in
 the level's upload, outside the graph, so a replayed level must give exactly
@@ -52,16 +54,29 @@ def _rows(res):
     return [(r.label, r.index, r.value, r.score, r.n_scored) for r in res]
 
 
-def _pair():
+MODES = ["native", "graph"]
+
+
+def _pair(mode):
     from hyperopt_amd.engine import DeviceHistory, Engine
     eager, graph = Engine(), Engine()
-    eager.graphs, graph.graphs = False, True
+    eager.graphs = eager.native = False
+    graph.graphs, graph.native = mode == "graph", mode == "native"
     return eager, graph, DeviceHistory
 
 
+def _replays(eng):
+    """(recorded, replayed-or-re-issued, eager) level counts."""
+    st = eng.graph_stats
+    if eng.native:
+        return len(eng._oplists), st.get("native", 0), st["eager"]
+    return st["captured"], st["replayed"], st["eager"]
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("n_cand", [24, 1 << 18])
-def test_replayed_level_equals_eager(n_cand):
-    eager, graph, DeviceHistory = _pair()
+def test_replayed_level_equals_eager(n_cand, mode):
+    eager, graph, DeviceHistory = _pair(mode)
     mat, active, losses = _history(3000, 11)
     he = DeviceHistory(eager, len(SPACE), cap=4096)
     hg = DeviceHistory(graph, len(SPACE), cap=4096)
@@ -72,10 +87,10 @@ def test_replayed_level_equals_eager(n_cand):
         a = eager.run(works, history=he, is_below=isb)
         b = graph.run(works, history=hg, is_below=isb)
         assert _rows(a) == _rows(b), step
-    st = graph.graph_stats
     # the first call sizes the workspace, a call whose key repeats the previous
-    # one's is captured, every later call replays
-    assert st["captured"] == 1 and st["replayed"] >= 4 and st["eager"] + st["replayed"] == 6, st
+    # one's is recorded, every later call replays
+    cap, rep, eag = _replays(graph)
+    assert cap == 1 and rep >= 4 and eag + rep == 6, (cap, rep, eag)
     # the winners moved with the keys (the replay did not reuse old inputs)
     idx = set()
     for s in (10, 11):
@@ -84,8 +99,9 @@ def test_replayed_level_equals_eager(n_cand):
     assert len(idx) == 2
 
 
-def test_growing_history_never_replays_stale_graph():
-    eager, graph, DeviceHistory = _pair()
+@pytest.mark.parametrize("mode", MODES)
+def test_growing_history_never_replays_stale_graph(mode):
+    eager, graph, DeviceHistory = _pair(mode)
     mat, active, losses = _history(2400, 5)
     he = DeviceHistory(eager, len(SPACE), cap=512)
     hg = DeviceHistory(graph, len(SPACE), cap=512)
@@ -102,14 +118,15 @@ def test_growing_history_never_replays_stale_graph():
         for h in (he, hg):
             h.append(mat[T:T + 250], active[T:T + 250])
         T += 250
-    st = graph.graph_stats
-    assert st["captured"] >= 4 and st["replayed"] >= 4, st
+    cap, rep, eag = _replays(graph)
+    assert rep >= 8, (cap, rep, eag)
 
 
-def test_other_structure_between_replays():
+@pytest.mark.parametrize("mode", MODES)
+def test_other_structure_between_replays(mode):
     """A larger level in between grows the workspace (new pointers): the
     first structure's graph is dropped and re-captured, never replayed stale."""
-    eager, graph, DeviceHistory = _pair()
+    eager, graph, DeviceHistory = _pair(mode)
     mat, active, losses = _history(3000, 2)
     he = DeviceHistory(eager, len(SPACE), cap=4096)
     hg = DeviceHistory(graph, len(SPACE), cap=4096)
@@ -123,10 +140,12 @@ def test_other_structure_between_replays():
         assert _rows(a) == _rows(b), step
 
 
-def test_timers_from_graph_nodes():
-    """Timer groups inside a replayed graph are external event-record nodes:
-    their durations are read after the level and look like kernel times."""
-    _, graph, DeviceHistory = _pair()
+@pytest.mark.parametrize("mode", MODES)
+def test_timers_of_replayed_levels(mode):
+    """Timer groups inside a replayed level are event records of its own
+    (graph nodes / tpe_run_ops records): their durations are read after the
+    level and look like kernel times."""
+    _, graph, DeviceHistory = _pair(mode)
     mat, active, losses = _history(3000, 4)
     hg = DeviceHistory(graph, len(SPACE), cap=4096)
     hg.append(mat, active)
@@ -134,10 +153,38 @@ def test_timers_from_graph_nodes():
     for step in range(5):
         works, isb = _works(mat, active, losses, 3000, step, 1 << 20)
         graph.run(works, history=hg, is_below=isb, timers=timers, timer_groups={"table"})
-    st = graph.graph_stats
-    assert st["replayed"] >= 3 and st["eager"] + st["replayed"] == 5, st
+    cap, rep, eag = _replays(graph)
+    assert rep >= 3 and eag + rep == 5, (cap, rep, eag)
     ms = [a.elapsed_time(b) for a, b in timers["table"]]
     assert len(ms) == 5
     assert all(0.0 < m < 50.0 for m in ms), ms
     # replayed durations agree with the eager ones (same kernel, same work)
     assert max(ms[-3:]) < 3.0 * min(ms[:2]) + 0.05
+
+
+def test_native_batch_deferred_equals_eager():
+    """suggest_many's path: WorkBatch levels with deferred readbacks through
+    the native launcher equal eager single runs."""
+    from hyperopt_amd.engine import WorkBatch
+    eager, native, DeviceHistory = _pair("native")
+    mat, active, losses = _history(2000, 8)
+    hists = []
+    for eng in (eager, native):
+        h = DeviceHistory(eng, len(SPACE), cap=2048)
+        h.append(mat, active)
+        hists.append(h)
+    for step in range(5):
+        works, isb = _works(mat, active, losses, 2000, step, 1 << 12)
+        n_b = [np.size(w.obs_below) for w in works]
+        n_a = [w.n_above for w in works]
+        keys = [w.key for w in works]
+        out = []
+        for eng, h in zip((eager, native), hists):
+            b = WorkBatch(("t",) + tuple(n_b) + tuple(n_a), n_b, n_a, keys, [0] * len(works),
+                          lambda works=works: works)
+            p = eng.run(b, histories=[(h, None, isb)], defer=True)
+            r = p.result()
+            out.append((r.index.tolist(), r.value.tolist(), r.score.tolist(),
+                        r.n_scored.tolist()))
+        assert out[0] == out[1], step
+    assert native.graph_stats.get("native", 0) >= 3
