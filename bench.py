@@ -381,6 +381,12 @@ def main():
     hist = DeviceHistory(eng, len(space), cap=T_HIST)
     hist.append(mat)
 
+    # label-sharded levels on RCCL: the per-label argmax all-reduce runs inside
+    # the level, on its stream (tpe_best_scatter + tpe_maxloc_allreduce on
+    # torch's communicator), read back with the level's results
+    xcomm = hdist.comm_ptr() if (world > 1 and strong) else None
+    xchg = (xcomm, len(space), world, [u[0] for u in units]) if xcomm else None
+
     def step(k, timers=None, timer_groups=None, precision=None):
         prec = precision or args.precision
         if args.upload_history:
@@ -396,12 +402,14 @@ def main():
             isb[rb] = 1
             works = history_batch(space, mat, hist, rb, k, n_cand, cand_base, units, n_cand)
             r = eng.run(works, precision=prec, timers=timers, scorer=scorer,
-                        history=hist, is_below=isb, timer_groups=timer_groups)
+                        history=hist, is_below=isb, timer_groups=timer_groups, exchange=xchg)
             res = [LabelResult(space[u[0]][0], ix, v, sc, ns) for u, ix, v, sc, ns in
                    zip(units, r.index.tolist(), r.value.tolist(), r.score.tolist(),
                        r.n_scored.tolist())]
         if world > 1:
-            if strong:  # label-sharded level: every rank learns every label's winner
+            if strong and xchg is not None and not args.upload_history:
+                pass  # every rank already holds every label's winner (eng.last_exchange)
+            elif strong:  # label-sharded level: every rank learns every label's winner
                 hdist.gather_best(len(space), [(u[0], r) for u, r in zip(units, res)])
             else:
                 hdist.allreduce_best(res)
@@ -512,7 +520,8 @@ def main():
                                   "" if strong else " per GPU"),
                    "labels": len(space), "history": T_HIST, "candidates_per_label": n_cand,
                    "parallelism": ("label-sharded x%d (dist.plan_units), RCCL all-gather + "
-                                   "device max-loc" % world) if strong else
+                                   "device max-loc %s" % (world, "inside the level" if xchg
+                                                          else "(host path)")) if strong else
                                   ("candidate-sharded x%d, RCCL max-loc combine" % world),
                    "rank0_units": len(units)},
         "roofline": roofline,

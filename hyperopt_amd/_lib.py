@@ -63,6 +63,8 @@ OP_CODES = {name: i + 1 for i, name in enumerate((
     "tpe_lattice_compact", "tpe_score_quantized", "tpe_score_categorical", "tpe_sample"))}
 OP_EVENT_RECORD, OP_STREAM_WAIT, OP_MEMCPY, OP_STREAM_SYNC = range(len(OP_CODES) + 1,
                                                                   len(OP_CODES) + 5)
+OP_CODES["tpe_best_scatter"] = OP_STREAM_SYNC + 1
+OP_CODES["tpe_maxloc_allreduce"] = OP_STREAM_SYNC + 2
 PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
     PRIOR_CATEGORICAL = range(6)
 
@@ -109,6 +111,7 @@ _SIGNATURES = {
     "tpe_sample": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P]),
     "tpe_best_combine": (_I, [_P, _I, _I, _P, _P]),
     "tpe_maxloc_allreduce": (_I, [_P, _P, _P, _I, _P, _P]),
+    "tpe_best_scatter": (_I, [_P, _P, _I, _P, _I, _P]),
     "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
     "tpe_run_ops": (_I, [_P, _I, ctypes.POINTER(_I)]),
     "tpe_last_error": (ctypes.c_char_p, []),

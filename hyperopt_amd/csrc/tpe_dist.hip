@@ -55,7 +55,45 @@ const Rccl& rccl() {
 }  // namespace
 }  // namespace tpe
 
+namespace tpe {
+namespace {
+// label slot s <- the records of the jobs mapped to it, folded in job order
+// (a rank may hold several candidate ranges of one label); empty if none
+__global__ void k_scatter_best(const tpe_best* __restrict__ by_job,
+                               const int32_t* __restrict__ slot, int n_jobs,
+                               tpe_best* __restrict__ out, int n_slots) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slots) return;
+  tpe_best b;
+  b.score = 0.0;
+  b.index = -1;
+  b.value = 0.0;
+  int64_t n = 0;
+  for (int j = 0; j < n_jobs; ++j) {
+    if (slot[j] != s) continue;
+    const tpe_best o = by_job[j];
+    n += o.n_scored;
+    if (better(o.score, o.index, b.score, b.index)) b = o;
+  }
+  b.n_scored = n;
+  out[s] = b;
+}
+}  // namespace
+}  // namespace tpe
+
 using namespace tpe;
+
+extern "C" int tpe_best_scatter(const tpe_best* by_job, const int32_t* slot, int n_jobs,
+                                tpe_best* out, int n_slots, void* stream) {
+  if (n_jobs < 0 || n_slots < 0 || (n_slots > 0 && !out) || (n_jobs > 0 && (!by_job || !slot))) {
+    set_error("tpe_best_scatter: bad arguments (n_jobs=%d n_slots=%d)", n_jobs, n_slots);
+    return TPE_E_ARG;
+  }
+  if (n_slots == 0) return TPE_OK;
+  hipLaunchKernelGGL(k_scatter_best, dim3((n_slots + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, by_job, slot, n_jobs, out, n_slots);
+  return check_launch("tpe_best_scatter");
+}
 
 extern "C" int tpe_maxloc_allreduce(const tpe_best* local, tpe_best* gathered, tpe_best* out,
                                     int n_labels, void* comm, void* stream) {

@@ -108,6 +108,23 @@ def plan_units(kinds, n_total, world_size):
     return out
 
 
+def comm_ptr(group=None):
+    """The ncclComm_t address behind torch's RCCL process group (for
+    Engine.run(exchange=...)), or None (gloo, or a torch without the
+    accessor): the level's cross-rank argmax then stays on the host path."""
+    try:
+        import torch
+        import torch.distributed as dist
+        if dist.get_backend(group) != "nccl":
+            return None
+        pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        be = pg._get_backend(torch.device("cuda", torch.cuda.current_device()))
+        ptr = int(be._comm_ptr())
+        return ptr or None
+    except Exception:
+        return None
+
+
 def empty_records(n):
     rec = np.zeros(n, L.BEST_DTYPE)
     rec["index"] = -1

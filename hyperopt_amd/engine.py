@@ -493,7 +493,7 @@ class Engine:
             outputs=False, stream=None, timers=None, sample_only=False,
             pruned=True, scorer=None, posteriors=False, history=None, rows=None,
             is_below=None, histories=None, timer_groups=None,
-            table_scores=False, defer=False) -> List[LabelResult]:
+            table_scores=False, defer=False, exchange=None) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``;
         ``timer_groups`` (optional set) limits them to those groups (each event
@@ -522,7 +522,14 @@ class Engine:
         BatchResult, and with ``defer`` a _Pending whose ``result()`` waits
         for it -- the readback is queued behind the launches and the call
         returns at once, so the host can prepare the next batch while this one
-        runs (the next run on this engine first collects it)."""
+        runs (the next run on this engine first collects it).
+        ``exchange``: (comm, n_labels, world, slots) -- a label-sharded level
+        on one rank of ``world``: after scoring, the works' winners are folded
+        into n_labels label slots (``slots``: slot per work; tpe_best_scatter)
+        and all-reduced over the RCCL communicator ``comm`` (an ncclComm_t
+        address; tpe_maxloc_allreduce), on the level's stream; the combined
+        records (BEST_DTYPE, the same on every rank) come back with the level's
+        one readback as ``self.last_exchange``."""
         if not works:
             return []
         if self._inflight is not None:  # its pinned buffers are about to be reused
@@ -865,7 +872,15 @@ class Engine:
         # count, [64,...) tpe_best per job
         JS, BS = L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize
         n_jobs = len(order)
-        o_res = pack.add(np.zeros(64 + n_jobs * BS, np.uint8))
+        xbytes = 0
+        if exchange is not None:
+            x_comm, x_labels, x_world, x_slots = exchange
+            x_slots = np.asarray(x_slots, np.int32).reshape(-1)
+            if x_slots.size != len(order):
+                raise ValueError("exchange: %d slots for %d works" % (x_slots.size, len(order)))
+            o_xslot = pack.add(x_slots[np.asarray(order, np.int64)])
+            xbytes = int(x_labels) * BS
+        o_res = pack.add(np.zeros(64 + n_jobs * BS + xbytes, np.uint8))
         native_ok = self.native and not self.graphs and pkey is not None and not (
             outputs or sample_only or posteriors or table_scores)
         base = self._upload(pack, stream, copy=not native_ok)
@@ -907,6 +922,8 @@ class Engine:
                     cobs_off, lat_off,
                     (history.vals.data_ptr(), history.active.data_ptr(), history.ld, n_rows)
                     if history is not None else None,
+                    None if exchange is None else
+                    (int(x_comm), int(x_labels), int(x_world), x_slots.tobytes()),
                     self.side_stream, self.table_scorer, self.exact64,
                     "off" if timers is None else
                     ("all" if timer_groups is None else frozenset(timer_groups)))
@@ -934,6 +951,19 @@ class Engine:
                 cap.order(self._event(name), src, dst)
             else:
                 self._order(name, src, dst)
+
+        def stream_rec(name, src):  # event `name` marks `src`'s work so far
+            if isinstance(cap, _OpList):
+                cap.add(L.OP_EVENT_RECORD, self._event(name), src)
+            else:
+                L.hip_check(self._hip.hipEventRecord(self._event(name), src), "hipEventRecord")
+
+        def stream_wait(name, dst):  # `dst` waits for event `name`
+            if isinstance(cap, _OpList):
+                cap.add(L.OP_STREAM_WAIT, dst, self._event(name))
+            else:
+                L.hip_check(self._hip.hipStreamWaitEvent(dst, self._event(name), 0),
+                            "hipStreamWaitEvent")
 
         def launch_level(lib=lib):
             if hist_mode:
@@ -968,8 +998,13 @@ class Engine:
                     self._side = torch.cuda.Stream(self.device)
                 side = self._side
             side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
-            if side is not None:
-                stream_order("gathered", sp, side_p)
+            # main-stream issue order: gather, fit, table build, scorers; the
+            # side stream's launches are issued after the table build (host
+            # launches cost a few us each: at a one-eighth label share the main
+            # stream would otherwise idle behind them), ordered by
+            # two events recorded on the main stream as it goes
+            if side is not None and cat:
+                stream_rec("gathered", sp)
             # ---- posterior fit ------------------------------------------------------
             if fit_ids:
                 e0 = tick("fit")
@@ -977,13 +1012,18 @@ class Engine:
                                            n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
                                            d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
                 tock("fit", e0)
-            if cat:
+
+            def cat_fit():  # on the side stream once the lists are gathered
+                if side is not None:
+                    stream_wait("gathered", side_p)
                 e0 = tick("cat_fit", side)
                 d_p = base + o_p  # the posterior is formed in place in the staged pool
                 L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
                                               int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
                                               side_p), "tpe_cat_posterior")
                 tock("cat_fit", e0, side)
+            if cat and side is None:
+                cat_fit()
 
             if posteriors:
                 return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
@@ -1006,17 +1046,35 @@ class Engine:
             # quantized and categorical groups go to the side stream (after the job
             # table has landed); continuous groups stay on `stream`
             if side is not None:  # quantized groups need the continuous fit
-                stream_order("fitted", sp, side_p)
+                stream_rec("fitted", sp)
             table_calls = []
             jobs_ptr = jobs.__array_interface__["data"][0]
-            g_order = list(range(len(groups)))
-            if side is not None:  # side groups launched first
-                g_order.sort(key=lambda g: groups[g][0] not in SIDE_KINDS)
+            # launch order: the first sampled table group's build (the main
+            # stream's next kernels after the fit), then the side groups, then
+            # the main-stream scorers -- the host issues launches at a few us
+            # each, and at a one-eighth label share the main stream would
+            # otherwise sit idle behind the side stream's launches
+            g_order = [(g, "all") for g in range(len(groups))]
+            early = None
+            tgroups = [g for g, (k, ids) in enumerate(groups) if k == "table" and ids]
+            if side is not None:
+                if len(tgroups) == 1 and not inj(groups[tgroups[0]][1][0]):
+                    early = tgroups[0]  # (one table group: the workspace tables are its own)
+                g_order = ([(early, "build")] if early is not None else []) + \
+                    [(g, "all") for g in range(len(groups)) if groups[g][0] in SIDE_KINDS] + \
+                    [(g, "score" if g == early else "all") for g in range(len(groups))
+                     if groups[g][0] not in SIDE_KINDS]
             joined = side is None
-            for g in g_order:
+            side_started = side is None
+            for g, stage in g_order:
                 kind, ids = groups[g]
                 if not ids:
                     continue
+                if not side_started and kind in SIDE_KINDS:
+                    side_started = True
+                    if cat:
+                        cat_fit()
+                    stream_wait("fitted", side_p)
                 if sample_only:
                     if kind in ("cont", "lat", "qfb"):
                         a, b = _slice_of(groups, g)
@@ -1035,7 +1093,8 @@ class Engine:
                 ks = side_p if on_side else sp
                 kst = side if on_side else None
                 pname = "partial_side" if on_side else "partial"
-                e0 = tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst)
+                e0 = tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst) \
+                    if stage != "score" else None
                 if kind == "cont":
                     npart = lib.tpe_score_partials(hjp, nj)
                     d_part = self._buf("partial", 32 * max(npart, 1))
@@ -1057,6 +1116,7 @@ class Engine:
                                                  d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
                             "tpe_score_sorted")
                 elif kind == "table":
+                    # (stage "build" / "score": the two halves of an early-built group)
                     npart = lib.tpe_table_partials(hjp, nj)
                     d_part = self._buf("partial", 32 * max(npart, 1))
                     d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
@@ -1068,10 +1128,13 @@ class Engine:
                     d_wide = self._buf("wide_idx", 4 * n_comp)
                     max_comp = max_obs + 1
                     d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
-                    L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64, max_comp,
-                                                d_rh, d_rl, d_wide, d_tsc, d_tab, d_cells, d_stats,
-                                                sp), "tpe_table_build")
-                    tock("table_build", e0)
+                    if stage != "score":
+                        L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64,
+                                                    max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab,
+                                                    d_cells, d_stats, sp), "tpe_table_build")
+                        tock("table_build", e0)
+                    if stage == "build":
+                        continue
                     if not joined and self.side_stream == "2":
                         stream_order("joined", side_p, sp)
                         joined = True
@@ -1138,11 +1201,21 @@ class Engine:
                             "tpe_score_categorical")
                 tock(kind, e0, kst)
 
+            if not side_started:  # (no side group: only the categorical posterior)
+                if cat:
+                    cat_fit()
             if not joined:  # join before the readback
                 stream_order("joined", side_p, sp)
+            if exchange is not None:  # label-sharded level: the cross-rank argmax
+                d_xl = self._buf("xchg_local", x_labels * BS)
+                d_xg = self._buf("xchg_gathered", x_world * x_labels * BS)
+                L.check(lib.tpe_best_scatter(d_best, base + o_xslot, n_jobs, d_xl, x_labels, sp),
+                        "tpe_best_scatter")
+                L.check(lib.tpe_maxloc_allreduce(d_xl, d_xg, d_best + n_jobs * BS, x_labels,
+                                                 x_comm, sp), "tpe_maxloc_allreduce")
             return table_calls, False
 
-        nbytes = 64 + n_jobs * BS  # the result block read back at the end
+        nbytes = 64 + n_jobs * BS + xbytes  # the result block read back at the end
         ops = None
         if native_ok:
             ops = self._oplists.get(gkey)
@@ -1235,6 +1308,7 @@ class Engine:
             if caller_p is not None:  # the caller's later work follows this level
                 L.hip_check(self._hip.hipStreamWaitEvent(caller_p, ev, 0), "hipStreamWaitEvent")
             p = self._inflight = _Pending(self, ev, pin, nbytes, np.asarray(order, np.int64),
+                                          64 + n_jobs * BS if xbytes else None,
                                           bool(table_calls), after)
             return p if defer else p.result()
         if ops is None:
@@ -1242,7 +1316,9 @@ class Engine:
         if after is not None:
             after()
         res_h = pin[:nbytes].numpy().copy()
-        best_h = res_h[64:].view(L.BEST_DTYPE)
+        best_h = res_h[64:64 + n_jobs * BS].view(L.BEST_DTYPE)
+        self.last_exchange = res_h[64 + n_jobs * BS:].view(L.BEST_DTYPE).copy() if xbytes \
+            else None
         with torch.cuda.stream(stream):
             err = int(res_h[:4].view(np.int32)[0])
             self.last_pairs = None
@@ -1324,9 +1400,10 @@ class _Pending(object):
     with defer=True).  ``result()`` waits for it once, checks the error bits
     and returns the BatchResult (cached)."""
 
-    def __init__(self, eng, event, pin, nbytes, order, table, after=None):
+    def __init__(self, eng, event, pin, nbytes, order, xoff, table, after=None):
         self.eng, self.event, self.pin, self.nbytes = eng, event, pin, nbytes
         self.order, self.table, self.after = order, table, after
+        self.xoff = xoff  # offset of the exchanged label records (Engine.run exchange=)
         self._res = None
 
     def result(self):
@@ -1348,8 +1425,10 @@ class _Pending(object):
             eng.last_table_stats = {"exact_candidates": st[0], "failed_cells": st[1],
                                     "failed_score_cells": st[2]}
         _raise_errors(err)
-        best_h = res_h[64:].view(L.BEST_DTYPE)
         n = self.order.size
+        best_h = res_h[64:64 + n * L.BEST_DTYPE.itemsize].view(L.BEST_DTYPE)
+        eng.last_exchange = res_h[self.xoff:].view(L.BEST_DTYPE).copy() \
+            if self.xoff is not None else None
         by = np.empty(n, L.BEST_DTYPE)
         by[self.order] = best_h[:n]
         self._res = BatchResult(by["index"].copy(), by["value"].copy(), by["score"].copy(),

@@ -408,6 +408,14 @@ int tpe_prior_sample(const tpe_prior* priors, const tpe_prior* host_priors, int 
 int tpe_best_combine(const tpe_best* sets, int n_sets, int n_labels, tpe_best* out,
                      void* stream);
 
+/* ---- per-label records of one rank's level: slot s of `out` (n_slots
+ * tpe_best, device) <- the records of the jobs j with slot[j] == s (device
+ * int32 per job), folded in job order with the argmax rules; index -1 where
+ * no job maps to s.  The input of tpe_maxloc_allreduce for a label-sharded
+ * level. */
+int tpe_best_scatter(const tpe_best* by_job, const int32_t* slot, int n_jobs, tpe_best* out,
+                     int n_slots, void* stream);
+
 /* ---- cross-GPU max-loc (replaces the argmax of tpe.py:650-658
  * across ranks): all-gather of every rank's n_labels records over the caller's
  * RCCL communicator `comm` (an ncclComm_t; librccl.so.1 is bound at the first
@@ -450,6 +458,8 @@ enum {
   TPE_OP_MEMCPY,               /* hipMemcpyAsync(a[0] dst, a[1] src, a[2] bytes,
                                   a[3] hipMemcpyKind, a[4] stream)           */
   TPE_OP_STREAM_SYNC,          /* hipStreamSynchronize(a[0] stream)          */
+  TPE_OP_BEST_SCATTER,         /* tpe_best_scatter                           */
+  TPE_OP_MAXLOC_ALLREDUCE,     /* tpe_maxloc_allreduce (RCCL, stream-ordered) */
   TPE_OP_COUNT
 };
 #define TPE_OP_ARGS 23

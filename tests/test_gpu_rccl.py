@@ -55,3 +55,52 @@ def test_maxloc_allreduce_one_rank():
         np.testing.assert_array_equal(got["score"][ok], rec["score"][ok])
     finally:
         rccl.ncclCommDestroy(comm)
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_level_exchange_one_rank(native):
+    """Engine.run(exchange=...): a label-sharded level's winners folded into
+    label slots on the device and all-reduced over the communicator inside
+    the level (bench.py's multi-GPU step) equal the host fold of the
+    per-work results; replayed levels (native launcher) included."""
+    import torch
+    from hyperopt_amd import _lib as L
+    from hyperopt_amd import dist as hdist
+    from hyperopt_amd.engine import DeviceHistory, Engine, LabelWork
+    torch.cuda.set_device(0)
+    rccl, comm = _comm()
+    try:
+        eng = Engine()
+        eng.native = native
+        rng = np.random.RandomState(3)
+        T = 1500
+        mat = np.stack([rng.uniform(-5, 5, T), rng.normal(0, 2, T),
+                        np.round(rng.uniform(0, 20, T)), rng.randint(0, 6, T).astype(float)], 1)
+        hist = DeviceHistory(eng, 4, cap=2048)
+        hist.append(mat)
+        isb = np.zeros(T, np.uint8)
+        isb[np.argsort(rng.normal(size=T))[:10]] = 1
+        space = [("u", "uniform", (-5.0, 5.0)), ("n", "normal", (0.0, 2.0)),
+                 ("q", "quniform", (0.0, 20.0, 1.0)), ("c", "randint", (6,))]
+        # this "rank" holds labels 3, 0 and two candidate ranges of label 1 in
+        # slots of a 6-label level (slots 2, 4, 5 empty)
+        units = [(0, 3, 0, 1 << 16), (1, 0, 0, 1 << 16), (2, 1, 0, 1 << 15), (3, 1, 1 << 15, 1 << 15)]
+        for step in range(4):
+            works = []
+            for col, slot, start, count in units:
+                lab, kind, a = space[col]
+                below = mat[:, col][isb == 1]
+                works.append(LabelWork(lab, kind, a, below, None, n_cand=count,
+                                       key=97 * step + col, cand_base=start, col=col,
+                                       n_above=int((isb == 0).sum()), n_total=1 << 16))
+            res = eng.run(works, history=hist, is_below=isb,
+                          exchange=(comm.value, 6, 1, [u[1] for u in units]))
+            got = eng.last_exchange
+            want = hdist.gather_best(6, [(u[1], r) for u, r in zip(units, res)])
+            assert [(float(x["score"]), int(x["index"]), float(x["value"]), int(x["n_scored"]))
+                    for x in got] == want
+            assert got["index"][2] == -1 and got["n_scored"][1] == 1 << 16
+        if native:
+            assert eng.graph_stats.get("native", 0) >= 2
+    finally:
+        rccl.ncclCommDestroy(comm)

@@ -1,31 +1,44 @@
-"""Per-step GPU timeline from a rocprofv3 --kernel-trace --memory-copy-trace
-database (diagnostic): kernels and copies in start order with the idle gap
-before each, for the last step of the run.
+"""Per-level kernel timeline from a rocprofv3 --kernel-trace rocpd database:
+for the last level(s) of a run, every dispatch's start offset from the
+level's first kernel, duration, queue and the idle gap before it on the GPU
+(diagnostic for the multi-GPU critical path).
 
-    python tools/timeline.py <run_results.db> [first-kernel-of-step]
+    python tools/timeline.py gpurun_out/tl8 [levels=2] [first-kernel=k_gather_obs]
 """
+import glob
+import os
+import re
 import sqlite3
 import sys
 
-db = sqlite3.connect(sys.argv[1])
-marker = sys.argv[2] if len(sys.argv) > 2 else "k_gather_obs"
-rows = [("K", n, s, e) for n, s, e in db.execute("select name, start, end from kernels")]
-rows += [("C", "%s %dB" % (n, sz), s, e)
-         for n, s, e, sz in db.execute("select name, start, end, size from memory_copies")]
-rows.sort(key=lambda r: r[2])
-starts = [i for i, r in enumerate(rows) if r[0] == "K" and marker in r[1]]
-if len(starts) < 2:
-    raise SystemExit("need two steps starting with %s" % marker)
-seg = rows[starts[-2]:starts[-1]]
-t0 = seg[0][2]
-prev_end = None
-busy = 0
-for kind, name, s, e in seg:
-    gap = (s - prev_end) / 1e3 if prev_end is not None else 0.0
-    busy += e - s
-    print("%8.1f us  gap %7.1f  dur %7.1f  %s %s" % ((s - t0) / 1e3, gap, (e - s) / 1e3, kind,
-                                                     name[:70]))
-    prev_end = e if prev_end is None else max(prev_end, e)
-span = (seg[-1][3] - t0) / 1e3
-print("step span %.1f us, busy %.1f us, next step starts %.1f us after this one's start"
-      % (span, busy / 1e3, (rows[starts[-1]][2] - t0) / 1e3))
+
+def short(name):
+    m = re.search(r"(k_\w+|__amd_rocclr_\w+|at::native::\w+)", name)
+    return m.group(1) if m else name[:40]
+
+
+def main(src, levels=2, first="k_gather_obs"):
+    db = sorted(glob.glob(os.path.join(src, "**", "*.db"), recursive=True))[0]
+    c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    qcol = "queue_id" if "queue_id" in cols else ("stream_id" if "stream_id" in cols else None)
+    rows = list(c.execute("select name, start, end%s from kernels order by start"
+                          % ((", " + qcol) if qcol else "")))
+    starts = [i for i, r in enumerate(rows) if short(r[0]) == first]
+    for li in starts[-levels:]:
+        nxt = [s for s in starts if s > li]
+        seg = rows[li:nxt[0] if nxt else len(rows)]
+        t0 = seg[0][1]
+        busy_end = t0
+        print("level at dispatch %d: %d kernels, span %.1f us" % (
+            li, len(seg), (max(r[2] for r in seg) - t0) / 1e3))
+        for r in seg:
+            gap = max(0, r[1] - busy_end) / 1e3
+            busy_end = max(busy_end, r[2])
+            print("  %-28s start %7.1f  dur %6.1f  gap %5.1f  q %s" % (
+                short(r[0]), (r[1] - t0) / 1e3, (r[2] - r[1]) / 1e3, gap,
+                r[3] if qcol else "-"))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], *(int(a) if a.isdigit() else a for a in sys.argv[2:]))
