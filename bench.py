@@ -30,6 +30,11 @@ import platform
 import sys
 import time
 
+# kernel arguments in device memory: shorter launch-to-start latency for the
+# ~20 launches of a level (a one-eighth label share: 0.318 -> 0.292 ms,
+# DESIGN.md 6); read by the HIP runtime at initialisation, so before torch
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -121,12 +126,18 @@ def history_batch(space, mat, hist, rows_b, step, n_cand, cand_base, units, n_to
     from hyperopt_amd.engine import WorkBatch
     nb = hist.active_host[rows_b].sum(0)
     na = hist.n_active - nb
-    keys = np.asarray(label_keys(0, step, [lab for lab, _, _ in space]), np.uint64)
+    from hyperopt_amd.tpe import label_keys_array
+    keys = label_keys_array(0 * 1000003 + step, space_labels(space))
     j = np.fromiter((u[0] for u in units), np.int64, len(units))
     return WorkBatch(("bench-c3", tuple(units), n_total), nb[j], na[j], keys[j],
                      [cand_base + u[1] for u in units],
                      lambda: history_works(space, mat, hist, rows_b, step, n_cand, cand_base,
                                            units, n_total))
+
+
+def space_labels(space):
+    """The space's labels as a tuple (label_keys_array caches their hashes by it)."""
+    return tuple(lab for lab, _, _ in space)
 
 
 def label_key(seed, step, lab):

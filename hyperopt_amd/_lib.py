@@ -114,6 +114,7 @@ _SIGNATURES = {
     "tpe_best_scatter": (_I, [_P, _P, _I, _P, _I, _P]),
     "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
     "tpe_run_ops": (_I, [_P, _I, ctypes.POINTER(_I)]),
+    "tpe_smallest_rows": (_I64, [_P, _I64, _I64, _P]),
     "tpe_last_error": (ctypes.c_char_p, []),
     "tpe_abi_version": (_I, []),
     "tpe_struct_sizes": (_I, [_P, _I]),

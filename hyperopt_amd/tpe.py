@@ -35,6 +35,7 @@ import time
 
 import numpy as np
 
+from . import _lib as _L
 from . import dist as hdist
 from . import rand
 from .base import doc_loss
@@ -101,13 +102,29 @@ def _mix64_np(h):
     return h ^ (h >> np.uint64(31))
 
 
-def label_keys(seed, labels):
-    """label_key(seed, lab) for every label at once (uint64 array arithmetic
-    wraps like the masked Python integers)."""
-    s = np.uint64(_mix64((int(seed) * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF))
+@functools.lru_cache(maxsize=4096)
+def _label_hashes(labels):
+    """FNV-1a hashes of a tuple of labels, as a read-only uint64 array."""
     h = np.fromiter((_label_hash(lab) for lab in labels), np.uint64, len(labels))
+    h.flags.writeable = False
+    return h
+
+
+def label_keys_array(seed, labels):
+    """label_key(seed, lab) for every label at once, as a uint64 array (uint64
+    array arithmetic wraps like the masked Python integers)."""
+    s = np.uint64(_mix64((int(seed) * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF))
+    try:
+        h = _label_hashes(tuple(labels))
+    except TypeError:  # unhashable labels
+        h = np.fromiter((_label_hash(lab) for lab in labels), np.uint64, len(labels))
     with np.errstate(over="ignore"):
-        return _mix64_np(h ^ s).tolist()
+        return _mix64_np(h ^ s)
+
+
+def label_keys(seed, labels):
+    """label_key(seed, lab) for every label at once, as a list of ints."""
+    return label_keys_array(seed, labels).tolist()
 
 
 class History(object):
@@ -220,20 +237,19 @@ def split_masks(hist, gamma, gamma_cap=DEFAULT_LF):
 
 
 def _smallest_rows(losses, n):
-    """Rows of argsort(losses, kind="stable")[:n] (as a set), in O(T) for small n:
-    everything strictly below the n-th smallest loss, then the earliest rows
-    equal to it."""
+    """Rows of argsort(losses, kind="stable")[:n] in ascending row order, one
+    pass in C for the suggest path's small n (tpe_smallest_rows)."""
     T = losses.size
     if n <= 0:
         return np.zeros(0, np.int64)
     if n >= T:
         return np.arange(T)
-    v = np.partition(losses, n - 1)[n - 1]
-    if np.isnan(v):
-        return np.argsort(losses, kind="stable")[:n]
-    lt = np.flatnonzero(losses < v)
-    eq = np.flatnonzero(losses == v)[:n - lt.size]
-    return np.concatenate([lt, eq])
+    losses = np.ascontiguousarray(losses, dtype=np.float64)
+    out = np.empty(n, np.int64)
+    got = _L.load().tpe_smallest_rows(losses.ctypes.data, T, n, out.ctypes.data)
+    if got != n:
+        raise _L.TpeHipError("tpe_smallest_rows returned %d" % got)
+    return out
 
 
 def _precision(precision, n_ei, T):

@@ -470,6 +470,12 @@ typedef struct tpe_op {
 } tpe_op;                       /* 192 bytes */
 int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op);
 
+/* host: rows of the k smallest losses in np.argsort(losses, kind="stable")
+ * order (NaN after +inf, ties to the earlier row) -- the below split of
+ * ap_split_trials (tpe.py:623-646) -- written to out (host) in ascending row
+ * order; returns min(k, n), -1 on bad arguments. */
+int64_t tpe_smallest_rows(const double* losses, int64_t n, int64_t k, int64_t* out);
+
 const char* tpe_last_error(void);
 int tpe_abi_version(void);
 /* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table, tpe_gather,

@@ -308,3 +308,27 @@ def test_reachable_memo_matches_walk():
     for _ in range(2):  # second pass served from the memo
         for d in cases:
             assert dom.reachable(d) == dom._reachable_walk(d), d
+
+
+def test_smallest_rows_is_stable_argsort_prefix():
+    """tpe._smallest_rows (C one-pass split, tpe_smallest_rows) == the rows of
+    np.argsort(losses, kind="stable")[:n] -- ties to the earlier row, +inf and
+    NaN last -- for random, tied, infinite and NaN-laden losses."""
+    from hyperopt_amd.tpe import _smallest_rows
+    rng = np.random.RandomState(0)
+    for T in (1, 2, 7, 100, 1000, 10007):
+        for kind in ("normal", "ties", "inf", "nan", "desc"):
+            x = rng.normal(size=T)
+            if kind == "ties":
+                x = np.round(x * 2) / 2
+            elif kind == "inf":
+                x[rng.uniform(size=T) < 0.5] = np.inf
+            elif kind == "nan":
+                x[rng.uniform(size=T) < 0.7] = np.nan
+            elif kind == "desc":
+                x = -np.arange(T, dtype=float)
+            for n in (1, 3, 25, T // 2 + 1, T):
+                n = min(n, T)
+                want = np.sort(np.argsort(x, kind="stable")[:n])
+                got = np.sort(_smallest_rows(x, n))
+                np.testing.assert_array_equal(got, want, err_msg="%s T=%d n=%d" % (kind, T, n))
