@@ -426,6 +426,25 @@ def main():
                 hdist.allreduce_best(res)
         return works, res
 
+    xnote = "inside the level" if xchg else "(host path)"
+    if xchg is not None:
+        # first level: the in-level exchange checked against the host path
+        # (torch all-gather + host fold); every rank must agree to keep it
+        try:
+            _, res0 = step(0)
+            got = [(float(x["score"]), int(x["index"]), float(x["value"]), int(x["n_scored"]))
+                   for x in eng.last_exchange]
+            ok = got == hdist.gather_best(len(space), [(u[0], r) for u, r in zip(units, res0)])
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            ok, xnote = False, "(host path: in-level exchange failed: %r)" % (e,)
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()):
+            xchg = None
+            if ok:
+                xnote = "(host path: in-level exchange disagreed on some rank)"
+            elif "failed" not in xnote:
+                xnote = "(host path: in-level exchange disagreed with the host fold)"
     for k in range(args.warmup):
         step(k)
 
@@ -531,8 +550,7 @@ def main():
                                   "" if strong else " per GPU"),
                    "labels": len(space), "history": T_HIST, "candidates_per_label": n_cand,
                    "parallelism": ("label-sharded x%d (dist.plan_units), RCCL all-gather + "
-                                   "device max-loc %s" % (world, "inside the level" if xchg
-                                                          else "(host path)")) if strong else
+                                   "device max-loc %s" % (world, xnote)) if strong else
                                   ("candidate-sharded x%d, RCCL max-loc combine" % world),
                    "rank0_units": len(units)},
         "roofline": roofline,

@@ -29,11 +29,13 @@ typedef ncclResult_t (*AllGatherFn)(const void*, void*, size_t, ncclDataType_t, 
                                     hipStream_t);
 typedef ncclResult_t (*CommCountFn)(const ncclComm_t, int*);
 typedef const char* (*ErrorStringFn)(ncclResult_t);
+typedef ncclResult_t (*AsyncErrorFn)(ncclComm_t, ncclResult_t*);
 
 struct Rccl {
   AllGatherFn all_gather = nullptr;
   CommCountFn comm_count = nullptr;
   ErrorStringFn error_string = nullptr;
+  AsyncErrorFn async_error = nullptr;
   bool ok = false;
 };
 
@@ -48,9 +50,23 @@ const Rccl& rccl() {
     r.all_gather = reinterpret_cast<AllGatherFn>(dlsym(h, "ncclAllGather"));
     r.comm_count = reinterpret_cast<CommCountFn>(dlsym(h, "ncclCommCount"));
     r.error_string = reinterpret_cast<ErrorStringFn>(dlsym(h, "ncclGetErrorString"));
+    r.async_error = reinterpret_cast<AsyncErrorFn>(dlsym(h, "ncclCommGetAsyncError"));
     r.ok = r.all_gather && r.comm_count;
   });
   return r;
+}
+
+// A non-blocking communicator (torch creates them for eagerly initialised
+// process groups) may answer ncclInProgress: poll its state until the call
+// has been enqueued, as RCCL's non-blocking API asks.
+ncclResult_t settle(const Rccl& r, ncclComm_t comm, ncclResult_t e) {
+  while (e == ncclInProgress && r.async_error) {
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t q = r.async_error(comm, &st);
+    if (q != ncclSuccess) return q;
+    e = st;
+  }
+  return e;
 }
 }  // namespace
 }  // namespace tpe
@@ -108,14 +124,16 @@ extern "C" int tpe_maxloc_allreduce(const tpe_best* local, tpe_best* gathered, t
     return TPE_E_UNSUPPORTED;
   }
   int world = 0;
-  ncclResult_t e = r.comm_count(static_cast<ncclComm_t>(comm), &world);
+  ncclResult_t e = settle(r, static_cast<ncclComm_t>(comm),
+                          r.comm_count(static_cast<ncclComm_t>(comm), &world));
   if (e != ncclSuccess || world < 1) {
     set_error("tpe_maxloc_allreduce: ncclCommCount: %s",
               r.error_string ? r.error_string(e) : "error");
     return TPE_E_ARG;
   }
-  e = r.all_gather(local, gathered, (size_t)n_labels * sizeof(tpe_best), ncclUint8,
-                   static_cast<ncclComm_t>(comm), static_cast<hipStream_t>(stream));
+  e = settle(r, static_cast<ncclComm_t>(comm),
+             r.all_gather(local, gathered, (size_t)n_labels * sizeof(tpe_best), ncclUint8,
+                          static_cast<ncclComm_t>(comm), static_cast<hipStream_t>(stream)));
   if (e != ncclSuccess) {
     set_error("tpe_maxloc_allreduce: ncclAllGather: %s",
               r.error_string ? r.error_string(e) : "error");
