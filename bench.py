@@ -412,19 +412,24 @@ def main():
             isb = np.zeros(T_HIST, np.uint8)
             isb[rb] = 1
             works = history_batch(space, mat, hist, rb, k, n_cand, cand_base, units, n_cand)
-            r = eng.run(works, precision=prec, timers=timers, scorer=scorer,
-                        history=hist, is_below=isb, timer_groups=timer_groups, exchange=xchg)
-            res = [LabelResult(space[u[0]][0], ix, v, sc, ns) for u, ix, v, sc, ns in
-                   zip(units, r.index.tolist(), r.value.tolist(), r.score.tolist(),
-                       r.n_scored.tolist())]
+            res = eng.run(works, precision=prec, timers=timers, scorer=scorer,
+                          history=hist, is_below=isb, timer_groups=timer_groups, exchange=xchg)
         if world > 1:
             if strong and xchg is not None and not args.upload_history:
                 pass  # every rank already holds every label's winner (eng.last_exchange)
             elif strong:  # label-sharded level: every rank learns every label's winner
-                hdist.gather_best(len(space), [(u[0], r) for u, r in zip(units, res)])
+                hdist.gather_best(len(space), list(zip([u[0] for u in units], as_results(res))))
             else:
-                hdist.allreduce_best(res)
+                hdist.allreduce_best(as_results(res))
         return works, res
+
+    def as_results(res):
+        """LabelResults of a level (a WorkBatch level returns columns)."""
+        if isinstance(res, list):
+            return res
+        return [LabelResult(space[u[0]][0], ix, v, sc, ns) for u, ix, v, sc, ns in
+                zip(units, res.index.tolist(), res.value.tolist(), res.score.tolist(),
+                    res.n_scored.tolist())]
 
     xnote = "inside the level" if xchg else "(host path)"
     if xchg is not None:
@@ -434,7 +439,8 @@ def main():
             _, res0 = step(0)
             got = [(float(x["score"]), int(x["index"]), float(x["value"]), int(x["n_scored"]))
                    for x in eng.last_exchange]
-            ok = got == hdist.gather_best(len(space), [(u[0], r) for u, r in zip(units, res0)])
+            ok = got == hdist.gather_best(len(space), [(u[0], r) for u, r in
+                                                       zip(units, as_results(res0))])
         except Exception as e:  # noqa: BLE001 -- reported in the JSON line
             ok, xnote = False, "(host path: in-level exchange failed: %r)" % (e,)
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 11
+#define TPE_ABI_VERSION 12
 
 enum {
   TPE_OK = 0,
