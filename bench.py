@@ -351,6 +351,8 @@ def main():
                          "them from the HBM-resident history")
     ap.add_argument("--dense", action="store_true",
                     help="score with the dense fp32 kernel (same as --scorer dense)")
+    ap.add_argument("--timer-every", type=int, default=4,
+                    help="time the dominant kernel with HIP events on every k-th timed step")
     ap.add_argument("--scorer", default="auto", choices=("auto", "dense", "sorted", "table"),
                     help="fp32 kernel for the unquantized labels (engine.Engine.run)")
     args = ap.parse_args()
@@ -451,8 +453,13 @@ def main():
                 xnote = "(host path: in-level exchange disagreed on some rank)"
             elif "failed" not in xnote:
                 xnote = "(host path: in-level exchange disagreed with the host fold)"
+    group = {"dense": "cont", "sorted": "sorted"}.get(scorer, "table")
+    every = max(1, args.timer_every)
     for k in range(args.warmup):
         step(k)
+    if every > 1:  # the timed variant of the level recorded before timing starts
+        for k in range(2):
+            step(args.warmup + k, {}, {group})
 
     def barrier():
         if world > 1:
@@ -462,14 +469,15 @@ def main():
     # the dominant kernel group is timed with HIP events on its own stream inside
     # the timed region; the other groups only in an untimed pass afterwards
     # (every event pair adds a ~10 us timestamp barrier to the stream)
-    group = {"dense": "cont", "sorted": "sorted"}.get(scorer, "table")
     timers = {}
     step_times = []
     barrier()
     t_start = time.perf_counter()
     for k in range(args.steps):
         t0 = time.perf_counter()
-        works, res = step(args.warmup + k, timers, {group})
+        # HIP events around the dominant kernel on every `every`-th step
+        # (each event pair is a timestamp barrier on its stream)
+        works, res = step(args.warmup + k, timers if k % every == 0 else None, {group})
         step_times.append(time.perf_counter() - t0)
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -527,6 +535,7 @@ def main():
                 "unit": "TFLOP/s (builder-defined ops per candidate, DESIGN.md 3.1)",
                 "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
                 "algorithmic_ops_per_launch": ops, "avg_launch_ms": avg_ms,
+                "timed_launches": len(kms),
                 "dense_pairs_per_launch": dense_pairs,
                 "dense_equivalent_pairs_per_s": dense_pairs / sec if sec > 0 else None,
                 "direct_pair_ceiling_per_s": DIRECT_PAIR_CEILING,

@@ -11,8 +11,11 @@
 // point's parameter types by the call adapter below (the prototypes in
 // tpe_hip.h drive the conversion, so a record can only call a function with
 // exactly its declared arity).
+#include <chrono>
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -119,8 +122,17 @@ extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
     tpe::set_error("tpe_run_ops: n_ops=%d", n_ops);
     return TPE_E_ARG;
   }
+  // TPE_OPS_TRACE=1 (diagnostic): host time of every record on stderr
+  static const bool trace = getenv("TPE_OPS_TRACE") && getenv("TPE_OPS_TRACE")[0] == '1';
+  auto t_prev = std::chrono::steady_clock::now();
   for (int i = 0; i < n_ops; ++i) {
     const int rc = tpe::run_one(ops[i]);
+    if (trace) {
+      const auto t = std::chrono::steady_clock::now();
+      fprintf(stderr, "op %2d code %2d %7.2f us\n", i, ops[i].code,
+              std::chrono::duration<double, std::micro>(t - t_prev).count());
+      t_prev = t;
+    }
     if (rc != TPE_OK) {
       if (failed_op) *failed_op = i;
       return rc;

@@ -306,7 +306,8 @@ class Engine:
         self.native = os.environ.get("TPE_NATIVE_LAUNCH", "1") != "0"
         self._oplists = {}      # launch key -> _OpList
         self._oplist_once = None
-        self._replay = None     # _Replay of the last recorded WorkBatch level
+        self._replays = {}      # signature -> _Replay of a recorded WorkBatch level
+        self._staged_sig = None  # pack signature of what the pinned staging buffer holds
 
     # -- memory --------------------------------------------------------------
     def _buf(self, name, nbytes):
@@ -322,7 +323,7 @@ class Engine:
         return t.data_ptr()
 
     def _drop_oplists(self):
-        self._replay = None
+        self._replays.clear()
         for o in self._oplists.values():
             o.destroy(self._hip)
         self._oplists.clear()
@@ -380,6 +381,7 @@ class Engine:
         name = "stage" if slot == 0 else "stage%d" % slot
         dev = self._buf(name, pack.size)
         self._staged = (dev, pinned.data_ptr(), pack.size)
+        self._staged_sig = None  # (a replay may claim it once the level is recorded)
         if copy:
             L.hip_check(self._hip.hipMemcpyAsync(dev, pinned.data_ptr(), pack.size, L.H2D,
                                                  stream.cuda_stream), "hipMemcpyAsync")
@@ -537,14 +539,17 @@ class Engine:
         stream_arg = stream
         if self._inflight is not None:  # its pinned buffers are about to be reused
             self._inflight.result()
-        rp = self._replay
-        if rp is not None and isinstance(works, WorkBatch) and stream is None:
+        if self._replays and isinstance(works, WorkBatch) and stream is None:
             sig = _Replay.signature(self, works, prior_weight, lf, precision, outputs,
                                     self.torch.cuda.current_stream(self.device).cuda_stream,
                                     sample_only, pruned, scorer, posteriors, history, rows,
                                     is_below, histories, timers, timer_groups, table_scores,
                                     exchange)
-            if sig is not None and sig == rp.sig and rp.gen == self._gen:
+            rp = self._replays.get(sig) if sig is not None else None
+            # valid while the workspace is unchanged and the staging buffer
+            # still holds this level's pack (levels that differ only in their
+            # timer events share one)
+            if rp is not None and rp.gen == self._gen and self._staged_sig == rp.sig[:-1]:
                 return rp.run(self, works, is_below, timers, defer)
         if sample_only:
             outputs = True
@@ -1330,8 +1335,12 @@ class Engine:
                                         pruned, scorer, posteriors,
                                         history, rows, is_below, histories, timers,
                                         timer_groups, table_scores, exchange)
-                self._replay = None if sig is None else _Replay(
-                    sig, self._gen, ops, self._pinned[0], o_jobs, o_isb, p, pin)
+                if sig is not None:
+                    if len(self._replays) >= 8:
+                        self._replays.clear()
+                    self._replays[sig] = _Replay(sig, self._gen, ops, self._pinned[0], o_jobs,
+                                                 o_isb, p, pin)
+                    self._staged_sig = sig[:-1]
             return p if defer else p.result()
         if ops is None:
             L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
@@ -1491,12 +1500,13 @@ class _Replay(object):
         if exchange is not None:
             exchange = (int(exchange[0]), int(exchange[1]), int(exchange[2]),
                         np.asarray(exchange[3], np.int32).tobytes())
+        # (the timer spec last: the rest is the staged pack's signature)
         return (stream, works.key, works.n_below.tobytes(), works.n_above.tobytes(),
                 float(prior_weight), int(lf), int(precision), scorer, pruned,
                 np.size(is_below), history.vals.data_ptr(), history.active.data_ptr(), history.ld,
+                exchange, eng.side_stream, eng.table_scorer, eng.exact64,
                 "off" if timers is None else
-                ("all" if timer_groups is None else frozenset(timer_groups)),
-                exchange, eng.side_stream, eng.table_scorer, eng.exact64)
+                ("all" if timer_groups is None else frozenset(timer_groups)))
 
     def run(self, eng, batch, is_below, timers, defer):
         hm = eng.host_marks
@@ -1514,7 +1524,7 @@ class _Replay(object):
         if hm is not None:
             hm.append(("score launches", time.perf_counter()))
         if rc != 0:
-            eng._replay = None
+            eng._replays.clear()
             raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
                 rc, failed.value, eng.lib.tpe_last_error().decode(errors="replace")))
         eng.graph_stats["native"] = eng.graph_stats.get("native", 0) + 1

@@ -103,7 +103,7 @@ def make_engine():
     eng._graphs, eng._last_gkey, eng._gen, eng._own = {}, None, 0, None
     eng.graph_stats = {"captured": 0, "replayed": 0, "eager": 0}
     eng.native = os.environ.get("TPE_NATIVE_LAUNCH", "1") != "0"
-    eng._oplists, eng._oplist_once, eng._replay = {}, None, None
+    eng._oplists, eng._oplist_once, eng._replays, eng._staged_sig = {}, None, {}, None
     E.torch_shim = shim
     return eng
 
