@@ -284,6 +284,9 @@ class Engine:
         # once the above mixture has PRUNED64_MIN_COMP components, "dense"
         # always sums every component (tpe_score_continuous), "pruned" always prunes
         self.exact64 = os.environ.get("TPE_EXACT64", "auto")
+        # categorical posterior + scoring on the side stream before the fit
+        # (TPE_CAT_EARLY=1) or after it with the quantized labels (0)
+        self.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
         # level graphs (opt-in, TPE_GRAPHS=1): a level whose launch sequence
         # (kernels, grids, workspace pointers, every scalar argument) repeats
         # the previous call's is captured into a hipGraph once and replayed
@@ -1023,29 +1026,6 @@ class Engine:
             # from one event recorded on the main stream after the fit (the
             # categorical posterior could start at the gather, but the side
             # stream has the slack and the fork costs two more host calls)
-            # ---- posterior fit ------------------------------------------------------
-            if fit_ids:
-                e0 = tick("fit")
-                L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
-                                           n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
-                                           d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
-                tock("fit", e0)
-
-            def cat_fit():  # on the side stream (after the fitted fork)
-                e0 = tick("cat_fit", side)
-                d_p = base + o_p  # the posterior is formed in place in the staged pool
-                L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
-                                              int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
-                                              side_p), "tpe_cat_posterior")
-                tock("cat_fit", e0, side)
-            if cat and side is None:
-                cat_fit()
-
-            if posteriors:
-                return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
-                                             d_segs, stream, o_p), True
-
-            _hmark('jobs')
             d_cand = base + o_cand
             d_bl = d_al = d_x = None
             d_sc = None
@@ -1056,40 +1036,28 @@ class Engine:
             elif table_scores:
                 d_sc = self._buf("out_sc", 8 * max(out_off, 1))
                 d_x = self._buf("out_x", 8 * max(out_off, 1))
-
-            _hmark('fit')
-            # ---- scoring, one call per group ----------------------------------------
-            # quantized and categorical groups go to the side stream (after the job
-            # table has landed); continuous groups stay on `stream`
-            if side is not None:  # quantized groups need the continuous fit
-                stream_rec("fitted", sp)
             table_calls = []
             jobs_ptr = jobs.__array_interface__["data"][0]
-            # launch order: the first sampled table group's build (the main
-            # stream's next kernels after the fit), then the side groups, then
-            # the main-stream scorers -- the host issues launches at a few us
-            # each, and at a one-eighth label share the main stream would
-            # otherwise sit idle behind the side stream's launches
-            g_order = [(g, "all") for g in range(len(groups))]
-            early = None
-            tgroups = [g for g, (k, ids) in enumerate(groups) if k == "table" and ids]
-            if side is not None:
-                if len(tgroups) == 1 and not inj(groups[tgroups[0]][1][0]):
-                    early = tgroups[0]  # (one table group: the workspace tables are its own)
-                g_order = ([(early, "build")] if early is not None else []) + \
-                    [(g, "all") for g in range(len(groups)) if groups[g][0] in SIDE_KINDS] + \
-                    [(g, "score" if g == early else "all") for g in range(len(groups))
-                     if groups[g][0] not in SIDE_KINDS]
             joined = side is None
             side_started = side is None
-            for g, stage in g_order:
+
+            def cat_fit():  # on the side stream (after its fork)
+                e0 = tick("cat_fit", side)
+                d_p = base + o_p  # the posterior is formed in place in the staged pool
+                L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
+                                              int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
+                                              side_p), "tpe_cat_posterior")
+                tock("cat_fit", e0, side)
+
+            def launch_group(g, stage):
+                nonlocal joined, side_started
                 kind, ids = groups[g]
                 if not ids:
-                    continue
-                if not side_started and kind in SIDE_KINDS:
-                    side_started = True
+                    return
+                if not side_started and kind in SIDE_KINDS and not (cat_early and kind == "cat"):
+                    side_started = True  # the side stream's groups that need the fit
                     stream_wait("fitted", side_p)
-                    if cat:
+                    if cat and not cat_early:
                         cat_fit()
                 if sample_only:
                     if kind in ("cont", "lat", "qfb"):
@@ -1098,7 +1066,7 @@ class Engine:
                         L.check(lib.tpe_sample(base + o_jobs + a * L.JOB_DTYPE.itemsize,
                                                hj.ctypes.data_as(ctypes.c_void_p), b - a, d_segs,
                                                d_mu, d_sig, d_cdf, precision, d_x, sp), "tpe_sample")
-                    continue
+                    return
                 a, b = _slice_of(groups, g)
                 hj = jobs[a:b]
                 hjp = jobs_ptr + a * JS  # host copy of the slice (plain int: no ctypes object)
@@ -1150,7 +1118,7 @@ class Engine:
                                                     d_cells, d_stats, sp), "tpe_table_build")
                         tock("table_build", e0)
                     if stage == "build":
-                        continue
+                        return
                     if not joined and self.side_stream == "2":
                         stream_order("joined", side_p, sp)
                         joined = True
@@ -1217,8 +1185,62 @@ class Engine:
                             "tpe_score_categorical")
                 tock(kind, e0, kst)
 
+            # categorical labels need only the gathered lists: with cat_early
+            # their posterior and scoring go to the side stream before the
+            # fit, beside the latency-bound fit kernels instead of the
+            # VALU-bound table build and scorer
+            cat_early = side is not None and bool(cat) and self.cat_early
+            if cat_early:
+                stream_rec("gathered", sp)
+                stream_wait("gathered", side_p)
+                cat_fit()
+                for g, (k, ids) in enumerate(groups):
+                    if k == "cat" and ids:
+                        launch_group(g, "all")
+            # ---- posterior fit ------------------------------------------------------
+            if fit_ids:
+                e0 = tick("fit")
+                L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
+                                           n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
+                                           d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
+                tock("fit", e0)
+
+            if cat and side is None:
+                cat_fit()
+
+            if posteriors:
+                return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
+                                             d_segs, stream, o_p), True
+
+            _hmark('jobs')
+
+            _hmark('fit')
+            # ---- scoring, one call per group ----------------------------------------
+            # quantized and categorical groups go to the side stream (after the job
+            # table has landed); continuous groups stay on `stream`
+            if side is not None:  # quantized groups need the continuous fit
+                stream_rec("fitted", sp)
+            # launch order: the first sampled table group's build (the main
+            # stream's next kernels after the fit), then the side groups, then
+            # the main-stream scorers -- the host issues launches at a few us
+            # each, and at a one-eighth label share the main stream would
+            # otherwise sit idle behind the side stream's launches
+            g_order = [(g, "all") for g in range(len(groups))]
+            early = None
+            tgroups = [g for g, (k, ids) in enumerate(groups) if k == "table" and ids]
+            if side is not None:
+                if len(tgroups) == 1 and not inj(groups[tgroups[0]][1][0]):
+                    early = tgroups[0]  # (one table group: the workspace tables are its own)
+                g_order = ([(early, "build")] if early is not None else []) + \
+                    [(g, "all") for g in range(len(groups)) if groups[g][0] in SIDE_KINDS] + \
+                    [(g, "score" if g == early else "all") for g in range(len(groups))
+                     if groups[g][0] not in SIDE_KINDS]
+            for g, stage in g_order:
+                if not (cat_early and groups[g][0] == "cat"):
+                    launch_group(g, stage)
+
             if not side_started:  # (no side group: only the categorical posterior)
-                if cat:
+                if cat and not cat_early:
                     cat_fit()
             if not joined:  # join before the readback
                 stream_order("joined", side_p, sp)
