@@ -41,6 +41,7 @@ LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense 
 LAT_PACK_MAX = 1 << 16  # lattice slots of a level initialised through the upload (else memset)
 TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
+LAT_EARLY_MIN_CAND = 1 << 26  # lattice work beside the fit from this many table candidates
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
 SORTED_MIN_CAND = 1 << 12  # auto scorer: sorted/pruned path from this many (below: dense)
 SCORERS = ("auto", "dense", "sorted", "table")
@@ -287,6 +288,11 @@ class Engine:
         # categorical posterior + scoring on the side stream before the fit
         # (TPE_CAT_EARLY=1) or after it with the quantized labels (0)
         self.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
+        # opt-in (TPE_LAT_EARLY=1): quantized labels fitted first and sampled
+        # beside the continuous fit on levels with >= LAT_EARLY_MIN_CAND table
+        # candidates.  Off: the lattice sampler slows the latency-bound fit on
+        # the critical path more than it saves later (C3 0.94 -> 0.96-0.99 ms)
+        self.lat_early = os.environ.get("TPE_LAT_EARLY", "0") == "1"
         # level graphs (opt-in, TPE_GRAPHS=1): a level whose launch sequence
         # (kernels, grids, workspace pointers, every scalar argument) repeats
         # the previous call's is captured into a hipGraph once and replayed
@@ -1054,7 +1060,8 @@ class Engine:
                 kind, ids = groups[g]
                 if not ids:
                     return
-                if not side_started and kind in SIDE_KINDS and not (cat_early and kind == "cat"):
+                if not side_started and kind in SIDE_KINDS and not (
+                        (cat_early and kind == "cat") or (lat_early and kind == "lat")):
                     side_started = True  # the side stream's groups that need the fit
                     stream_wait("fitted", side_p)
                     if cat and not cat_early:
@@ -1190,6 +1197,12 @@ class Engine:
             # fit, beside the latency-bound fit kernels instead of the
             # VALU-bound table build and scorer
             cat_early = side is not None and bool(cat) and self.cat_early
+            lat_g = [g for g, (k, ids) in enumerate(groups) if k == "lat" and ids]
+            n_tab = int(sum(int(jobs["n_cand"][a:b].sum()) for a, b in
+                            (_slice_of(groups, g) for g, (k, ids) in enumerate(groups)
+                             if k == "table" and ids)))
+            lat_early = side is not None and bool(lat_g) and self.lat_early and \
+                n_tab >= LAT_EARLY_MIN_CAND
             if cat_early:
                 stream_rec("gathered", sp)
                 stream_wait("gathered", side_p)
@@ -1198,11 +1211,27 @@ class Engine:
                     if k == "cat" and ids:
                         launch_group(g, "all")
             # ---- posterior fit ------------------------------------------------------
+            # lat_early (a large level): the quantized labels' mixtures are
+            # fitted first, and their lattice work goes to the side stream
+            # beside the continuous labels' fit (latency-bound: the GPU has
+            # room) instead of beside the table build and scorer
             if fit_ids:
                 e0 = tick("fit")
-                L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs,
-                                           n_obs_total, d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n,
-                                           d_w32, d_pm, d_sm, sp), "tpe_parzen_fit")
+                parts = [(0, len(segs))]
+                if lat_early:  # segments: continuous labels first, then quantized
+                    nc2 = 2 * len(cont)
+                    parts = [(nc2, len(segs) - nc2), (0, nc2)]
+                for p0, pn in parts:
+                    if pn:
+                        L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs + p0 * L.SEG_DTYPE.itemsize,
+                                                   pn, max_obs, n_obs_total, d_w, d_mu, d_sig,
+                                                   d_cdf, d_c64, d_c32, d_c32n, d_w32, d_pm, d_sm,
+                                                   sp), "tpe_parzen_fit")
+                    if lat_early and p0 > 0:
+                        stream_rec("fitted_q", sp)
+                        stream_wait("fitted_q", side_p)
+                        for g in lat_g:
+                            launch_group(g, "all")
                 tock("fit", e0)
 
             if cat and side is None:
@@ -1236,7 +1265,8 @@ class Engine:
                     [(g, "score" if g == early else "all") for g in range(len(groups))
                      if groups[g][0] not in SIDE_KINDS]
             for g, stage in g_order:
-                if not (cat_early and groups[g][0] == "cat"):
+                if not (cat_early and groups[g][0] == "cat") and not (
+                        lat_early and groups[g][0] == "lat"):
                     launch_group(g, stage)
 
             if not side_started:  # (no side group: only the categorical posterior)
