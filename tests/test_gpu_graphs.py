@@ -188,3 +188,49 @@ def test_native_batch_deferred_equals_eager():
                         r.n_scored.tolist()))
         assert out[0] == out[1], step
     assert native.graph_stats.get("native", 0) >= 3
+
+
+def test_level_replay_equals_eager():
+    """The WorkBatch level replay (engine._Replay: the staged pack reused,
+    only keys / candidate bases / split flags rewritten) gives the eager
+    engine's winners when the keys AND the split change from call to call
+    (same counts: a different set of below rows each time), and a changed
+    count falls back to the full path."""
+    from hyperopt_amd.engine import WorkBatch
+    eager, native, DeviceHistory = _pair("native")
+    T = 3000
+    mat, active, losses = _history(T, 9)
+    active[:] = True  # every label active: any split of n_below rows keeps the counts
+    he = DeviceHistory(eager, len(SPACE), cap=4096)
+    hn = DeviceHistory(native, len(SPACE), cap=4096)
+    for h in (he, hn):
+        h.append(mat, active)
+    rng = np.random.RandomState(5)
+
+    # (no unbounded lattice: its range follows the below set, and a WorkBatch
+    # key must name it -- a new split would be a new structure)
+    space = [(j, e) for j, e in enumerate(SPACE) if e[1] != "qnormal"]
+
+    def batch(works, n_below):
+        keys = [w.key for w in works]
+        nb = [n_below] * len(works)
+        na = [T - n_below] * len(works)
+        return WorkBatch(("replay-test", n_below), nb, na, keys, [0] * len(works),
+                         lambda works=works: works)
+    for step in range(8):
+        n_below = 14 if step < 6 else 15  # the last two steps change the counts
+        isb = np.zeros(T, np.uint8)
+        isb[rng.choice(T, n_below, replace=False)] = 1
+        works = []
+        from hyperopt_amd.engine import LabelWork
+        for j, (lab, kind, a) in space:
+            works.append(LabelWork(lab, kind, a, mat[isb == 1, j], None, n_cand=1 << 16,
+                                   key=1000 * step + j, cand_base=0, col=j,
+                                   n_above=T - n_below))
+        out = []
+        for eng, h in ((eager, he), (native, hn)):
+            r = eng.run(batch(works, n_below), history=h, is_below=isb)
+            out.append((r.index.tolist(), r.value.tolist(), r.score.tolist(),
+                        r.n_scored.tolist()))
+        assert out[0] == out[1], step
+    assert native.graph_stats.get("replay", 0) >= 3, native.graph_stats
