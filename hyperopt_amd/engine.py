@@ -288,6 +288,9 @@ class Engine:
         # categorical posterior + scoring on the side stream before the fit
         # (TPE_CAT_EARLY=1) or after it with the quantized labels (0)
         self.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
+        # where the host issues that categorical work: "pre" (before the fit's
+        # launches), "post" (after them), "late" (after the table build)
+        self.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
         # opt-in (TPE_LAT_EARLY=1): quantized labels fitted first and sampled
         # beside the continuous fit on levels with >= LAT_EARLY_MIN_CAND table
         # candidates.  Off: the lattice sampler slows the latency-bound fit on
@@ -1046,6 +1049,7 @@ class Engine:
             jobs_ptr = jobs.__array_interface__["data"][0]
             joined = side is None
             side_started = side is None
+            cat_started = False
 
             def cat_fit():  # on the side stream (after its fork)
                 e0 = tick("cat_fit", side)
@@ -1056,10 +1060,14 @@ class Engine:
                 tock("cat_fit", e0, side)
 
             def launch_group(g, stage):
-                nonlocal joined, side_started
+                nonlocal joined, side_started, cat_started
                 kind, ids = groups[g]
                 if not ids:
                     return
+                if cat_early and kind == "cat" and not cat_started:
+                    cat_started = True  # the categorical work needs only the gather
+                    stream_wait("gathered", side_p)
+                    cat_fit()
                 if not side_started and kind in SIDE_KINDS and not (
                         (cat_early and kind == "cat") or (lat_early and kind == "lat")):
                     side_started = True  # the side stream's groups that need the fit
@@ -1193,9 +1201,12 @@ class Engine:
                 tock(kind, e0, kst)
 
             # categorical labels need only the gathered lists: with cat_early
-            # their posterior and scoring go to the side stream before the
-            # fit, beside the latency-bound fit kernels instead of the
-            # VALU-bound table build and scorer
+            # the side stream starts their posterior and scoring from an event
+            # recorded after the gather, so they run beside the latency-bound
+            # fit kernels instead of the VALU-bound table build and scorer
+            # (issued on the host after the fit's launches: the fit is not
+            # delayed, and the table build still reaches the GPU before the
+            # fit ends)
             cat_early = side is not None and bool(cat) and self.cat_early
             lat_g = [g for g, (k, ids) in enumerate(groups) if k == "lat" and ids]
             n_tab = int(sum(int(jobs["n_cand"][a:b].sum()) for a, b in
@@ -1205,11 +1216,10 @@ class Engine:
                 n_tab >= LAT_EARLY_MIN_CAND
             if cat_early:
                 stream_rec("gathered", sp)
-                stream_wait("gathered", side_p)
-                cat_fit()
-                for g, (k, ids) in enumerate(groups):
-                    if k == "cat" and ids:
-                        launch_group(g, "all")
+                if self.cat_issue == "pre":  # issued before the fit's launches
+                    for g, (k, ids) in enumerate(groups):
+                        if k == "cat" and ids:
+                            launch_group(g, "all")
             # ---- posterior fit ------------------------------------------------------
             # lat_early (a large level): the quantized labels' mixtures are
             # fitted first, and their lattice work goes to the side stream
@@ -1260,13 +1270,19 @@ class Engine:
             if side is not None:
                 if len(tgroups) == 1 and not inj(groups[tgroups[0]][1][0]):
                     early = tgroups[0]  # (one table group: the workspace tables are its own)
-                g_order = ([(early, "build")] if early is not None else []) + \
-                    [(g, "all") for g in range(len(groups)) if groups[g][0] in SIDE_KINDS] + \
+                side_gs = [g for g in range(len(groups)) if groups[g][0] in SIDE_KINDS]
+                # categorical groups first, issued right after the fit's
+                # launches (they wait for the gather only, so they run beside
+                # the fit; the table build is still issued before the fit ends)
+                cat_gs = [g for g in side_gs if cat_early and groups[g][0] == "cat"]
+                pre = [(g, "all") for g in cat_gs] if self.cat_issue == "post" else []
+                late = [(g, "all") for g in cat_gs] if self.cat_issue == "late" else []
+                g_order = pre + ([(early, "build")] if early is not None else []) + late + \
+                    [(g, "all") for g in side_gs if g not in cat_gs] + \
                     [(g, "score" if g == early else "all") for g in range(len(groups))
                      if groups[g][0] not in SIDE_KINDS]
             for g, stage in g_order:
-                if not (cat_early and groups[g][0] == "cat") and not (
-                        lat_early and groups[g][0] == "lat"):
+                if not (lat_early and groups[g][0] == "lat"):
                     launch_group(g, stage)
 
             if not side_started:  # (no side group: only the categorical posterior)

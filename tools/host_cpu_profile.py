@@ -100,6 +100,7 @@ def make_engine():
     eng.table_scorer = "cubic"
     eng.exact64 = "auto"
     eng.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
+    eng.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
     eng.lat_early = os.environ.get("TPE_LAT_EARLY", "0") == "1"
     eng.graphs = False
     eng._graphs, eng._last_gkey, eng._gen, eng._own = {}, None, 0, None
