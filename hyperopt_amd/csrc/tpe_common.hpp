@@ -24,6 +24,7 @@ constexpr double kLn2 = 0.6931471805599453;
 // ---------------------------------------------------------------------------
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+void defer_launch_checks(bool on);
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (counter-based; one call = 4 independent 32-bit words)

@@ -125,6 +125,11 @@ extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
   // TPE_OPS_TRACE=1 (diagnostic): host time of every record on stderr
   static const bool trace = getenv("TPE_OPS_TRACE") && getenv("TPE_OPS_TRACE")[0] == '1';
   auto t_prev = std::chrono::steady_clock::now();
+  // launch status read once for the whole batch (check_launch), not per record
+  struct Defer {
+    Defer() { tpe::defer_launch_checks(true); }
+    ~Defer() { tpe::defer_launch_checks(false); }
+  } defer;
   for (int i = 0; i < n_ops; ++i) {
     const int rc = tpe::run_one(ops[i]);
     if (trace) {
@@ -136,6 +141,13 @@ extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
     if (rc != TPE_OK) {
       if (failed_op) *failed_op = i;
       return rc;
+    }
+  }
+  if (n_ops > 0) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      tpe::set_error("tpe_run_ops: a launch of the batch failed: %s", hipGetErrorString(e));
+      return TPE_E_LAUNCH;
     }
   }
   return TPE_OK;

@@ -10,6 +10,7 @@
 namespace tpe {
 namespace {
 thread_local char g_err[512] = "";
+thread_local int g_defer_check = 0;  // > 0 inside tpe_run_ops (see defer_launch_checks)
 }
 
 void set_error(const char* fmt, ...) {
@@ -19,7 +20,13 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+// Inside a batch of records (tpe_run_ops) the launch status is read once at
+// the end of the batch instead of after every entry point: hipGetLastError
+// costs a few us of host time per call.
+void defer_launch_checks(bool on) { g_defer_check += on ? 1 : -1; }
+
 int check_launch(const char* what) {
+  if (g_defer_check > 0) return TPE_OK;
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("%s: %s", what, hipGetErrorString(e));
