@@ -234,3 +234,31 @@ def test_level_replay_equals_eager():
                         r.n_scored.tolist()))
         assert out[0] == out[1], step
     assert native.graph_stats.get("replay", 0) >= 3, native.graph_stats
+
+
+@pytest.mark.parametrize("variant", ["lat_early", "cat_pre", "cat_late", "cat_off"])
+def test_issue_orders_give_the_same_level(variant, monkeypatch):
+    """The side-stream issue variants (categorical work issued before the fit /
+    after it / after the table build / after the fit with the quantized work;
+    lattice work beside the continuous fit) only move launches between
+    streams and in time: every label's winner equals the default engine's."""
+    from hyperopt_amd import engine as E
+    monkeypatch.setattr(E, "LAT_EARLY_MIN_CAND", 0)
+    base, other, DeviceHistory = _pair("native")
+    base.native = True
+    if variant == "lat_early":
+        other.lat_early = True
+    elif variant == "cat_off":
+        other.cat_early = False
+    else:
+        other.cat_issue = variant.split("_")[1]
+    mat, active, losses = _history(2500, 13)
+    hb = DeviceHistory(base, len(SPACE), cap=4096)
+    ho = DeviceHistory(other, len(SPACE), cap=4096)
+    for h in (hb, ho):
+        h.append(mat, active)
+    for step in range(4):
+        works, isb = _works(mat, active, losses, 2500, step, 1 << 17)
+        a = base.run(works, history=hb, is_below=isb)
+        b = other.run(works, history=ho, is_below=isb)
+        assert _rows(a) == _rows(b), (variant, step)
