@@ -24,7 +24,10 @@ def main(src, levels=2, first="k_gather_obs"):
     qcol = "queue_id" if "queue_id" in cols else ("stream_id" if "stream_id" in cols else None)
     rows = list(c.execute("select name, start, end%s from kernels order by start"
                           % ((", " + qcol) if qcol else "")))
-    starts = [i for i, r in enumerate(rows) if short(r[0]) == first]
+    starts = []
+    for i, r in enumerate(rows):  # a level's first `first` kernel (a second one
+        if short(r[0]) == first and (not starts or r[1] - rows[starts[-1]][1] > 100e3):
+            starts.append(i)      # within 100 us is the same level's, on the side stream)
     for li in starts[-levels:]:
         nxt = [s for s in starts if s > li]
         seg = rows[li:nxt[0] if nxt else len(rows)]
