@@ -125,6 +125,7 @@ _hip = None
 
 H2D, D2H = 1, 2  # hipMemcpyKind
 EVENT_NO_TIMING = 0x2  # hipEventDisableTiming
+EVENT_NO_SYSTEM_FENCE = 0x20000000  # hipEventDisableSystemFence (device-scope release)
 CAPTURE_RELAXED = 2  # hipStreamCaptureModeRelaxed
 CAPTURE_SET_DEPENDENCIES = 1  # hipStreamSetCaptureDependencies
 

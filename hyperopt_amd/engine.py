@@ -46,6 +46,7 @@ PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above compon
 SORTED_MIN_CAND = 1 << 12  # auto scorer: sorted/pruned path from this many (below: dense)
 SCORERS = ("auto", "dense", "sorted", "table")
 SIDE_KINDS = ("lat", "qfb", "qinj", "cat")  # groups scored on the side stream
+HOST_EVENTS = ("result",)  # events the host waits on (system-scope release kept)
 _ALIGN = 256
 
 CONTINUOUS = ("uniform", "quniform", "loguniform", "qloguniform",
@@ -296,6 +297,12 @@ class Engine:
         # candidates.  Off: the lattice sampler slows the latency-bound fit on
         # the critical path more than it saves later (C3 0.94 -> 0.96-0.99 ms)
         self.lat_early = os.environ.get("TPE_LAT_EARLY", "0") == "1"
+        # stream-ordering events (one stream of this device waits for another)
+        # without the system-scope fence: a device-scope release is all a
+        # consumer on the same GPU needs, and the system-scope one writes back
+        # the L2s (~14 us of idle GPU per event on C3 levels).  The host-read
+        # "result" event keeps it.  TPE_DEVICE_EVENTS=0: every event system-scope.
+        self.device_events = os.environ.get("TPE_DEVICE_EVENTS", "1") == "1"
         # level graphs (opt-in, TPE_GRAPHS=1): a level whose launch sequence
         # (kernels, grids, workspace pointers, every scalar argument) repeats
         # the previous call's is captured into a hipGraph once and replayed
@@ -356,7 +363,10 @@ class Engine:
         e = self._events.get(name)
         if e is None:
             h = ctypes.c_void_p()
-            L.hip_check(self._hip.hipEventCreateWithFlags(ctypes.byref(h), L.EVENT_NO_TIMING),
+            flags = L.EVENT_NO_TIMING
+            if self.device_events and name not in HOST_EVENTS:
+                flags |= L.EVENT_NO_SYSTEM_FENCE
+            L.hip_check(self._hip.hipEventCreateWithFlags(ctypes.byref(h), flags),
                         "hipEventCreateWithFlags")
             e = self._events[name] = h
         return e
