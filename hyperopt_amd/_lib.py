@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -65,6 +65,7 @@ OP_EVENT_RECORD, OP_STREAM_WAIT, OP_MEMCPY, OP_STREAM_SYNC = range(len(OP_CODES)
                                                                   len(OP_CODES) + 5)
 OP_CODES["tpe_best_scatter"] = OP_STREAM_SYNC + 1
 OP_CODES["tpe_maxloc_allreduce"] = OP_STREAM_SYNC + 2
+OP_CODES["tpe_lattice_suggest"] = OP_STREAM_SYNC + 3
 PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
     PRIOR_CATEGORICAL = range(6)
 
@@ -102,6 +103,8 @@ _SIGNATURES = {
     "tpe_score_continuous": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P,
                                   _P, _I64, _P, _P]),
     "tpe_lattice_sample": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "tpe_lattice_suggest": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P,
+                                 _P]),
     "tpe_lattice_compact": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
     "tpe_quantized_partials": (_I64, [_P, _I, _I64]),
     "tpe_score_quantized": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _I64,

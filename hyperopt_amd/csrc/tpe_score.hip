@@ -780,122 +780,144 @@ __host__ __device__ __forceinline__ bool lattice_pow2(const tpe_job& j) {
          j.lat_n <= kLatLds;
 }
 
+// Candidates [start, min(n_cand, limit)) of every job (start a multiple of the
+// kBS * kLatR tile); need (nullable): only the jobs whose flag is set.
 template <bool POW2>
 __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
-    int32_t* __restrict__ err, int n_tiles, int n_jobs) {
+    int32_t* __restrict__ err, int n_tiles, int n_jobs, int64_t start, int64_t limit,
+    const int32_t* __restrict__ need) {
   extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
   __shared__ float s_stage[kLatR * kBS];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
-  // XCD-aware work order (as k_score_table): each XCD sweeps a contiguous
-  // eighth of the (job, tile) list, so a job's first-index atomics stay in
-  // few XCDs' L2s
-  const int64_t W = (int64_t)n_tiles * n_jobs, per = (W + 7) / 8;
-  const int64_t wi = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (wi >= W) return;
-  const int job = (int)(wi / n_tiles);
-  const tpe_job J = jobs[job];
-  const int64_t base = (wi - (int64_t)job * n_tiles) * (kBS * kLatR);
-  if (base >= J.n_cand) return;
-  const tpe_seg SB = segs[J.below];
-  const bool lgmm = J.family == TPE_LGMM1;
-  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
-  // the first kLatLds slots of the lattice are deduplicated in LDS (for the
-  // wide lattices of unbounded labels that is where the mass sits); slots
-  // beyond go to the global marks directly, each read before its atomic
-  const int n_loc = (int)min((int64_t)kLatLds, J.lat_n);
-  for (int s = threadIdx.x; s < n_loc; s += kBS) lfirst[s] = 0xFFFFFFFFu;
-  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
-  __syncthreads();
-  if constexpr (POW2) {
-    // kLatR consecutive candidates per thread (draw32_pairs); q a power of two:
-    // x * (1/q) is exact in fp32, so rintf gives np.round(x / q) (tpe.py:106)
-    // exactly and the slot needs no fp64 work
-    const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
-    const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
-    float x[kLatR];
-    draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList,
-                        x);
-    const float inv_q32 = (float)(1.0 / J.q);
-    const int kmin = (int)J.lat_kmin, nl = (int)J.lat_n;
-#pragma unroll
-    for (int r = 0; r < kLatR; ++r) {
-      if (r >= nv) continue;
-      const float t = rintf(x[r] * inv_q32);
-      const int slot = (fabsf(t) < 2147483648.0f) ? (int)t - kmin : -1;
-      if (slot < 0 || slot >= nl) {
-        atomicOr(err, 2);
-        continue;
-      }
-      // most draws land on slots already holding a smaller index: a plain read
-      // first keeps the atomics (and their same-address serialisation) rare
-      const uint32_t rel = (uint32_t)(t0 + r - base);
-#ifdef TPE_DIAG_NO_MARK  // diagnostic builds only: slots computed, not marked
-      if (rel == 0xFFFFFFFFu) lfirst[slot] = rel;
-#else
-      if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
-#endif
-    }
-  } else {
-    // np.round(x / q) (tpe.py:106) without a division per draw: t = x * (1/q) is
-    // within 3.4e-16 |t| of fl(x / q), so rint(t) == rint(fl(x / q)) unless
-    // fl(x / q) sits that close to a half-integer -- those few redo the division
-    const double inv_q = 1.0 / J.q;
-    auto mark = [&](double v, int64_t li) {
-      const double t = v * inv_q;
-      double k = rint(t);
-      if (fabs(fabs(t - k) - 0.5) <= 8e-16 * fabs(t)) k = rint(v / J.q);
-      const int64_t slot = (int64_t)k - J.lat_kmin;
-      if (slot < 0 || slot >= J.lat_n) {
-        atomicOr(err, 2);
-        return;
-      }
-      if (slot < n_loc) {
-        const uint32_t rel = (uint32_t)(li - base);
-        if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
-      } else {
-        unsigned long long* dst = &slot_first[J.lat_off + slot];
-        const unsigned long long g = (unsigned long long)(J.cand_base + li);
-        if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
-      }
-    };
-    if (J.flags & TPE_F_DRAW32) {
+  // one (job, tile) work item
+  auto tile = [&](int job, int64_t base) __attribute__((always_inline)) {
+    const tpe_job J = jobs[job];
+    const int64_t n_lim = min(J.n_cand, limit);
+    if (base >= n_lim || base < start) return;
+    const tpe_seg SB = segs[J.below];
+    const bool lgmm = J.family == TPE_LGMM1;
+    const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+    // the first kLatLds slots of the lattice are deduplicated in LDS (for the
+    // wide lattices of unbounded labels that is where the mass sits); slots
+    // beyond go to the global marks directly, each read before its atomic
+    const int n_loc = (int)min((int64_t)kLatLds, J.lat_n);
+    for (int s = threadIdx.x; s < n_loc; s += kBS) lfirst[s] = 0xFFFFFFFFu;
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
+    __syncthreads();
+    if constexpr (POW2) {
+      // kLatR consecutive candidates per thread (draw32_pairs); q a power of two:
+      // x * (1/q) is exact in fp32, so rintf gives np.round(x / q) (tpe.py:106)
+      // exactly and the slot needs no fp64 work
       const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
-      const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
+      const int nv = (int)max((int64_t)0, min((int64_t)kLatR, n_lim - t0));
       float x[kLatR];
       draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
                           (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList,
                           x);
+      const float inv_q32 = (float)(1.0 / J.q);
+      const int kmin = (int)J.lat_kmin, nl = (int)J.lat_n;
 #pragma unroll
-      for (int r = 0; r < kLatR; ++r)
-        if (r < nv) mark((double)x[r], t0 + r);
-    } else {
       for (int r = 0; r < kLatR; ++r) {
-        const int64_t li = base + r * kBS + threadIdx.x;
-        if (li >= J.n_cand) break;
-        double v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
-        if (lgmm) v = exp(v);
-        mark(v, li);
+        if (r >= nv) continue;
+        const float t = rintf(x[r] * inv_q32);
+        const int slot = (fabsf(t) < 2147483648.0f) ? (int)t - kmin : -1;
+        if (slot < 0 || slot >= nl) {
+          atomicOr(err, 2);
+          continue;
+        }
+        // most draws land on slots already holding a smaller index: a plain read
+        // first keeps the atomics (and their same-address serialisation) rare
+        const uint32_t rel = (uint32_t)(t0 + r - base);
+#ifdef TPE_DIAG_NO_MARK  // diagnostic builds only: slots computed, not marked
+        if (rel == 0xFFFFFFFFu) lfirst[slot] = rel;
+#else
+        if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
+#endif
+      }
+    } else {
+      // np.round(x / q) (tpe.py:106) without a division per draw: t = x * (1/q) is
+      // within 3.4e-16 |t| of fl(x / q), so rint(t) == rint(fl(x / q)) unless
+      // fl(x / q) sits that close to a half-integer -- those few redo the division
+      const double inv_q = 1.0 / J.q;
+      auto mark = [&](double v, int64_t li) {
+        const double t = v * inv_q;
+        double k = rint(t);
+        if (fabs(fabs(t - k) - 0.5) <= 8e-16 * fabs(t)) k = rint(v / J.q);
+        const int64_t slot = (int64_t)k - J.lat_kmin;
+        if (slot < 0 || slot >= J.lat_n) {
+          atomicOr(err, 2);
+          return;
+        }
+        if (slot < n_loc) {
+          const uint32_t rel = (uint32_t)(li - base);
+          if (rel < lfirst[slot]) atomicMin(&lfirst[slot], rel);
+        } else {
+          unsigned long long* dst = &slot_first[J.lat_off + slot];
+          const unsigned long long g = (unsigned long long)(J.cand_base + li);
+          if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
+        }
+      };
+      if (J.flags & TPE_F_DRAW32) {
+        const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
+        const int nv = (int)max((int64_t)0, min((int64_t)kLatR, n_lim - t0));
+        float x[kLatR];
+        draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
+                            (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList,
+                            x);
+#pragma unroll
+        for (int r = 0; r < kLatR; ++r)
+          if (r < nv) mark((double)x[r], t0 + r);
+      } else {
+        for (int r = 0; r < kLatR; ++r) {
+          const int64_t li = base + r * kBS + threadIdx.x;
+          if (li >= n_lim) break;
+          double v = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
+          if (lgmm) v = exp(v);
+          mark(v, li);
+        }
       }
     }
-  }
-  __syncthreads();
-  // blocks run roughly in index order, so the global slot mostly holds a
-  // smaller index already: an agent-scope load first keeps the (cross-XCD)
-  // atomics to the blocks that improve a slot
+    __syncthreads();
+    // blocks run roughly in index order, so the global slot mostly holds a
+    // smaller index already: an agent-scope load first keeps the (cross-XCD)
+    // atomics to the blocks that improve a slot
 #ifdef TPE_DIAG_NO_FLUSH  // diagnostic builds only: block results dropped
-  if (n_loc > 0x7FFFFFF0)
+    if (n_loc > 0x7FFFFFF0)
 #endif
-  for (int s = threadIdx.x; s < n_loc; s += kBS) {
-    const uint32_t f = lfirst[s];
-    if (f == 0xFFFFFFFFu) continue;
-    unsigned long long* dst = &slot_first[J.lat_off + s];
-    const unsigned long long g = (unsigned long long)(J.cand_base + base + f);
-    if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
+    for (int s = threadIdx.x; s < n_loc; s += kBS) {
+      const uint32_t f = lfirst[s];
+      if (f == 0xFFFFFFFFu) continue;
+      unsigned long long* dst = &slot_first[J.lat_off + s];
+      const unsigned long long g = (unsigned long long)(J.cand_base + base + f);
+      if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(dst, g);
+    }
+  };  // tile
+  const int64_t tb = (int64_t)kBS * kLatR;
+  if (!need) {
+    // XCD-aware work order (as k_score_table): each XCD sweeps a contiguous
+    // eighth of the (job, tile) list, so a job's first-index atomics stay in
+    // few XCDs' L2s
+    const int64_t W = (int64_t)n_tiles * n_jobs, per = (W + 7) / 8;
+    const int64_t wi = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (wi >= W) return;
+    const int job = (int)(wi / n_tiles);
+    tile(job, (wi - (int64_t)job * n_tiles) * tb);
+  } else {
+    // the conditional rest of the streams: a grid-stride loop over the tiles
+    // of the jobs whose flag is set, so a launch whose jobs are all settled is
+    // a small grid that reads the flags and exits (a one-tile-per-block grid
+    // of ~10^4 such blocks cost ~80 us of dispatch)
+    for (int job = 0; job < n_jobs; ++job) {
+      if (!need[job]) continue;  // block-uniform
+      for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        __syncthreads();  // the previous tile's LDS reads are done
+        tile(job, t * tb);
+      }
+    }
   }
 }
 
@@ -929,7 +951,7 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
   double lub = 0.0, llb = 0.0;
   if (lg) {
     lb = fmax(0.0, lb);
-    if (ub < 0.0 && threadIdx.x == 0) atomicOr(err, 1);  // tpe.py:196-197
+    if (ub < 0.0 && threadIdx.x == 0 && err) atomicOr(err, 1);  // tpe.py:196-197
     lub = log(ub < kEps ? kEps : ub);
     llb = log(lb < kEps ? kEps : lb);
   }
@@ -985,6 +1007,102 @@ __global__ __launch_bounds__(kBS) void k_score_q(
     if (out_bl) out_bl[J.out_off + pos] = bl;
     if (out_al) out_al[J.out_off + pos] = al;
     *P = tpe_best{bl - al, idx, v, 0};
+  }
+}
+
+// Prefix-first lattice argmax (tpe_lattice_suggest).  A lattice value's score
+// does not depend on where it is drawn, and the reference's winner is the
+// best-scoring value that occurs in the stream, at its first occurrence
+// (np.argmax: first index of the maximum).  So after the first `prefix`
+// candidates the winner is settled unless some value not yet seen scores
+// strictly higher (or is NaN while the best seen is not): a value first seen
+// later has a larger index and loses every tie.  k_score_slots scores every
+// slot of the lattice (seen or not), k_lattice_decide takes the argmax over
+// the seen ones and flags the jobs where an unseen slot could still win; only
+// those draw the rest of their stream (the sampler with `need`) and decide
+// again over everything seen.
+__global__ __launch_bounds__(kBS) void k_score_slots(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ w, const double* __restrict__ mu,
+    const double* __restrict__ sigma, tpe_best* __restrict__ partial, int32_t* __restrict__ err) {
+  __shared__ double sh[kBS / kWave];
+  const tpe_job J = jobs[blockIdx.y];
+  const int64_t s = blockIdx.x;
+  if (s >= J.lat_n) return;  // block-uniform
+  const double v = (double)(J.lat_kmin + s) * J.q;  // np.round(x/q) * q, as k_lattice_compact
+  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err, sh);
+  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err, sh);
+  if (threadIdx.x == 0)
+    partial[(int64_t)blockIdx.y * gridDim.x + s] = tpe_best{bl - al, -1, v, 0};
+}
+
+// Can the sampler put a draw on slot s at all?  Only unseen slots that could
+// win ask; a "yes" costs the rest of the stream, a wrong "no" would cost
+// parity, so the test is a superset: some below component's draw range
+// (mean +- 5.8 sigma for fp32 Box-Muller draws, 8.7 for fp64 ones, widened
+// for fp32 rounding) meets the slot's rounding bin, and the bin meets the
+// bounds -- or holds a bound, where the sampler's last-resort clamp lands.
+// (The lattice brackets the bounds with a slot on each side that no draw
+// reaches; their probability mass is negative or 0/0, their score NaN.)
+__device__ __forceinline__ bool slot_reachable(const tpe_job& J, const tpe_seg& SB,
+                                               const double* __restrict__ mu,
+                                               const double* __restrict__ sigma, int64_t s) {
+  const double k = (double)(J.lat_kmin + s);
+  double lo = (k - 0.5) * J.q, hi = (k + 0.5) * J.q;  // the bin of np.round(x / q) == k
+  if (J.family == TPE_LGMM1) {  // the sampler's coordinate: log x
+    if (!(hi > 0.0)) return false;
+    lo = lo > 0.0 ? log(lo) : -INFINITY;
+    hi = log(hi);
+  }
+  const double m = 1e-6 * (fabs(lo) + fabs(hi)) + 1e-300;
+  lo -= m;
+  hi += m;
+  const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  if (lo_on && hi < J.low) return false;
+  if (hi_on && lo > J.high) return false;
+  if ((lo_on && lo <= J.low && J.low <= hi) || (hi_on && lo <= J.high && J.high <= hi))
+    return true;
+  const double z = (J.flags & TPE_F_DRAW32) ? 5.8 : 8.7;
+  for (int c = 0; c <= SB.n_obs; ++c) {
+    const double mc = mu[SB.comp_off + c], r = z * sigma[SB.comp_off + c];
+    const double mm = 1e-6 * (fabs(mc) + r);
+    if (mc - r - mm <= hi && lo <= mc + r + mm) return true;
+  }
+  return false;
+}
+
+// one block per job; seen-ness and first indices from slot_first.  pass 0:
+// best over the seen slots, need = an unseen, reachable slot could win (jobs
+// whose whole stream was the prefix never need more); pass 1 (need jobs
+// only): best over every slot seen in the whole stream
+__global__ __launch_bounds__(kBS) void k_lattice_decide(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ mu, const double* __restrict__ sigma,
+    const tpe_best* __restrict__ partial, int64_t nper,
+    const unsigned long long* __restrict__ slot_first, int64_t prefix, int pass,
+    int32_t* __restrict__ need, tpe_best* __restrict__ best) {
+  __shared__ BestT red[kBS / kWave];
+  const int j = blockIdx.x;
+  if (pass == 1 && !need[j]) return;  // block-uniform
+  const tpe_job J = jobs[j];
+  const tpe_best* P = partial + (int64_t)j * nper;
+  const unsigned long long* F = slot_first + J.lat_off;
+  BestT b{0.0, -1, 0.0};
+  for (int64_t s = threadIdx.x; s < J.lat_n; s += kBS) {
+    const unsigned long long f = F[s];
+    if (f != ~0ull) best_update(b, P[s].score, (int64_t)f, P[s].value);
+  }
+  b = block_best<kBS>(b, red);
+  int open = 0;
+  if (pass == 0 && J.n_cand > prefix) {
+    for (int64_t s = threadIdx.x; s < J.lat_n && !open; s += kBS)
+      open = F[s] == ~0ull && better(P[s].score, INT64_MAX, b.score, b.index) &&
+             slot_reachable(J, segs[J.below], mu, sigma, s);
+    open = __syncthreads_or(open);
+  }
+  if (threadIdx.x == 0) {
+    best[j] = tpe_best{b.score, b.index, b.value, J.n_cand};
+    if (pass == 0) need[j] = open;
   }
 }
 
@@ -1345,6 +1463,43 @@ extern "C" int tpe_score_continuous(const tpe_job* jobs, const tpe_job* host_job
   return check_launch("tpe_score_continuous");
 }
 
+// k_lattice_sample over candidates [start, min(n_cand, limit)) of every job
+// (of the jobs with need[j] set, when need is given); false (error set) when
+// the grid is too large
+static bool launch_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                  const tpe_seg* segs, const double* mu, const double* sigma,
+                                  const double* wcdf, uint64_t* slot_first, int32_t* err,
+                                  int64_t start, int64_t limit, const int32_t* need,
+                                  hipStream_t st, const char* who) {
+  int64_t gx = 1;
+  for (int i = 0; i < n_jobs; ++i) {
+    const int64_t n = std::min(host_jobs[i].n_cand, limit);
+    gx = std::max(gx, (n + (int64_t)kBS * kLatR - 1) / ((int64_t)kBS * kLatR));
+  }
+  const int64_t per = (gx * n_jobs + 7) / 8;
+  if (gx > INT32_MAX || 8 * per > INT32_MAX) {
+    set_error("%s: %lld work items", who, (long long)(gx * n_jobs));
+    return false;
+  }
+  bool pow2 = true;
+  int64_t n_loc = 1;
+  for (int i = 0; i < n_jobs; ++i) {
+    pow2 = pow2 && lattice_pow2(host_jobs[i]);
+    n_loc = std::max(n_loc, std::min((int64_t)kLatLds, host_jobs[i].lat_n));
+  }
+  const size_t lds = (size_t)n_loc * sizeof(uint32_t);
+  unsigned long long* sf = (unsigned long long*)slot_first;
+  // with need: a grid-stride grid (k_lattice_sample): two blocks per CU
+  const unsigned grid = need ? (unsigned)std::min<int64_t>(8 * per, 512) : (unsigned)(8 * per);
+  if (pow2)
+    hipLaunchKernelGGL(k_lattice_sample<true>, dim3(grid), dim3(kBS), lds, st, jobs, segs, mu,
+                       sigma, wcdf, sf, err, (int)gx, n_jobs, start, limit, need);
+  else
+    hipLaunchKernelGGL(k_lattice_sample<false>, dim3(grid), dim3(kBS), lds, st, jobs, segs, mu,
+                       sigma, wcdf, sf, err, (int)gx, n_jobs, start, limit, need);
+  return true;
+}
+
 extern "C" int tpe_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                                   const tpe_seg* segs, const double* mu, const double* sigma,
                                   const double* wcdf, uint64_t* slot_first, int32_t* err,
@@ -1369,28 +1524,68 @@ extern "C" int tpe_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
   for (int i = 0; i < n_jobs; ++i) ready = ready && (host_jobs[i].flags & TPE_F_LATTICE_READY);
   if (!ready && hipMemsetAsync(slot_first, 0xFF, (size_t)end * sizeof(uint64_t), st) != hipSuccess)
     return check_launch("tpe_lattice_sample memset");
-  const int64_t gx = max_blocks(host_jobs, n_jobs, (int64_t)kBS * kLatR, -1);
-  const int64_t per = (gx * n_jobs + 7) / 8;
-  if (gx > INT32_MAX || 8 * per > INT32_MAX) {
-    set_error("tpe_lattice_sample: %lld work items", (long long)(gx * n_jobs));
+  if (!launch_lattice_sample(jobs, host_jobs, n_jobs, segs, mu, sigma, wcdf, slot_first, err, 0,
+                             INT64_MAX, nullptr, st, "tpe_lattice_sample"))
     return TPE_E_UNSUPPORTED;
-  }
-  bool pow2 = true;
-  int64_t n_loc = 1;
-  for (int i = 0; i < n_jobs; ++i) {
-    pow2 = pow2 && lattice_pow2(host_jobs[i]);
-    n_loc = std::max(n_loc, std::min((int64_t)kLatLds, host_jobs[i].lat_n));
-  }
-  const size_t lds = (size_t)n_loc * sizeof(uint32_t);
-  if (pow2)
-    hipLaunchKernelGGL(k_lattice_sample<true>, dim3((unsigned)(8 * per)), dim3(kBS), lds, st, jobs,
-                       segs, mu, sigma, wcdf, (unsigned long long*)slot_first, err, (int)gx,
-                       n_jobs);
-  else
-    hipLaunchKernelGGL(k_lattice_sample<false>, dim3((unsigned)(8 * per)), dim3(kBS), lds, st,
-                       jobs, segs, mu, sigma, wcdf, (unsigned long long*)slot_first, err, (int)gx,
-                       n_jobs);
   return check_launch("tpe_lattice_sample");
+}
+
+extern "C" int tpe_lattice_suggest(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                   const tpe_seg* segs, const double* w, const double* mu,
+                                   const double* sigma, const double* wcdf, uint64_t* slot_first,
+                                   int64_t prefix, tpe_best* partial, int64_t n_partial,
+                                   int32_t* need, tpe_best* best, int32_t* err, void* stream) {
+  if (!check_jobs("tpe_lattice_suggest", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (!jobs || !segs || !w || !mu || !sigma || !wcdf || !slot_first || !partial || !need ||
+      !best || !err) {
+    set_error("tpe_lattice_suggest: null pointer");
+    return TPE_E_ARG;
+  }
+  if (prefix <= 0 || prefix % ((int64_t)kBS * kLatR) != 0) {
+    set_error("tpe_lattice_suggest: prefix %lld is not a positive multiple of %d",
+              (long long)prefix, kBS * kLatR);
+    return TPE_E_ARG;
+  }
+  int64_t end = 0, max_n = 1;
+  for (int i = 0; i < n_jobs; ++i) {
+    const tpe_job& j = host_jobs[i];
+    if (!(j.flags & TPE_F_QUANT) || j.family == TPE_CAT || !(j.q > 0) || j.lat_n <= 0 ||
+        (j.flags & TPE_F_INJECTED)) {
+      set_error("tpe_lattice_suggest: job %d is not a sampled quantized job with a lattice", i);
+      return TPE_E_ARG;
+    }
+    end = std::max(end, j.lat_off + j.lat_n);
+    max_n = std::max(max_n, j.lat_n);
+  }
+  if (max_n > INT32_MAX || max_n * n_jobs > n_partial) {
+    set_error("tpe_lattice_suggest: partial workspace %lld < %lld slots", (long long)n_partial,
+              (long long)(max_n * n_jobs));
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  bool ready = true;
+  for (int i = 0; i < n_jobs; ++i) ready = ready && (host_jobs[i].flags & TPE_F_LATTICE_READY);
+  if (!ready && hipMemsetAsync(slot_first, 0xFF, (size_t)end * sizeof(uint64_t), st) != hipSuccess)
+    return check_launch("tpe_lattice_suggest memset");
+  unsigned long long* sf = (unsigned long long*)slot_first;
+  if (!launch_lattice_sample(jobs, host_jobs, n_jobs, segs, mu, sigma, wcdf, slot_first, err, 0,
+                             prefix, nullptr, st, "tpe_lattice_suggest"))
+    return TPE_E_UNSUPPORTED;
+  hipLaunchKernelGGL(k_score_slots, dim3((unsigned)max_n, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
+                     segs, w, mu, sigma, partial, err);
+  hipLaunchKernelGGL(k_lattice_decide, dim3(n_jobs), dim3(kBS), 0, st, jobs, segs, mu, sigma,
+                     partial, max_n, sf, prefix, 0, need, best);
+  bool more = false;
+  for (int i = 0; i < n_jobs; ++i) more = more || host_jobs[i].n_cand > prefix;
+  if (more) {  // the rest of the streams that need it (blocks of the others exit at once)
+    if (!launch_lattice_sample(jobs, host_jobs, n_jobs, segs, mu, sigma, wcdf, slot_first, err,
+                               prefix, INT64_MAX, need, st, "tpe_lattice_suggest"))
+      return TPE_E_UNSUPPORTED;
+    hipLaunchKernelGGL(k_lattice_decide, dim3(n_jobs), dim3(kBS), 0, st, jobs, segs, mu, sigma,
+                       partial, max_n, sf, prefix, 1, need, best);
+  }
+  return check_launch("tpe_lattice_suggest");
 }
 
 extern "C" int tpe_lattice_compact(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,

@@ -42,6 +42,8 @@ LAT_PACK_MAX = 1 << 16  # lattice slots of a level initialised through the uploa
 TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
 LAT_EARLY_MIN_CAND = 1 << 26  # lattice work beside the fit from this many table candidates
+LAT_PREFIX = 1 << 16  # lattice argmax: candidates drawn before the early decision
+LAT_SUGGEST_MAX_SLOTS = 1 << 10  # ... for lattices of at most this many slots (all scored)
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
 SORTED_MIN_CAND = 1 << 12  # auto scorer: sorted/pruned path from this many (below: dense)
 SCORERS = ("auto", "dense", "sorted", "table")
@@ -297,6 +299,10 @@ class Engine:
         # candidates.  Off: the lattice sampler slows the latency-bound fit on
         # the critical path more than it saves later (C3 0.94 -> 0.96-0.99 ms)
         self.lat_early = os.environ.get("TPE_LAT_EARLY", "0") == "1"
+        # quantized labels of a suggest level: decide the argmax after the first
+        # lat_prefix candidates where no unseen lattice value can still win
+        # (tpe_lattice_suggest); 0 (TPE_LAT_PREFIX=0): every stream drawn in full
+        self.lat_prefix = int(os.environ.get("TPE_LAT_PREFIX", str(LAT_PREFIX)))
         # stream-ordering events (one stream of this device waits for another)
         # without the system-scope fence: a device-scope release is all a
         # consumer on the same GPU needs, and the system-scope one writes back
@@ -964,7 +970,8 @@ class Engine:
                     if history is not None else None,
                     None if exchange is None else
                     (int(x_comm), int(x_labels), int(x_world), x_slots.tobytes()),
-                    self.side_stream, self.table_scorer, self.exact64,
+                    self.side_stream, self.table_scorer, self.exact64, self.lat_prefix,
+                    self.cat_early, self.cat_issue, self.lat_early,
                     "off" if timers is None else
                     ("all" if timer_groups is None else frozenset(timer_groups)))
         cap = None  # _LevelGraph being captured / _OpList being recorded (tick/tock follow it)
@@ -1179,16 +1186,29 @@ class Engine:
                     else:
                         d_slot = self._buf("lat_slot", 8 * lat_off)
                         d_cnt = self._buf("lat_cnt", 8 * nj)
-                    L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_slot,
-                                                   d_err, ks), "tpe_lattice_sample")
-                    L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt, ks),
-                            "tpe_lattice_compact")
                     max_vals = int(hj["lat_n"].max())
-                    npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                    d_part = self._buf(pname, 32 * max(npart, 1))
-                    L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_vals,
-                                                    d_first, d_cnt, max_vals, None, None, d_part,
-                                                    npart, db, d_err, ks), "tpe_score_quantized")
+                    if self.lat_prefix and max_vals <= LAT_SUGGEST_MAX_SLOTS and \
+                            int(hj["n_cand"].max()) > self.lat_prefix:
+                        # prefix first: the rest of a stream only where an unseen
+                        # value could still win (tpe_lattice_suggest)
+                        npart = nj * max_vals
+                        d_part = self._buf(pname, 32 * npart)
+                        d_need = self._buf("lat_need", 4 * nj)
+                        L.check(lib.tpe_lattice_suggest(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
+                                                        d_slot, self.lat_prefix, d_part, npart,
+                                                        d_need, db, d_err, ks),
+                                "tpe_lattice_suggest")
+                    else:
+                        L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
+                                                       d_slot, d_err, ks), "tpe_lattice_sample")
+                        L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt,
+                                                        ks), "tpe_lattice_compact")
+                        npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+                        d_part = self._buf(pname, 32 * max(npart, 1))
+                        L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig,
+                                                        d_vals, d_first, d_cnt, max_vals, None, None,
+                                                        d_part, npart, db, d_err, ks),
+                                "tpe_score_quantized")
                 elif kind in ("qfb", "qinj"):
                     vals = d_cand
                     if kind == "qfb":

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 12
+#define TPE_ABI_VERSION 13
 
 enum {
   TPE_OK = 0,
@@ -367,6 +367,20 @@ int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs, int n_job
                         const int64_t* counts, int64_t max_vals, double* out_bl,
                         double* out_al, tpe_best* partial, int64_t n_partial,
                         tpe_best* best, int32_t* err, void* stream);
+/* The suggest path's lattice argmax, prefix first (replaces sample + compact
+ * + score + reduce for sampled jobs without per-candidate outputs; the
+ * result is the same tpe_best).  Draws the first `prefix` candidates of every
+ * job (a positive multiple of 4096), scores every lattice slot, and takes the
+ * best seen value at its first index; a job where a slot not yet seen scores
+ * higher (or NaN) draws the rest of its stream and decides again.  A value
+ * first seen after the prefix can only win by a strictly better score, so
+ * the winner is np.argmax's over the whole stream either way.
+ * partial: >= n_jobs * max(lat_n) tpe_best; need: int32 per job (written). */
+int tpe_lattice_suggest(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                        const tpe_seg* segs, const double* w, const double* mu,
+                        const double* sigma, const double* wcdf, uint64_t* slot_first,
+                        int64_t prefix, tpe_best* partial, int64_t n_partial, int32_t* need,
+                        tpe_best* best, int32_t* err, void* stream);
 
 /* ---- categorical labels: sample (or read) + score + argmax ---------------- */
 int64_t tpe_categorical_partials(const tpe_job* host_jobs, int n_jobs);
@@ -460,6 +474,7 @@ enum {
   TPE_OP_STREAM_SYNC,          /* hipStreamSynchronize(a[0] stream)          */
   TPE_OP_BEST_SCATTER,         /* tpe_best_scatter                           */
   TPE_OP_MAXLOC_ALLREDUCE,     /* tpe_maxloc_allreduce (RCCL, stream-ordered) */
+  TPE_OP_LATTICE_SUGGEST,      /* tpe_lattice_suggest                        */
   TPE_OP_COUNT
 };
 #define TPE_OP_ARGS 23

@@ -135,3 +135,39 @@ def test_draw32_quantized_chi2(engine, kind, args):
     table = table[:, table.sum(0) > 0]
     p = stats.chi2_contingency(table)[1]
     assert p > 1e-4, p
+
+
+def test_lattice_prefix_decision_equals_full_stream(engine):
+    """tpe_lattice_suggest (the suggest path: first `lat_prefix` candidates,
+    the rest of a stream only where an unseen lattice value could still win)
+    gives the full-stream winner byte for byte, and np.argmax's over the
+    stream.  The history makes the best values rare: below and above both sit
+    at 50, so the top scores are at the edges of [0, 100], where the below
+    mixture has only its prior's mass (~1e-4 per value) -- after 4096 draws
+    those values are mostly unseen, the decision stays open and the rest of
+    the stream is drawn.  Some key's winner lies past the prefix, which pass
+    0 alone cannot produce."""
+    from hyperopt_amd.engine import LabelWork
+    kind, args = KINDS[0]
+    rng = np.random.RandomState(0)
+    below = np.clip(np.round(rng.normal(50.0, 1.0, 25)), 0, 100)
+    above = np.clip(np.round(rng.normal(50.0, 10.0, T - 25)), 0, 100)
+    old = engine.lat_prefix
+    late = 0
+    try:
+        for key in range(4240, 4246):
+            out = {}
+            for p in (0, 4096, 1 << 16):
+                engine.lat_prefix = p
+                w = LabelWork("q", kind, args, below, above, n_cand=N, key=key)
+                r, = engine.run([w], precision=32)
+                out[p] = (r.score, r.index, r.value, r.n_scored)
+            assert out[4096] == out[0], (key, out[4096], out[0])
+            assert out[1 << 16] == out[0], (key, out[1 << 16], out[0])
+            s, = engine.run([w], precision=32, sample_only=True)
+            best, score = _stream_argmax(w, s.cand)
+            assert out[0][1] == best, (key, out[0], best)
+            late += out[0][1] >= 4096
+    finally:
+        engine.lat_prefix = old
+    assert late > 0
