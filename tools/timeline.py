@@ -4,6 +4,10 @@ level's first kernel, duration, queue and the idle gap before it on the GPU
 (diagnostic for the multi-GPU critical path).
 
     python tools/timeline.py gpurun_out/tl8 [levels=2] [first-kernel=k_gather_obs]
+
+The last level of a bench.py trace is its untimed all-groups timer pass
+(HIP events around every kernel group, ~10 us each on the stream): look at
+the levels before it for the timed steps' timeline.
 """
 import glob
 import os
