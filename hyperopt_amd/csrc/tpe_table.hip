@@ -409,6 +409,44 @@ __device__ __forceinline__ double wave_max_dpp(double v) {
   }
   return r;
 }
+// The nine P_n sums of a wave at once (transposed butterfly).  Per DPP stage
+// each lane keeps half of its live values and adds its partner's copy of
+// them: stage 1 pairs lane i with 15-i of its row (row mirror, bit 3 chooses
+// the half), stage 2 with 7-i of its half-row (half mirror, bit 2), stages 3
+// and 4 with i^2 and i^1 (quad perms); a stage's partner always holds the same
+// subset as the lane, because the mirrors come first.  After four stages lane
+// p of each row holds its row's sum of P_rev4(p) (rev4: the 4-bit reversal);
+// two cross-row exchanges complete the totals.  Returns lane L's total of
+// P_rev4(L) (L < 16; rev4(L) >= 9 gives 0): 11 exchange-adds instead of the
+// 9 x 4 of one wave_sum_dpp per term.
+template <int CTRL, int M>
+__device__ __forceinline__ void fold_stage(float (&w)[16], bool hi) {
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const float keep = hi ? w[2 * j + 1] : w[2 * j], send = hi ? w[2 * j] : w[2 * j + 1];
+    w[j] = keep + dpp_f<CTRL>(send);
+  }
+}
+__device__ __forceinline__ float wave_sum9_transposed(const float (&P)[9]) {
+  const int lane = lane_id();
+  float w[16];
+#pragma unroll
+  for (int n = 0; n < 16; ++n) w[n] = n < 9 ? P[n] : 0.0f;
+  fold_stage<kDppMirror, 5>(w, (lane >> 3) & 1);      // 9 live -> 5
+  w[5] = 0.0f;
+  fold_stage<kDppHalfMirror, 3>(w, (lane >> 2) & 1);  // -> 3
+  w[3] = 0.0f;
+  fold_stage<kDppXor2, 2>(w, (lane >> 1) & 1);        // -> 2
+  fold_stage<kDppXor1, 1>(w, lane & 1);               // -> 1
+  float v = w[0];
+  v += __shfl_xor(v, 16, kWave);
+  v += __shfl_xor(v, 32, kWave);
+  return v;
+}
+__device__ __forceinline__ int rev4(int p) {
+  return ((p & 1) << 3) | ((p & 2) << 1) | ((p & 4) >> 1) | ((p & 8) >> 3);
+}
+
 __device__ __forceinline__ float wave_sum_f(float v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -501,18 +539,15 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
 #pragma unroll
     for (int n = 0; n < kP; ++n) P[n] *= r;
   }
-#pragma unroll
-  for (int n = 0; n < kP; ++n) P[n] = wave_sum_dpp(P[n]);
+  static_assert(kP == 9, "wave_sum9_transposed folds nine terms");
+  const float v = wave_sum9_transposed(P);  // lane L < 16: the total of P_rev4(L)
   bad = __any(bad);
-  if (lane < kP) {
-    float v = P[0];
-#pragma unroll
-    for (int n = 1; n < kP; ++n)
-      if (lane == n) v = P[n];
-    if (lane < kP32)
-      cell[2 * lane + mix] = v;
+  const int n = rev4(lane & 15);
+  if (lane < 16 && n < kP) {
+    if (n < kP32)
+      cell[2 * n + mix] = v;
     else
-      reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (lane - kP32) + mix] = (_Float16)v;
+      reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (n - kP32) + mix] = (_Float16)v;
   }
   m_out = m0;
   return bad;
