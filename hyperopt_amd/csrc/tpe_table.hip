@@ -339,27 +339,6 @@ __device__ __forceinline__ int last_le(const double* a, int n, double v) {
   return lo - 1;
 }
 
-// first k with a[k] >= v (gt: a[k] > v), a non-decreasing, n if none; every
-// lane of the wave gets it.  64-ary narrowing: one probe load per lane per
-// step, so 10^4 components take 3 dependent loads instead of 14.
-__device__ __forceinline__ int wave_first(const double* a, int n, double v, bool gt) {
-  const int lane = lane_id();
-  int lo = 0, hi = n;  // answer in [lo, hi]
-  while (lo < hi) {
-    const int stride = (hi - lo + kWave - 1) / kWave;
-    const int idx = lo + lane * stride;
-    bool p = true;
-    if (idx < hi) p = gt ? (a[idx] > v) : (a[idx] >= v);
-    const uint64_t m = __ballot(p);
-    const int f = m ? __builtin_ctzll(m) : kWave;
-    if (f == 0) break;  // a[lo] qualifies
-    const int nlo = lo + (f - 1) * stride + 1;
-    hi = min(lo + f * stride, hi);
-    lo = nlo;
-  }
-  return lo;
-}
-
 __device__ __forceinline__ double wave_max_d(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
@@ -458,23 +437,55 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// A cell's two reach windows at once: four searches of wave_first's kind in
+// one pass, one per 16-lane group -- g = 0 / 2: the first k of the below /
+// above mixture with reach_hi[k] >= y0 - h, g = 1 / 3: the first k with
+// reach_lo[k] > y0 + h (the window ends one before it).  16-ary narrowing:
+// 10^4 components take 4 dependent probes, for all four searches together
+// instead of 3 for each.  Every lane gets all four answers.
+struct Windows {
+  int lo_b, end_b, lo_a, end_a;
+};
+__device__ __forceinline__ Windows cell_windows(const tpe_seg& SB, const tpe_seg& SA,
+                                                const double* __restrict__ reach_hi,
+                                                const double* __restrict__ reach_lo, double y0,
+                                                double h) {
+  const int lane = lane_id(), g = lane >> 4, l = lane & 15;
+  const tpe_seg& S = g < 2 ? SB : SA;
+  const bool gt = g & 1;
+  const double* a = (gt ? reach_lo : reach_hi) + S.comp_off;
+  const double v = gt ? y0 + h : y0 - h;
+  int lo = 0, hi = S.n_obs + 1;  // answer in [lo, hi]
+  while (__any(lo < hi)) {
+    const bool active = lo < hi;
+    const int stride = (hi - lo + 15) / 16;
+    const int idx = lo + l * stride;
+    bool p = true;  // probes past the end qualify
+    if (active && idx < hi) p = gt ? (a[idx] > v) : (a[idx] >= v);
+    const uint32_t m = (uint32_t)(__ballot(p) >> (g * 16)) & 0xFFFFu;
+    const int f = m ? __builtin_ctz(m) : 16;
+    if (active) {
+      if (f == 0) {
+        hi = lo;  // a[lo] qualifies
+      } else {
+        const int nlo = lo + (f - 1) * stride + 1;
+        hi = min(lo + f * stride, hi);
+        lo = nlo;
+      }
+    }
+  }
+  return Windows{__builtin_amdgcn_readlane(lo, 0), __builtin_amdgcn_readlane(lo, 16),
+                 __builtin_amdgcn_readlane(lo, 32), __builtin_amdgcn_readlane(lo, 48)};
+}
+
 // one wave builds one mixture's expansion on one cell; returns the failed flag
+// (k_lo .. k_hi: the cell's reach window, cell_windows)
 __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __restrict__ sigma,
-                                          const double* __restrict__ coef64,
-                                          const double* __restrict__ reach_hi,
-                                          const double* __restrict__ reach_lo,
+                                          const double* __restrict__ coef64, int k_lo, int k_hi,
                                           const int32_t* __restrict__ wide_idx, int n_wide,
                                           double T, double y0, double h, float* cell,
                                           int mix, double& m_out) {
-  const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
-#ifdef TPE_DIAG_BSEARCH
-  const int k_lo = first_ge(reach_hi + off, nc, y0 - h);
-  const int k_hi = last_le(reach_lo + off, nc, y0 + h);
-#else
-  const int k_lo = wave_first(reach_hi + off, nc, y0 - h, false);
-  const int k_hi = wave_first(reach_lo + off, nc, y0 + h, true) - 1;
-#endif
   const int nwin = max(0, k_hi - k_lo + 1);
   const int items = nwin + n_wide;
   const int lane = lane_id();
@@ -669,9 +680,10 @@ __global__ __launch_bounds__(kBS) void k_table_build(
     float* region = cells + J.tbl_off * (kSlotB / 4);
     float* out = region + c * kCellF;
     double mb, ma;
-    const bool bb = build_mix(SB, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below,
+    const Windows w = cell_windows(SB, SA, reach_hi, reach_lo, y0, g.h);
+    const bool bb = build_mix(SB, sigma, coef64, w.lo_b, w.end_b - 1, wide_idx, Tb.n_wide_below,
                               Tb.T_below, y0, g.h, out, 0, mb);
-    const bool ba = build_mix(SA, sigma, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above,
+    const bool ba = build_mix(SA, sigma, coef64, w.lo_a, w.end_a - 1, wide_idx, Tb.n_wide_above,
                               Tb.T_above, y0, g.h, out, 1, ma);
     if (lane_id() == 0) {
       // dword 15: the score offset m_below - m_above, NaN marks a failed cell
