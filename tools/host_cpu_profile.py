@@ -102,6 +102,8 @@ def make_engine():
     eng.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
     eng.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
     eng.lat_early = os.environ.get("TPE_LAT_EARLY", "0") == "1"
+    eng.lat_prefix = int(os.environ.get("TPE_LAT_PREFIX", str(E.LAT_PREFIX)))
+    eng.device_events = True
     eng.graphs = False
     eng._graphs, eng._last_gkey, eng._gen, eng._own = {}, None, 0, None
     eng.graph_stats = {"captured": 0, "replayed": 0, "eager": 0}
