@@ -18,7 +18,10 @@ label of its own global index range.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
 
-Prints ONE JSON line on rank 0.
+With --gpus N > 1 and no torch.distributed environment (WORLD_SIZE unset)
+the script launches itself as N ranks (torch.distributed.run, one process
+per GPU) before touching the GPU, and prints rank 0's line.  Prints ONE JSON
+line on rank 0.
 """
 from __future__ import annotations
 
@@ -43,6 +46,9 @@ sys.path.insert(0, HERE)
 T_HIST = 10_000
 N_CAND = 1 << 22
 FP32_PEAK_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles
+# per SIMD at 2.4 GHz (MI355X_MICROARCH.md: v_fma_f32 wave64 2 cycles)
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2
 FLOPS_PER_PAIR = 9  # unquantized GMM1/LGMM1 pair
 OPS_PER_TABLE_CAND = 56  # fast table scorer (score cubic per cell), per candidate
 DIRECT_PAIR_CEILING = 9.81e12  # pairs/s of the exp-bound direct loop (profiles/r01_valu_microbench.txt)
@@ -191,14 +197,16 @@ def _cpu_model():
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(space, vals, losses, n=20480, workers=16):
+def cpu_baseline(space, vals, losses, n=20480, workers=64):
     """The oracle (numpy restatement of tpe.suggest's per-label pipeline,
     /root/reference/hyperopt/tpe.py:837-964) on a bounded sample of C3 --
     test infrastructure only, never on the product path.  Two variants
     (BASELINE.md "CPU-baseline plan"): one process over one label of each kind
     (numpy elementwise code is single-threaded), and label-parallel
-    multiprocessing, one label per worker over min(16, cpu_count) spawned
-    workers (the box's CPU share), timed after the workers have started."""
+    multiprocessing, one label per worker over every CPU this process may run
+    on (os.sched_getaffinity), at most `workers` spawned processes (each holds
+    a few hundred MB of numpy temporaries), timed after the workers have
+    started."""
     import multiprocessing as mp
     sp = split(vals, losses)
     by_kind = {}
@@ -209,8 +217,13 @@ def cpu_baseline(space, vals, losses, n=20480, workers=16):
     done = sum(_cpu_label((kind, a, sp[lab][0], sp[lab][1], n, 5)) for lab, kind, a in picks)
     dt1 = time.perf_counter() - t0
     ncpu = os.cpu_count() or 1
-    nw = max(1, min(workers, ncpu))
-    order = [s for group in zip(*by_kind.values()) for s in group][:nw]  # kinds interleaved
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = ncpu
+    nw = max(1, min(workers, allowed))
+    order = [s for group in zip(*by_kind.values()) for s in group]  # kinds interleaved
+    order = (order * ((nw + len(order) - 1) // len(order)))[:nw]  # one label per worker
     tasks = [(kind, a, sp[lab][0], sp[lab][1], n, 5 + i) for i, (lab, kind, a) in enumerate(order)]
     multi = None
     try:
@@ -228,7 +241,7 @@ def cpu_baseline(space, vals, losses, n=20480, workers=16):
             "sample": "oracle/tpe_oracle.py numpy pipeline (fit+sample+score+argmax), 5 labels "
                       "(uniform, loguniform, quniform, normal, choice8) x %d candidates, 10k-trial "
                       "history, %.2f s" % (n, dt1),
-            "cpu_model": _cpu_model(), "os_cpu_count": ncpu,
+            "cpu_model": _cpu_model(), "os_cpu_count": ncpu, "sched_affinity_cpus": allowed,
             "label_parallel": multi}
 
 
@@ -333,6 +346,38 @@ def valu_issue(prof, n_launch_cand):
     return out
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(n):
+    """--gpus N without a torch.distributed environment: run this script as N
+    ranks under torch.distributed.run (a child process; this process never
+    touches the GPU), pass rank 0's JSON line through, exit with its code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def drawn_per_step(eng, space, units):
+    """Candidates this rank drew in its last level: every candidate of a
+    table or categorical unit; of a quantized unit, eng.lat_prefix when the
+    prefix-first lattice argmax settled it (need flag 0), else all."""
+    quant = [c for j, _, c in units if space[j][1].startswith("q")]
+    drawn = sum(c for j, _, c in units if not space[j][1].startswith("q"))
+    buf = eng._bufs.get("lat_need")
+    prefix = eng.lat_prefix
+    if not quant or buf is None or not prefix or max(quant) <= prefix:
+        return drawn + sum(quant)
+    need = buf[:4 * len(quant)].cpu().numpy().view(np.int32)
+    return drawn + sum(c if (n or c <= prefix) else prefix for c, n in zip(quant, need.tolist()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -356,11 +401,18 @@ def main():
     ap.add_argument("--scorer", default="auto", choices=("auto", "dense", "sorted", "table"),
                     help="fp32 kernel for the unquantized labels (engine.Engine.run)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BENCH_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU (ranks
     # share cuda:0; the winners are combined on the host) -- never for numbers
@@ -509,7 +561,7 @@ def main():
         exec_pairs = dense_pairs if group == "cont" else (eng.last_pairs or dense_pairs)
         ops = exec_pairs * FLOPS_PER_PAIR
         work = {"flops_per_pair": FLOPS_PER_PAIR, "evaluated_pairs_per_launch": exec_pairs}
-    achieved = ops / sec / 1e12 if sec > 0 else float("nan")
+    builder_tflops = ops / sec / 1e12 if sec > 0 else float("nan")
     all_timers = {}
     for k in range(3):
         step(args.warmup + args.steps + k, all_timers)
@@ -520,35 +572,63 @@ def main():
     per_rank = sum(c for _, _, c in units)
     total_cand = (len(space) * n_cand if strong else per_rank * world) * args.steps
     value = total_cand / elapsed
+    # candidates actually drawn: a quantized label's prefix-first lattice
+    # argmax (tpe_lattice_suggest) decides most labels from the first
+    # eng.lat_prefix draws of its stream (exact by construction);
+    # the per-job "need" flags of the last level say which labels drew it all
+    drawn = drawn_per_step(eng, space, units)
+    if world > 1:
+        t = torch.tensor([float(drawn)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        drawn = int(t.item())
     # per-launch HBM bytes / VALU figures of the dominant kernel, from the PMC
     # passes of tools/profile_round.sh (tools/make_traffic.py)
     traffic, prof = None, {}
     tfile = os.path.join(HERE, "profiles", "traffic.json")
     if os.path.exists(tfile):
         prof = json.load(open(tfile))
-        if prof.get("kernel") and prof["kernel"] in kname:
-            traffic = prof.get("bytes_per_launch")
-        else:
-            prof = {}
-    roofline = {"bound": "valu", "kernel": kname, "achieved": achieved,
-                "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s (builder-defined ops per candidate, DESIGN.md 3.1)",
-                "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
-                "algorithmic_ops_per_launch": ops, "avg_launch_ms": avg_ms,
-                "timed_launches": len(kms),
-                "dense_pairs_per_launch": dense_pairs,
-                "dense_equivalent_pairs_per_s": dense_pairs / sec if sec > 0 else None,
-                "direct_pair_ceiling_per_s": DIRECT_PAIR_CEILING,
-                "valu_busy": prof.get("valu_busy"), "traffic_source": prof.get("source"),
-                "valu_issue": valu_issue(prof, n_cont) if prof else None}
-    roofline.update(work)
+        if not (prof.get("kernel") and prof["kernel"] in kname and
+                prof.get("candidates_per_launch") in (None, n_cont)):
+            prof = {}  # another kernel or another workload: not this launch's counters
+        traffic = prof.get("bytes_per_launch")
+    issue = valu_issue(prof, n_cont) if prof else None
+    dense_ps = dense_pairs / sec if sec > 0 else None
+    roofline = {"kernel": kname, "avg_launch_ms": avg_ms, "timed_launches": len(kms),
+                "traffic": traffic, "traffic_source": prof.get("source"),
+                "valu_busy": prof.get("valu_busy"), "valu_issue": issue,
+                # SURVEY 8(d)'s count: the (candidate, component) pairs the
+                # reference evaluates at 9 flop each -- the table scorer does not
+                # evaluate them (one cubic per cell), so this rate is reported, not
+                # held against the FP32 peak
+                "dense_equivalent": {"pairs_per_launch": dense_pairs, "pairs_per_s": dense_ps,
+                                     "tflops_at_9_flop_per_pair":
+                                         dense_ps * FLOPS_PER_PAIR / 1e12 if dense_ps else None,
+                                     "direct_pair_ceiling_per_s": DIRECT_PAIR_CEILING},
+                "builder_ops": dict(work, achieved_tflops=builder_tflops,
+                                    peak_tflops=FP32_PEAK_TFLOPS,
+                                    frac=builder_tflops / FP32_PEAK_TFLOPS)}
+    if issue and prof.get("valu_insts_per_launch") and sec > 0:
+        # VALU issue efficiency: the dominant kernel's VALU wave-instructions
+        # per launch (PMC SQ_INSTS_VALU) over its live launch time, against one
+        # wave64 VALU instruction per 2 cycles on every SIMD
+        ach = prof["valu_insts_per_launch"] / sec
+        roofline.update({"bound": "valu-issue", "achieved": ach, "peak": VALU_ISSUE_PEAK,
+                         "unit": "VALU wave-instructions/s", "frac": ach / VALU_ISSUE_PEAK})
+    else:  # no PMC figures for this workload: the builder's operation count
+        roofline.update({"bound": "valu", "achieved": builder_tflops, "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s (builder-defined ops per candidate, DESIGN.md 3.1)",
+                         "frac": builder_tflops / FP32_PEAK_TFLOPS})
     if group == "table":
         roofline["l2_gather_bytes_per_launch"] = 16 * n_cont  # one 16-B score cubic per candidate
         roofline["build_ms"] = group_ms.get("table_build")
+        roofline["band_rescore_ms"] = group_ms.get("band")
     line = {
         "metric": "EI candidates scored/sec (50-dim, 10k trials)",
         "value": value,
         "unit": "EI candidates/s",
+        "candidates_drawn_per_step": drawn,
+        "candidates_decided_per_step": total_cand // args.steps,
+        "value_drawn": drawn * args.steps / elapsed,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,

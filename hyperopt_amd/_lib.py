@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -41,7 +41,7 @@ JOB_DTYPE = np.dtype([
 TABLE_DTYPE = np.dtype([
     ("lo", "<f8"), ("hi", "<f8"), ("h_below", "<f8"), ("h_above", "<f8"), ("origin", "<f8"),
     ("h", "<f8"), ("inv_h", "<f4"), ("inv_w", "<f4"), ("nb", "<i4"), ("n_wide_below", "<i4"),
-    ("n_wide_above", "<i4"), ("pad", "<i4"), ("T_below", "<f8"), ("T_above", "<f8")],
+    ("n_wide_above", "<i4"), ("slope", "<f4"), ("T_below", "<f8"), ("T_above", "<f8")],
     align=True)
 GATHER_DTYPE = np.dtype([
     ("col", "<i4"), ("below", "<i4"), ("dst_off", "<i8"), ("offset", "<i8"), ("count", "<i8"),
@@ -51,6 +51,7 @@ HISTORY_DTYPE = np.dtype([
     ("rows_off", "<i8"), ("isb_off", "<i8")], align=True)
 BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
                        ("n_scored", "<i8")], align=True)
+BAND_DTYPE = np.dtype([("index", "<i8"), ("y", "<f4"), ("hi", "<f4")], align=True)
 PRIOR_DTYPE = np.dtype([("kind", "<i4"), ("n_cat", "<i4"), ("a", "<f8"), ("b", "<f8"),
                         ("q", "<f8"), ("p_off", "<i8"), ("key", "<u8")], align=True)
 OP_ARGS = 23
@@ -66,6 +67,7 @@ OP_EVENT_RECORD, OP_STREAM_WAIT, OP_MEMCPY, OP_STREAM_SYNC = range(len(OP_CODES)
 OP_CODES["tpe_best_scatter"] = OP_STREAM_SYNC + 1
 OP_CODES["tpe_maxloc_allreduce"] = OP_STREAM_SYNC + 2
 OP_CODES["tpe_lattice_suggest"] = OP_STREAM_SYNC + 3
+OP_CODES["tpe_band_rescore"] = OP_STREAM_SYNC + 4
 PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
     PRIOR_CATEGORICAL = range(6)
 
@@ -94,8 +96,9 @@ _SIGNATURES = {
     "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_table": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
                              _P, _P, _P]),
-    "tpe_score_table_fast": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P,
-                                  _P, _P]),
+    "tpe_score_table_fast": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P,
+                                  _P, _I64, _P, _P]),
+    "tpe_band_rescore": (_I, [_P, _P, _I, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]),
     "tpe_pruned64_partials": (_I64, [_P, _I]),
     "tpe_score_pruned64": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P,
                                 _P, _P, _P, _I64, _P, _P]),
@@ -129,8 +132,6 @@ _hip = None
 H2D, D2H = 1, 2  # hipMemcpyKind
 EVENT_NO_TIMING = 0x2  # hipEventDisableTiming
 EVENT_NO_SYSTEM_FENCE = 0x20000000  # hipEventDisableSystemFence (device-scope release)
-CAPTURE_RELAXED = 2  # hipStreamCaptureModeRelaxed
-CAPTURE_SET_DEPENDENCIES = 1  # hipStreamSetCaptureDependencies
 
 
 def hip():
@@ -147,25 +148,9 @@ def hip():
                            ("hipStreamWaitEvent", [_P, _P, ctypes.c_uint]),
                            ("hipEventSynchronize", [_P]),
                            ("hipStreamSynchronize", [_P]),
-                           # level graphs (Engine.run): capture once, replay per call
                            ("hipGetLastError", []),
                            ("hipEventElapsedTime", [ctypes.POINTER(ctypes.c_float), _P, _P]),
-                           ("hipEventDestroy", [_P]),
-                           ("hipStreamBeginCapture", [_P, _I]),
-                           ("hipStreamEndCapture", [_P, ctypes.POINTER(_P)]),
-                           ("hipGraphInstantiate", [ctypes.POINTER(_P), _P, _P, _P,
-                                                    ctypes.c_size_t]),
-                           ("hipGraphLaunch", [_P, _P]),
-                           ("hipStreamGetCaptureInfo_v2",
-                            [_P, ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_ulonglong),
-                             ctypes.POINTER(_P), ctypes.POINTER(ctypes.POINTER(_P)),
-                             ctypes.POINTER(ctypes.c_size_t)]),
-                           ("hipGraphAddEventRecordNode",
-                            [ctypes.POINTER(_P), _P, ctypes.POINTER(_P), ctypes.c_size_t, _P]),
-                           ("hipStreamUpdateCaptureDependencies",
-                            [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.c_uint]),
-                           ("hipGraphExecDestroy", [_P]),
-                           ("hipGraphDestroy", [_P])):
+                           ("hipEventDestroy", [_P])):
             fn = getattr(h, name)
             fn.restype = _I
             fn.argtypes = args

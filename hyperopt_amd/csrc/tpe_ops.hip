@@ -85,6 +85,7 @@ int run_one(const tpe_op& op) {
     TPE_CALL(TPE_OP_BEST_SCATTER, tpe_best_scatter);
     TPE_CALL(TPE_OP_MAXLOC_ALLREDUCE, tpe_maxloc_allreduce);
     TPE_CALL(TPE_OP_LATTICE_SUGGEST, tpe_lattice_suggest);
+    TPE_CALL(TPE_OP_BAND_RESCORE, tpe_band_rescore);
 #undef TPE_CALL
     case TPE_OP_EVENT_RECORD:
       return runtime(hipEventRecord((hipEvent_t)ptr(op.a[0]),

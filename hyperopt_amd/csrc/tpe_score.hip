@@ -278,6 +278,9 @@ __global__ __launch_bounds__(kBS) void k_score32(
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
+  // x: the given value (INJ) or the fp32 draw in the mixture's coordinate
+  // (log x for LGMM1, whose value is exp(y) evaluated in fp64: log(value) is
+  // then y itself, see cand_value in tpe_table.hip)
   float x[kR32], y[kR32];
   if (INJ) {
 #pragma unroll
@@ -290,19 +293,16 @@ __global__ __launch_bounds__(kBS) void k_score32(
 #pragma unroll
     for (int r = 0; r < kR32; ++r) {
       const int64_t li = base + r * kBS + threadIdx.x;
-      float v = 1.0f;
-      if (li < J.n_cand) {
-        v = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
-        if (lgmm) v = __expf(v);
-      }
-      x[r] = v;
+      x[r] = li < J.n_cand ? draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low,
+                                    (float)J.high)
+                           : 1.0f;
     }
   }
 #pragma unroll
   for (int r = 0; r < kR32; ++r) {
     const int64_t li = base + r * kBS + threadIdx.x;
     if (li < J.n_cand)
-      y[r] = lgmm ? __logf(x[r]) : x[r];
+      y[r] = (lgmm && INJ) ? __logf(x[r]) : x[r];
     else
       y[r] = (float)SA.center;  // inactive lanes sit on the prior mean
   }
@@ -316,15 +316,15 @@ __global__ __launch_bounds__(kBS) void k_score32(
     if (li >= J.n_cand) continue;
     double bl = lb[r], al = la[r];
     if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
-      const double lx = (double)__logf(x[r]);
-      bl -= lx;
-      al -= lx;
+      bl -= (double)y[r];
+      al -= (double)y[r];
     }
+    const double v = (lgmm && !INJ) ? exp((double)x[r]) : (double)x[r];
     const int64_t o = J.out_off + li;
     if (out_bl) out_bl[o] = bl;
     if (out_al) out_al[o] = al;
-    if (out_x) out_x[o] = (double)x[r];
-    best_update(b, bl - al, J.cand_base + li, (double)x[r]);
+    if (out_x) out_x[o] = v;
+    best_update(b, bl - al, J.cand_base + li, v);
   }
   b = block_best<kBS>(b, red);
   if (threadIdx.x == 0) *P = tpe_best{b.score, b.index, b.value, 0};
@@ -426,11 +426,11 @@ __device__ __forceinline__ int bin_of(float y, float lo, float scale) {
   return (int)t;
 }
 
-// the candidate exactly as k_score32<false> draws it
-__device__ __forceinline__ float cand32(const Mix& M, const tpe_job& J, int64_t li, bool lgmm,
-                                        bool lo_on, bool hi_on) {
-  float v = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
-  return lgmm ? __expf(v) : v;
+// the candidate exactly as k_score32<false> draws it, in the mixture's
+// coordinate (log x for LGMM1: its value is exp(y) in fp64)
+__device__ __forceinline__ float cand32(const Mix& M, const tpe_job& J, int64_t li, bool lo_on,
+                                        bool hi_on) {
+  return draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low, (float)J.high);
 }
 
 // K1: draw every candidate once (kept in `gen`, generation order, coalesced)
@@ -447,15 +447,14 @@ __global__ __launch_bounds__(kBS) void k_sort_count(
   for (int i = threadIdx.x; i < kNB; i += kBS) h[i] = 0u;
   const Mix M = stage_mix(segs[J.below], wcdf, mu, sigma, s_mix);
   __syncthreads();
-  const bool lgmm = J.family == TPE_LGMM1;
   const bool lo_on = J.flags & TPE_F_LOW, hi_on = J.flags & TPE_F_HIGH;
   const float lo = (float)J.bin_lo, scale = (float)(kNB / (J.bin_hi - J.bin_lo));
   for (int r = 0; r < kSortR; ++r) {
     const int64_t li = base + r * kBS + threadIdx.x;
     if (li >= J.n_cand) break;
-    const float x = cand32(M, J, li, lgmm, lo_on, hi_on);
-    gen[J.sort_off + li] = x;
-    atomicAdd(&h[bin_of(lgmm ? __logf(x) : x, lo, scale)], 1u);
+    const float y = cand32(M, J, li, lo_on, hi_on);
+    gen[J.sort_off + li] = y;
+    atomicAdd(&h[bin_of(y, lo, scale)], 1u);
   }
   __syncthreads();
   uint32_t* row = counts + 2 * J.cnt_off + (int64_t)blockIdx.x * kNB;
@@ -569,14 +568,13 @@ __global__ __launch_bounds__(kBS) void k_sort_scatter(const tpe_job* __restrict_
   lstart[2 * threadIdx.x] = cur[2 * threadIdx.x] = part[threadIdx.x];
   lstart[2 * threadIdx.x + 1] = cur[2 * threadIdx.x + 1] = part[threadIdx.x] + c0;
   __syncthreads();
-  const bool lgmm = J.family == TPE_LGMM1;
   const float lo = (float)J.bin_lo, scale = (float)(kNB / (J.bin_hi - J.bin_lo));
   const int n = (int)min((int64_t)kSortPer, J.n_cand - base);
   for (int r = 0; r < kSortR; ++r) {
     const int e = r * kBS + threadIdx.x;
     if (e >= n) break;
-    const float x = gen[J.sort_off + base + e];
-    const int b = bin_of(lgmm ? __logf(x) : x, lo, scale);
+    const float x = gen[J.sort_off + base + e];  // (the mixture coordinate)
+    const int b = bin_of(x, lo, scale);
     const uint32_t lp = atomicAdd(&cur[b], 1u);
     sx[lp] = x;
     si[lp] = (uint32_t)(base + e);
@@ -634,9 +632,9 @@ __global__ __launch_bounds__(kBS) void k_score_sorted(
   for (int r = 0; r < kR32; ++r) {
     const int64_t p = base + r * kBS + threadIdx.x;
     if (p < J.n_cand) {
-      x[r] = sorted_x[J.sort_off + p];
+      x[r] = sorted_x[J.sort_off + p];  // the mixture coordinate
       li[r] = sorted_i[J.sort_off + p];
-      y[r] = lgmm ? __logf(x[r]) : x[r];
+      y[r] = x[r];
       ymin = fminf(ymin, y[r]);
       ymax = fmaxf(ymax, y[r]);
       const float t = fmaf(y[r] - cen, cp.x, cp.y);
@@ -748,12 +746,12 @@ __global__ __launch_bounds__(kBS) void k_score_sorted(
     const int64_t p = base + r * kBS + threadIdx.x;
     if (p >= J.n_cand) continue;
     double bl = lb[r], al = la[r];
-    if (lgmm) {
-      const double lx = (double)__logf(x[r]);
-      bl -= lx;
-      al -= lx;
+    if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216): log of exp(y) is y
+      bl -= (double)y[r];
+      al -= (double)y[r];
     }
-    best_update(b, bl - al, J.cand_base + (int64_t)li[r], (double)x[r]);
+    best_update(b, bl - al, J.cand_base + (int64_t)li[r],
+                lgmm ? exp((double)x[r]) : (double)x[r]);
   }
   b = block_best<kBS>(b, red);
   if (threadIdx.x == 0) {
@@ -1030,8 +1028,13 @@ __global__ __launch_bounds__(kBS) void k_score_slots(
   const int64_t s = blockIdx.x;
   if (s >= J.lat_n) return;  // block-uniform
   const double v = (double)(J.lat_kmin + s) * J.q;  // np.round(x/q) * q, as k_lattice_compact
-  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err, sh);
-  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err, sh);
+  // every slot is scored, drawn or not: a slot below 0 (the bracket under a
+  // qloguniform / qlognormal lattice, never drawn) must not raise the
+  // reference's negative-argument error (tpe.py:196-197) -- a drawn value
+  // x = round(exp(y)/q)*q >= 0 never has ub = x + q/2 < 0, so no err here
+  (void)err;
+  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, nullptr, sh);
+  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, nullptr, sh);
   if (threadIdx.x == 0)
     partial[(int64_t)blockIdx.y * gridDim.x + s] = tpe_best{bl - al, -1, v, 0};
 }
@@ -1325,17 +1328,22 @@ __global__ __launch_bounds__(kBS) void k_sample(const tpe_job* __restrict__ jobs
   if (sizeof(T) == 4) {
     // the fp32 stream exactly as the scorers draw it: kLatR consecutive
     // candidates per thread through draw32_pairs (the table scorer's and the
-    // DRAW32 lattice sampler's code), LGMM1 values as __expf(y)
+    // DRAW32 lattice sampler's code); LGMM1 values as exp(y) in fp64 for
+    // unquantized labels (the scorers' values), __expf(y) for quantized ones
+    // (the lattice sampler's slots)
+    const bool quant = J.flags & TPE_F_QUANT;
     const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
     const int nv = (int)max((int64_t)0, min((int64_t)kLatR, J.n_cand - t0));
     float x[kLatR];
     draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                        (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList, x);
+                        (float)J.high, lgmm && quant,
+                        s_stage + (threadIdx.x / kWave) * (kLatR * kWave),
+                        s_list + (threadIdx.x / kWave) * kRetryList, x);
 #pragma unroll
     for (int r = 0; r < kLatR; ++r) {
       if (r >= nv) continue;
-      double v = (double)x[r];
-      if (J.flags & TPE_F_QUANT) v = rint(v / J.q) * J.q;
+      double v = (lgmm && !quant) ? exp((double)x[r]) : (double)x[r];
+      if (quant) v = rint(v / J.q) * J.q;
       out_x[J.out_off + t0 + r] = v;
     }
     return;

@@ -593,9 +593,10 @@ __device__ __forceinline__ const float4* score_cells_of(const char* region, int6
 }
 
 __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__ jobs,
-                                                     const tpe_table* __restrict__ tables,
+                                                     tpe_table* __restrict__ tables,
                                                      float* __restrict__ cells,
                                                      unsigned long long* __restrict__ stats) {
+  __shared__ float fred[kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
   const int nb = tables[blockIdx.y].nb;
   char* region = reinterpret_cast<char*>(cells) + J.tbl_off * kSlotB;
@@ -608,6 +609,7 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
   const double u = l == 0 ? nd0 : l == 1 ? nd1 : l == 2 ? nd2 : l == 3 ? nd3
                  : -kU + 2.0 * kU * (double)(l - 4) / (kScoreChecks - 1);
   const float uf = (float)u;
+  float slope = 0.0f;  // max |f'(u)| bound over this thread's unflagged cells (lane 0 of a group)
   // group-uniform trip count: every lane of a group runs the shuffles
   for (int64_t c = (int64_t)blockIdx.x * kScoreCellsPerBlock + sub; c < nb;
        c += (int64_t)gridDim.x * kScoreCellsPerBlock) {
@@ -651,8 +653,14 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
       const bool bad = (mk & ((1ull << kScoreLanes) - 1)) != 0;
       outs[c] = bad ? make_float4(__int_as_float(0x7FC00000), 0.0f, 0.0f, 0.0f) : q;
       if (bad && stats) atomicAdd(stats + 2, 1ull);
+      // |f'(u)| <= |c1| + 2|c2||u| + 3|c3|u^2 on |u| <= 1.05: the slope term of the
+      // scorer's error bound (u is rounded to fp32 there)
+      if (!bad) slope = fmaxf(slope, fabsf(q.y) + 2.1f * fabsf(q.z) + 3.31f * fabsf(q.w));
     }
   }
+  slope = block_max<kBS, float>(slope, fred);
+  if (threadIdx.x == 0 && slope > 0.0f)  // non-negative floats order as their bits
+    atomicMax(reinterpret_cast<unsigned int*>(&tables[blockIdx.y].slope), __float_as_uint(slope));
 }
 
 __global__ __launch_bounds__(kBS) void k_table_build(
@@ -671,6 +679,7 @@ __global__ __launch_bounds__(kBS) void k_table_build(
     W->inv_h = (float)(1.0 / g.h);
     W->inv_w = (float)(0.5 / g.h);
     W->nb = g.nb;
+    W->slope = 0.0f;  // raised by k_table_score (the next launch)
   }
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const int wid = threadIdx.x / kWave;
@@ -854,7 +863,7 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       const int64_t o = J.out_off + t0 + r;
       if (out_bl) out_bl[o] = bl;
       if (out_al) out_al[o] = al;
-      if (out_x) out_x[o] = (double)(exp_out ? __expf(y) : y);
+      if (out_x) out_x[o] = exp_out ? exp((double)y) : (double)y;
     };
     const int nvalid = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
     // cell of every candidate of the thread (byte offset in the job's table)
@@ -963,9 +972,9 @@ __global__ __launch_bounds__(kBS) void k_score_table(
       }
     }
     // the winner's value (by: the given value, or y of a sampled candidate --
-    // exp(y) for LGMM1, the same fp32 exp the other scorers store)
-    const float bx = exp_out ? __expf(by) : by;
-    if (br >= 0) best_update(run, (double)bs, J.cand_base + t0 + br, (double)bx);
+    // exp(y) in fp64 for LGMM1, the value every fp32 scorer gives)
+    const double bx = exp_out ? exp((double)by) : (double)by;
+    if (br >= 0) best_update(run, (double)bs, J.cand_base + t0 + br, bx);
   }  // tiles
   const BestT best = block_best<kBS>(run, red);
   if (stats) {
@@ -975,6 +984,36 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
 }
 
+// fp32 score error bound of the fast path, per candidate:
+//   |s32 - s64| <= kEpsAbs + kEpsSlope * slope + kEpsRel * |s32|
+// for a candidate scored by its cell's cubic or two-polynomial cell: each
+// mixture's polynomial 1.0e-6 (relative, so 1.0e-6 in its log), the stored
+// polynomial's fp32 evaluation at the build's check points 3e-7, the cubic's
+// fit (checked at 16 points against 1e-6 + 2^-22 |f|, taken twice) and its
+// fp32 rounding (offset 2^-24 |m_b - m_a|, three FMAs ~2^-22 (|f| + slope)),
+// and u's rounding (slope 2^-23), `slope` = tpe_table.slope.  A candidate of
+// the exact fp32 log-sum-exp fallback adds kEpsLse * (M_b + M_a + 4) (two
+// sequential fp32 sums of M terms).
+constexpr float kEpsAbs = 5.0e-6f, kEpsSlope = 4.0e-7f, kEpsRel = 1.0e-6f, kEpsLse = 1.2e-7f;
+
+// order-preserving float -> uint32 code (larger float, larger code; code 0 is
+// below every float: "no value yet")
+__device__ __forceinline__ uint32_t ord_enc(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord_dec(uint32_t e) {
+  if (e == 0u) return -INFINITY;
+  return __uint_as_float((e & 0x80000000u) ? (e & 0x7FFFFFFFu) : ~e);
+}
+
+// the value of an unquantized candidate drawn as y in fp32: y (GMM1) or
+// exp(y) evaluated in fp64 (LGMM1) -- so log(value) is y up to fp64 rounding
+// and the value's exact score is the score at y
+__device__ __forceinline__ double cand_value(float y, bool lgmm) {
+  return lgmm ? exp((double)y) : (double)y;
+}
+
 // Fast path for sampled candidates (the suggest path: no per-candidate
 // log-densities asked for).  Same draws as k_score_table (draw32_pairs), same
 // cell index; the score comes from the cell's 16-B cubic (k_table_score):
@@ -982,19 +1021,28 @@ __global__ __launch_bounds__(kBS) void k_score_table(
 // FMAs instead of two degree-8 polynomials and two logs.  Loads run four
 // candidates ahead.  Candidates on a flagged score cell (or off the grid)
 // take the two-polynomial cell, then the exact log-sum-exp, after the loop.
-// out_score / out_x (nullable, tests): per-candidate score and value.
+// Then the band (tpe_hip.h, tpe_score_table_fast): the block's best lower
+// bound s32 - eps goes into the job's running maximum G (atomic max on its
+// order code), and every candidate of the block whose upper bound s32 + eps
+// reaches the G known at that point is appended to the job's band list for
+// k_band_rescore (its value re-drawn: a draw is a function of its index).
+// out_score / out_x (nullable, tests): per-candidate fp32 score and value.
 __global__ __launch_bounds__(kBS) void k_score_table_fast(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, const float4* __restrict__ coef32,
     const tpe_table* __restrict__ tables, const float* __restrict__ cells,
+    tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
     double* __restrict__ out_score, double* __restrict__ out_x, tpe_best* __restrict__ partial,
     unsigned long long* __restrict__ stats, int n_tiles, int n_jobs) {
   __shared__ MixLds s_mix;
-  __shared__ float s_stage[(kBS / kWave) * kTR * kWave];  // retry staging, then fallback stash
+  // retry staging, then each lane's scores (slot r of lane l at r * 64 + l)
+  __shared__ float s_stage[(kBS / kWave) * kTR * kWave];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   __shared__ BestT red[kBS / kWave];
   __shared__ int nred[kBS / kWave];
+  __shared__ float fred[kBS / kWave];
+  __shared__ float s_g;
   int job, bx;
   {  // XCD-aware work order (see k_score_table)
     const int64_t W = (int64_t)n_tiles * n_jobs, per = (W + 7) / 8;
@@ -1054,14 +1102,18 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
       bs = take ? s : bs;
       by = take ? y : by;
       br = take ? r : br;
+      stage[r * kWave + lane] = s;  // kept for the band
       if (out_score) out_score[J.out_off + t0 + r] = (double)s;
     }
-    if (out_x && valid) out_x[J.out_off + t0 + r] = (double)(lgmm ? __expf(y) : y);
+    if (out_x && valid) out_x[J.out_off + t0 + r] = cand_value(y, lgmm);
   }
   int n_fb = 0;
+  uint32_t lsem = 0;  // candidates scored by the exact fp32 log-sum-exp
+  const uint32_t fbm = fb;
   if (__any(fb != 0)) {
     // fallback: the two-polynomial cell, else the exact fp32 log-sum-exp;
-    // the lane's candidates wait in its own column of the wave's stage
+    // the lane's candidates wait in its own column of the wave's stage, and
+    // their scores replace them there
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < kTR; ++r)
@@ -1082,7 +1134,9 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
         s = q3.w + (__builtin_amdgcn_logf(pb) - __builtin_amdgcn_logf(pa)) * kLn2T;
       } else {
         s = lse_exact32(coef32 + SB.comp_off, SB, y) - lse_exact32(coef32 + SA.comp_off, SA, y);
+        lsem |= 1u << r;
       }
+      stage[r * kWave + lane] = s;
       if (out_score) out_score[J.out_off + t0 + r] = (double)s;
       const bool na = s != s, nbn = bs != bs;
       const bool take =
@@ -1096,13 +1150,299 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
     }
   }
   BestT run{0.0, -1, 0.0};
-  if (br >= 0) run = BestT{(double)bs, J.cand_base + t0 + br, (double)(lgmm ? __expf(by) : by)};
+  if (br >= 0) run = BestT{(double)bs, J.cand_base + t0 + br, cand_value(by, lgmm)};
   const BestT best = block_best<kBS>(run, red);
   if (stats) {
     const int ne = block_sum<kBS, int>(n_fb, nred);
     if (threadIdx.x == 0 && ne) atomicAdd(stats, (unsigned long long)ne);
   }
   if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
+
+  // ---- the band: candidates that can still be the exact winner --------------
+  const float ea = kEpsAbs + kEpsSlope * Tb.slope;
+  const float el = ea + kEpsLse * (float)(SB.n_obs + SA.n_obs + 4);
+  auto eps = [&](int r, float s) __attribute__((always_inline)) -> float {
+    return (((lsem >> r) & 1u) ? el : ea) + kEpsRel * fabsf(s);
+  };
+  // the thread's best candidate's lower bound (a lower bound of G); NaN: none
+  const float lo_t = (br >= 0 && bs == bs) ? bs - eps(br, bs) : -INFINITY;
+  const float blo = block_max<kBS, float>(lo_t, fred);
+  uint32_t* ctl = band_ctl + 2 * (int64_t)job;
+  if (threadIdx.x == 0) {
+    const uint32_t old = atomicMax(ctl, blo > -INFINITY ? ord_enc(blo) : 0u);
+    s_g = fmaxf(blo, ord_dec(old));
+  }
+  __syncthreads();
+  const float G = s_g;
+  // upper bound of the thread's candidates scored on the table (monotone in s);
+  // NaN scores and fallback candidates are checked one by one
+  const float hi_t = br >= 0 ? bs + ea + kEpsRel * fabsf(bs) : -INFINITY;
+  if (fbm != 0u || !(hi_t < G)) {
+    tpe_band* B = band + (int64_t)job * band_cap;
+    for (int r = 0; r < nvalid; ++r) {
+      const float s = stage[r * kWave + lane];
+      const float hi = s + eps(r, s);
+      if (hi < G) continue;  // (NaN scores go on)
+      const int64_t g = J.cand_base + t0 + r;
+      const float y = draw32(M, J.key, g, lo_on, hi_on, (float)J.low, (float)J.high);
+      const uint32_t p = atomicAdd(ctl + 1, 1u);
+      if ((int64_t)p < band_cap) B[p] = tpe_band{g, y, hi};
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// exact re-score of the band (one block per job)
+// ---------------------------------------------------------------------------
+// A band candidate y is scored in fp64 through the table cell c that holds it
+// (the fp32 cell index, a function of y alone): both mixtures are expanded
+// around the cell centre y0 as e^m sum_{n<=kBandD} P_n u^n, u = (y - y0)/h,
+// over every component whose largest term on the cell reaches e^-45 / M of
+// the prior component's smallest one there (a lower bound of the sum): the
+// rest add < e^-45 of it.  A component's series exp(A u + B u^2) converges
+// like rho^n / n!, rho = 1.05|A| + 1.1025|B|; with rho <= kBandRho the tail
+// past degree 24 is < 1e-20 of its term, and components with a larger rho (far
+// out relative to their bandwidth) are summed term by term instead.  Rounding
+// of the P_n sums is ~1e-14 relative: the fp64 accuracy of a direct sum over
+// 10^4 terms.  Survivors off the grid, or of a cell with more slow components
+// than fit the list, take the direct online log-sum-exp over every component
+// (k_score64's arithmetic).  Every survivor's score depends on its y alone, so
+// the winner does not depend on how candidates are sharded over ranks.
+constexpr int kBandD = 24;           // expansion degree
+constexpr int kBandChunk = 2048;     // survivors held in LDS at a time
+constexpr int kBandDirect = 128;     // slow components summed term by term, per mixture
+constexpr double kBandTau = 45.0;    // exclusion margin (nats) on top of log(M)
+constexpr double kBandRho = 1.5;     // admissible 1.05 |A| + 1.1025 |B|
+
+struct BandMix {  // one mixture's expansion on one cell (LDS)
+  double P[kBandD + 1];
+  double m;
+  int n_dir;
+  int dir[kBandDirect];
+};
+
+// expansion of mixture S on the cell (y0, h); all threads; false: too many
+// slow components (the cell's survivors take the direct sum)
+__device__ bool band_expand(const tpe_seg& S, const double* __restrict__ coef64, double y0,
+                            double h, BandMix& E, double* dred) {
+  const int nc = S.n_obs + 1;
+  const int64_t off = S.comp_off;
+  const double4 cp = ld4(coef64, off + S.prior_pos);
+  const double far = (fabs(y0 - cp.x) + 1.05 * h) * cp.y;
+  const double T = cp.z - 0.5 * far * far - (log((double)nc) + kBandTau);
+  // scale: the largest included term at the centre
+  double m = -INFINITY;
+  for (int k = threadIdx.x; k < nc; k += kBS) {
+    const double4 c = ld4(coef64, off + k);
+    const double zn = fmax(fabs(y0 - c.x) - 1.05 * h, 0.0) * c.y;
+    if (c.z - 0.5 * zn * zn >= T) {
+      const double z0 = (y0 - c.x) * c.y;
+      m = fmax(m, c.z - 0.5 * z0 * z0);
+    }
+  }
+  m = block_max<kBS, double>(m, dred);
+  if (threadIdx.x == 0) E.n_dir = 0;
+  __syncthreads();
+  double P[kBandD + 1];
+#pragma unroll
+  for (int n = 0; n <= kBandD; ++n) P[n] = 0.0;
+  for (int k = threadIdx.x; k < nc; k += kBS) {
+    const double4 c = ld4(coef64, off + k);
+    const double zn = fmax(fabs(y0 - c.x) - 1.05 * h, 0.0) * c.y;
+    if (!(c.z - 0.5 * zn * zn >= T)) continue;
+    const double hi2 = h * c.y * c.y;
+    const double A = -(y0 - c.x) * hi2, B = -0.5 * h * hi2;
+    if (1.05 * fabs(A) + 1.1025 * fabs(B) > kBandRho) {
+      const int p = atomicAdd(&E.n_dir, 1);
+      if (p < kBandDirect) E.dir[p] = k;
+      continue;
+    }
+    const double z0 = (y0 - c.x) * c.y;
+    double cm = 0.0, cc = exp(c.z - 0.5 * z0 * z0 - m);  // e * c_n
+    P[0] += cc;
+#pragma unroll
+    for (int n = 0; n < kBandD; ++n) {
+      const double cn = fma(A, cc, 2.0 * B * cm) * (1.0 / (double)(n + 1));
+      P[n + 1] += cn;
+      cm = cc;
+      cc = cn;
+    }
+  }
+  // block sums of the kBandD + 1 terms (fixed order: deterministic)
+#pragma unroll
+  for (int n = 0; n <= kBandD; ++n) {
+    double v = P[n];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    P[n] = v;
+  }
+  __syncthreads();  // (E.n_dir complete; the previous user of E.P is done)
+  const int wid = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int n = 0; n <= kBandD; ++n) dred[wid * (kBandD + 1) + n] = P[n];
+  }
+  __syncthreads();
+  if (threadIdx.x <= kBandD) {
+    double t = 0.0;
+    for (int w = 0; w < kBS / kWave; ++w) t += dred[w * (kBandD + 1) + threadIdx.x];
+    E.P[threadIdx.x] = t;
+  }
+  if (threadIdx.x == 0) E.m = m;
+  __syncthreads();
+  return E.n_dir <= kBandDirect;
+}
+
+// log of the mixture at y from its cell expansion (u = (y - y0) / h)
+__device__ __forceinline__ double band_eval(const BandMix& E, const double* __restrict__ coef64,
+                                            int64_t off, double u, double y) {
+  double p = E.P[kBandD];
+#pragma unroll
+  for (int n = kBandD - 1; n >= 0; --n) p = fma(p, u, E.P[n]);
+  for (int i = 0; i < E.n_dir; ++i) {
+    const double4 c = ld4(coef64, off + E.dir[i]);
+    const double t = (y - c.x) * c.y;
+    p += exp(c.z - 0.5 * t * t - E.m);
+  }
+  return log(p) + E.m;
+}
+
+// log of the mixture at y summed directly over every component (online
+// log-sum-exp, k_score64's arithmetic)
+__device__ __forceinline__ double band_direct(const tpe_seg& S, const double* __restrict__ coef64,
+                                              double y) {
+  double mo = -INFINITY, so = 0.0;
+  for (int k = 0; k < S.n_obs + 1; ++k) {
+    const double4 c = ld4(coef64, S.comp_off + k);
+    const double t = (y - c.x) * c.y;
+    const double v = -0.5 * (t * t) + c.z;
+    const bool up = v > mo;
+    const double e = exp(up ? mo - v : v - mo);
+    so = up ? so * e + 1.0 : so + e;
+    mo = up ? v : mo;
+  }
+  return log(so) + mo;
+}
+
+__global__ __launch_bounds__(kBS) void k_band_rescore(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
+    const tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
+    const tpe_best* __restrict__ partial, int64_t nper, tpe_best* __restrict__ best) {
+  __shared__ BestT red[kBS / kWave];
+  __shared__ double dred[(kBS / kWave) * (kBandD + 1)];
+  __shared__ BandMix s_eb, s_ea;
+  __shared__ float s_y[kBandChunk];
+  __shared__ int64_t s_i[kBandChunk];
+  __shared__ int s_c[kBandChunk];
+  __shared__ int s_n, s_scan[kBS / kWave];
+  const int j = blockIdx.x;
+  const tpe_job J = jobs[j];
+  // the fp32 winner (kept when the band overflowed)
+  BestT b32{0.0, -1, 0.0};
+  for (int64_t i = threadIdx.x; i < nper; i += kBS) {
+    const tpe_best p = partial[(int64_t)j * nper + i];
+    best_update(b32, p.score, p.index, p.value);
+  }
+  b32 = block_best<kBS>(b32, red);
+  uint32_t* ctl = band_ctl + 2 * (int64_t)j;
+  const float G = ord_dec(ctl[0]);
+  const int64_t n = (int64_t)ctl[1];
+  __syncthreads();  // every thread has read the controls
+  if (threadIdx.x == 0) {
+    ctl[0] = 0u;  // ready for the next call
+    ctl[1] = 0u;
+  }
+  if (n > band_cap) {
+    if (threadIdx.x == 0) best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
+    return;
+  }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const tpe_table Tb = tables[j];
+  const bool lgmm = J.family == TPE_LGMM1;
+  const float g0 = (float)Tb.origin, inv_w = Tb.inv_w, h32 = (float)Tb.h;
+  const tpe_band* B = band + (int64_t)j * band_cap;
+  BestT bx{0.0, -1, 0.0};
+  int64_t e0 = 0;
+  while (__syncthreads_or(e0 < n)) {
+    // gather the next survivors (s32 + eps >= G) into LDS, in entry order
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    while (e0 < n && s_n + kBS <= kBandChunk) {
+      const int64_t e = e0 + threadIdx.x;
+      bool keep = false;
+      tpe_band E{};
+      if (e < n) {
+        E = B[e];
+        keep = !(E.hi < G);
+      }
+      // block exclusive scan of keep
+      const int lane = lane_id(), wid = threadIdx.x / kWave;
+      const uint64_t bal = __ballot(keep);
+      const int wpre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) s_scan[wid] = __popcll(bal);
+      __syncthreads();
+      int off = s_n;
+      for (int w = 0; w < wid; ++w) off += s_scan[w];
+      if (keep) {
+        const int p = off + wpre;
+        s_y[p] = E.y;
+        s_i[p] = E.index;
+        // the fp32 cell (as the scorer forms it); -2: off the grid (direct)
+        const float t = (E.y - g0) * inv_w;
+        int c = (t >= 0.0f) ? (int)t : 0;
+        c = min(c, Tb.nb - 1);
+        const double u = ((double)E.y - (double)cell_centre(g0, h32, c)) / Tb.h;
+        s_c[p] = (fabs(u) <= (double)kULim && E.y == E.y) ? c : -2;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBS / kWave; ++w) tot += s_scan[w];
+        s_n += tot;
+      }
+      __syncthreads();
+      e0 += kBS;
+    }
+    const int ns = s_n;
+    // one cell at a time (smallest unprocessed cell index first)
+    for (;;) {
+      int cmin = INT32_MAX;
+      for (int p = threadIdx.x; p < ns; p += kBS)
+        if (s_c[p] >= 0) cmin = min(cmin, s_c[p]);
+      cmin = -block_max<kBS, int>(-cmin, s_scan);
+      if (cmin == INT32_MAX) break;
+      const double y0 = (double)cell_centre(g0, h32, cmin);
+      const bool okb = band_expand(SB, coef64, y0, Tb.h, s_eb, dred);
+      const bool oka = band_expand(SA, coef64, y0, Tb.h, s_ea, dred);
+      for (int p = threadIdx.x; p < ns; p += kBS) {
+        if (s_c[p] != cmin) continue;
+        const double y = (double)s_y[p];
+        double lb, la;
+        if (okb && oka) {
+          const double u = (y - y0) / Tb.h;
+          lb = band_eval(s_eb, coef64, SB.comp_off, u, y);
+          la = band_eval(s_ea, coef64, SA.comp_off, u, y);
+        } else {
+          lb = band_direct(SB, coef64, y);
+          la = band_direct(SA, coef64, y);
+        }
+        best_update(bx, lb - la, s_i[p], cand_value(s_y[p], lgmm));
+        s_c[p] = -1;
+      }
+      __syncthreads();
+    }
+    // off-grid survivors: the direct sum, one per thread
+    for (int p = threadIdx.x; p < ns; p += kBS) {
+      if (s_c[p] != -2) continue;
+      const double y = (double)s_y[p];
+      best_update(bx, band_direct(SB, coef64, y) - band_direct(SA, coef64, y), s_i[p],
+                  cand_value(s_y[p], lgmm));
+    }
+    __syncthreads();
+  }
+  bx = block_best<kBS>(bx, red);
+  if (threadIdx.x == 0) best[j] = tpe_best{bx.score, bx.index, bx.value, J.n_cand};
 }
 
 // ---------------------------------------------------------------------------
@@ -1255,11 +1595,18 @@ __global__ __launch_bounds__(kBS) void k_score_pruned64(
       const int64_t li = base + i;
       if (INJ) {
         x = cand[J.cand_off + li];
+        y = lgmm ? log(x) : x;
+      } else if (J.flags & TPE_F_DRAW32) {
+        // the table path's fp32 stream (the exact re-score of an overflowed band)
+        const float y32 = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low,
+                                 (float)J.high);
+        y = (double)y32;
+        x = cand_value(y32, lgmm);
       } else {
         x = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
         if (lgmm) x = exp(x);
+        y = lgmm ? log(x) : x;
       }
-      y = lgmm ? log(x) : x;
     }
     s_key[i] = y;
     s_x[i] = x;
@@ -1309,6 +1656,13 @@ __global__ __launch_bounds__(kBS) void k_reduce_t(const tpe_job* __restrict__ jo
   b = block_best<kBS>(b, red);
   if (threadIdx.x == 0)
     best[blockIdx.x] = tpe_best{b.score, b.index, b.value, jobs[blockIdx.x].n_cand};
+}
+
+// scorer blocks (tiles) per job of the fast path: the partial layout
+int64_t tpe_table_fast_tiles(const tpe_job* hj, int n) {
+  int64_t gx = 1;
+  for (int i = 0; i < n; ++i) gx = std::max(gx, (hj[i].n_cand + kTile - 1) / kTile);
+  return gx;
 }
 
 bool check_table_jobs(const char* fn, const tpe_job* hj, int n, bool* inj) {
@@ -1433,10 +1787,10 @@ extern "C" int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, in
 extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                                     const tpe_seg* segs, const double* mu, const double* sigma,
                                     const double* wcdf, const float* coef32,
-                                    const tpe_table* tables, const float* cells,
-                                    double* out_score, double* out_x, tpe_best* partial,
-                                    int64_t n_partial, tpe_best* best, uint64_t* stats,
-                                    void* stream) {
+                                    const tpe_table* tables, const float* cells, tpe_band* band,
+                                    int64_t band_cap, uint32_t* band_ctl, double* out_score,
+                                    double* out_x, tpe_best* partial, int64_t n_partial,
+                                    uint64_t* stats, void* stream) {
   bool inj = false;
   if (!check_table_jobs("tpe_score_table_fast", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
   if (n_jobs == 0) return TPE_OK;
@@ -1444,13 +1798,16 @@ extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_job
     set_error("tpe_score_table_fast: sampled jobs only (injected candidates: tpe_score_table)");
     return TPE_E_ARG;
   }
-  if (!jobs || !segs || !mu || !sigma || !wcdf || !coef32 || !tables || !cells || !partial ||
-      !best) {
+  if (!jobs || !segs || !mu || !sigma || !wcdf || !coef32 || !tables || !cells || !band ||
+      !band_ctl || !partial) {
     set_error("tpe_score_table_fast: null pointer");
     return TPE_E_ARG;
   }
-  int64_t gx = 1;
-  for (int i = 0; i < n_jobs; ++i) gx = std::max(gx, (host_jobs[i].n_cand + kTile - 1) / kTile);
+  if (band_cap < 1 || band_cap > ((int64_t)1 << 31)) {
+    set_error("tpe_score_table_fast: band_cap=%lld", (long long)band_cap);
+    return TPE_E_ARG;
+  }
+  const int64_t gx = tpe_table_fast_tiles(host_jobs, n_jobs);
   if (gx * n_jobs > n_partial) {
     set_error("tpe_score_table_fast: partial workspace %lld < %lld", (long long)n_partial,
               (long long)(gx * n_jobs));
@@ -1463,10 +1820,41 @@ extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_job
   }
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_score_table_fast, dim3((unsigned)(8 * per)), dim3(kBS), 0, st, jobs, segs,
-                     mu, sigma, wcdf, reinterpret_cast<const float4*>(coef32), tables, cells,
-                     out_score, out_x, partial, (unsigned long long*)stats, (int)gx, n_jobs);
-  hipLaunchKernelGGL(k_reduce_t, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
+                     mu, sigma, wcdf, reinterpret_cast<const float4*>(coef32), tables, cells, band,
+                     band_cap, band_ctl, out_score, out_x, partial, (unsigned long long*)stats,
+                     (int)gx, n_jobs);
   return check_launch("tpe_score_table_fast");
+}
+
+extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                const tpe_seg* segs, const double* coef64,
+                                const tpe_table* tables, const tpe_band* band, int64_t band_cap,
+                                uint32_t* band_ctl, const tpe_best* partial, int64_t n_partial,
+                                tpe_best* best, void* stream) {
+  bool inj = false;
+  if (!check_table_jobs("tpe_band_rescore", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  if (inj) {
+    set_error("tpe_band_rescore: sampled jobs only");
+    return TPE_E_ARG;
+  }
+  if (!jobs || !segs || !coef64 || !tables || !band || !band_ctl || !partial || !best) {
+    set_error("tpe_band_rescore: null pointer");
+    return TPE_E_ARG;
+  }
+  if (band_cap < 1 || band_cap > ((int64_t)1 << 31)) {
+    set_error("tpe_band_rescore: band_cap=%lld", (long long)band_cap);
+    return TPE_E_ARG;
+  }
+  const int64_t gx = tpe_table_fast_tiles(host_jobs, n_jobs);
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_band_rescore: partial workspace %lld < %lld", (long long)n_partial,
+              (long long)(gx * n_jobs));
+    return TPE_E_ARG;
+  }
+  hipLaunchKernelGGL(k_band_rescore, dim3(n_jobs), dim3(kBS), 0, (hipStream_t)stream, jobs, segs,
+                     coef64, tables, band, band_cap, band_ctl, partial, gx, best);
+  return check_launch("tpe_band_rescore");
 }
 
 extern "C" int64_t tpe_pruned64_partials(const tpe_job* host_jobs, int n_jobs) {

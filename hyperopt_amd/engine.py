@@ -41,7 +41,7 @@ LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense 
 LAT_PACK_MAX = 1 << 16  # lattice slots of a level initialised through the upload (else memset)
 TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
-LAT_EARLY_MIN_CAND = 1 << 26  # lattice work beside the fit from this many table candidates
+BAND_CAP = 1 << 16  # per job: candidates the table path re-scores exactly (tpe_score_table_fast)
 LAT_PREFIX = 1 << 16  # lattice argmax: candidates drawn before the early decision
 LAT_SUGGEST_MAX_SLOTS = 1 << 10  # ... for lattices of at most this many slots (all scored)
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
@@ -294,11 +294,6 @@ class Engine:
         # where the host issues that categorical work: "pre" (before the fit's
         # launches), "post" (after them), "late" (after the table build)
         self.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
-        # opt-in (TPE_LAT_EARLY=1): quantized labels fitted first and sampled
-        # beside the continuous fit on levels with >= LAT_EARLY_MIN_CAND table
-        # candidates.  Off: the lattice sampler slows the latency-bound fit on
-        # the critical path more than it saves later (C3 0.94 -> 0.96-0.99 ms)
-        self.lat_early = os.environ.get("TPE_LAT_EARLY", "0") == "1"
         # quantized labels of a suggest level: decide the argmax after the first
         # lat_prefix candidates where no unseen lattice value can still win
         # (tpe_lattice_suggest); 0 (TPE_LAT_PREFIX=0): every stream drawn in full
@@ -309,20 +304,8 @@ class Engine:
         # the L2s (~14 us of idle GPU per event on C3 levels).  The host-read
         # "result" event keeps it.  TPE_DEVICE_EVENTS=0: every event system-scope.
         self.device_events = os.environ.get("TPE_DEVICE_EVENTS", "1") == "1"
-        # level graphs (opt-in, TPE_GRAPHS=1): a level whose launch sequence
-        # (kernels, grids, workspace pointers, every scalar argument) repeats
-        # the previous call's is captured into a hipGraph once and replayed
-        # with one hipGraphLaunch (the per-call inputs -- split flags, counts,
-        # Philox keys -- arrive through the level's upload, outside the graph).
-        # Off by default: on ROCm 7 a replayed C3 level is slower than the
-        # eager launches (1.21 vs 1.13 ms on one stream, 1.33 vs 1.06 ms with
-        # the side stream)
-        self.graphs = os.environ.get("TPE_GRAPHS", "0") == "1"
-        self._graphs = {}       # launch key -> _LevelGraph
-        self._last_gkey = None  # launch key of the previous eager level
         self._gen = 0           # bumped whenever a workspace buffer is (re)allocated
-        self._own = None        # the engine's own stream (capture needs a non-null stream)
-        self.graph_stats = {"captured": 0, "replayed": 0, "eager": 0}
+        self.graph_stats = {"eager": 0}  # levels issued eagerly / re-issued ("native", "replay")
         # native level launcher (default; TPE_NATIVE_LAUNCH=0: one ctypes call
         # per entry point): a level whose launch key repeats the previous
         # call's is recorded once as tpe_run_ops records -- upload, every
@@ -344,7 +327,21 @@ class Engine:
             t = self.torch.empty(_align(int(nbytes * 1.25)), dtype=self.torch.uint8,
                                  device=self.device)
             self._bufs[name] = t
-            self._gen += 1  # captured graphs hold the old pointers
+            self._gen += 1  # recorded levels hold the old pointers
+        return t.data_ptr()
+
+    def _zbuf(self, name, nbytes):
+        """A workspace buffer that is zero when (re)allocated (kernels that use
+        it leave it zero again, e.g. the band controls)."""
+        t = self._bufs.get(name)
+        nbytes = max(int(nbytes), 16)
+        if t is None or t.numel() < nbytes:
+            if t is not None:
+                self._retired.append(t)
+            t = self.torch.zeros(_align(int(nbytes * 1.25)), dtype=self.torch.uint8,
+                                 device=self.device)
+            self._bufs[name] = t
+            self._gen += 1
         return t.data_ptr()
 
     def _drop_oplists(self):
@@ -352,11 +349,6 @@ class Engine:
         for o in self._oplists.values():
             o.destroy(self._hip)
         self._oplists.clear()
-
-    def _drop_graphs(self):
-        for g in self._graphs.values():
-            g.destroy(self._hip)
-        self._graphs.clear()
 
     def _ones(self, n):
         """n all-ones uint64 words (cached)."""
@@ -625,19 +617,6 @@ class Engine:
                     (w.n_above if w.obs_above is None else np.size(w.obs_above) for w in works),
                     np.int64, len(works))),)
             cached = self._plans.get(pkey) if pkey is not None else None
-        # graph-eligible levels run on the engine's own stream (ordered after
-        # the caller's): stream capture is not allowed on the null stream
-        graph_ok = self.graphs and pkey is not None and not (
-            outputs or sample_only or posteriors or table_scores)
-        caller_p = None
-        if graph_ok:
-            if self._own is None:
-                self._own = torch.cuda.Stream(self.device)
-            if self._own.cuda_stream != stream.cuda_stream:
-                caller_p = sp
-                stream = self._own
-                sp = ctypes.c_void_p(stream.cuda_stream)
-                self._order("enter", caller_p, sp)
         pack = _Pack()
         if cached is not None:
             cols = (batch.n_below, batch.n_above, batch.keys, batch.cand_base) \
@@ -926,7 +905,7 @@ class Engine:
             o_xslot = pack.add(x_slots[np.asarray(order, np.int64)])
             xbytes = int(x_labels) * BS
         o_res = pack.add(np.zeros(64 + n_jobs * BS + xbytes, np.uint8))
-        native_ok = self.native and not self.graphs and pkey is not None and not (
+        native_ok = self.native and pkey is not None and not (
             outputs or sample_only or posteriors or table_scores)
         base = self._upload(pack, stream, copy=not native_ok)
         d_segs = base + o_segs if o_segs is not None else None
@@ -957,12 +936,12 @@ class Engine:
             d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
         self.last_plan = (segs, csegs, g_arr if hist_mode else None, jobs, cached is not None)
 
-        # ---- the level's launches (eager, captured into a graph, or replayed) ----
+        # ---- the level's launches (eager, or recorded and re-issued) ------------
         # Every argument below is a workspace pointer (unchanged while _gen is),
         # an offset into the staged pack, or a size covered by the launch key;
         # the values that change from call to call live in the uploaded pack.
         gkey = None
-        if graph_ok or native_ok:
+        if native_ok:
             gkey = (pkey, self._gen, sp.value, tuple(off for off, _ in pack.parts), n_obs_total,
                     max_obs,
                     cobs_off, lat_off,
@@ -971,10 +950,11 @@ class Engine:
                     None if exchange is None else
                     (int(x_comm), int(x_labels), int(x_world), x_slots.tobytes()),
                     self.side_stream, self.table_scorer, self.exact64, self.lat_prefix,
-                    self.cat_early, self.cat_issue, self.lat_early,
+                    self.cat_early, self.cat_issue,
                     "off" if timers is None else
                     ("all" if timer_groups is None else frozenset(timer_groups)))
-        cap = None  # _LevelGraph being captured / _OpList being recorded (tick/tock follow it)
+        cap = None  # _OpList being recorded (tick/tock follow it)
+        band_jobs = []  # (first, end) job positions scored by tpe_score_table_fast
 
         def tick(name, on=None):
             if timers is None or (timer_groups is not None and name not in timer_groups):
@@ -1063,6 +1043,7 @@ class Engine:
                 d_sc = self._buf("out_sc", 8 * max(out_off, 1))
                 d_x = self._buf("out_x", 8 * max(out_off, 1))
             table_calls = []
+            band_jobs.clear()
             jobs_ptr = jobs.__array_interface__["data"][0]
             joined = side is None
             side_started = side is None
@@ -1085,8 +1066,7 @@ class Engine:
                     cat_started = True  # the categorical work needs only the gather
                     stream_wait("gathered", side_p)
                     cat_fit()
-                if not side_started and kind in SIDE_KINDS and not (
-                        (cat_early and kind == "cat") or (lat_early and kind == "lat")):
+                if not side_started and kind in SIDE_KINDS and not (cat_early and kind == "cat"):
                     side_started = True  # the side stream's groups that need the fit
                     stream_wait("fitted", side_p)
                     if cat and not cat_early:
@@ -1159,11 +1139,22 @@ class Engine:
                         L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32,
                                                     d_tab, d_cells, d_cand, d_bl, d_al, d_x, d_part,
                                                     npart, db, d_stats, sp), "tpe_score_table")
-                    else:  # the suggest path: one score cubic per candidate
+                    else:  # the suggest path: one score cubic per candidate, exact argmax
+                        d_band = self._buf("band", L.BAND_DTYPE.itemsize * BAND_CAP * nj)
+                        d_bctl = self._zbuf("band_ctl", 8 * nj)
                         L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
-                                                         d_c32, d_tab, d_cells, d_sc, d_x, d_part,
-                                                         npart, db, d_stats, sp),
+                                                         d_c32, d_tab, d_cells, d_band, BAND_CAP,
+                                                         d_bctl, d_sc, d_x, d_part, npart,
+                                                         d_stats, sp),
                                 "tpe_score_table_fast")
+                        tock("table", e0)
+                        e0 = tick("band")
+                        L.check(lib.tpe_band_rescore(dj, hjp, nj, d_segs, d_c64, d_tab, d_band,
+                                                     BAND_CAP, d_bctl, d_part, npart, db, sp),
+                                "tpe_band_rescore")
+                        tock("band", e0)
+                        e0 = None
+                        band_jobs.append((a, b))
                     table_calls.append(nj)
                 elif kind == "pruned64":
                     npart = lib.tpe_pruned64_partials(hjp, nj)
@@ -1238,12 +1229,6 @@ class Engine:
             # delayed, and the table build still reaches the GPU before the
             # fit ends)
             cat_early = side is not None and bool(cat) and self.cat_early
-            lat_g = [g for g, (k, ids) in enumerate(groups) if k == "lat" and ids]
-            n_tab = int(sum(int(jobs["n_cand"][a:b].sum()) for a, b in
-                            (_slice_of(groups, g) for g, (k, ids) in enumerate(groups)
-                             if k == "table" and ids)))
-            lat_early = side is not None and bool(lat_g) and self.lat_early and \
-                n_tab >= LAT_EARLY_MIN_CAND
             if cat_early:
                 stream_rec("gathered", sp)
                 if self.cat_issue == "pre":  # issued before the fit's launches
@@ -1251,27 +1236,11 @@ class Engine:
                         if k == "cat" and ids:
                             launch_group(g, "all")
             # ---- posterior fit ------------------------------------------------------
-            # lat_early (a large level): the quantized labels' mixtures are
-            # fitted first, and their lattice work goes to the side stream
-            # beside the continuous labels' fit (latency-bound: the GPU has
-            # room) instead of beside the table build and scorer
             if fit_ids:
                 e0 = tick("fit")
-                parts = [(0, len(segs))]
-                if lat_early:  # segments: continuous labels first, then quantized
-                    nc2 = 2 * len(cont)
-                    parts = [(nc2, len(segs) - nc2), (0, nc2)]
-                for p0, pn in parts:
-                    if pn:
-                        L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs + p0 * L.SEG_DTYPE.itemsize,
-                                                   pn, max_obs, n_obs_total, d_w, d_mu, d_sig,
-                                                   d_cdf, d_c64, d_c32, d_c32n, d_w32, d_pm, d_sm,
-                                                   sp), "tpe_parzen_fit")
-                    if lat_early and p0 > 0:
-                        stream_rec("fitted_q", sp)
-                        stream_wait("fitted_q", side_p)
-                        for g in lat_g:
-                            launch_group(g, "all")
+                L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs, n_obs_total,
+                                           d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n, d_w32,
+                                           d_pm, d_sm, sp), "tpe_parzen_fit")
                 tock("fit", e0)
 
             if cat and side is None:
@@ -1312,8 +1281,7 @@ class Engine:
                     [(g, "score" if g == early else "all") for g in range(len(groups))
                      if groups[g][0] not in SIDE_KINDS]
             for g, stage in g_order:
-                if not (lat_early and groups[g][0] == "lat"):
-                    launch_group(g, stage)
+                launch_group(g, stage)
 
             if not side_started:  # (no side group: only the categorical posterior)
                 if cat and not cat_early:
@@ -1343,6 +1311,7 @@ class Engine:
                 cap = rec
                 try:
                     rec.table_calls, _ = launch_level(rec)
+                    rec.band_jobs = list(band_jobs)
                 finally:
                     cap = None
                 pin = self._res_pinned(nbytes)
@@ -1366,26 +1335,6 @@ class Engine:
             if ops is None:  # eager: the deferred upload first
                 dst, src, nb = self._staged
                 L.hip_check(self._hip.hipMemcpyAsync(dst, src, nb, L.H2D, sp), "hipMemcpyAsync")
-        graph = self._graphs.get(gkey) if (gkey is not None and graph_ok) else None
-        if graph is None and graph_ok and gkey == self._last_gkey:
-            # the second call in a row with this launch key: capture it
-            cap = _LevelGraph()
-            try:
-                graph = cap.capture(self, sp, launch_level)
-            except L.TpeHipError:  # capture unsupported here: eager from now on
-                self.graphs = False
-                self._drop_graphs()
-                graph = None
-            finally:
-                cap = None
-            if graph is not None and graph.gen == self._gen:
-                if len(self._graphs) >= 8 or any(g.gen != self._gen for g in self._graphs.values()):
-                    self._drop_graphs()
-                self._graphs[gkey] = graph
-                self.graph_stats["captured"] += 1
-            elif graph is not None:  # a buffer grew during the capture: not replayable
-                graph.destroy(self._hip)
-                graph = None
         if ops is not None:
             failed = ctypes.c_int(-1)
             rc = self.lib.tpe_run_ops(ops.ptr, ops.n, ctypes.byref(failed))
@@ -1394,10 +1343,7 @@ class Engine:
                     rc, failed.value, self.lib.tpe_last_error().decode(errors="replace")))
             self.graph_stats["native"] = self.graph_stats.get("native", 0) + 1
             table_calls = ops.table_calls
-        elif graph is not None:
-            L.hip_check(self._hip.hipGraphLaunch(graph.exec, sp), "hipGraphLaunch")
-            self.graph_stats["replayed"] += 1
-            table_calls = graph.table_calls
+            band_jobs = ops.band_jobs
         else:
             table_calls, post = launch_level()
             if post:
@@ -1405,6 +1351,12 @@ class Engine:
             self._last_gkey = gkey
             self.graph_stats["eager"] += 1
         _hmark('score launches')
+        # the exact re-score of a band that overflowed (a plateau of equal fp32
+        # scores; tpe_score_table_fast leaves n_scored = -1): after the readback
+        fix = None
+        if band_jobs:
+            fix = functools.partial(self._band_fix, list(band_jobs), d_segs, max_obs + 1, n_comp,
+                                    sp.value, exchange is not None)
         # ---- results: one device->host copy of the result block into pinned memory
         # (issued by the records themselves on the native path)
         pin = self._res_pinned(nbytes)
@@ -1412,18 +1364,15 @@ class Engine:
             L.hip_check(self._hip.hipMemcpyAsync(pin.data_ptr(), d_res, nbytes, L.D2H, sp),
                         "hipMemcpyAsync")
         after = None
-        timed = ops if ops is not None else graph
-        if timed is not None and timed.timed and timers is not None:
-            after = functools.partial(timed.read_timers, self._hip, timers)
+        if ops is not None and ops.timed and timers is not None:
+            after = functools.partial(ops.read_timers, self._hip, timers)
         if batch is not None:  # queued readback (see _Pending)
             ev = self._event("result")
             if ops is None:
                 L.hip_check(self._hip.hipEventRecord(ev, sp), "hipEventRecord")
-            if caller_p is not None:  # the caller's later work follows this level
-                L.hip_check(self._hip.hipStreamWaitEvent(caller_p, ev, 0), "hipStreamWaitEvent")
             p = self._inflight = _Pending(self, ev, pin, nbytes, np.asarray(order, np.int64),
                                           64 + n_jobs * BS if xbytes else None,
-                                          bool(table_calls), after)
+                                          bool(table_calls), after, fix, jobs)
             if ops is not None and self._oplists.get(gkey) is ops and history is not None:
                 # a recorded level: the next call with the same signature only
                 # rewrites its keys and split flags in the staged pack (_Replay)
@@ -1446,6 +1395,8 @@ class Engine:
             after()
         res_h = pin[:nbytes].numpy().copy()
         best_h = res_h[64:64 + n_jobs * BS].view(L.BEST_DTYPE)
+        if fix is not None:
+            fix(best_h, jobs)
         self.last_exchange = res_h[64 + n_jobs * BS:].view(L.BEST_DTYPE).copy() if xbytes \
             else None
         with torch.cuda.stream(stream):
@@ -1486,6 +1437,41 @@ class Engine:
         _hmark("results")
         return results
 
+
+    def _band_fix(self, band_jobs, d_segs, max_comp, n_comp, stream, exchanged, best_h, jobs):
+        """Jobs of the table path whose band overflowed (n_scored == -1: more
+        than BAND_CAP candidates within the fp32 error bound of the maximum --
+        a plateau of equal scores) are re-scored exactly: their fp32 candidate
+        stream (TPE_F_DRAW32) through tpe_score_pruned64, every candidate in
+        fp64.  Patches ``best_h`` (launch order) in place."""
+        pos = [p for a, b in band_jobs for p in range(a, b) if best_h["n_scored"][p] < 0]
+        if not pos:
+            return
+        if exchanged:
+            raise L.TpeHipError("band overflow on %d label(s) of a level with an in-level "
+                                "exchange: run the level without exchange=" % len(pos))
+        torch, lib = self.torch, self.lib
+        hj = np.ascontiguousarray(jobs[np.asarray(pos)].copy())
+        hj["flags"] |= L.F_DRAW32
+        nj = hj.size
+        dj = torch.from_numpy(hj.view(np.uint8).copy()).to(self.device)
+        npart = lib.tpe_pruned64_partials(hj.ctypes.data, nj)
+        d_part = self._buf("partial_fix", 32 * max(npart, 1))
+        out = torch.empty(nj * L.BEST_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+        sp = ctypes.c_void_p(stream)
+        L.check(lib.tpe_score_pruned64(
+            dj.data_ptr(), hj.ctypes.data, nj, d_segs, self._bufs["mu"].data_ptr(),
+            self._bufs["sigma"].data_ptr(), self._bufs["wcdf"].data_ptr(),
+            self._bufs["coef64"].data_ptr(), max_comp, self._buf("reach_hi", 8 * n_comp),
+            self._buf("reach_lo", 8 * n_comp), self._buf("wide_idx", 4 * n_comp),
+            self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp)),
+            self._buf("tables_fix", L.TABLE_DTYPE.itemsize * nj), None, None, None, None,
+            d_part, npart, out.data_ptr(), sp), "tpe_score_pruned64 (band overflow)")
+        L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
+        res = out.cpu().numpy().view(L.BEST_DTYPE)
+        for k, p in enumerate(pos):
+            best_h[p] = res[k]
+        self.band_overflows = getattr(self, "band_overflows", 0) + len(pos)
 
     def _read_posteriors(self, works, fit_ids, cat, segs, csegs, n_comp, n_p, d_segs, stream,
                          o_p):
@@ -1529,9 +1515,11 @@ class _Pending(object):
     with defer=True).  ``result()`` waits for it once, checks the error bits
     and returns the BatchResult (cached)."""
 
-    def __init__(self, eng, event, pin, nbytes, order, xoff, table, after=None):
+    def __init__(self, eng, event, pin, nbytes, order, xoff, table, after=None, fix=None,
+                 jobs=None):
         self.eng, self.event, self.pin, self.nbytes = eng, event, pin, nbytes
         self.order, self.table, self.after = order, table, after
+        self.fix, self.jobs = fix, jobs  # band overflow re-score (Engine._band_fix)
         self.xoff = xoff  # offset of the exchanged label records (Engine.run exchange=)
         self._res = None
 
@@ -1556,6 +1544,8 @@ class _Pending(object):
         _raise_errors(err)
         n = self.order.size
         best_h = res_h[64:64 + n * L.BEST_DTYPE.itemsize].view(L.BEST_DTYPE)
+        if self.fix is not None:
+            self.fix(best_h, self.jobs)
         eng.last_exchange = res_h[self.xoff:].view(L.BEST_DTYPE).copy() \
             if self.xoff is not None else None
         by = np.empty(n, L.BEST_DTYPE)
@@ -1583,6 +1573,7 @@ class _Replay(object):
         self.host = host
         self.order = pending.order
         self.nbytes, self.xoff, self.table = pending.nbytes, pending.xoff, pending.table
+        self.fix = pending.fix
         self.res_pin = res_pin
 
     @staticmethod
@@ -1591,7 +1582,7 @@ class _Replay(object):
                   table_scores, exchange):
         if (history is None or rows is not None or histories is not None or outputs
                 or sample_only or posteriors or table_scores or stream is None
-                or not eng.native or eng.graphs):
+                or not eng.native):
             return None  # (stream: the caller's current stream handle; None: given explicitly)
         if scorer is None:
             scorer = "auto" if pruned else "dense"
@@ -1631,7 +1622,7 @@ class _Replay(object):
         if self.ops.timed and timers is not None:
             after = functools.partial(self.ops.read_timers, eng._hip, timers)
         p = eng._inflight = _Pending(eng, eng._event("result"), self.res_pin, self.nbytes, oi,
-                                     self.xoff, self.table, after)
+                                     self.xoff, self.table, after, self.fix, self.jobs)
         return p if defer else p.result()
 
     @staticmethod
@@ -1640,8 +1631,8 @@ class _Replay(object):
 
 
 class _Timed(object):
-    """A kernel-group duration read from a replayed level graph's event
-    nodes, in the shape of Engine.run's (start, end) timer pairs:
+    """A kernel-group duration read from a re-issued level's event records,
+    in the shape of Engine.run's (start, end) timer pairs:
     ``pair[0].elapsed_time(pair[1])`` gives milliseconds."""
     __slots__ = ("ms",)
 
@@ -1729,81 +1720,6 @@ class _OpList(_Timing):
     def destroy(self, hip):
         for h in self.events:
             hip.hipEventDestroy(h)
-        self.events = []
-
-
-class _LevelGraph(_Timing):
-    """One level's launch sequence captured into a hipGraph (Engine.run).
-
-    Captured from the launches of a level whose launch key repeats (the
-    kernels, grids, workspace pointers and scalar arguments are then equal),
-    replayed by one hipGraphLaunch after the level's upload.  Timer groups
-    become external event-record nodes; their durations are read after the
-    level's readback (``read_timers``)."""
-    __slots__ = ("exec", "graph", "gen", "table_calls", "timed", "events")
-
-    def __init__(self):
-        self.exec = self.graph = None
-        self.gen = -1
-        self.table_calls = []
-        self.timed = []   # (group, start event, end event) recorded by graph nodes
-        self.events = []
-
-    def record(self, hip, stream):
-        """A timing event recorded by a node of the graph being captured on
-        `stream`: the node is added to the capture's graph after the stream's
-        current dependencies and becomes the stream's only dependency (HIP
-        captures a plain hipEventRecord as an ordering edge only, and refuses
-        hipEventRecordExternal during capture)."""
-        h = self._new_event(hip)
-        sp = ctypes.c_void_p(stream.cuda_stream)
-        status, cid, graph = ctypes.c_int(), ctypes.c_ulonglong(), ctypes.c_void_p()
-        deps, n_deps = ctypes.POINTER(ctypes.c_void_p)(), ctypes.c_size_t()
-        L.hip_check(hip.hipStreamGetCaptureInfo_v2(sp, ctypes.byref(status), ctypes.byref(cid),
-                                                   ctypes.byref(graph), ctypes.byref(deps),
-                                                   ctypes.byref(n_deps)),
-                    "hipStreamGetCaptureInfo_v2")
-        node = ctypes.c_void_p()
-        L.hip_check(hip.hipGraphAddEventRecordNode(ctypes.byref(node), graph, deps, n_deps.value,
-                                                   h), "hipGraphAddEventRecordNode")
-        L.hip_check(hip.hipStreamUpdateCaptureDependencies(sp, ctypes.byref(node), 1,
-                                                           L.CAPTURE_SET_DEPENDENCIES),
-                    "hipStreamUpdateCaptureDependencies")
-        return h
-
-    def capture(self, eng, sp, launch):
-        hip = eng._hip
-        gen0 = eng._gen
-        L.hip_check(hip.hipStreamBeginCapture(sp, L.CAPTURE_RELAXED), "hipStreamBeginCapture")
-        g = ctypes.c_void_p()
-        try:
-            self.table_calls, _ = launch()
-        except BaseException:
-            hip.hipStreamEndCapture(sp, ctypes.byref(g))
-            if g.value:
-                hip.hipGraphDestroy(g)
-            hip.hipGetLastError()  # the failed capture's status is not the next launch's
-            self.destroy(hip)
-            raise
-        L.hip_check(hip.hipStreamEndCapture(sp, ctypes.byref(g)), "hipStreamEndCapture")
-        self.graph = g
-        e = ctypes.c_void_p()
-        rc = hip.hipGraphInstantiate(ctypes.byref(e), g, None, None, 0)
-        if rc != 0:
-            self.destroy(hip)
-            L.hip_check(rc, "hipGraphInstantiate")
-        self.exec = e
-        self.gen = gen0 if eng._gen == gen0 else -1
-        return self
-
-    def destroy(self, hip):
-        if self.exec is not None:
-            hip.hipGraphExecDestroy(self.exec)
-        if self.graph is not None:
-            hip.hipGraphDestroy(self.graph)
-        for h in self.events:
-            hip.hipEventDestroy(h)
-        self.exec = self.graph = None
         self.events = []
 
 

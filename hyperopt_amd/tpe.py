@@ -360,7 +360,9 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
             # (whole labels, or candidate ranges when labels < ranks) and the
             # winners are combined across ranks (hyperopt_amd/dist.py)
             units = hdist.plan_units([domain.specs[lab].kind for lab in level], n_ei, ws)[rank]
-            if obs.device and _space_sig(domain) is not None:
+            if not units:  # more ranks than shards of this level: nothing here, but
+                res = []   # the rank still joins the winners' all-gather below
+            elif obs.device and _space_sig(domain) is not None:
                 res = _level_batch(eng, domain, obs, level, units, seed, n_ei, col,
                                    prior_weight, linear_forgetting, prec)
             else:

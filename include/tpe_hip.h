@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 13
+#define TPE_ABI_VERSION 14
 
 enum {
   TPE_OK = 0,
@@ -52,12 +52,14 @@ enum {
   TPE_F_DRAW32 = 16,    /* sampled quantized job: draw in fp32 (set only when
                            every lattice index |k| <= 2^12, so fp32 resolves a
                            slot to < 2^-11 of q)                              */
-  TPE_F_LATTICE_READY = 32 /* lattice job: the caller has already set its
+  TPE_F_LATTICE_READY = 32, /* lattice job: the caller has already set its
                            slot_first region [lat_off, lat_off + lat_n) to
                            all-ones and its `counts` entry to 0 (e.g. in the
                            level's upload); when every job of a
                            tpe_lattice_sample / tpe_lattice_compact call has
                            it, those calls skip their memsets               */
+  /* (TPE_F_DRAW32 on an unquantized job: the fp32 candidate stream -- the
+     table path's -- scored exactly by tpe_score_pruned64)                   */
 };
 
 /*
@@ -288,7 +290,9 @@ typedef struct tpe_table {
   float inv_h, inv_w;   /* 1/h and 1/(2h)                                    */
   int32_t nb;           /* cells used (<= job.tbl_cap)                       */
   int32_t n_wide_below, n_wide_above;
-  int32_t pad;
+  float slope;          /* max over unflagged cells of |c1| + 2.1|c2| + 3.31|c3|:
+                           a bound of |df/du| on |u| <= 1.05 (score cubics),
+                           written by tpe_table_build                        */
   double T_below, T_above; /* log-term floor: components whose term stays
                               below it on a cell are left out               */
 } tpe_table;
@@ -309,21 +313,53 @@ int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                     const float* cells, const double* cand, double* out_bl, double* out_al,
                     double* out_x, tpe_best* partial, int64_t n_partial, tpe_best* best,
                     uint64_t* stats, void* stream);
-/* The suggest path (sampled jobs only): the same draws and argmax as
- * tpe_score_table, each candidate scored by its cell's score cubic -- one
- * 16-B load and three FMAs -- or, on a flagged cubic, by the two-polynomial
- * cell, then the exact log-sum-exp.  out_score / out_x (nullable): the
- * per-candidate score (below - above log-density) and value at job.out_off.
- * Partial workspace: tpe_table_partials(). */
+/* The suggest path (sampled jobs only), in two calls.
+ * tpe_score_table_fast: the same draws as tpe_score_table; each candidate is
+ * scored by its cell's score cubic -- one 16-B load and three FMAs -- or, on a
+ * flagged cubic, by the two-polynomial cell, then the exact fp32
+ * log-sum-exp.  Writes the per-block fp32 winners to `partial` and the band.
+ * tpe_band_rescore: the winner decided EXACTLY -- np.argmax (tpe.py:649-658)
+ * over the fp64 scores of every candidate that can still be the maximum.
+ *
+ * Band.  With eps(s) the bound of |s32 - s64| (polynomial
+ * 1.0e-6 per mixture, cubic fit, fp32 rounding), candidate i can be the exact
+ * winner only if s32_i + eps_i >= G := max_k (s32_k - eps_k).  Each scorer
+ * block publishes its best s32_k - eps_k into band_ctl (atomic max) and
+ * appends its candidates with s32 + eps >= the maximum known so far to
+ * `band`; tpe_band_rescore keeps those with s32 + eps >= the final G and
+ * re-scores them in fp64 -- per table cell, a degree-24 expansion of both
+ * mixtures around the cell centre over every component within e^-45 of the
+ * sum (components whose series would converge slowly summed term by term) --
+ * and takes the np.argmax winner (largest score, then smallest index):
+ * best[j] = {fp64 score, index, value (x, or exp(y) in fp64 for LGMM1),
+ * n_cand}.  A job whose band got more than band_cap entries (a plateau of
+ * near-equal scores) keeps the fp32 winner with n_scored = -1: the caller
+ * re-scores it exactly (tpe_score_pruned64 with TPE_F_DRAW32).
+ * band: band_cap entries per job; band_ctl: 2 uint32 per job, zero before
+ * the first call -- tpe_band_rescore leaves them zero again.  Both calls take
+ * the same job list and partial workspace (tpe_table_partials()).
+ * out_score / out_x (nullable, tests): the per-candidate fp32 score and value
+ * at job.out_off. */
+typedef struct tpe_band {
+  int64_t index;        /* global candidate index                            */
+  float y;              /* candidate in the scoring coordinate (fp32 draw)   */
+  float hi;             /* s32 + eps: upper bound of its exact score          */
+} tpe_band;
 int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                          const tpe_seg* segs, const double* mu, const double* sigma,
                          const double* wcdf, const float* coef32, const tpe_table* tables,
-                         const float* cells, double* out_score, double* out_x,
-                         tpe_best* partial, int64_t n_partial, tpe_best* best, uint64_t* stats,
-                         void* stream);
+                         const float* cells, tpe_band* band, int64_t band_cap,
+                         uint32_t* band_ctl, double* out_score, double* out_x, tpe_best* partial,
+                         int64_t n_partial, uint64_t* stats, void* stream);
+int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                     const tpe_seg* segs, const double* coef64, const tpe_table* tables,
+                     const tpe_band* band, int64_t band_cap, uint32_t* band_ctl,
+                     const tpe_best* partial, int64_t n_partial, tpe_best* best, void* stream);
 
 /* ---- continuous candidates, exact fp64 with pruning (parity mode) ----------
- * Same results as tpe_score_continuous(precision=64) up to fp64 rounding: the
+ * Same results as tpe_score_continuous(precision=64) up to fp64 rounding (a
+ * sampled job with TPE_F_DRAW32 scores the fp32 stream of the table path
+ * instead -- the exact re-score of a job whose band overflowed): the
  * plan of tpe_table_build (with an e^-40 exclusion margin and the fp64
  * sampler's |z| < 8.7 range) finds, per mixture, the components whose term
  * can reach e^-40 of the sum somewhere on the candidate range, with reach
@@ -475,6 +511,7 @@ enum {
   TPE_OP_BEST_SCATTER,         /* tpe_best_scatter                           */
   TPE_OP_MAXLOC_ALLREDUCE,     /* tpe_maxloc_allreduce (RCCL, stream-ordered) */
   TPE_OP_LATTICE_SUGGEST,      /* tpe_lattice_suggest                        */
+  TPE_OP_BAND_RESCORE,         /* tpe_band_rescore                           */
   TPE_OP_COUNT
 };
 #define TPE_OP_ARGS 23

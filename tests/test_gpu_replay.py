@@ -1,14 +1,13 @@
 """Replayed levels (Engine.run): a level whose launch key repeats is
-recorded on its second call and replayed afterwards -- by the native level
-launcher (default: tpe_run_ops records, csrc/tpe_ops.hip) or as a captured
-hipGraph (opt-in TPE_GRAPHS=1).
+recorded on its second call and re-issued afterwards by the native level
+launcher (tpe_run_ops records, csrc/tpe_ops.hip).
 
 The per-call inputs (split flags, observation counts, Philox keys) travel in
-the level's upload, outside the graph, so a replayed level must give exactly
+the level's upload, outside the records, so a replayed level must give exactly
 what an eager engine gives on the same inputs: every label's winner index,
 value, score and n_scored, byte for byte, for every prior kind and scorer
 path.  A changed history (new counts), a grown workspace buffer or another
-structure must never replay a stale graph.
+structure must never replay stale records.
 """
 import numpy as np
 import pytest
@@ -54,57 +53,55 @@ def _rows(res):
     return [(r.label, r.index, r.value, r.score, r.n_scored) for r in res]
 
 
-MODES = ["native", "graph"]
+MODES = ["native"]
 
 
 def _pair(mode):
     from hyperopt_amd.engine import DeviceHistory, Engine
-    eager, graph = Engine(), Engine()
-    eager.graphs = eager.native = False
-    graph.graphs, graph.native = mode == "graph", mode == "native"
-    return eager, graph, DeviceHistory
+    eager, native = Engine(), Engine()
+    eager.native = False
+    native.native = True
+    return eager, native, DeviceHistory
 
 
 def _replays(eng):
-    """(recorded, replayed-or-re-issued, eager) level counts."""
+    """(recorded, re-issued, eager) level counts."""
     st = eng.graph_stats
-    if eng.native:
-        return len(eng._oplists), st.get("native", 0), st["eager"]
-    return st["captured"], st["replayed"], st["eager"]
+    return len(eng._oplists), st.get("native", 0), st["eager"]
 
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("n_cand", [24, 1 << 18])
 def test_replayed_level_equals_eager(n_cand, mode):
-    eager, graph, DeviceHistory = _pair(mode)
+    eager, native, DeviceHistory = _pair(mode)
     mat, active, losses = _history(3000, 11)
     he = DeviceHistory(eager, len(SPACE), cap=4096)
-    hg = DeviceHistory(graph, len(SPACE), cap=4096)
+    hg = DeviceHistory(native, len(SPACE), cap=4096)
     for h in (he, hg):
         h.append(mat, active)
-    for step in range(6):  # new Philox keys every call, same counts: graph hits
+    for step in range(6):  # new Philox keys every call, same counts: recorded, then re-issued
         works, isb = _works(mat, active, losses, 3000, step, n_cand)
         a = eager.run(works, history=he, is_below=isb)
-        b = graph.run(works, history=hg, is_below=isb)
+        b = native.run(works, history=hg, is_below=isb)
         assert _rows(a) == _rows(b), step
     # the first call sizes the workspace, a call whose key repeats the previous
     # one's is recorded, every later call replays
-    cap, rep, eag = _replays(graph)
+    cap, rep, eag = _replays(native)
     assert cap == 1 and rep >= 4 and eag + rep == 6, (cap, rep, eag)
     # the winners moved with the keys (the replay did not reuse old inputs)
     idx = set()
     for s in (10, 11):
         works, isb = _works(mat, active, losses, 3000, s, n_cand)
-        idx.add(tuple(r[1] for r in _rows(graph.run(works, history=hg, is_below=isb))))
+        idx.add(tuple(r[1] for r in _rows(native.run(works, history=hg, is_below=isb))))
     assert len(idx) == 2
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_growing_history_never_replays_stale_graph(mode):
-    eager, graph, DeviceHistory = _pair(mode)
+def test_growing_history_never_replays_stale_records(mode):
+    eager, native, DeviceHistory = _pair(mode)
     mat, active, losses = _history(2400, 5)
     he = DeviceHistory(eager, len(SPACE), cap=512)
-    hg = DeviceHistory(graph, len(SPACE), cap=512)
+    hg = DeviceHistory(native, len(SPACE), cap=512)
     T = 400
     for h in (he, hg):
         h.append(mat[:T], active[:T])
@@ -112,48 +109,48 @@ def test_growing_history_never_replays_stale_graph(mode):
         works, isb = _works(mat, active, losses, T, step, 1 << 16)
         for _ in range(3):  # three calls per history size: capture, then replay
             a = eager.run(works, history=he, is_below=isb)
-            b = graph.run(works, history=hg, is_below=isb)
+            b = native.run(works, history=hg, is_below=isb)
             assert _rows(a) == _rows(b), (step, T)
         # more trials (the history buffers grow past their capacity too)
         for h in (he, hg):
             h.append(mat[T:T + 250], active[T:T + 250])
         T += 250
-    cap, rep, eag = _replays(graph)
+    cap, rep, eag = _replays(native)
     assert rep >= 8, (cap, rep, eag)
 
 
 @pytest.mark.parametrize("mode", MODES)
 def test_other_structure_between_replays(mode):
     """A larger level in between grows the workspace (new pointers): the
-    first structure's graph is dropped and re-captured, never replayed stale."""
-    eager, graph, DeviceHistory = _pair(mode)
+    first structure's records are dropped and re-recorded, never replayed stale."""
+    eager, native, DeviceHistory = _pair(mode)
     mat, active, losses = _history(3000, 2)
     he = DeviceHistory(eager, len(SPACE), cap=4096)
-    hg = DeviceHistory(graph, len(SPACE), cap=4096)
+    hg = DeviceHistory(native, len(SPACE), cap=4096)
     for h in (he, hg):
         h.append(mat, active)
     for step, n_cand in enumerate([1 << 14, 1 << 14, 1 << 14, 1 << 20, 1 << 20, 1 << 14,
                                    1 << 14, 1 << 14]):
         works, isb = _works(mat, active, losses, 3000, step, n_cand)
         a = eager.run(works, history=he, is_below=isb)
-        b = graph.run(works, history=hg, is_below=isb)
+        b = native.run(works, history=hg, is_below=isb)
         assert _rows(a) == _rows(b), step
 
 
 @pytest.mark.parametrize("mode", MODES)
 def test_timers_of_replayed_levels(mode):
     """Timer groups inside a replayed level are event records of its own
-    (graph nodes / tpe_run_ops records): their durations are read after the
+    (tpe_run_ops records): their durations are read after the
     level and look like kernel times."""
-    _, graph, DeviceHistory = _pair(mode)
+    _, native, DeviceHistory = _pair(mode)
     mat, active, losses = _history(3000, 4)
-    hg = DeviceHistory(graph, len(SPACE), cap=4096)
+    hg = DeviceHistory(native, len(SPACE), cap=4096)
     hg.append(mat, active)
     timers = {}
     for step in range(5):
         works, isb = _works(mat, active, losses, 3000, step, 1 << 20)
-        graph.run(works, history=hg, is_below=isb, timers=timers, timer_groups={"table"})
-    cap, rep, eag = _replays(graph)
+        native.run(works, history=hg, is_below=isb, timers=timers, timer_groups={"table"})
+    cap, rep, eag = _replays(native)
     assert rep >= 3 and eag + rep == 5, (cap, rep, eag)
     ms = [a.elapsed_time(b) for a, b in timers["table"]]
     assert len(ms) == 5
@@ -236,19 +233,14 @@ def test_level_replay_equals_eager():
     assert native.graph_stats.get("replay", 0) >= 3, native.graph_stats
 
 
-@pytest.mark.parametrize("variant", ["lat_early", "cat_pre", "cat_late", "cat_off"])
-def test_issue_orders_give_the_same_level(variant, monkeypatch):
+@pytest.mark.parametrize("variant", ["cat_pre", "cat_late", "cat_off"])
+def test_issue_orders_give_the_same_level(variant):
     """The side-stream issue variants (categorical work issued before the fit /
-    after it / after the table build / after the fit with the quantized work;
-    lattice work beside the continuous fit) only move launches between
-    streams and in time: every label's winner equals the default engine's."""
-    from hyperopt_amd import engine as E
-    monkeypatch.setattr(E, "LAT_EARLY_MIN_CAND", 0)
+    after it / after the table build / after the fit with the quantized work)
+    only move launches between streams and in time: every label's winner
+    equals the default engine's."""
     base, other, DeviceHistory = _pair("native")
-    base.native = True
-    if variant == "lat_early":
-        other.lat_early = True
-    elif variant == "cat_off":
+    if variant == "cat_off":
         other.cat_early = False
     else:
         other.cat_issue = variant.split("_")[1]
