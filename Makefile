@@ -2,7 +2,7 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := hyperopt_amd/csrc
-SRCS := $(CSRC)/tpe_fit.hip $(CSRC)/tpe_parzen.hip $(CSRC)/tpe_score.hip $(CSRC)/tpe_table.hip $(CSRC)/tpe_history.hip $(CSRC)/tpe_prior.hip $(CSRC)/tpe_dist.hip $(CSRC)/tpe_util.hip $(CSRC)/tpe_ops.hip
+SRCS := $(CSRC)/tpe_fit.hip $(CSRC)/tpe_parzen.hip $(CSRC)/tpe_score.hip $(CSRC)/tpe_table.hip $(CSRC)/tpe_history.hip $(CSRC)/tpe_sorted.hip $(CSRC)/tpe_prior.hip $(CSRC)/tpe_dist.hip $(CSRC)/tpe_util.hip $(CSRC)/tpe_ops.hip
 OBJS := $(SRCS:.hip=.o)
 LIB := hyperopt_amd/libtpe_hip.so
 # -ffp-contract=off: no implicit FMA fusion, so expressions written to

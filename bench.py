@@ -245,6 +245,42 @@ def cpu_baseline(space, vals, losses, n=20480, workers=64):
             "label_parallel": multi}
 
 
+def append_steps(eng, space, mat, hist, losses, n_cand, units, steps=20, warmup=3):
+    """The engine step with the history growing by one trial per step, as an
+    fmin loop grows it: each step appends a trial (a prior draw, N(0,1) loss)
+    to the HBM history, and the level merges it into the sorted orders
+    (tpe_history_order), re-splits and re-fits -- so the incremental-sort
+    cache is paid for inside the timed region.  p50 / mean per step."""
+    import torch
+    rng = np.random.RandomState(11)
+    T0, n = mat.shape[0], warmup + steps
+    big = np.empty((T0 + n, mat.shape[1]))
+    big[:T0] = mat
+    lo = np.empty(T0 + n)
+    lo[:T0] = losses
+    extra = [mat[i] for i in rng.randint(T0, size=n)]  # the new trials (prior draws)
+    new_loss = rng.normal(size=n)
+    times = []
+    for k in range(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        T = T0 + k + 1
+        big[T - 1] = extra[k]
+        lo[T - 1] = new_loss[k]
+        hist.append(big[T - 1:T])
+        rb = below_rows(lo[:T])
+        isb = np.zeros(T, np.uint8)
+        isb[rb] = 1
+        works = history_batch(space, big[:T], hist, rb, 5000 + k, n_cand, 0, units, n_cand)
+        eng.run(works, precision=32, history=hist, is_below=isb)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = np.array(times[warmup:]) * 1e3
+    return {"p50_ms": float(np.median(t)), "mean_ms": float(t.mean()), "steps": int(t.size),
+            "config": "C3 engine step, history + 1 trial per step (append, sorted-order merge, "
+                      "split, fit, score)"}
+
+
 def readme_suggest_p50():
     """Config C1 (BASELINE configs[0]): the README space, fmin(max_evals=100,
     n_EI_candidates=24, rstate=RandomState(3)) through the drop-in API; p50 of
@@ -665,6 +701,7 @@ def main():
                             "note": "exact fp64 scoring of every label: component-pruned "
                                     "k_score_pruned64 for the 10k-component above mixtures "
                                     "(e^-40 margin), dense k_score64 for smaller ones"}
+        line["append_step"] = append_steps(eng, space, mat, hist, losses, n_cand, units)
         line["dropin_suggest"] = dropin_suggest_p50(space, vals, losses, n_cand)
         line["readme_suggest"] = readme_suggest_p50()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

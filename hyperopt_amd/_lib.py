@@ -52,6 +52,7 @@ HISTORY_DTYPE = np.dtype([
 BEST_DTYPE = np.dtype([("score", "<f8"), ("index", "<i8"), ("value", "<f8"),
                        ("n_scored", "<i8")], align=True)
 BAND_DTYPE = np.dtype([("index", "<i8"), ("y", "<f4"), ("hi", "<f4")], align=True)
+COLSPEC_DTYPE = np.dtype([("col", "<i4"), ("transform", "<i4"), ("floor", "<f8")], align=True)
 PRIOR_DTYPE = np.dtype([("kind", "<i4"), ("n_cat", "<i4"), ("a", "<f8"), ("b", "<f8"),
                         ("q", "<f8"), ("p_off", "<i8"), ("key", "<u8")], align=True)
 OP_ARGS = 23
@@ -68,6 +69,8 @@ OP_CODES["tpe_best_scatter"] = OP_STREAM_SYNC + 1
 OP_CODES["tpe_maxloc_allreduce"] = OP_STREAM_SYNC + 2
 OP_CODES["tpe_lattice_suggest"] = OP_STREAM_SYNC + 3
 OP_CODES["tpe_band_rescore"] = OP_STREAM_SYNC + 4
+OP_CODES["tpe_fit_sorted"] = OP_STREAM_SYNC + 5
+OP_CODES["tpe_history_order"] = OP_STREAM_SYNC + 6
 PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
     PRIOR_CATEGORICAL = range(6)
 
@@ -99,6 +102,11 @@ _SIGNATURES = {
     "tpe_score_table_fast": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P,
                                   _P, _I64, _P, _P]),
     "tpe_band_rescore": (_I, [_P, _P, _I, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]),
+    "tpe_history_order_scratch_bytes": (_I64, [_I, _I64]),
+    "tpe_history_order": (_I, [_P, _I64, _P, _P, _I, _I64, _I64, _P, _P, _P]),
+    "tpe_fit_sorted_scratch_bytes": (_I64, [_I, _I64]),
+    "tpe_fit_sorted": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P,
+                            _P, _P, _P]),
     "tpe_pruned64_partials": (_I64, [_P, _I]),
     "tpe_score_pruned64": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P,
                                 _P, _P, _P, _I64, _P, _P]),
@@ -180,11 +188,12 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    sizes = (ctypes.c_int32 * 9)()
-    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 9)
+    sizes = (ctypes.c_int32 * 11)()
+    lib.tpe_struct_sizes(ctypes.cast(sizes, _P), 11)
     want = (SEG_DTYPE.itemsize, CAT_SEG_DTYPE.itemsize, JOB_DTYPE.itemsize, BEST_DTYPE.itemsize,
             TABLE_DTYPE.itemsize, GATHER_DTYPE.itemsize, HISTORY_DTYPE.itemsize,
-            PRIOR_DTYPE.itemsize, OP_DTYPE.itemsize)
+            PRIOR_DTYPE.itemsize, OP_DTYPE.itemsize, BAND_DTYPE.itemsize,
+            COLSPEC_DTYPE.itemsize)
     if lib.tpe_abi_version() != ABI_VERSION:
         raise ImportError("hyperopt_amd: libtpe_hip.so ABI %d, expected %d (rebuild with make)"
                           % (lib.tpe_abi_version(), ABI_VERSION))

@@ -33,9 +33,12 @@ struct U4 {
   uint32_t x, y, z, w;
 };
 
+#ifndef TPE_PHILOX_ROUNDS  // diagnostic builds only (tools/diag_variants.sh): 10 in the product
+#define TPE_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < TPE_PHILOX_ROUNDS; ++r) {
     // 64-bit products: one v_mad_u64_u32 per multiply gives both halves
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
@@ -187,6 +190,25 @@ __device__ __forceinline__ double lognormal_cdf_logx(double logx, double mu, dou
   const double bottom = fmax(__dmul_rn(kSqrt2, sigma), kEps);
   const double z = (logx - mu) / bottom;
   return __dadd_rn(0.5, __dmul_rn(0.5, erf(z)));
+}
+
+// total order of (value) used by the fit's sorts: ascending, -0.0 == +0.0, NaN
+// last (np.sort / np.argsort put NaN last)
+__device__ __forceinline__ uint64_t order_key(double v) {
+  if (v != v) return ~0ull - 1;
+  if (v == 0.0) v = 0.0;
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+
+// the fit's observation transform (ap_*_sampler, tpe.py:506-572): log of
+// np.maximum(obs, floor) for the log-domain priors (NaN stays NaN)
+__device__ __forceinline__ double obs_transform(double v, int transform, double floor) {
+  if (transform == TPE_OBS_LOG) {
+    if (v < floor) v = floor;
+    v = log(v);
+  }
+  return v;
 }
 
 // float -> ordered position inside a 64-lane wave's work split

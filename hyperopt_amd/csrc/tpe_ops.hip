@@ -86,6 +86,8 @@ int run_one(const tpe_op& op) {
     TPE_CALL(TPE_OP_MAXLOC_ALLREDUCE, tpe_maxloc_allreduce);
     TPE_CALL(TPE_OP_LATTICE_SUGGEST, tpe_lattice_suggest);
     TPE_CALL(TPE_OP_BAND_RESCORE, tpe_band_rescore);
+    TPE_CALL(TPE_OP_FIT_SORTED, tpe_fit_sorted);
+    TPE_CALL(TPE_OP_HISTORY_ORDER, tpe_history_order);
 #undef TPE_CALL
     case TPE_OP_EVENT_RECORD:
       return runtime(hipEventRecord((hipEvent_t)ptr(op.a[0]),

@@ -72,15 +72,6 @@ __host__ __device__ __forceinline__ int64_t scratch_bytes(int n_seg, int max_obs
          8 * (int64_t)n_seg * comp_tiles(max_obs) * kPartStride;
 }
 
-// total order of (value) used by the sort: ascending, -0.0 == +0.0, NaN last
-// (np.sort / np.argsort put NaN last)
-__device__ __forceinline__ uint64_t order_key(double v) {
-  if (v != v) return ~0ull - 1;
-  if (v == 0.0) v = 0.0;
-  const uint64_t b = (uint64_t)__double_as_longlong(v);
-  return (b >> 63) ? ~b : (b | (1ull << 63));
-}
-
 // number of entries < key (lower) / <= key (upper) in sorted a[0, n)
 __device__ __forceinline__ int count_lt(const uint64_t* a, int n, uint64_t key) {
   int lo = 0, hi = n;

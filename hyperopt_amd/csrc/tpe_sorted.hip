@@ -1,0 +1,520 @@
+// tpe_sorted.hip -- the Parzen fit from a sorted, HBM-resident history.
+//
+// adaptive_parzen_normal (hyperopt/tpe.py:399-467) sorts each label's below /
+// above observations on every suggest.  Both sets are subsets of the label's
+// whole history, and a stable sort of a subset is the whole history's stable
+// order with the other rows removed.  So the history keeps, per label column,
+// its rows sorted by (transformed value, row) -- updated when trials are
+// appended (tpe_history_order: the new rows sorted in LDS, then merged into
+// the existing order, O(T) per append instead of O(T log T) per suggest) --
+// and a suggest's fit is one kernel per segment (tpe_fit_sorted):
+//
+//   1. rows in row (tid) order: which belong to the segment (active for the
+//      label, on its side of the split), each one's position in the segment's
+//      tid-ordered list (the linear-forgetting ramp follows it, tpe.py:441-447)
+//      and how many lie below the prior mean (its searchsorted 'left' slot,
+//      tpe.py:427; the len == 1 rule of tpe.py:414-421);
+//   2. the column's sorted order compacted to the segment: means and ramp
+//      weights in sorted order, the prior inserted at its slot;
+//   3. bandwidths and clip (tpe.py:430-459), normalisation, p_accept
+//      (tpe.py:145-150), fp64 / fp32 coefficients and cumulative weights --
+//      the arithmetic of k_fit_comp / k_fit_coef / k_fit_coef32 in
+//      tpe_parzen.hip, with its reduction order (256-component tiles, the
+//      same wave butterflies and tile folds), so both fits give the same bits.
+//
+// Rows are ordered by (key(transform(v)), row): row order is tid order for an
+// identity row list, and ties keep tid order -- np.argsort(kind="stable") of
+// the reference's list (tie semantics).
+#include <algorithm>
+
+#include "tpe_common.hpp"
+
+namespace tpe {
+namespace {
+constexpr int kSB = 1024;            // block size of every kernel here
+constexpr int kSWaves = kSB / kWave;
+constexpr int kNew = 2048;           // new rows sorted per tpe_history_order call
+constexpr int kTileF = 256;          // reduction tile of the multi-kernel fit (kFitBS)
+constexpr int kRowsPT = 16;          // rows per thread per compaction pass
+constexpr int kPass = kRowsPT * kSB; // rows per compaction pass
+constexpr int kSlots = kRowsPT * kSWaves;
+constexpr int kMaxTiles = 512;       // components per segment <= kMaxTiles * kTileF
+constexpr double kSqrt2Pi = 2.5066282746310002;
+
+__device__ __forceinline__ uint64_t row_key(const double* __restrict__ V, int64_t row,
+                                            const tpe_colspec& C) {
+  return order_key(obs_transform(V[row], C.transform, C.floor));
+}
+
+// ---- order maintenance -----------------------------------------------------
+// K1: the new rows [n_old, n_old + k) of every spec's column, sorted by
+// (key, row) in LDS (bitonic over the next power of two)
+__global__ __launch_bounds__(kSB) void k_order_sort_new(const double* __restrict__ vals,
+                                                        int64_t ld,
+                                                        const tpe_colspec* __restrict__ specs,
+                                                        int64_t n_old, int k,
+                                                        uint64_t* __restrict__ new_keys,
+                                                        int32_t* __restrict__ new_rows) {
+  __shared__ uint64_t skey[kNew];
+  __shared__ uint16_t sidx[kNew];
+  const tpe_colspec C = specs[blockIdx.x];
+  const double* V = vals + (int64_t)C.col * ld;
+  int N = 2;
+  while (N < k) N <<= 1;
+  for (int e = threadIdx.x; e < N; e += kSB) {
+    skey[e] = e < k ? row_key(V, n_old + e, C) : ~0ull;
+    sidx[e] = (uint16_t)e;
+  }
+  __syncthreads();
+  for (int s = 2; s <= N; s <<= 1) {
+    for (int j = s >> 1; j > 0; j >>= 1) {
+      for (int e = threadIdx.x; e < N / 2; e += kSB) {
+        const int i = ((e & ~(j - 1)) << 1) | (e & (j - 1)), l = i + j;
+        const uint64_t ka = skey[i], kb = skey[l];
+        const uint16_t ia = sidx[i], ib = sidx[l];
+        const bool gt = (ka > kb) || (ka == kb && ia > ib);
+        if (gt == ((i & s) == 0)) {
+          skey[i] = kb;
+          skey[l] = ka;
+          sidx[i] = ib;
+          sidx[l] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  uint64_t* K = new_keys + (int64_t)blockIdx.x * kNew;
+  int32_t* R = new_rows + (int64_t)blockIdx.x * kNew;
+  for (int e = threadIdx.x; e < k; e += kSB) {
+    K[e] = skey[e];
+    R[e] = (int32_t)(n_old + sidx[e]);
+  }
+}
+
+// K2: merge -- an old entry at i goes to i + #(new keys < its key), a new one
+// at j to j + #(old keys <= its key): old rows precede new rows (smaller row
+// ids) on equal keys, so the merged order is again by (key, row)
+__global__ __launch_bounds__(256) void k_order_merge(const double* __restrict__ vals, int64_t ld,
+                                                     const tpe_colspec* __restrict__ specs,
+                                                     const int32_t* __restrict__ order,
+                                                     int64_t n_old, int k,
+                                                     const uint64_t* __restrict__ new_keys,
+                                                     const int32_t* __restrict__ new_rows,
+                                                     int32_t* __restrict__ merged) {
+  const tpe_colspec C = specs[blockIdx.y];
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = n_old + k;
+  if (e >= n) return;
+  const double* V = vals + (int64_t)C.col * ld;
+  const int32_t* O = order + (int64_t)C.col * ld;
+  const uint64_t* K = new_keys + (int64_t)blockIdx.y * kNew;
+  int32_t* M = merged + (int64_t)blockIdx.y * n;
+  if (e < n_old) {
+    const int32_t row = O[e];
+    const uint64_t key = row_key(V, row, C);
+    int lo = 0, hi = k;  // #(new keys < key)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (K[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    M[e + lo] = row;
+  } else {
+    const int j = (int)(e - n_old);
+    const uint64_t key = K[j];
+    int64_t lo = 0, hi = n_old;  // #(old keys <= key)
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (row_key(V, O[mid], C) <= key) lo = mid + 1; else hi = mid;
+    }
+    M[j + lo] = new_rows[(int64_t)blockIdx.y * kNew + j];
+  }
+}
+
+// K3: the merged orders back into the history's order matrix
+__global__ __launch_bounds__(256) void k_order_copy(const tpe_colspec* __restrict__ specs,
+                                                    const int32_t* __restrict__ merged, int64_t n,
+                                                    int64_t ld, int32_t* __restrict__ order) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < n) order[(int64_t)specs[blockIdx.y].col * ld + e] = merged[(int64_t)blockIdx.y * n + e];
+}
+
+// ---- the fit ------------------------------------------------------------------
+// Block-wide stream compaction over items [0, n) in item order, kRowsPT items
+// per thread per pass (the loads of a pass in flight together): take(i, v)
+// says whether item i is kept (and loads its payload), emit(i, rank, v) gets
+// its rank among the kept items.  Returns the number kept.
+template <class Take, class Emit>
+__device__ int64_t block_compact(int64_t n, Take take, Emit emit, int* wsum, int64_t* carry_s) {
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  if (threadIdx.x == 0) *carry_s = 0;
+  __syncthreads();
+  for (int64_t p0 = 0; p0 < n; p0 += kPass) {
+    bool tk[kRowsPT];
+    int64_t pl[kRowsPT];
+#pragma unroll
+    for (int t = 0; t < kRowsPT; ++t) {
+      const int64_t i = p0 + (int64_t)t * kSB + threadIdx.x;
+      pl[t] = 0;
+      tk[t] = i < n && take(i, pl[t]);
+    }
+    int before[kRowsPT];
+#pragma unroll
+    for (int t = 0; t < kRowsPT; ++t) {
+      const uint64_t bal = __ballot(tk[t]);
+      before[t] = __popcll(bal & lt);
+      if (lane == 0) wsum[t * kSWaves + wid] = __popcll(bal);
+    }
+    __syncthreads();
+    // exclusive scan of the kSlots (tile, wave) counts, slot order = item order
+    const int c = threadIdx.x < kSlots ? wsum[threadIdx.x] : 0;
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int o = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += o;
+    }
+    __syncthreads();
+    if (threadIdx.x < kSlots && lane == kWave - 1) wsum[kSlots + wid] = incl;
+    __syncthreads();
+    int wave_base = 0;
+    for (int q = 0; q < wid && q < kSlots / kWave; ++q) wave_base += wsum[kSlots + q];
+    const int64_t carry = *carry_s;
+    if (threadIdx.x < kSlots) wsum[threadIdx.x] = wave_base + incl - c;
+    int total = 0;
+    for (int q = 0; q < kSlots / kWave; ++q) total += wsum[kSlots + q];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kRowsPT; ++t)
+      if (tk[t]) emit(p0 + (int64_t)t * kSB + threadIdx.x,
+                      carry + wsum[t * kSWaves + wid] + before[t], pl[t]);
+    __syncthreads();
+    if (threadIdx.x == 0) *carry_s = carry + total;
+    __syncthreads();
+  }
+  return *carry_s;
+}
+
+// The 256-thread block_sum of tpe_parzen.hip over values held by threads
+// 0..255 (the other threads pass 0): wave butterflies, then the four wave
+// totals in order.  Called by every thread; every thread gets the sum.
+__device__ __forceinline__ double sum256(double v, double* sh) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+  __syncthreads();
+  const int wid = threadIdx.x / kWave;
+  if (lane_id() == 0 && wid < 4) sh[wid] = v;
+  __syncthreads();
+  double r = sh[0];
+  r += sh[1];
+  r += sh[2];
+  r += sh[3];
+  __syncthreads();
+  return r;
+}
+
+// the per-tile wave totals of one pass: tile (4 waves) sums in wave order,
+// as block_sum<256> folds them
+__device__ __forceinline__ void tile_sums(double v, double* wt, double* out, int tile0,
+                                          int tiles) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+  const int wid = threadIdx.x / kWave;
+  if (lane_id() == 0) wt[wid] = v;
+  __syncthreads();
+  if (threadIdx.x < kSB / kTileF) {
+    const int t = tile0 + (int)threadIdx.x;
+    if (t < tiles) {
+      double r = wt[4 * threadIdx.x];
+      r += wt[4 * threadIdx.x + 1];
+      r += wt[4 * threadIdx.x + 2];
+      r += wt[4 * threadIdx.x + 3];
+      out[t] = r;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kSB) void k_fit_sorted(
+    const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
+    const int32_t* __restrict__ order, int64_t n_rows, const uint8_t* __restrict__ is_below,
+    const tpe_gather* __restrict__ gathers, tpe_seg* __restrict__ segs,
+    int32_t* __restrict__ gi_scr, double* __restrict__ w, double* __restrict__ mu,
+    double* __restrict__ sigma, double* __restrict__ wcdf, double* __restrict__ coef64,
+    float* __restrict__ coef32, int32_t* __restrict__ err) {
+  __shared__ int wsum[kSlots + kSlots / kWave];
+  __shared__ int64_t carry_s;
+  __shared__ double sh[4], wt[kSWaves];
+  __shared__ double p_w[kMaxTiles], p_d[kMaxTiles], p_l[kMaxTiles];
+  __shared__ int s_lt;
+  __shared__ double s_x0, shm[kSWaves];
+  tpe_seg* S = segs + blockIdx.x;
+  const tpe_gather G = gathers[blockIdx.x];
+  const int64_t col = G.col;
+  const uint8_t side = G.below ? 1 : 0;
+  const double* V = vals + col * ld;
+  const uint8_t* A = active + col * ld;
+  const int32_t* O = order + col * ld;
+  int32_t* GI = gi_scr + (int64_t)blockIdx.x * n_rows;
+  const int transform = S->transform;
+  const double floor_ = S->floor, pmu = S->prior_mu;
+  const uint64_t kp = order_key(pmu);
+  const int64_t coff = S->comp_off;
+  if (threadIdx.x == 0) {
+    s_lt = 0;
+    s_x0 = 0.0;
+  }
+  // 1. rows in tid order: position in the segment's list, count below the prior
+  int lt = 0;
+  const int64_t n = block_compact(
+      n_rows,
+      [&](int64_t r, int64_t& pl) {
+        const bool t = A[r] && is_below[r] == side;
+        if (t) {
+          const double v = obs_transform(V[r], transform, floor_);
+          lt += order_key(v) < kp ? 1 : 0;
+          pl = __double_as_longlong(v);
+        }
+        return t;
+      },
+      [&](int64_t r, int64_t rank, int64_t pl) {
+        GI[r] = (int32_t)rank;
+        if (rank == 0) s_x0 = __longlong_as_double(pl);
+      },
+      wsum, &carry_s);
+  atomicAdd(&s_lt, lt);
+  if (n != G.count) {  // the segment was sized for another count: nothing written
+    if (threadIdx.x == 0 && err) atomicOr(err, 4);
+    return;
+  }
+  __syncthreads();
+  const int nn = (int)n, lf = S->lf;
+  // the prior's slot: searchsorted(obs, prior_mu, 'left') (tpe.py:427), or the
+  // len == 1 rule (tpe.py:414-421)
+  const int prior_pos = n >= 2 ? s_lt : (n == 1 ? ((pmu < s_x0) ? 0 : 1) : 0);
+  // 2. the column's sorted order compacted to the segment
+  block_compact(
+      n_rows,
+      [&](int64_t e, int64_t& pl) {
+        const int32_t row = O[e];
+        pl = row;
+        return A[row] && is_below[row] == side;
+      },
+      [&](int64_t e, int64_t p, int64_t row) {
+        const int64_t pos = p + (p >= prior_pos ? 1 : 0);
+        mu[coff + pos] = obs_transform(V[row], transform, floor_);
+        w[coff + pos] = lf_weight(GI[row], nn, lf);  // ramp in tid order (tpe.py:441-447)
+      },
+      wsum, &carry_s);
+  if (threadIdx.x == 0) {
+    mu[coff + prior_pos] = pmu;
+    w[coff + prior_pos] = S->prior_weight;
+    S->prior_pos = prior_pos;
+  }
+  __syncthreads();  // (block-scope: the means and weights are visible to the block)
+  // 3. bandwidths + per-tile sums (k_fit_comp)
+  const int nc = nn + 1;
+  const int tiles = (nc + kTileF - 1) / kTileF;
+  const double ps = S->prior_sigma;
+  for (int k0 = 0; k0 < nc; k0 += kSB) {
+    const int k = k0 + threadIdx.x;
+    double wk = 0.0, dphi = 0.0;
+    if (k < nc) {
+      double s;
+      if (nn == 0) {
+        s = ps;
+      } else if (nn == 1) {
+        s = (k == prior_pos) ? ps : ps * 0.5;
+      } else if (k == 0) {
+        s = mu[coff + 1] - mu[coff];
+      } else if (k == nc - 1) {
+        s = mu[coff + nc - 1] - mu[coff + nc - 2];
+      } else {
+        s = fmax(mu[coff + k] - mu[coff + k - 1], mu[coff + k + 1] - mu[coff + k]);
+      }
+      const double lo_clip = ps / fmin(100.0, 1.0 + (double)nc);  // tpe.py:455
+      s = fmin(fmax(s, lo_clip), ps);
+      if (k == prior_pos) s = ps;
+      sigma[coff + k] = s;
+      wk = w[coff + k];
+      if (S->bounded) {
+        const double m = mu[coff + k];
+        dphi = normal_cdf(S->high, m, s) - normal_cdf(S->low, m, s);
+      }
+    }
+    tile_sums(wk, wt, p_w, k0 / kTileF, tiles);
+    tile_sums(wk * dphi, wt, p_d, k0 / kTileF, tiles);
+  }
+  __syncthreads();
+  // 4. normalisation, p_accept, coefficients, cumulative weights (k_fit_coef)
+  double a = 0.0, b = 0.0;
+  if (threadIdx.x < kTileF)
+    for (int t = threadIdx.x; t < tiles; t += kTileF) {
+      a += p_w[t];
+      b += p_d[t];
+    }
+  const double wsum_ = sum256(a, sh);
+  const double pacc = S->bounded ? sum256(b, sh) / wsum_ : 1.0;
+  const bool lg = S->family == TPE_LGMM1;
+  for (int k0 = 0; k0 < nc; k0 += kSB) {
+    const int k = k0 + threadIdx.x;
+    const int tile = k / kTileF;  // this pass holds tiles k0/256 .. k0/256 + 3
+    double wr = 0.0, lmax = -INFINITY;
+    if (k < nc) {
+      wr = w[coff + k];
+      const double wk = wr / wsum_;
+      w[coff + k] = wk;
+      const double m = mu[coff + k], s = sigma[coff + k];
+      double lc, inv;
+      if (lg) {  // LGMM1_lpdf: no p_accept (tpe.py:284-287)
+        const double sp = fmax(s, kEps);
+        lc = log(wk) - log(sp * kSqrt2Pi);
+        inv = 1.0 / sp;
+      } else {  // GMM1_lpdf (tpe.py:152-158)
+        const double z = sqrt(kTwoPi * (s * s));
+        lc = log(wk / z / pacc);
+        inv = 1.0 / fmax(s, kEps);
+      }
+      double* c = coef64 + 4 * (coff + k);
+      c[0] = m;
+      c[1] = inv;
+      c[2] = lc;
+      c[3] = wk;
+      lmax = lc * kLog2e;
+    }
+    // inclusive scan of the raw weights inside the 256-tile (wave shfl_up, then
+    // the tile's earlier waves in order), plus the earlier tiles' total
+    const int lane = lane_id(), wid = threadIdx.x / kWave;
+    double v = wr;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const double u = __shfl_up(v, o, kWave);
+      if (lane >= o) v += u;
+    }
+    if (lane == kWave - 1) wt[wid] = v;
+    __syncthreads();
+    for (int q = wid & ~3; q < wid; ++q) v += wt[q];
+    // the tile's base: block_sum<256> of the earlier tiles' sums (k_fit_coef's `before`)
+    double base = 0.0;
+    for (int tt = k0 / kTileF; tt < k0 / kTileF + kSB / kTileF; ++tt) {
+      double bt = 0.0;
+      if (threadIdx.x < kTileF)
+        for (int t = threadIdx.x; t < tiles; t += kTileF)
+          if (t < tt) bt += p_w[t];
+      bt = sum256(bt, sh);
+      if (tt == tile) base = bt;
+    }
+    if (k < nc) wcdf[coff + k] = (base + v) / wsum_;
+    // per-tile max of the log2 coefficients
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) lmax = fmax(lmax, __shfl_xor(lmax, off, kWave));
+    __syncthreads();
+    if (lane == 0) wt[wid] = lmax;
+    __syncthreads();
+    if (threadIdx.x < kSB / kTileF && k0 / kTileF + (int)threadIdx.x < tiles) {
+      const int q = 4 * threadIdx.x;
+      p_l[k0 / kTileF + threadIdx.x] = fmax(fmax(fmax(wt[q], wt[q + 1]), wt[q + 2]), wt[q + 3]);
+    }
+    __syncthreads();
+  }
+  // 5. fp32 coefficients (k_fit_coef32)
+  double mx = -INFINITY;
+  for (int t = threadIdx.x; t < tiles; t += kSB) mx = fmax(mx, p_l[t]);
+  const double cmax = block_max<kSB, double>(mx, shm);
+  const double center = (double)(float)pmu;
+  const double sq = 0.8493218002880191;  // sqrt(0.5 * log2(e))
+  for (int k = threadIdx.x; k < nc; k += kSB) {
+    const double* c = coef64 + 4 * (coff + k);
+    const double a32 = c[1] * sq;
+    float* f = coef32 + 4 * (coff + k);
+    f[0] = (float)a32;
+    f[1] = (float)(-(c[0] - center) * a32);
+    f[2] = (float)(c[2] * kLog2e - cmax);
+    f[3] = 0.0f;
+  }
+  if (threadIdx.x == 0) {
+    S->p_accept = pacc;
+    S->cmax = cmax;
+    S->center = center;
+  }
+}
+}  // namespace
+}  // namespace tpe
+
+using namespace tpe;
+
+extern "C" int64_t tpe_history_order_scratch_bytes(int n_specs, int64_t n_rows) {
+  if (n_specs < 0 || n_rows < 0) return -1;
+  return (int64_t)n_specs * ((int64_t)kNew * 12 + 4 * std::max<int64_t>(n_rows, 1)) + 256;
+}
+
+extern "C" int tpe_history_order(const double* vals, int64_t ld, const tpe_colspec* specs,
+                                 const tpe_colspec* host_specs, int n_specs, int64_t n_old,
+                                 int64_t n_new, int32_t* order, void* scratch, void* stream) {
+  if (n_specs < 0 || n_specs > 65535 || n_old < 0 || n_new < 0 || n_new > kNew ||
+      n_old + n_new > ld || n_old + n_new > INT32_MAX) {
+    set_error("tpe_history_order: n_specs=%d n_old=%lld n_new=%lld ld=%lld (at most %d new rows "
+              "per call)", n_specs, (long long)n_old, (long long)n_new, (long long)ld, kNew);
+    return TPE_E_ARG;
+  }
+  if (n_specs == 0 || n_new == 0) return TPE_OK;
+  if (!vals || !specs || !host_specs || !order || !scratch) {
+    set_error("tpe_history_order: null pointer");
+    return TPE_E_ARG;
+  }
+  for (int i = 0; i < n_specs; ++i)
+    if (host_specs[i].col < 0 || (host_specs[i].transform != TPE_OBS_IDENTITY &&
+                                  host_specs[i].transform != TPE_OBS_LOG)) {
+      set_error("tpe_history_order: spec %d has a bad column / transform", i);
+      return TPE_E_ARG;
+    }
+  char* p = static_cast<char*>(scratch);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(p);
+  int32_t* rows = reinterpret_cast<int32_t*>(p + (int64_t)n_specs * kNew * 8);
+  int32_t* merged = reinterpret_cast<int32_t*>(p + (int64_t)n_specs * kNew * 12);
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n = n_old + n_new;
+  const dim3 g((unsigned)((n + 255) / 256), (unsigned)n_specs);
+  hipLaunchKernelGGL(k_order_sort_new, dim3(n_specs), dim3(kSB), 0, st, vals, ld, specs, n_old,
+                     (int)n_new, keys, rows);
+  hipLaunchKernelGGL(k_order_merge, g, dim3(256), 0, st, vals, ld, specs, order, n_old,
+                     (int)n_new, keys, rows, merged);
+  hipLaunchKernelGGL(k_order_copy, g, dim3(256), 0, st, specs, merged, n, ld, order);
+  return check_launch("tpe_history_order");
+}
+
+extern "C" int64_t tpe_fit_sorted_scratch_bytes(int n_seg, int64_t n_rows) {
+  if (n_seg < 0 || n_rows < 0) return -1;
+  return 4 * (int64_t)std::max(n_seg, 1) * std::max<int64_t>(n_rows, 1);
+}
+
+extern "C" int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t ld,
+                              const int32_t* order, int64_t n_rows, const uint8_t* is_below,
+                              const tpe_gather* gathers, const tpe_gather* host_gathers,
+                              tpe_seg* segs, int n_seg, void* scratch, double* w, double* mu,
+                              double* sigma, double* wcdf, double* coef64, float* coef32,
+                              int32_t* err, void* stream) {
+  if (n_seg < 0 || n_seg > 65535 || n_rows < 0 || n_rows > ld || n_rows > INT32_MAX) {
+    set_error("tpe_fit_sorted: n_seg=%d n_rows=%lld ld=%lld", n_seg, (long long)n_rows,
+              (long long)ld);
+    return TPE_E_ARG;
+  }
+  if (n_seg == 0) return TPE_OK;
+  if (!vals || !active || !order || !is_below || !gathers || !host_gathers || !segs ||
+      !scratch || !w || !mu || !sigma || !wcdf || !coef64 || !coef32) {
+    set_error("tpe_fit_sorted: null pointer");
+    return TPE_E_ARG;
+  }
+  for (int i = 0; i < n_seg; ++i) {
+    const tpe_gather& g = host_gathers[i];
+    if (g.col < 0 || g.to_int || g.count < 0 || g.count + 1 > (int64_t)kMaxTiles * kTileF) {
+      set_error("tpe_fit_sorted: segment %d: column %d, count %lld (at most %d observations)",
+                i, g.col, (long long)g.count, kMaxTiles * kTileF - 1);
+      return TPE_E_ARG;
+    }
+  }
+  hipLaunchKernelGGL(k_fit_sorted, dim3(n_seg), dim3(kSB), 0, (hipStream_t)stream, vals, active,
+                     ld, order, n_rows, is_below, gathers, segs,
+                     reinterpret_cast<int32_t*>(scratch), w, mu, sigma, wcdf, coef64, coef32, err);
+  return check_launch("tpe_fit_sorted");
+}

@@ -1082,6 +1082,15 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   float bs = -INFINITY, by = 0.0f;
   int br = -1;
   uint32_t fb = 0;  // candidates the score cells do not cover
+#ifdef TPE_DIAG_SKIP_SCORE  // diagnostic builds only: the sampler alone
+#pragma unroll
+  for (int r = 0; r < kTR; ++r)
+    if (r < nvalid && x[r] > bs) {
+      bs = x[r];
+      by = x[r];
+      br = r;
+    }
+#else
   float4 q[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) q[r] = sc[cell_of(x[r])];
@@ -1107,6 +1116,7 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
     }
     if (out_x && valid) out_x[J.out_off + t0 + r] = cand_value(y, lgmm);
   }
+#endif
   int n_fb = 0;
   uint32_t lsem = 0;  // candidates scored by the exact fp32 log-sum-exp
   const uint32_t fbm = fb;
@@ -1159,6 +1169,9 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
 
   // ---- the band: candidates that can still be the exact winner --------------
+#ifdef TPE_DIAG_NO_BAND  // diagnostic builds only: the fp32 winner alone
+  return;
+#endif
   const float ea = kEpsAbs + kEpsSlope * Tb.slope;
   const float el = ea + kEpsLse * (float)(SB.n_obs + SA.n_obs + 4);
   auto eps = [&](int r, float s) __attribute__((always_inline)) -> float {

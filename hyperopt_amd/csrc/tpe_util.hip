@@ -41,13 +41,14 @@ extern "C" int tpe_abi_version(void) { return TPE_ABI_VERSION; }
 
 // sizes of the ABI structs, so bindings can check their mirrors
 extern "C" int tpe_struct_sizes(int32_t* out, int n) {
-  const int32_t s[9] = {(int32_t)sizeof(tpe_seg),     (int32_t)sizeof(tpe_cat_seg),
-                        (int32_t)sizeof(tpe_job),     (int32_t)sizeof(tpe_best),
-                        (int32_t)sizeof(tpe_table),   (int32_t)sizeof(tpe_gather),
-                        (int32_t)sizeof(tpe_history), (int32_t)sizeof(tpe_prior),
-                        (int32_t)sizeof(tpe_op)};
-  for (int i = 0; i < n && i < 9; ++i) out[i] = s[i];
-  return 9;
+  const int32_t s[11] = {(int32_t)sizeof(tpe_seg),     (int32_t)sizeof(tpe_cat_seg),
+                         (int32_t)sizeof(tpe_job),     (int32_t)sizeof(tpe_best),
+                         (int32_t)sizeof(tpe_table),   (int32_t)sizeof(tpe_gather),
+                         (int32_t)sizeof(tpe_history), (int32_t)sizeof(tpe_prior),
+                         (int32_t)sizeof(tpe_op),      (int32_t)sizeof(tpe_band),
+                         (int32_t)sizeof(tpe_colspec)};
+  for (int i = 0; i < n && i < 11; ++i) out[i] = s[i];
+  return 11;
 }
 
 // ---- host: the below split's rows (ap_split_trials, tpe.py:623-646) -------

@@ -213,6 +213,12 @@ class DeviceHistory:
         self.rows = 0
         self.cap = 0
         self.vals = self.active = None
+        # per fitted column: its rows sorted by (transformed value, row)
+        # (tpe_history_order; the fit's sort kept across suggests), the
+        # (transform, floor) it was sorted with and how many rows it covers
+        self.order = None
+        self.order_spec = {}
+        self.order_rows = {}
         self.active_host = np.zeros((0, self.n_labels), bool)
         self.n_active = np.zeros(self.n_labels, np.int64)
         self._grow(max(int(cap), 16))
@@ -230,6 +236,11 @@ class DeviceHistory:
             a[:, :self.rows].copy_(self.active[:, :self.rows])
         ah = np.zeros((cap, self.n_labels), bool)
         ah[:self.rows] = self.active_host[:self.rows]
+        if self.order is not None:
+            o = t.zeros((self.n_labels, cap), dtype=t.int32, device=self.device)
+            if self.rows:
+                o[:, :self.rows].copy_(self.order[:, :self.rows])
+            self.order = o
         self.vals, self.active, self.active_host, self.cap = v, a, ah, cap
 
     def append(self, vals, active=None):
@@ -251,6 +262,60 @@ class DeviceHistory:
         self.active_host[r0:r0 + k] = active
         self.n_active += active.sum(0)
         self.rows += k
+
+    ORDER_CHUNK = 2048  # new rows merged per tpe_history_order call
+
+    def ensure_order(self, eng, stream, cols, transforms, floors):
+        # (stream: the level's torch stream)
+        """Bring the sorted orders of columns ``cols`` (with the fit's
+        transform / floor per column) up to every row, on ``stream``: new rows
+        are merged in (tpe_history_order), a column first seen -- or seen with
+        another transform -- is built from scratch the same way."""
+        t = self.torch
+        if self.order is None:
+            self.order = t.zeros((self.n_labels, self.cap), dtype=t.int32, device=self.device)
+        key = (self.rows, len(cols))
+        if self.__dict__.get("_ordered") == key and all(
+                self.order_rows.get(c) == self.rows for c in np.asarray(cols).tolist()):
+            return  # (every column current: nothing appended since)
+        todo = {}
+        for c, tr, fl in zip(np.asarray(cols).tolist(), np.asarray(transforms).tolist(),
+                             np.asarray(floors).tolist()):
+            spec = (int(tr), float(fl))
+            if self.order_spec.get(c) != spec:
+                self.order_spec[c] = spec
+                self.order_rows[c] = 0
+            if self.order_rows[c] < self.rows:
+                todo.setdefault(self.order_rows[c], []).append((c,) + spec)
+        if not todo:
+            return
+        lib = eng.lib
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        cache = self.__dict__.setdefault("_spec_dev", {})
+        for n_old, specs in todo.items():
+            hit = cache.get(tuple(specs))
+            if hit is None:  # the column specs on the device (kept: the same every append)
+                arr = np.zeros(len(specs), L.COLSPEC_DTYPE)
+                arr["col"], arr["transform"], arr["floor"] = zip(*specs)
+                with t.cuda.stream(stream):
+                    dev = t.from_numpy(arr.view(np.uint8).copy()).to(self.device)
+                if len(cache) > 16:
+                    cache.clear()
+                hit = cache[tuple(specs)] = (arr, dev)
+            arr, dev = hit
+            scratch = eng._buf("order_scratch",
+                               lib.tpe_history_order_scratch_bytes(len(specs), self.rows))
+            n = n_old
+            while n < self.rows:
+                k = min(self.ORDER_CHUNK, self.rows - n)
+                L.check(lib.tpe_history_order(self.vals.data_ptr(), self.ld, dev.data_ptr(),
+                                              arr.ctypes.data, len(specs), n, k,
+                                              self.order.data_ptr(), scratch, sp),
+                        "tpe_history_order")
+                n += k
+            for c, _, _ in specs:
+                self.order_rows[c] = self.rows
+        self._ordered = key
 
 
 class Engine:
@@ -297,13 +362,18 @@ class Engine:
         # quantized labels of a suggest level: decide the argmax after the first
         # lat_prefix candidates where no unseen lattice value can still win
         # (tpe_lattice_suggest); 0 (TPE_LAT_PREFIX=0): every stream drawn in full
-        self.lat_prefix = int(os.environ.get("TPE_LAT_PREFIX", str(LAT_PREFIX)))
+        self.lat_prefix = _lat_prefix(os.environ.get("TPE_LAT_PREFIX", str(LAT_PREFIX)))
         # stream-ordering events (one stream of this device waits for another)
         # without the system-scope fence: a device-scope release is all a
         # consumer on the same GPU needs, and the system-scope one writes back
         # the L2s (~14 us of idle GPU per event on C3 levels).  The host-read
         # "result" event keeps it.  TPE_DEVICE_EVENTS=0: every event system-scope.
         self.device_events = os.environ.get("TPE_DEVICE_EVENTS", "1") == "1"
+        # the fit from the history's sorted orders (tpe_fit_sorted) where the
+        # level reads one history with its identity row list; "0": the
+        # gather + sort + merge fit (tpe_parzen_fit) everywhere
+        self.sorted_fit = os.environ.get("TPE_SORTED_FIT", "1") == "1"
+        self._last_gkey = None  # launch key of the previous eager level
         self._gen = 0           # bumped whenever a workspace buffer is (re)allocated
         self.graph_stats = {"eager": 0}  # levels issued eagerly / re-issued ("native", "replay")
         # native level launcher (default; TPE_NATIVE_LAUNCH=0: one ctypes call
@@ -343,6 +413,35 @@ class Engine:
             self._bufs[name] = t
             self._gen += 1
         return t.data_ptr()
+
+    def _presize(self, n_comp, n_obs_total, max_obs, cobs_off, n_seg, tjobs, n_rows):
+        """Every workspace buffer whose size follows a level's per-call sizes
+        (mixture pools, observation pools, fit / table scratch), grown here,
+        before the launch key is formed: a level re-issued from its records
+        (which hold the pointers) then finds every buffer large enough, and a
+        buffer that had to grow (new pointer, _gen bumped) forces a new
+        recording."""
+        sizes = (n_comp, n_obs_total, max_obs, cobs_off, n_seg, tjobs, n_rows)
+        last = self.__dict__.get("_presized")
+        if last is not None and last[0] == self._gen and all(
+                a <= b for a, b in zip(sizes, last[1])) and n_seg == last[1][4] and \
+                tjobs == last[1][5]:
+            return  # every buffer already holds these sizes (buffers only grow)
+        lib = self.lib
+        if n_comp:
+            for name, per in (("w", 8), ("mu", 8), ("sigma", 8), ("wcdf", 8), ("coef64", 32),
+                              ("coef32", 16), ("reach_hi", 8), ("reach_lo", 8),
+                              ("wide_idx", 4), ("coef32n", 16), ("wide32", 16), ("pm", 4),
+                              ("sm", 4)):
+                self._buf(name, per * n_comp)
+            self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(n_seg, max_obs, n_obs_total))
+        self._buf("obs_dev", 8 * max(n_obs_total, 1))
+        self._buf("cobs_dev", 8 * max(cobs_off, 1))
+        if tjobs:
+            self._buf("table_scratch", lib.tpe_table_scratch_bytes(tjobs, max_obs + 1))
+        if n_rows:
+            self._buf("fit_sorted_scratch", lib.tpe_fit_sorted_scratch_bytes(n_seg, n_rows))
+        self._presized = (self._gen, sizes)
 
     def _drop_oplists(self):
         self._replays.clear()
@@ -570,7 +669,9 @@ class Engine:
             # still holds this level's pack (levels that differ only in their
             # timer events share one)
             if rp is not None and rp.gen == self._gen and self._staged_sig == rp.sig[:-1]:
-                return rp.run(self, works, is_below, timers, defer)
+                out = rp.run(self, works, is_below, timers, defer)
+                if out is not None:
+                    return out
         if sample_only:
             outputs = True
         if scorer is None:
@@ -593,6 +694,7 @@ class Engine:
         if history is not None and histories is not None:
             raise ValueError("give either history or histories")
         hist_mode = history is not None or histories is not None
+        n_rows = 0  # split flags uploaded (single-history levels)
         if table_scores:  # the fast table path's per-candidate scores (test hook)
             outputs = False
         batch = works if isinstance(works, WorkBatch) else None
@@ -861,11 +963,11 @@ class Engine:
                  g_arr["to_int"], g_arr["hist"]) = (np.array(c) for c in zip(*gathers))
             o_g = pack.add(g_arr)
             if histories is None:
+                # (the split flags and row list go last in the pack, after the
+                # result block: a level whose history grew keeps every other
+                # offset, so its records can be re-issued, _Replay)
                 isb = np.ascontiguousarray(is_below, dtype=np.uint8)
                 n_rows = isb.size
-                o_isb = pack.add(isb)
-                o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) \
-                    if rows is not None else None
             else:  # row lists / flags at offsets of the staged pack (the `aux` base)
                 h_arr = np.zeros(len(histories), L.HISTORY_DTYPE)
                 for h, (dh, h_rows, h_isb) in enumerate(histories):
@@ -905,6 +1007,11 @@ class Engine:
             o_xslot = pack.add(x_slots[np.asarray(order, np.int64)])
             xbytes = int(x_labels) * BS
         o_res = pack.add(np.zeros(64 + n_jobs * BS + xbytes, np.uint8))
+        o_isb = o_rows = None
+        if hist_mode and histories is None:
+            o_isb = pack.add(isb)
+            o_rows = pack.add(np.ascontiguousarray(rows, dtype=np.int32)) \
+                if rows is not None else None
         native_ok = self.native and pkey is not None and not (
             outputs or sample_only or posteriors or table_scores)
         base = self._upload(pack, stream, copy=not native_ok)
@@ -915,26 +1022,35 @@ class Engine:
         # every workspace pointer before the first launch: the launches then
         # follow each other without host work in between
         d_w = d_mu = d_sig = d_cdf = d_c64 = d_c32 = d_logp = d_ccdf = None
+        nfs = 2 * len(fit_ids)
+        prune = bool(fit_ids) and any(k == "sorted" and ids for k, ids in groups)
+        # the fit from the history's sorted orders (tpe_fit_sorted): one kernel
+        # instead of gather + sort + merge ranks + three coefficient kernels;
+        # needs the single history with its identity row list (row = tid order)
+        sorted_fit = bool(fit_ids) and self.sorted_fit and history is not None and \
+            histories is None and rows is None and not prune
+        tjobs = max([b - a for a, b in (_slice_of(groups, g) for g, (k, ids) in enumerate(groups)
+                                        if k in ("table", "pruned64") and ids)], default=0)
+        self._presize(n_comp, n_obs_total, max_obs, cobs_off, len(segs), tjobs,
+                      n_rows if sorted_fit else 0)
         if fit_ids:
-            d_w = self._buf("w", 8 * n_comp)
-            d_mu = self._buf("mu", 8 * n_comp)
-            d_sig = self._buf("sigma", 8 * n_comp)
-            d_cdf = self._buf("wcdf", 8 * n_comp)
-            d_c64 = self._buf("coef64", 32 * n_comp)
-            d_c32 = self._buf("coef32", 16 * n_comp)
-            d_c32n = self._buf("coef32n", 16 * n_comp)
-            d_w32 = self._buf("wide32", 16 * n_comp)
-            d_pm = self._buf("pm", 4 * n_comp)
-            d_sm = self._buf("sm", 4 * n_comp)
-            d_fs = self._buf("fit_scratch", lib.tpe_fit_scratch_bytes(len(segs), max_obs,
-                                                                       n_obs_total))
-            prune = any(k == "sorted" and ids for k, ids in groups)
-            if not prune:
-                d_c32n = d_w32 = d_pm = d_sm = None
+            d_w, d_mu, d_sig, d_cdf = (self._bufs[k].data_ptr() for k in ("w", "mu", "sigma",
+                                                                            "wcdf"))
+            d_c64, d_c32 = self._bufs["coef64"].data_ptr(), self._bufs["coef32"].data_ptr()
+            d_fs = self._bufs["fit_scratch"].data_ptr()
+            d_c32n = d_w32 = d_pm = d_sm = None
+            if prune:
+                d_c32n = self._buf("coef32n", 16 * n_comp)
+                d_w32 = self._buf("wide32", 16 * n_comp)
+                d_pm = self._buf("pm", 4 * n_comp)
+                d_sm = self._buf("sm", 4 * n_comp)
         if cat:
             d_logp = self._buf("cat_logp", 8 * p_pool.size)
             d_ccdf = self._buf("cat_cdf", 8 * p_pool.size)
         self.last_plan = (segs, csegs, g_arr if hist_mode else None, jobs, cached is not None)
+        if sorted_fit:
+            history.ensure_order(self, stream, g_arr["col"][:nfs:2], segs["transform"][::2],
+                                 segs["floor"][::2])
 
         # ---- the level's launches (eager, or recorded and re-issued) ------------
         # Every argument below is a workspace pointer (unchanged while _gen is),
@@ -942,10 +1058,12 @@ class Engine:
         # the values that change from call to call live in the uploaded pack.
         gkey = None
         if native_ok:
-            gkey = (pkey, self._gen, sp.value, tuple(off for off, _ in pack.parts), n_obs_total,
-                    max_obs,
-                    cobs_off, lat_off,
-                    (history.vals.data_ptr(), history.active.data_ptr(), history.ld, n_rows)
+            # (the per-call sizes -- history rows, observation totals, the largest
+            # mixture, the pack size -- are size words of the records, rewritten
+            # when a recorded level is re-issued: _Replay)
+            gkey = (pkey, self._gen, sp.value, tuple(off for off, _ in pack.parts), lat_off,
+                    (history.vals.data_ptr(), history.active.data_ptr(), history.ld,
+                     history.order.data_ptr() if sorted_fit else None, rows is None)
                     if history is not None else None,
                     None if exchange is None else
                     (int(x_comm), int(x_labels), int(x_world), x_slots.tobytes()),
@@ -997,13 +1115,17 @@ class Engine:
                 d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
                 d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
                 e0 = tick("gather")
+                g0 = nfs if sorted_fit else 0  # (the sorted fit reads the history itself)
                 if histories is None:
-                    L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
-                                               history.ld,
-                                               base + o_rows if o_rows is not None else None,
-                                               n_rows, base + o_isb, base + o_g,
-                                               g_arr.ctypes.data_as(ctypes.c_void_p), len(g_arr),
-                                               d_obs, d_cobs, d_err, sp), "tpe_gather_obs")
+                    if len(g_arr) > g0:
+                        L.check(lib.tpe_gather_obs(history.vals.data_ptr(),
+                                                   history.active.data_ptr(), history.ld,
+                                                   base + o_rows if o_rows is not None else None,
+                                                   _V("n_rows", n_rows), base + o_isb,
+                                                   base + o_g + g0 * L.GATHER_DTYPE.itemsize,
+                                                   g_arr.ctypes.data + g0 * L.GATHER_DTYPE.itemsize,
+                                                   len(g_arr) - g0, d_obs, d_cobs, d_err, sp),
+                                "tpe_gather_obs")
                 else:
                     L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
                                                      len(h_arr), base, base + o_g,
@@ -1122,7 +1244,7 @@ class Engine:
                     d_rh = self._buf("reach_hi", 8 * n_comp)
                     d_rl = self._buf("reach_lo", 8 * n_comp)
                     d_wide = self._buf("wide_idx", 4 * n_comp)
-                    max_comp = max_obs + 1
+                    max_comp = _V("max_comp", max_obs + 1)
                     d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
                     if stage != "score":
                         L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64,
@@ -1163,7 +1285,7 @@ class Engine:
                     d_rh = self._buf("reach_hi", 8 * n_comp)
                     d_rl = self._buf("reach_lo", 8 * n_comp)
                     d_wide = self._buf("wide_idx", 4 * n_comp)
-                    max_comp = max_obs + 1
+                    max_comp = _V("max_comp", max_obs + 1)
                     d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
                     L.check(lib.tpe_score_pruned64(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c64,
                                                    max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab, d_cand,
@@ -1236,9 +1358,21 @@ class Engine:
                         if k == "cat" and ids:
                             launch_group(g, "all")
             # ---- posterior fit ------------------------------------------------------
-            if fit_ids:
+            if fit_ids and sorted_fit:
                 e0 = tick("fit")
-                L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), max_obs, n_obs_total,
+                d_fss = self._buf("fit_sorted_scratch",
+                                  lib.tpe_fit_sorted_scratch_bytes(len(segs), n_rows))
+                L.check(lib.tpe_fit_sorted(history.vals.data_ptr(), history.active.data_ptr(),
+                                           history.ld, history.order.data_ptr(),
+                                           _V("n_rows", n_rows),
+                                           base + o_isb, base + o_g, g_arr.ctypes.data, d_segs,
+                                           len(segs), d_fss, d_w, d_mu, d_sig, d_cdf, d_c64,
+                                           d_c32, d_err, sp), "tpe_fit_sorted")
+                tock("fit", e0)
+            elif fit_ids:
+                e0 = tick("fit")
+                L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), _V("max_obs", max_obs),
+                                           _V("n_obs_total", n_obs_total),
                                            d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n, d_w32,
                                            d_pm, d_sm, sp), "tpe_parzen_fit")
                 tock("fit", e0)
@@ -1307,7 +1441,7 @@ class Engine:
                 gen0 = self._gen
                 rec = _OpList(self.lib)
                 dst, src, nb = self._staged
-                rec.add(L.OP_MEMCPY, dst, src, nb, L.H2D, sp)
+                rec.add(L.OP_MEMCPY, dst, src, _V("pack_size", nb), L.H2D, sp)
                 cap = rec
                 try:
                     rec.table_calls, _ = launch_level(rec)
@@ -1336,6 +1470,13 @@ class Engine:
                 dst, src, nb = self._staged
                 L.hip_check(self._hip.hipMemcpyAsync(dst, src, nb, L.H2D, sp), "hipMemcpyAsync")
         if ops is not None:
+            ops.set_sizes(dict(n_rows=n_rows, max_obs=max_obs, n_obs_total=n_obs_total,
+                               max_comp=max_obs + 1, pack_size=pack.size))
+            keep = ops.keep  # the host copies the entry points validate: this call's
+            keep[0][...] = jobs
+            keep[1][...] = fb_jobs
+            if keep[2] is not None:
+                keep[2][...] = g_arr
             failed = ctypes.c_int(-1)
             rc = self.lib.tpe_run_ops(ops.ptr, ops.n, ctypes.byref(failed))
             if rc != 0:
@@ -1385,8 +1526,11 @@ class Engine:
                 if sig is not None:
                     if len(self._replays) >= 8:
                         self._replays.clear()
-                    self._replays[sig] = _Replay(sig, self._gen, ops, self._pinned[0], o_jobs,
-                                                 o_isb, p, pin)
+                    self._replays[sig] = _Replay(
+                        sig, self._gen, ops, self._pinned[0], pkey, p, pin,
+                        dict(segs=o_segs, csegs=o_csegs, g=o_g, jobs=o_jobs, fb=o_fb, isb=o_isb),
+                        history if sorted_fit else None, tjobs,
+                        (list(band_jobs), d_segs, sp.value, exchange is not None))
                     self._staged_sig = sig[:-1]
             return p if defer else p.result()
         if ops is None:
@@ -1556,25 +1700,34 @@ class _Pending(object):
 
 
 class _Replay(object):
-    """The fast path for a WorkBatch level that repeats the previous recorded
-    one in everything but its Philox keys / candidate bases and split flags
-    (bench.py's steps; any suggest whose history did not change): the staged
-    pack from that call is still in its pinned buffer, so only the job table's
-    key / cand_base columns and the split flags are rewritten in place and the
-    level's records are re-issued -- no plan, no packing, no launch-key work.
-    ``signature`` is every other input the pack and the records depend on."""
+    """The fast path for a WorkBatch level whose structure repeats the last
+    recorded one -- every suggest of an fmin loop (the history grew by a trial:
+    new counts, one more split flag) and bench.py's steps: the staged pack
+    from that call is still in its pinned buffer with every per-structure part
+    in place (prior pools, lattice slots, result block), so the per-call parts
+    -- segment sizes, gather counts, the job table's keys and candidate bases,
+    the split flags (the pack's last part) -- are rewritten there from the
+    cached plan (Engine._plan_fast / _jobs_fast), the records' size words
+    (history rows, observation totals, the largest mixture, the pack size) are
+    rewritten, and the records are re-issued: no Python planning of the
+    level, no packing, no per-launch host calls.  ``signature`` is every other
+    input the pack and the records depend on; a workspace buffer that would
+    have to grow (a new pointer) sends the call down the full path instead."""
 
-    def __init__(self, sig, gen, ops, pinned, o_jobs, o_isb, pending, res_pin):
-        self.sig, self.gen, self.ops = sig, gen, ops
-        host = pinned.numpy()
-        n = pending.order.size
-        self.jobs = host[o_jobs:o_jobs + n * L.JOB_DTYPE.itemsize].view(L.JOB_DTYPE)
-        self.o_isb = o_isb
-        self.host = host
+    def __init__(self, sig, gen, ops, pinned, pkey, pending, res_pin, offs, history, tjobs,
+                 fix_args):
+        self.sig, self.gen, self.ops, self.pkey = sig, gen, ops, pkey
+        self.pinned, self.host = pinned, pinned.numpy()
+        self.offs, self.history, self.tjobs, self.fix_args = offs, history, tjobs, fix_args
         self.order = pending.order
         self.nbytes, self.xoff, self.table = pending.nbytes, pending.xoff, pending.table
-        self.fix = pending.fix
         self.res_pin = res_pin
+        n = self.order.size
+        o = offs["jobs"]
+        self.jobs_view = self.host[o:o + n * L.JOB_DTYPE.itemsize].view(L.JOB_DTYPE)
+        self.counts = None  # (n_below, n_above, rows) the staged pack holds
+        self.hist_rows = None
+        self.fix = None
 
     @staticmethod
     def signature(eng, works, prior_weight, lf, precision, outputs, stream, sample_only, pruned,
@@ -1590,22 +1743,75 @@ class _Replay(object):
             exchange = (int(exchange[0]), int(exchange[1]), int(exchange[2]),
                         np.asarray(exchange[3], np.int32).tobytes())
         # (the timer spec last: the rest is the staged pack's signature)
-        return (stream, works.key, works.n_below.tobytes(), works.n_above.tobytes(),
-                float(prior_weight), int(lf), int(precision), scorer, pruned,
-                np.size(is_below), history.vals.data_ptr(), history.active.data_ptr(), history.ld,
-                exchange, eng.side_stream, eng.table_scorer, eng.exact64,
+        return (stream, works.key, float(prior_weight), int(lf), int(precision), scorer, pruned,
+                history.vals.data_ptr(), history.active.data_ptr(), history.ld,
+                exchange, eng.side_stream, eng.table_scorer, eng.exact64, eng.lat_prefix,
+                eng.cat_early, eng.cat_issue, eng.device_events, eng.sorted_fit,
                 "off" if timers is None else
                 ("all" if timer_groups is None else frozenset(timer_groups)))
 
+    def _put(self, name, arr):
+        off = self.offs[name]
+        if off is not None and arr.size:
+            self.host[off:off + arr.nbytes] = arr.reshape(-1).view(np.uint8)
+
     def run(self, eng, batch, is_below, timers, defer):
+        """Re-issue the level for ``batch``; None when it cannot (the caller
+        then runs the full path)."""
         hm = eng.host_marks
         if hm is not None:
             hm.append(("start", time.perf_counter()))
-        oi = self.order
-        self.jobs["key"] = batch.keys[oi]
-        self.jobs["cand_base"] = batch.cand_base[oi]
-        self.host[self.o_isb:self.o_isb + self.nbytes_isb(is_below)] = \
-            np.asarray(is_below, np.uint8).reshape(-1)
+        isb = np.ascontiguousarray(is_below, dtype=np.uint8).reshape(-1)
+        n_rows = isb.size
+        counts = (batch.n_below.tobytes(), batch.n_above.tobytes(), n_rows)
+        if counts == self.counts and (self.history is None or
+                                      self.history.rows == self.hist_rows):
+            # the same counts as the staged pack's: keys, bases and flags only
+            oi = self.order
+            self.jobs_view["key"] = batch.keys[oi]
+            self.jobs_view["cand_base"] = batch.cand_base[oi]
+            self._put("isb", isb)
+            return self._issue(eng, timers, defer, self.jobs_view, hm)
+        P = eng._plans.get(self.pkey)
+        if P is None or self.pkey[-1] != eng._big64(self.pkey[4], batch.n_above):
+            return None
+        (_, _, _, fit_ids, _, nf, segs, _, n_obs_total, n_comp, max_obs, csegs, _, _, _,
+         cobs_off, _, _, _, _, _, g_arr) = eng._plan_fast(P, batch.n_below, batch.n_above)
+        jobs, _, fb_jobs = eng._jobs_fast(P, batch.keys, batch.cand_base)[:3]
+        pack_size = self.offs["isb"] + max(n_rows, 1)
+        gen0 = eng._gen
+        if pack_size > self.pinned.numel():
+            return None
+        eng._buf("stage", pack_size)
+        eng._presize(n_comp, n_obs_total, max_obs, cobs_off, len(segs), self.tjobs,
+                     n_rows if self.history is not None else 0)
+        if eng._gen != gen0:
+            return None
+        if self.history is not None:  # rows appended since: merged into the sorted orders
+            nfs = 2 * nf
+            self.history.ensure_order(eng, eng.torch.cuda.current_stream(eng.device),
+                                      g_arr["col"][:nfs:2], segs["transform"][::2],
+                                      segs["floor"][::2])
+        for name, arr in (("segs", segs), ("csegs", csegs), ("g", g_arr), ("jobs", jobs),
+                          ("fb", fb_jobs), ("isb", isb)):
+            self._put(name, arr)
+        keep = self.ops.keep  # the host copies the entry points validate
+        keep[0][...] = jobs
+        keep[1][...] = fb_jobs
+        if keep[2] is not None:
+            keep[2][...] = g_arr
+        self.ops.set_sizes(dict(n_rows=n_rows, max_obs=max_obs, n_obs_total=n_obs_total,
+                                max_comp=max_obs + 1, pack_size=pack_size))
+        self.counts = counts
+        self.hist_rows = self.history.rows if self.history is not None else None
+        band_jobs, d_segs, stream, exchanged = self.fix_args
+        self.fix = None
+        if band_jobs:
+            self.fix = functools.partial(eng._band_fix, band_jobs, d_segs, max_obs + 1, n_comp,
+                                         stream, exchanged)
+        return self._issue(eng, timers, defer, jobs, hm)
+
+    def _issue(self, eng, timers, defer, jobs, hm):
         if hm is not None:
             hm.append(("plan", time.perf_counter()))
         failed = ctypes.c_int(-1)
@@ -1621,13 +1827,9 @@ class _Replay(object):
         after = None
         if self.ops.timed and timers is not None:
             after = functools.partial(self.ops.read_timers, eng._hip, timers)
-        p = eng._inflight = _Pending(eng, eng._event("result"), self.res_pin, self.nbytes, oi,
-                                     self.xoff, self.table, after, self.fix, self.jobs)
+        p = eng._inflight = _Pending(eng, eng._event("result"), self.res_pin, self.nbytes,
+                                     self.order, self.xoff, self.table, after, self.fix, jobs)
         return p if defer else p.result()
-
-    @staticmethod
-    def nbytes_isb(is_below):
-        return np.size(is_below)
 
 
 class _Timed(object):
@@ -1641,6 +1843,17 @@ class _Timed(object):
 
     def elapsed_time(self, _end):
         return self.ms
+
+
+class _V(int):
+    """A size argument of a level's launches (history rows, observation totals,
+    the largest mixture, the pack size): an int to ctypes, and a named word
+    to _OpList, which notes where it sits so a re-issue can rewrite it."""
+
+    def __new__(cls, name, value):
+        v = super().__new__(cls, int(value))
+        v.name = name
+        return v
 
 
 def _word(a):
@@ -1709,18 +1922,39 @@ class _OpList(_Timing):
 
     def finish(self, keep):
         arr = np.zeros(len(self.rows), L.OP_DTYPE)
+        self.sizes = []  # (record, argument, size name): the words _Replay rewrites
         for i, (code, args) in enumerate(self.rows):
             if len(args) > L.OP_ARGS:
                 raise ValueError("op %d has %d arguments" % (code, len(args)))
             arr["code"][i], arr["n_args"][i] = code, len(args)
             arr["a"][i, :len(args)] = [_word(a) for a in args]
+            self.sizes += [(i, j, a.name) for j, a in enumerate(args) if isinstance(a, _V)]
         self.arr, self.keep, self.rows = arr, keep, None
         self.ptr, self.n = arr.ctypes.data, len(arr)
+
+    def set_sizes(self, values):
+        """Rewrite the size words of the records (names of _V arguments)."""
+        a = self.arr["a"]
+        for i, j, name in self.sizes:
+            a[i, j] = values[name]
 
     def destroy(self, hip):
         for h in self.events:
             hip.hipEventDestroy(h)
         self.events = []
+
+
+def _lat_prefix(text):
+    """TPE_LAT_PREFIX: 0 (every stream drawn in full) or a positive multiple
+    of 4096 (tpe_lattice_suggest's prefix); anything else is an error here,
+    not a failed launch later."""
+    try:
+        v = int(text)
+    except ValueError:
+        raise ValueError("TPE_LAT_PREFIX must be an integer, got %r" % (text,))
+    if v < 0 or v % 4096:
+        raise ValueError("TPE_LAT_PREFIX must be 0 or a positive multiple of 4096, got %d" % v)
+    return v
 
 
 def _raise_errors(err):

@@ -252,13 +252,19 @@ def _smallest_rows(losses, n):
     return out
 
 
+FP32_MIN_CAND = 1 << 16  # engine.TABLE_MIN_CAND: the cell-table path's threshold
+
+
 def _precision(precision, n_ei, T):
     if precision is None:
         env = os.environ.get("HYPEROPT_AMD_PRECISION", "")
         if env:
             precision = int(env)
         else:
-            precision = 64 if n_ei * max(T, 1) <= (1 << 24) else 32
+            # fp32 only where the table path runs (its argmax is made exact by
+            # the band re-score, tpe_band_rescore); every smaller or cheaper
+            # level is scored exactly in fp64
+            precision = 32 if (n_ei >= FP32_MIN_CAND and n_ei * max(T, 1) > (1 << 24)) else 64
     if precision not in (32, 64):
         raise ValueError("precision must be 32 or 64", precision)
     return precision

@@ -202,6 +202,41 @@ int tpe_gather_obs_multi(const tpe_history* hists, const tpe_history* host_hists
                          const tpe_gather* host_gathers, int n_gathers, double* obs_f64,
                          int64_t* obs_i64, int32_t* err, void* stream);
 
+/* ---- sorted history: the Parzen fit without a per-suggest sort ------------
+ * adaptive_parzen_normal (tpe.py:399-467) sorts each below / above set; both
+ * are subsets of the label's history, and a stable sort of a subset is the
+ * history's stable order with the other rows left out.  The history keeps,
+ * for every fitted column, its rows sorted by (transformed value, row) in
+ * `order` (label-major like vals: column col's order at order + col * ld);
+ * tpe_history_order merges rows [n_old, n_old + n_new) (n_new <= 2048 per
+ * call) into the order of rows [0, n_old) -- O(rows) per append.  The
+ * transform is the fit's: log(max(v, floor)) for TPE_OBS_LOG (NaN last).
+ * scratch: tpe_history_order_scratch_bytes(n_specs, n_old + n_new) bytes. */
+typedef struct tpe_colspec {
+  int32_t col;          /* history column                                    */
+  int32_t transform;    /* TPE_OBS_*                                         */
+  double floor;         /* TPE_OBS_LOG: log(max(v, floor))                   */
+} tpe_colspec;
+int64_t tpe_history_order_scratch_bytes(int n_specs, int64_t n_rows);
+int tpe_history_order(const double* vals, int64_t ld, const tpe_colspec* specs,
+                      const tpe_colspec* host_specs, int n_specs, int64_t n_old, int64_t n_new,
+                      int32_t* order, void* scratch, void* stream);
+/* The fit of segment i (segs[i]) from the sorted history: gathers[i] names its
+ * column, side (below: 1) and observation count (identity row list: row r of
+ * the history is position r, is_below[r] its split flag, n_rows of them).
+ * One kernel: the segment's rows in tid order (linear-forgetting positions,
+ * the prior's searchsorted slot), the column's order compacted to the
+ * segment (means and weights in sorted order), then bandwidths, p_accept and
+ * the coefficients exactly as tpe_parzen_fit computes them (same bits).  A
+ * count other than gathers[i].count sets bit 4 of *err (nothing written).
+ * scratch: tpe_fit_sorted_scratch_bytes(n_seg, n_rows) bytes. */
+int64_t tpe_fit_sorted_scratch_bytes(int n_seg, int64_t n_rows);
+int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t ld, const int32_t* order,
+                   int64_t n_rows, const uint8_t* is_below, const tpe_gather* gathers,
+                   const tpe_gather* host_gathers, tpe_seg* segs, int n_seg, void* scratch,
+                   double* w, double* mu, double* sigma, double* wcdf, double* coef64,
+                   float* coef32, int32_t* err, void* stream);
+
 /* ---- categorical posterior (tpe.py:578-615) ------------------------------ */
 /* p_pool: probabilities (mode 1 also reads the prior p from it at
  * prior_p_off); logp_pool / cdf_pool: log p and cumulative p at p_off.
@@ -512,6 +547,8 @@ enum {
   TPE_OP_MAXLOC_ALLREDUCE,     /* tpe_maxloc_allreduce (RCCL, stream-ordered) */
   TPE_OP_LATTICE_SUGGEST,      /* tpe_lattice_suggest                        */
   TPE_OP_BAND_RESCORE,         /* tpe_band_rescore                           */
+  TPE_OP_FIT_SORTED,           /* tpe_fit_sorted                             */
+  TPE_OP_HISTORY_ORDER,        /* tpe_history_order                          */
   TPE_OP_COUNT
 };
 #define TPE_OP_ARGS 23
@@ -531,7 +568,7 @@ int64_t tpe_smallest_rows(const double* losses, int64_t n, int64_t k, int64_t* o
 const char* tpe_last_error(void);
 int tpe_abi_version(void);
 /* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table, tpe_gather,
- * tpe_history, tpe_prior, tpe_op) to out[0..n); returns 9 */
+ * tpe_history, tpe_prior, tpe_op, tpe_band, tpe_colspec) to out[0..n); returns 11 */
 int tpe_struct_sizes(int32_t* out, int n);
 
 #ifdef __cplusplus

@@ -31,12 +31,14 @@ def test_header_symbols_exported():
 def test_struct_sizes_and_abi():
     lib = L.load()
     assert lib.tpe_abi_version() == L.ABI_VERSION == 14
-    sizes = (ctypes.c_int32 * 9)()
-    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 9) == 9
+    sizes = (ctypes.c_int32 * 11)()
+    assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 11) == 11
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
                             L.JOB_DTYPE.itemsize, L.BEST_DTYPE.itemsize, L.TABLE_DTYPE.itemsize,
                             L.GATHER_DTYPE.itemsize, L.HISTORY_DTYPE.itemsize,
-                            L.PRIOR_DTYPE.itemsize, L.OP_DTYPE.itemsize)
+                            L.PRIOR_DTYPE.itemsize, L.OP_DTYPE.itemsize, L.BAND_DTYPE.itemsize,
+                            L.COLSPEC_DTYPE.itemsize)
+    assert L.BAND_DTYPE.itemsize == 16 and L.COLSPEC_DTYPE.itemsize == 16
     assert L.OP_DTYPE.itemsize == 192
 
 

@@ -170,3 +170,36 @@ def test_plan_units_partition():
     mean = sum(cost) / 8
     assert max(cost) - mean <= 1.0
     assert all(c == 1 << 22 for u in plan for _, _, c in u)
+
+
+def _empty_rank_worker(rank, world, port, q):
+    """A one-label level with n_EI = 24 on 4 ranks: the plan leaves rank 3
+    without units; it must still join the winners' all-gather
+    (tpe.suggest skips the engine for it) so the other ranks do not hang."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    units = hdist.plan_units(["uniform"], 24, world)[rank]
+    local = [(i, LabelResult("x", start + 1, 0.1 * (start + 1), float(start), count))
+             for i, start, count in units]
+    q.put((rank, len(units), hdist.gather_best(1, local)))
+    dist.destroy_process_group()
+
+
+def test_rank_without_units_joins_the_gather():
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_rank_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: (n, best) for r, n, best in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [out[r][0] for r in range(world)] == [1, 1, 1, 0]
+    for r in range(world):  # the highest-scoring shard (start 16) wins everywhere
+        assert out[r][1] == [(16.0, 17, 0.1 * 17, 24)]

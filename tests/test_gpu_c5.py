@@ -144,3 +144,40 @@ def test_nested_suggest_at_100k_rescored_by_oracle(engine, nested_100k, seed):
     assert n_levels >= 2
     live = {lab for lab, v in got.items() if v}
     assert live == set(walk)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "normal"])
+def test_c5_size_fp32_suggest_path_is_the_exact_argmax(kind):
+    """BASELINE configs[4] at its stated size on one label: a 100k-trial
+    history (above mixture ~1e5 components) and 2^24 EI candidates through the
+    fp32 suggest path (cell table, score cubics, exact fp64 re-score of the
+    band): the winner is np.argmax (tpe.py:649-658) over the exact fp64 scores
+    of the same 2^24 candidates (the stream materialised by sample_only,
+    scored by the pruned fp64 kernel) -- index, value and score -- and the
+    winner and runner-up agree with the oracle."""
+    from hyperopt_amd.engine import Engine, LabelWork
+    eng = Engine()
+    rng = np.random.RandomState(5 + len(kind))
+    obs = _obs(kind, T, rng)
+    losses = rng.normal(size=T)
+    below, above = O.ap_split_trials(np.arange(T), obs, np.arange(T), losses, 0.25)
+    n = 1 << 24
+    w = LabelWork("x", kind, ARGS[kind], below, above, n_cand=n, key=0xC5)
+    r, = eng.run([w], precision=32)
+    assert eng.last_table_stats is not None and r.n_scored == n
+    s, = eng.run([w], precision=32, sample_only=True)
+    cand = s.cand
+    eng.exact64 = "pruned"
+    x, = eng.run([LabelWork("x", kind, ARGS[kind], below, above, cand=cand)], precision=64,
+                 outputs=True)
+    s64 = x.below_llik - x.above_llik
+    best = int(np.argmax(s64))
+    assert r.index == best, (r.index, best, s64[r.index], s64[best])
+    assert r.value == cand[best]
+    np.testing.assert_allclose(r.score, s64[best], rtol=1e-12, atol=1e-12)
+    second = int(np.argmax(np.where(np.arange(n) == best, -np.inf, s64)))
+    pick = np.array([best, second])
+    with np.errstate(all="ignore"):
+        ref = O.continuous_label_scores(kind, ARGS[kind], below, above, cand[pick])
+    np.testing.assert_allclose(ref["below_llik"] - ref["above_llik"], s64[pick], rtol=1e-6,
+                               atol=1e-9)

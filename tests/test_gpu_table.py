@@ -198,12 +198,12 @@ def test_table_winner_at_c3_size_is_the_exact_argmax(engine, kind, args, gen, se
 @pytest.mark.parametrize("kind,args,gen", C3_KINDS[:2])
 def test_table_band_overflow_rescored_exactly(kind, args, gen, monkeypatch):
     """More candidates within the fp32 error bound of the maximum than the
-    band holds (BAND_CAP shrunk to 64 here; on real histories a plateau of
+    band holds (BAND_CAP shrunk to 2 here; on real histories a plateau of
     near-equal scores): the engine re-scores that label's whole fp32 stream in
     fp64 (tpe_score_pruned64 with TPE_F_DRAW32) -- the winner is still the
     exact argmax."""
     import hyperopt_amd.engine as E
-    monkeypatch.setattr(E, "BAND_CAP", 64)
+    monkeypatch.setattr(E, "BAND_CAP", 2)
     eng = E.Engine()
     T, n = 10_000, 1 << 20
     rng = np.random.RandomState(41)

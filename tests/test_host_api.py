@@ -227,6 +227,9 @@ def test_label_key_and_precision():
     assert tpe.label_key(1, "x") != tpe.label_key(1, "y")
     assert tpe._precision(None, 24, 100) == 64
     assert tpe._precision(None, 1 << 22, 10_000) == 32
+    # fp32 only where the cell-table path (exact argmax by the band re-score) runs
+    assert tpe._precision(None, 4096, 1_000_000) == 64
+    assert tpe._precision(None, 1 << 16, 1_000) == 32
     with pytest.raises(ValueError):
         tpe._precision(16, 1, 1)
 
@@ -332,3 +335,13 @@ def test_smallest_rows_is_stable_argsort_prefix():
                 want = np.sort(np.argsort(x, kind="stable")[:n])
                 got = np.sort(_smallest_rows(x, n))
                 np.testing.assert_array_equal(got, want, err_msg="%s T=%d n=%d" % (kind, T, n))
+
+
+def test_lat_prefix_setting_is_validated():
+    """TPE_LAT_PREFIX (engine.lat_prefix): 0 or a multiple of 4096, checked
+    when the engine reads it, not at the first quantized launch."""
+    from hyperopt_amd.engine import _lat_prefix
+    assert _lat_prefix("0") == 0 and _lat_prefix("65536") == 65536
+    for bad in ("1000", "-4096", "abc"):
+        with pytest.raises(ValueError):
+            _lat_prefix(bad)

@@ -13,7 +13,7 @@ for v in "$@"; do
   defs=$(echo "$v" | sed 's/^/-D/; s/,/ -D/g')
   name=$(echo "$v" | sed 's/TPE_DIAG_//g; s/TPE_//g; s/,/+/g; s/=/_/g')
   objs=""
-  for f in tpe_fit tpe_parzen tpe_score tpe_table tpe_history tpe_prior tpe_dist tpe_util tpe_ops; do
+  for f in tpe_fit tpe_parzen tpe_score tpe_table tpe_history tpe_sorted tpe_prior tpe_dist tpe_util tpe_ops; do
     /opt/rocm/bin/hipcc $F $defs -c $C/$f.hip -o /tmp/diag_${name}_$f.o
     objs="$objs /tmp/diag_${name}_$f.o"
   done

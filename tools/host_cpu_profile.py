@@ -45,7 +45,7 @@ class _Event(object):
 
 def _torch_shim():
     t = types.SimpleNamespace()
-    for name in ("uint8", "float64", "int64", "from_numpy", "device"):
+    for name in ("uint8", "float64", "int64", "int32", "from_numpy", "device"):
         setattr(t, name, getattr(torch, name))
 
     def empty(*shape, dtype=None, device=None, pin_memory=False):
@@ -101,19 +101,20 @@ def make_engine():
     eng.exact64 = "auto"
     eng.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
     eng.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
-    eng.lat_early = os.environ.get("TPE_LAT_EARLY", "0") == "1"
     eng.lat_prefix = int(os.environ.get("TPE_LAT_PREFIX", str(E.LAT_PREFIX)))
     eng.device_events = True
-    eng.graphs = False
-    eng._graphs, eng._last_gkey, eng._gen, eng._own = {}, None, 0, None
-    eng.graph_stats = {"captured": 0, "replayed": 0, "eager": 0}
+    eng.sorted_fit = os.environ.get("TPE_SORTED_FIT", "1") == "1"
+    eng._last_gkey, eng._gen = None, 0
+    eng.graph_stats = {"eager": 0}
     eng.native = os.environ.get("TPE_NATIVE_LAUNCH", "1") != "0"
     eng._oplists, eng._oplist_once, eng._replays, eng._staged_sig = {}, None, {}, None
     E.torch_shim = shim
     return eng
 
 
-def main(world=1, rank=0, prof=False):
+def main(world=1, rank=0, prof=False, append=False):
+    """append: one trial appended to the history before every step (as fmin
+    does): new counts every level, re-issued records (engine._Replay)."""
     eng = make_engine()
     space = bench.c3_space()
     vals, losses = bench.c3_history(space)
@@ -121,12 +122,20 @@ def main(world=1, rank=0, prof=False):
     hist = E.DeviceHistory(eng, len(space), cap=bench.T_HIST)
     hist.append(mat)
     units = hdist.plan_units([k for _, k, _ in space], bench.N_CAND, world)[rank]
+    extra = np.random.RandomState(5)
+    state = {"mat": mat, "losses": losses}
 
     def step(k):
-        rb = bench.below_rows(losses)
-        isb = np.zeros(bench.T_HIST, np.uint8)
+        if append:
+            row = state["mat"][extra.randint(state["mat"].shape[0])][None]
+            hist.append(row)
+            state["mat"] = np.concatenate([state["mat"], row])
+            state["losses"] = np.append(state["losses"], extra.normal())
+        lo, m = state["losses"], state["mat"]
+        rb = bench.below_rows(lo)
+        isb = np.zeros(lo.size, np.uint8)
         isb[rb] = 1
-        works = bench.history_batch(space, mat, hist, rb, k, bench.N_CAND, 0, units,
+        works = bench.history_batch(space, m, hist, rb, k, bench.N_CAND, 0, units,
                                     bench.N_CAND)
         return eng.run(works, precision=32, history=hist, is_below=isb)
     for k in range(5):
@@ -136,8 +145,9 @@ def main(world=1, rank=0, prof=False):
     for k in range(n):
         step(10 + k)
     dt = (time.perf_counter() - t0) / n
-    print("world %d rank %d (%d units): host %.1f us per step, native %s" % (
-        world, rank, len(units), dt * 1e6, eng.graph_stats.get("native", 0) > 0))
+    print("world %d rank %d (%d units)%s: host %.1f us per step, stats %s" % (
+        world, rank, len(units), " +1 trial per step" if append else "", dt * 1e6,
+        eng.graph_stats))
     if prof:
         pr = cProfile.Profile()
         pr.enable()
@@ -183,4 +193,5 @@ if __name__ == "__main__":
     if "--marks" in sys.argv:
         marks(*(int(a) for a in args))
     else:
-        main(*(int(a) for a in args), prof="--cprofile" in sys.argv)
+        main(*(int(a) for a in args), prof="--cprofile" in sys.argv,
+             append="--append" in sys.argv)

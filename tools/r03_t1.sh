@@ -1,5 +1,6 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_table.py -x -v --timeout 240 --timeout-method thread > gpurun_out/r03_t1_table.log 2>&1 || exit 1
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r03_t1_gpu_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_sorted_fit.py tests/test_gpu_table.py tests/test_gpu_history.py -x -v --timeout 240 --timeout-method thread > gpurun_out/r03_t1_new.log 2>&1 || exit 1
 timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/r03_t1_bench.json 2> gpurun_out/r03_t1_bench.err || exit 1
+bash tools/r03_variants.sh r03_var base NO_BAND PHILOX_ROUNDS_7 NO_PHILOX NO_COMP NO_BM SKIP_SCORE NO_RETRY || exit 1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r03_t1_gpu_tests.log 2>&1 || exit 1
