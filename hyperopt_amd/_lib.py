@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -101,7 +101,8 @@ _SIGNATURES = {
                              _P, _P, _P]),
     "tpe_score_table_fast": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P,
                                   _P, _I64, _P, _P]),
-    "tpe_band_rescore": (_I, [_P, _P, _I, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]),
+    "tpe_band_rescore": (_I, [_P, _P, _I, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P]),
+    "tpe_band_work_bytes": (_I64, [_I]),
     "tpe_history_order_scratch_bytes": (_I64, [_I, _I64]),
     "tpe_history_order": (_I, [_P, _I64, _P, _P, _I, _I64, _I64, _P, _P, _P]),
     "tpe_fit_sorted_scratch_bytes": (_I64, [_I, _I64]),

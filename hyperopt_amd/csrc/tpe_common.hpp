@@ -214,4 +214,10 @@ __device__ __forceinline__ double obs_transform(double v, int transform, double 
 // float -> ordered position inside a 64-lane wave's work split
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
+// the fit's bandwidth / coefficient launches (tpe_parzen.hip), shared by
+// tpe_parzen_fit and tpe_fit_sorted
+int64_t fit_part_doubles(int max_obs);
+void fit_tail(tpe_seg* segs, int n_seg, int max_obs, double* part, double* w, const double* mu,
+              double* sigma, double* wcdf, double* coef64, float* coef32, hipStream_t st);
+
 }  // namespace tpe

@@ -485,6 +485,21 @@ __global__ __launch_bounds__(kFitBS) void k_fit_prune(tpe_seg* __restrict__ segs
   for (int k = k0; k < k1; ++k) sm[off + k] = fminf(sm[off + k], after);
 }
 }  // namespace
+
+// K3-K5 over mixtures whose means and raw weights are in place (prior_pos
+// set): shared with tpe_fit_sorted (tpe_sorted.hip), whose compaction
+// replaces K1-K2.  part: n_seg * fit_part_doubles(max_obs) doubles.
+int64_t fit_part_doubles(int max_obs) { return comp_tiles(max_obs) * kPartStride; }
+void fit_tail(tpe_seg* segs, int n_seg, int max_obs, double* part, double* w, const double* mu,
+              double* sigma, double* wcdf, double* coef64, float* coef32, hipStream_t st) {
+  const FitScratch sc{nullptr, nullptr, nullptr, part};
+  const int gc = (int)comp_tiles(max_obs);
+  hipLaunchKernelGGL(k_fit_comp, dim3(gc, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu, sigma);
+  hipLaunchKernelGGL(k_fit_coef, dim3(gc, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu, sigma,
+                     wcdf, coef64);
+  hipLaunchKernelGGL(k_fit_coef32, dim3(gc, n_seg), dim3(kFitBS), 0, st, segs, sc, coef64,
+                     coef32);
+}
 }  // namespace tpe
 
 using namespace tpe;
@@ -538,12 +553,7 @@ extern "C" int tpe_parzen_fit(const double* obs, void* scratch, tpe_seg* segs, i
                        (size_t)8 * std::max(max_obs, 1), st, segs, sc, w, mu);
   else
     hipLaunchKernelGGL(k_fit_rank<false>, dim3(gr, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu);
-  const int gc = (int)comp_tiles(max_obs);
-  hipLaunchKernelGGL(k_fit_comp, dim3(gc, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu, sigma);
-  hipLaunchKernelGGL(k_fit_coef, dim3(gc, n_seg), dim3(kFitBS), 0, st, segs, sc, w, mu, sigma,
-                     wcdf, coef64);
-  hipLaunchKernelGGL(k_fit_coef32, dim3(gc, n_seg), dim3(kFitBS), 0, st, segs, sc, coef64,
-                     coef32);
+  fit_tail(segs, n_seg, max_obs, sc.part, w, mu, sigma, wcdf, coef64, coef32, st);
   if (prune)
     hipLaunchKernelGGL(k_fit_prune, dim3(n_seg), dim3(kFitBS), 0, st, segs, mu, sigma, coef64,
                        coef32, coef32n, wide32, pm, sm);

@@ -7,7 +7,8 @@
 // its rows sorted by (transformed value, row) -- updated when trials are
 // appended (tpe_history_order: the new rows sorted in LDS, then merged into
 // the existing order, O(T) per append instead of O(T log T) per suggest) --
-// and a suggest's fit is one kernel per segment (tpe_fit_sorted):
+// and a suggest's fit (tpe_fit_sorted) is one compaction block per segment,
+// then the fit's bandwidth / coefficient launches:
 //
 //   1. rows in row (tid) order: which belong to the segment (active for the
 //      label, on its side of the split), each one's position in the segment's
@@ -17,10 +18,9 @@
 //   2. the column's sorted order compacted to the segment: means and ramp
 //      weights in sorted order, the prior inserted at its slot;
 //   3. bandwidths and clip (tpe.py:430-459), normalisation, p_accept
-//      (tpe.py:145-150), fp64 / fp32 coefficients and cumulative weights --
-//      the arithmetic of k_fit_comp / k_fit_coef / k_fit_coef32 in
-//      tpe_parzen.hip, with its reduction order (256-component tiles, the
-//      same wave butterflies and tile folds), so both fits give the same bits.
+//      (tpe.py:145-150), fp64 / fp32 coefficients and cumulative weights:
+//      the multi-kernel fit's own launches (fit_tail, tpe_parzen.hip), many
+//      blocks per segment, so both fits give the same bits.
 //
 // Rows are ordered by (key(transform(v)), row): row order is tid order for an
 // identity row list, and ties keep tid order -- np.argsort(kind="stable") of
@@ -34,12 +34,9 @@ namespace {
 constexpr int kSB = 1024;            // block size of every kernel here
 constexpr int kSWaves = kSB / kWave;
 constexpr int kNew = 2048;           // new rows sorted per tpe_history_order call
-constexpr int kTileF = 256;          // reduction tile of the multi-kernel fit (kFitBS)
 constexpr int kRowsPT = 16;          // rows per thread per compaction pass
 constexpr int kPass = kRowsPT * kSB; // rows per compaction pass
 constexpr int kSlots = kRowsPT * kSWaves;
-constexpr int kMaxTiles = 512;       // components per segment <= kMaxTiles * kTileF
-constexpr double kSqrt2Pi = 2.5066282746310002;
 
 __device__ __forceinline__ uint64_t row_key(const double* __restrict__ V, int64_t row,
                                             const tpe_colspec& C) {
@@ -195,59 +192,16 @@ __device__ int64_t block_compact(int64_t n, Take take, Emit emit, int* wsum, int
   return *carry_s;
 }
 
-// The 256-thread block_sum of tpe_parzen.hip over values held by threads
-// 0..255 (the other threads pass 0): wave butterflies, then the four wave
-// totals in order.  Called by every thread; every thread gets the sum.
-__device__ __forceinline__ double sum256(double v, double* sh) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
-  __syncthreads();
-  const int wid = threadIdx.x / kWave;
-  if (lane_id() == 0 && wid < 4) sh[wid] = v;
-  __syncthreads();
-  double r = sh[0];
-  r += sh[1];
-  r += sh[2];
-  r += sh[3];
-  __syncthreads();
-  return r;
-}
-
-// the per-tile wave totals of one pass: tile (4 waves) sums in wave order,
-// as block_sum<256> folds them
-__device__ __forceinline__ void tile_sums(double v, double* wt, double* out, int tile0,
-                                          int tiles) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
-  const int wid = threadIdx.x / kWave;
-  if (lane_id() == 0) wt[wid] = v;
-  __syncthreads();
-  if (threadIdx.x < kSB / kTileF) {
-    const int t = tile0 + (int)threadIdx.x;
-    if (t < tiles) {
-      double r = wt[4 * threadIdx.x];
-      r += wt[4 * threadIdx.x + 1];
-      r += wt[4 * threadIdx.x + 2];
-      r += wt[4 * threadIdx.x + 3];
-      out[t] = r;
-    }
-  }
-  __syncthreads();
-}
-
 __global__ __launch_bounds__(kSB) void k_fit_sorted(
     const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
     const int32_t* __restrict__ order, int64_t n_rows, const uint8_t* __restrict__ is_below,
     const tpe_gather* __restrict__ gathers, tpe_seg* __restrict__ segs,
     int32_t* __restrict__ gi_scr, double* __restrict__ w, double* __restrict__ mu,
-    double* __restrict__ sigma, double* __restrict__ wcdf, double* __restrict__ coef64,
-    float* __restrict__ coef32, int32_t* __restrict__ err) {
+    int32_t* __restrict__ err) {
   __shared__ int wsum[kSlots + kSlots / kWave];
   __shared__ int64_t carry_s;
-  __shared__ double sh[4], wt[kSWaves];
-  __shared__ double p_w[kMaxTiles], p_d[kMaxTiles], p_l[kMaxTiles];
   __shared__ int s_lt;
-  __shared__ double s_x0, shm[kSWaves];
+  __shared__ double s_x0;
   tpe_seg* S = segs + blockIdx.x;
   const tpe_gather G = gathers[blockIdx.x];
   const int64_t col = G.col;
@@ -311,132 +265,6 @@ __global__ __launch_bounds__(kSB) void k_fit_sorted(
     w[coff + prior_pos] = S->prior_weight;
     S->prior_pos = prior_pos;
   }
-  __syncthreads();  // (block-scope: the means and weights are visible to the block)
-  // 3. bandwidths + per-tile sums (k_fit_comp)
-  const int nc = nn + 1;
-  const int tiles = (nc + kTileF - 1) / kTileF;
-  const double ps = S->prior_sigma;
-  for (int k0 = 0; k0 < nc; k0 += kSB) {
-    const int k = k0 + threadIdx.x;
-    double wk = 0.0, dphi = 0.0;
-    if (k < nc) {
-      double s;
-      if (nn == 0) {
-        s = ps;
-      } else if (nn == 1) {
-        s = (k == prior_pos) ? ps : ps * 0.5;
-      } else if (k == 0) {
-        s = mu[coff + 1] - mu[coff];
-      } else if (k == nc - 1) {
-        s = mu[coff + nc - 1] - mu[coff + nc - 2];
-      } else {
-        s = fmax(mu[coff + k] - mu[coff + k - 1], mu[coff + k + 1] - mu[coff + k]);
-      }
-      const double lo_clip = ps / fmin(100.0, 1.0 + (double)nc);  // tpe.py:455
-      s = fmin(fmax(s, lo_clip), ps);
-      if (k == prior_pos) s = ps;
-      sigma[coff + k] = s;
-      wk = w[coff + k];
-      if (S->bounded) {
-        const double m = mu[coff + k];
-        dphi = normal_cdf(S->high, m, s) - normal_cdf(S->low, m, s);
-      }
-    }
-    tile_sums(wk, wt, p_w, k0 / kTileF, tiles);
-    tile_sums(wk * dphi, wt, p_d, k0 / kTileF, tiles);
-  }
-  __syncthreads();
-  // 4. normalisation, p_accept, coefficients, cumulative weights (k_fit_coef)
-  double a = 0.0, b = 0.0;
-  if (threadIdx.x < kTileF)
-    for (int t = threadIdx.x; t < tiles; t += kTileF) {
-      a += p_w[t];
-      b += p_d[t];
-    }
-  const double wsum_ = sum256(a, sh);
-  const double pacc = S->bounded ? sum256(b, sh) / wsum_ : 1.0;
-  const bool lg = S->family == TPE_LGMM1;
-  for (int k0 = 0; k0 < nc; k0 += kSB) {
-    const int k = k0 + threadIdx.x;
-    const int tile = k / kTileF;  // this pass holds tiles k0/256 .. k0/256 + 3
-    double wr = 0.0, lmax = -INFINITY;
-    if (k < nc) {
-      wr = w[coff + k];
-      const double wk = wr / wsum_;
-      w[coff + k] = wk;
-      const double m = mu[coff + k], s = sigma[coff + k];
-      double lc, inv;
-      if (lg) {  // LGMM1_lpdf: no p_accept (tpe.py:284-287)
-        const double sp = fmax(s, kEps);
-        lc = log(wk) - log(sp * kSqrt2Pi);
-        inv = 1.0 / sp;
-      } else {  // GMM1_lpdf (tpe.py:152-158)
-        const double z = sqrt(kTwoPi * (s * s));
-        lc = log(wk / z / pacc);
-        inv = 1.0 / fmax(s, kEps);
-      }
-      double* c = coef64 + 4 * (coff + k);
-      c[0] = m;
-      c[1] = inv;
-      c[2] = lc;
-      c[3] = wk;
-      lmax = lc * kLog2e;
-    }
-    // inclusive scan of the raw weights inside the 256-tile (wave shfl_up, then
-    // the tile's earlier waves in order), plus the earlier tiles' total
-    const int lane = lane_id(), wid = threadIdx.x / kWave;
-    double v = wr;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const double u = __shfl_up(v, o, kWave);
-      if (lane >= o) v += u;
-    }
-    if (lane == kWave - 1) wt[wid] = v;
-    __syncthreads();
-    for (int q = wid & ~3; q < wid; ++q) v += wt[q];
-    // the tile's base: block_sum<256> of the earlier tiles' sums (k_fit_coef's `before`)
-    double base = 0.0;
-    for (int tt = k0 / kTileF; tt < k0 / kTileF + kSB / kTileF; ++tt) {
-      double bt = 0.0;
-      if (threadIdx.x < kTileF)
-        for (int t = threadIdx.x; t < tiles; t += kTileF)
-          if (t < tt) bt += p_w[t];
-      bt = sum256(bt, sh);
-      if (tt == tile) base = bt;
-    }
-    if (k < nc) wcdf[coff + k] = (base + v) / wsum_;
-    // per-tile max of the log2 coefficients
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) lmax = fmax(lmax, __shfl_xor(lmax, off, kWave));
-    __syncthreads();
-    if (lane == 0) wt[wid] = lmax;
-    __syncthreads();
-    if (threadIdx.x < kSB / kTileF && k0 / kTileF + (int)threadIdx.x < tiles) {
-      const int q = 4 * threadIdx.x;
-      p_l[k0 / kTileF + threadIdx.x] = fmax(fmax(fmax(wt[q], wt[q + 1]), wt[q + 2]), wt[q + 3]);
-    }
-    __syncthreads();
-  }
-  // 5. fp32 coefficients (k_fit_coef32)
-  double mx = -INFINITY;
-  for (int t = threadIdx.x; t < tiles; t += kSB) mx = fmax(mx, p_l[t]);
-  const double cmax = block_max<kSB, double>(mx, shm);
-  const double center = (double)(float)pmu;
-  const double sq = 0.8493218002880191;  // sqrt(0.5 * log2(e))
-  for (int k = threadIdx.x; k < nc; k += kSB) {
-    const double* c = coef64 + 4 * (coff + k);
-    const double a32 = c[1] * sq;
-    float* f = coef32 + 4 * (coff + k);
-    f[0] = (float)a32;
-    f[1] = (float)(-(c[0] - center) * a32);
-    f[2] = (float)(c[2] * kLog2e - cmax);
-    f[3] = 0.0f;
-  }
-  if (threadIdx.x == 0) {
-    S->p_accept = pacc;
-    S->cmax = cmax;
-    S->center = center;
-  }
 }
 }  // namespace
 }  // namespace tpe
@@ -483,9 +311,15 @@ extern "C" int tpe_history_order(const double* vals, int64_t ld, const tpe_colsp
   return check_launch("tpe_history_order");
 }
 
+// scratch: the per-row list positions (int32 per segment and row), then the
+// fit tail's tile partials (counts are <= n_rows)
+static int64_t gi_bytes(int n_seg, int64_t n_rows) {
+  return (4 * (int64_t)std::max(n_seg, 1) * std::max<int64_t>(n_rows, 1) + 255) / 256 * 256;
+}
 extern "C" int64_t tpe_fit_sorted_scratch_bytes(int n_seg, int64_t n_rows) {
-  if (n_seg < 0 || n_rows < 0) return -1;
-  return 4 * (int64_t)std::max(n_seg, 1) * std::max<int64_t>(n_rows, 1);
+  if (n_seg < 0 || n_rows < 0 || n_rows > INT32_MAX) return -1;
+  return gi_bytes(n_seg, n_rows) +
+         8 * (int64_t)std::max(n_seg, 1) * fit_part_doubles((int)n_rows);
 }
 
 extern "C" int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t ld,
@@ -507,14 +341,18 @@ extern "C" int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t
   }
   for (int i = 0; i < n_seg; ++i) {
     const tpe_gather& g = host_gathers[i];
-    if (g.col < 0 || g.to_int || g.count < 0 || g.count + 1 > (int64_t)kMaxTiles * kTileF) {
-      set_error("tpe_fit_sorted: segment %d: column %d, count %lld (at most %d observations)",
-                i, g.col, (long long)g.count, kMaxTiles * kTileF - 1);
+    if (g.col < 0 || g.to_int || g.count < 0 || g.count > n_rows) {
+      set_error("tpe_fit_sorted: segment %d: column %d, count %lld (at most n_rows = %lld "
+                "observations)", i, g.col, (long long)g.count, (long long)n_rows);
       return TPE_E_ARG;
     }
   }
-  hipLaunchKernelGGL(k_fit_sorted, dim3(n_seg), dim3(kSB), 0, (hipStream_t)stream, vals, active,
-                     ld, order, n_rows, is_below, gathers, segs,
-                     reinterpret_cast<int32_t*>(scratch), w, mu, sigma, wcdf, coef64, coef32, err);
+  int max_obs = 0;
+  for (int i = 0; i < n_seg; ++i) max_obs = std::max(max_obs, (int)host_gathers[i].count);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_fit_sorted, dim3(n_seg), dim3(kSB), 0, st, vals, active, ld, order, n_rows,
+                     is_below, gathers, segs, reinterpret_cast<int32_t*>(scratch), w, mu, err);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(scratch) + gi_bytes(n_seg, n_rows));
+  fit_tail(segs, n_seg, max_obs, part, w, mu, sigma, wcdf, coef64, coef32, st);
   return check_launch("tpe_fit_sorted");
 }

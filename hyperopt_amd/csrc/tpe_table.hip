@@ -1025,7 +1025,7 @@ __device__ __forceinline__ double cand_value(float y, bool lgmm) {
 // bound s32 - eps goes into the job's running maximum G (atomic max on its
 // order code), and every candidate of the block whose upper bound s32 + eps
 // reaches the G known at that point is appended to the job's band list for
-// k_band_rescore (its value re-drawn: a draw is a function of its index).
+// the band kernels (k_band_select / k_band_expand / k_band_final).
 // out_score / out_x (nullable, tests): per-candidate fp32 score and value.
 __global__ __launch_bounds__(kBS) void k_score_table_fast(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   // the thread's best candidate's lower bound (a lower bound of G); NaN: none
   const float lo_t = (br >= 0 && bs == bs) ? bs - eps(br, bs) : -INFINITY;
   const float blo = block_max<kBS, float>(lo_t, fred);
-  uint32_t* ctl = band_ctl + 2 * (int64_t)job;
+  uint32_t* ctl = band_ctl + 4 * (int64_t)job;
   if (threadIdx.x == 0) {
     const uint32_t old = atomicMax(ctl, blo > -INFINITY ? ord_enc(blo) : 0u);
     s_g = fmaxf(blo, ord_dec(old));
@@ -1192,20 +1192,21 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   const float hi_t = br >= 0 ? bs + ea + kEpsRel * fabsf(bs) : -INFINITY;
   if (fbm != 0u || !(hi_t < G)) {
     tpe_band* B = band + (int64_t)job * band_cap;
-    for (int r = 0; r < nvalid; ++r) {
+#pragma unroll
+    for (int r = 0; r < kTR; ++r) {
+      if (r >= nvalid) break;
       const float s = stage[r * kWave + lane];
       const float hi = s + eps(r, s);
       if (hi < G) continue;  // (NaN scores go on)
-      const int64_t g = J.cand_base + t0 + r;
-      const float y = draw32(M, J.key, g, lo_on, hi_on, (float)J.low, (float)J.high);
       const uint32_t p = atomicAdd(ctl + 1, 1u);
-      if ((int64_t)p < band_cap) B[p] = tpe_band{g, y, hi};
+      if ((int64_t)p < band_cap) B[p] = tpe_band{J.cand_base + t0 + r, x[r], hi};
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// exact re-score of the band (one block per job)
+// exact re-score of the band: select (block per job), expand (block per
+// cell and mixture), final (block per job)
 // ---------------------------------------------------------------------------
 // A band candidate y is scored in fp64 through the table cell c that holds it
 // (the fp32 cell index, a function of y alone): both mixtures are expanded
@@ -1217,26 +1218,33 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
 // past degree 24 is < 1e-20 of its term, and components with a larger rho (far
 // out relative to their bandwidth) are summed term by term instead.  Rounding
 // of the P_n sums is ~1e-14 relative: the fp64 accuracy of a direct sum over
-// 10^4 terms.  Survivors off the grid, or of a cell with more slow components
-// than fit the list, take the direct online log-sum-exp over every component
-// (k_score64's arithmetic).  Every survivor's score depends on its y alone, so
-// the winner does not depend on how candidates are sharded over ranks.
+// 10^4 terms.  Survivors off the grid, of a cell past the kBandCells listed,
+// or of a cell with more slow components than fit the list, take the direct
+// online log-sum-exp over every component (k_score64's arithmetic).  Every
+// survivor's score depends on its y alone, so the winner does not depend on
+// how candidates are sharded over ranks.
 constexpr int kBandD = 24;           // expansion degree
-constexpr int kBandChunk = 2048;     // survivors held in LDS at a time
 constexpr int kBandDirect = 128;     // slow components summed term by term, per mixture
 constexpr double kBandTau = 45.0;    // exclusion margin (nats) on top of log(M)
 constexpr double kBandRho = 1.5;     // admissible 1.05 |A| + 1.1025 |B|
+constexpr int kBandCells = 64;       // cells expanded per job (sorted; the rest: direct)
+constexpr int kBandBits = 32768;     // cell bitmap of the select kernel (LDS)
+constexpr int kBandSlots = 16;       // expand blocks per job and mixture (grid-stride over cells)
 
-struct BandMix {  // one mixture's expansion on one cell (LDS)
+struct BandMix {  // one mixture's expansion on one cell
   double P[kBandD + 1];
   double m;
-  int n_dir;
+  int n_dir;  // -1: too many slow components (the cell's survivors take the direct sum)
+  int pad;
   int dir[kBandDirect];
 };
+struct BandWork {  // per job (tpe_band_work_bytes)
+  int cell[kBandCells];
+  BandMix mix[kBandCells][2];
+};
 
-// expansion of mixture S on the cell (y0, h); all threads; false: too many
-// slow components (the cell's survivors take the direct sum)
-__device__ bool band_expand(const tpe_seg& S, const double* __restrict__ coef64, double y0,
+// expansion of mixture S on the cell (y0, h) into E (LDS); all threads
+__device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64, double y0,
                             double h, BandMix& E, double* dred) {
   const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
@@ -1289,7 +1297,7 @@ __device__ bool band_expand(const tpe_seg& S, const double* __restrict__ coef64,
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
     P[n] = v;
   }
-  __syncthreads();  // (E.n_dir complete; the previous user of E.P is done)
+  __syncthreads();  // (E.n_dir complete; dred free)
   const int wid = threadIdx.x / kWave;
   if (lane_id() == 0) {
 #pragma unroll
@@ -1301,9 +1309,11 @@ __device__ bool band_expand(const tpe_seg& S, const double* __restrict__ coef64,
     for (int w = 0; w < kBS / kWave; ++w) t += dred[w * (kBandD + 1) + threadIdx.x];
     E.P[threadIdx.x] = t;
   }
-  if (threadIdx.x == 0) E.m = m;
+  if (threadIdx.x == 0) {
+    E.m = m;
+    if (E.n_dir > kBandDirect) E.n_dir = -1;
+  }
   __syncthreads();
-  return E.n_dir <= kBandDirect;
 }
 
 // log of the mixture at y from its cell expansion (u = (y - y0) / h)
@@ -1312,7 +1322,8 @@ __device__ __forceinline__ double band_eval(const BandMix& E, const double* __re
   double p = E.P[kBandD];
 #pragma unroll
   for (int n = kBandD - 1; n >= 0; --n) p = fma(p, u, E.P[n]);
-  for (int i = 0; i < E.n_dir; ++i) {
+  const int nd = E.n_dir;
+  for (int i = 0; i < nd; ++i) {
     const double4 c = ld4(coef64, off + E.dir[i]);
     const double t = (y - c.x) * c.y;
     p += exp(c.z - 0.5 * t * t - E.m);
@@ -1337,122 +1348,190 @@ __device__ __forceinline__ double band_direct(const tpe_seg& S, const double* __
   return log(so) + mo;
 }
 
-__global__ __launch_bounds__(kBS) void k_band_rescore(
-    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
-    const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
-    const tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
-    const tpe_best* __restrict__ partial, int64_t nper, tpe_best* __restrict__ best) {
+// the fp32 cell of a band candidate (as the scorer forms it); -2: off the
+// grid (the direct sum)
+__device__ __forceinline__ int band_cell(const tpe_table& Tb, float y) {
+  const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
+  const float t = (y - g0) * Tb.inv_w;
+  int c = (t >= 0.0f) ? (int)t : 0;
+  c = min(c, Tb.nb - 1);
+  const double u = ((double)y - (double)cell_centre(g0, h32, c)) / Tb.h;
+  return (fabs(u) <= (double)kULim && y == y) ? c : -2;
+}
+
+// band_ctl words per job: [0] G (order code), [1] entries, [2] survivors
+// (kBandOverflow: the band overflowed), [3] listed cells
+constexpr uint32_t kBandOverflow = 0xFFFFFFFFu;
+
+// Select: keep the entries with hi >= the final G, compacted in place (entry
+// order), and list their distinct cells (ascending, at most kBandCells) in
+// the job's BandWork.  A job whose band overflowed gets the fp32 winner with
+// n_scored = -1.
+__global__ __launch_bounds__(kBS) void k_band_select(
+    const tpe_job* __restrict__ jobs, const tpe_table* __restrict__ tables,
+    tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
+    const tpe_best* __restrict__ partial, int64_t nper, tpe_best* __restrict__ best,
+    BandWork* __restrict__ work) {
   __shared__ BestT red[kBS / kWave];
-  __shared__ double dred[(kBS / kWave) * (kBandD + 1)];
-  __shared__ BandMix s_eb, s_ea;
-  __shared__ float s_y[kBandChunk];
-  __shared__ int64_t s_i[kBandChunk];
-  __shared__ int s_c[kBandChunk];
-  __shared__ int s_n, s_scan[kBS / kWave];
+  __shared__ int s_scan[kBS / kWave];
+  __shared__ uint32_t s_bits[kBandBits / 32];
   const int j = blockIdx.x;
-  const tpe_job J = jobs[j];
-  // the fp32 winner (kept when the band overflowed)
-  BestT b32{0.0, -1, 0.0};
-  for (int64_t i = threadIdx.x; i < nper; i += kBS) {
-    const tpe_best p = partial[(int64_t)j * nper + i];
-    best_update(b32, p.score, p.index, p.value);
-  }
-  b32 = block_best<kBS>(b32, red);
-  uint32_t* ctl = band_ctl + 2 * (int64_t)j;
+  uint32_t* ctl = band_ctl + 4 * (int64_t)j;
   const float G = ord_dec(ctl[0]);
   const int64_t n = (int64_t)ctl[1];
   __syncthreads();  // every thread has read the controls
   if (threadIdx.x == 0) {
-    ctl[0] = 0u;  // ready for the next call
+    ctl[0] = 0u;  // ready for the next scorer call
     ctl[1] = 0u;
   }
   if (n > band_cap) {
-    if (threadIdx.x == 0) best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
+    // the fp32 winner; the caller re-scores the job exactly
+    BestT b32{0.0, -1, 0.0};
+    for (int64_t i = threadIdx.x; i < nper; i += kBS) {
+      const tpe_best p = partial[(int64_t)j * nper + i];
+      best_update(b32, p.score, p.index, p.value);
+    }
+    b32 = block_best<kBS>(b32, red);
+    if (threadIdx.x == 0) {
+      best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
+      ctl[2] = kBandOverflow;
+      ctl[3] = 0u;
+    }
     return;
   }
+  const tpe_table Tb = tables[j];
+  for (int w = threadIdx.x; w < kBandBits / 32; w += kBS) s_bits[w] = 0u;
+  __syncthreads();
+  tpe_band* B = band + (int64_t)j * band_cap;
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+  int64_t kept = 0;
+  for (int64_t e0 = 0; e0 < n; e0 += kBS) {
+    const int64_t e = e0 + threadIdx.x;
+    tpe_band E{};
+    bool keep = false;
+    if (e < n) {
+      E = B[e];
+      keep = !(E.hi < G);  // (NaN bounds stay)
+    }
+    const uint64_t bal = __ballot(keep);
+    if (lane == 0) s_scan[wid] = __popcll(bal);
+    __syncthreads();  // (every entry of the chunk is read before any is written)
+    int64_t p = kept + __popcll(bal & ((1ull << lane) - 1ull));
+    int tot = 0;
+    for (int w = 0; w < kBS / kWave; ++w) {
+      p += (w < wid) ? s_scan[w] : 0;
+      tot += s_scan[w];
+    }
+    if (keep) {
+      B[p] = E;
+      const int c = band_cell(Tb, E.y);
+      if (c >= 0 && c < kBandBits) atomicOr(&s_bits[c >> 5], 1u << (c & 31));
+    }
+    kept += tot;
+    __syncthreads();  // s_scan reused
+  }
+  // the listed cells: bitmap words in order, kBandBits / 32 / kBS per thread
+  constexpr int kPer = kBandBits / 32 / kBS;
+  int cnt = 0;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) cnt += __popc(s_bits[threadIdx.x * kPer + i]);
+  int pos = block_scan_sum(cnt, s_scan) - cnt;  // exclusive prefix
+  int total = 0;  // (s_scan holds the wave totals)
+  for (int w = 0; w < kBS / kWave; ++w) total += s_scan[w];
+  for (int i = 0; i < kPer && pos < kBandCells; ++i) {
+    uint32_t b = s_bits[threadIdx.x * kPer + i];
+    while (b && pos < kBandCells) {
+      work[j].cell[pos++] = (threadIdx.x * kPer + i) * 32 + __builtin_ctz(b);
+      b &= b - 1;
+    }
+  }
+  if (threadIdx.x == 0) {
+    ctl[2] = (uint32_t)kept;
+    ctl[3] = (uint32_t)min(total, kBandCells);
+  }
+}
+
+// Expand: block (slot, job, mixture) expands its mixture on listed cells
+// slot, slot + kBandSlots, ... into the job's BandWork.
+__global__ __launch_bounds__(kBS) void k_band_expand(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
+    const uint32_t* __restrict__ band_ctl, BandWork* __restrict__ work) {
+  __shared__ double dred[(kBS / kWave) * (kBandD + 1)];
+  __shared__ BandMix s_e;
+  const int j = blockIdx.y;
+  const uint32_t ns = band_ctl[4 * (int64_t)j + 2];
+  const int nc = (int)band_ctl[4 * (int64_t)j + 3];
+  if (ns == kBandOverflow || ns == 0u || (int)blockIdx.x >= nc) return;
+  const tpe_job J = jobs[j];
+  const tpe_seg S = segs[blockIdx.z ? J.above : J.below];
+  const tpe_table Tb = tables[j];
+  const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
+  for (int k = blockIdx.x; k < nc; k += kBandSlots) {
+    const int c = work[j].cell[k];
+    band_expand(S, coef64, (double)cell_centre(g0, h32, c), Tb.h, s_e, dred);
+    BandMix& G = work[j].mix[k][blockIdx.z];
+    if (threadIdx.x <= kBandD) G.P[threadIdx.x] = s_e.P[threadIdx.x];
+    const int nd = s_e.n_dir;
+    if (threadIdx.x == 0) {
+      G.m = s_e.m;
+      G.n_dir = nd;
+    }
+    for (int i = threadIdx.x; i < nd; i += kBS) G.dir[i] = s_e.dir[i];
+    __syncthreads();  // s_e reused
+  }
+}
+
+// Final: every survivor scored in fp64 (its cell's expansions, else the
+// direct sum); np.argmax over them -> best[j]; the controls left zero.
+__global__ __launch_bounds__(kBS) void k_band_final(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
+    const tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
+    tpe_best* __restrict__ best, const BandWork* __restrict__ work) {
+  __shared__ BestT red[kBS / kWave];
+  __shared__ int s_cell[kBandCells];
+  const int j = blockIdx.x;
+  uint32_t* ctl = band_ctl + 4 * (int64_t)j;
+  const uint32_t ns = ctl[2];
+  const int nc = (int)ctl[3];
+  for (int k = threadIdx.x; k < nc; k += kBS) s_cell[k] = work[j].cell[k];
+  __syncthreads();  // (controls read; cells staged)
+  if (threadIdx.x == 0) {
+    ctl[2] = 0u;
+    ctl[3] = 0u;
+  }
+  if (ns == kBandOverflow) return;  // (best[j] written by k_band_select)
+  const tpe_job J = jobs[j];
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const tpe_table Tb = tables[j];
   const bool lgmm = J.family == TPE_LGMM1;
-  const float g0 = (float)Tb.origin, inv_w = Tb.inv_w, h32 = (float)Tb.h;
+  const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
   const tpe_band* B = band + (int64_t)j * band_cap;
   BestT bx{0.0, -1, 0.0};
-  int64_t e0 = 0;
-  while (__syncthreads_or(e0 < n)) {
-    // gather the next survivors (s32 + eps >= G) into LDS, in entry order
-    if (threadIdx.x == 0) s_n = 0;
-    __syncthreads();
-    while (e0 < n && s_n + kBS <= kBandChunk) {
-      const int64_t e = e0 + threadIdx.x;
-      bool keep = false;
-      tpe_band E{};
-      if (e < n) {
-        E = B[e];
-        keep = !(E.hi < G);
+  for (int64_t p = threadIdx.x; p < (int64_t)ns; p += kBS) {
+    const tpe_band E = B[p];
+    const double y = (double)E.y;
+    const int c = band_cell(Tb, E.y);
+    int k = -1;
+    if (c >= 0) {  // binary search of the listed cells
+      int lo = 0, hi = nc;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_cell[mid] < c) lo = mid + 1; else hi = mid;
       }
-      // block exclusive scan of keep
-      const int lane = lane_id(), wid = threadIdx.x / kWave;
-      const uint64_t bal = __ballot(keep);
-      const int wpre = __popcll(bal & ((1ull << lane) - 1ull));
-      if (lane == 0) s_scan[wid] = __popcll(bal);
-      __syncthreads();
-      int off = s_n;
-      for (int w = 0; w < wid; ++w) off += s_scan[w];
-      if (keep) {
-        const int p = off + wpre;
-        s_y[p] = E.y;
-        s_i[p] = E.index;
-        // the fp32 cell (as the scorer forms it); -2: off the grid (direct)
-        const float t = (E.y - g0) * inv_w;
-        int c = (t >= 0.0f) ? (int)t : 0;
-        c = min(c, Tb.nb - 1);
-        const double u = ((double)E.y - (double)cell_centre(g0, h32, c)) / Tb.h;
-        s_c[p] = (fabs(u) <= (double)kULim && E.y == E.y) ? c : -2;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int w = 0; w < kBS / kWave; ++w) tot += s_scan[w];
-        s_n += tot;
-      }
-      __syncthreads();
-      e0 += kBS;
+      k = (lo < nc && s_cell[lo] == c) ? lo : -1;
     }
-    const int ns = s_n;
-    // one cell at a time (smallest unprocessed cell index first)
-    for (;;) {
-      int cmin = INT32_MAX;
-      for (int p = threadIdx.x; p < ns; p += kBS)
-        if (s_c[p] >= 0) cmin = min(cmin, s_c[p]);
-      cmin = -block_max<kBS, int>(-cmin, s_scan);
-      if (cmin == INT32_MAX) break;
-      const double y0 = (double)cell_centre(g0, h32, cmin);
-      const bool okb = band_expand(SB, coef64, y0, Tb.h, s_eb, dred);
-      const bool oka = band_expand(SA, coef64, y0, Tb.h, s_ea, dred);
-      for (int p = threadIdx.x; p < ns; p += kBS) {
-        if (s_c[p] != cmin) continue;
-        const double y = (double)s_y[p];
-        double lb, la;
-        if (okb && oka) {
-          const double u = (y - y0) / Tb.h;
-          lb = band_eval(s_eb, coef64, SB.comp_off, u, y);
-          la = band_eval(s_ea, coef64, SA.comp_off, u, y);
-        } else {
-          lb = band_direct(SB, coef64, y);
-          la = band_direct(SA, coef64, y);
-        }
-        best_update(bx, lb - la, s_i[p], cand_value(s_y[p], lgmm));
-        s_c[p] = -1;
-      }
-      __syncthreads();
+    double lb, la;
+    if (k >= 0 && work[j].mix[k][0].n_dir >= 0 && work[j].mix[k][1].n_dir >= 0) {
+      const double u = (y - (double)cell_centre(g0, h32, c)) / Tb.h;
+      lb = band_eval(work[j].mix[k][0], coef64, SB.comp_off, u, y);
+      la = band_eval(work[j].mix[k][1], coef64, SA.comp_off, u, y);
+    } else {
+      lb = band_direct(SB, coef64, y);
+      la = band_direct(SA, coef64, y);
     }
-    // off-grid survivors: the direct sum, one per thread
-    for (int p = threadIdx.x; p < ns; p += kBS) {
-      if (s_c[p] != -2) continue;
-      const double y = (double)s_y[p];
-      best_update(bx, band_direct(SB, coef64, y) - band_direct(SA, coef64, y), s_i[p],
-                  cand_value(s_y[p], lgmm));
-    }
-    __syncthreads();
+    best_update(bx, lb - la, E.index, cand_value(E.y, lgmm));
   }
   bx = block_best<kBS>(bx, red);
   if (threadIdx.x == 0) best[j] = tpe_best{bx.score, bx.index, bx.value, J.n_cand};
@@ -1839,11 +1918,16 @@ extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_job
   return check_launch("tpe_score_table_fast");
 }
 
+extern "C" int64_t tpe_band_work_bytes(int n_jobs) {
+  if (n_jobs < 0) return -1;
+  return (int64_t)sizeof(BandWork) * std::max(n_jobs, 1);
+}
+
 extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                                 const tpe_seg* segs, const double* coef64,
-                                const tpe_table* tables, const tpe_band* band, int64_t band_cap,
+                                const tpe_table* tables, tpe_band* band, int64_t band_cap,
                                 uint32_t* band_ctl, const tpe_best* partial, int64_t n_partial,
-                                tpe_best* best, void* stream) {
+                                tpe_best* best, void* work, void* stream) {
   bool inj = false;
   if (!check_table_jobs("tpe_band_rescore", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
   if (n_jobs == 0) return TPE_OK;
@@ -1851,7 +1935,7 @@ extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, i
     set_error("tpe_band_rescore: sampled jobs only");
     return TPE_E_ARG;
   }
-  if (!jobs || !segs || !coef64 || !tables || !band || !band_ctl || !partial || !best) {
+  if (!jobs || !segs || !coef64 || !tables || !band || !band_ctl || !partial || !best || !work) {
     set_error("tpe_band_rescore: null pointer");
     return TPE_E_ARG;
   }
@@ -1865,8 +1949,14 @@ extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, i
               (long long)(gx * n_jobs));
     return TPE_E_ARG;
   }
-  hipLaunchKernelGGL(k_band_rescore, dim3(n_jobs), dim3(kBS), 0, (hipStream_t)stream, jobs, segs,
-                     coef64, tables, band, band_cap, band_ctl, partial, gx, best);
+  hipStream_t st = (hipStream_t)stream;
+  BandWork* W = static_cast<BandWork*>(work);
+  hipLaunchKernelGGL(k_band_select, dim3(n_jobs), dim3(kBS), 0, st, jobs, tables, band, band_cap,
+                     band_ctl, partial, gx, best, W);
+  hipLaunchKernelGGL(k_band_expand, dim3(kBandSlots, n_jobs, 2), dim3(kBS), 0, st, jobs, segs,
+                     coef64, tables, band_ctl, W);
+  hipLaunchKernelGGL(k_band_final, dim3(n_jobs), dim3(kBS), 0, st, jobs, segs, coef64, tables,
+                     band, band_cap, band_ctl, best, W);
   return check_launch("tpe_band_rescore");
 }
 

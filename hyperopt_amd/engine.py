@@ -274,10 +274,10 @@ class DeviceHistory:
         t = self.torch
         if self.order is None:
             self.order = t.zeros((self.n_labels, self.cap), dtype=t.int32, device=self.device)
-        key = (self.rows, len(cols))
-        if self.__dict__.get("_ordered") == key and all(
-                self.order_rows.get(c) == self.rows for c in np.asarray(cols).tolist()):
-            return  # (every column current: nothing appended since)
+        key = (self.rows, np.asarray(cols).tobytes(), np.asarray(transforms).tobytes(),
+               np.asarray(floors, np.float64).tobytes())
+        if self.__dict__.get("_ordered") == key:
+            return  # (the same columns and transforms, nothing appended since)
         todo = {}
         for c, tr, fl in zip(np.asarray(cols).tolist(), np.asarray(transforms).tolist(),
                              np.asarray(floors).tolist()):
@@ -1263,7 +1263,8 @@ class Engine:
                                                     npart, db, d_stats, sp), "tpe_score_table")
                     else:  # the suggest path: one score cubic per candidate, exact argmax
                         d_band = self._buf("band", L.BAND_DTYPE.itemsize * BAND_CAP * nj)
-                        d_bctl = self._zbuf("band_ctl", 8 * nj)
+                        d_bctl = self._zbuf("band_ctl", 16 * nj)
+                        d_bwork = self._buf("band_work", lib.tpe_band_work_bytes(nj))
                         L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
                                                          d_c32, d_tab, d_cells, d_band, BAND_CAP,
                                                          d_bctl, d_sc, d_x, d_part, npart,
@@ -1272,7 +1273,8 @@ class Engine:
                         tock("table", e0)
                         e0 = tick("band")
                         L.check(lib.tpe_band_rescore(dj, hjp, nj, d_segs, d_c64, d_tab, d_band,
-                                                     BAND_CAP, d_bctl, d_part, npart, db, sp),
+                                                     BAND_CAP, d_bctl, d_part, npart, db,
+                                                     d_bwork, sp),
                                 "tpe_band_rescore")
                         tock("band", e0)
                         e0 = None

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 14
+#define TPE_ABI_VERSION 15
 
 enum {
   TPE_OK = 0,
@@ -361,17 +361,19 @@ int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
  * winner only if s32_i + eps_i >= G := max_k (s32_k - eps_k).  Each scorer
  * block publishes its best s32_k - eps_k into band_ctl (atomic max) and
  * appends its candidates with s32 + eps >= the maximum known so far to
- * `band`; tpe_band_rescore keeps those with s32 + eps >= the final G and
- * re-scores them in fp64 -- per table cell, a degree-24 expansion of both
- * mixtures around the cell centre over every component within e^-45 of the
- * sum (components whose series would converge slowly summed term by term) --
- * and takes the np.argmax winner (largest score, then smallest index):
+ * `band`; tpe_band_rescore keeps those with s32 + eps >= the final G
+ * (compacted in place) and re-scores them in fp64 -- per table cell, a
+ * degree-24 expansion of both mixtures around the cell centre over every
+ * component within e^-45 of the sum (components whose series would converge
+ * slowly summed term by term; one block per cell and mixture) -- and takes
+ * the np.argmax winner (largest score, then smallest index):
  * best[j] = {fp64 score, index, value (x, or exp(y) in fp64 for LGMM1),
  * n_cand}.  A job whose band got more than band_cap entries (a plateau of
  * near-equal scores) keeps the fp32 winner with n_scored = -1: the caller
  * re-scores it exactly (tpe_score_pruned64 with TPE_F_DRAW32).
- * band: band_cap entries per job; band_ctl: 2 uint32 per job, zero before
- * the first call -- tpe_band_rescore leaves them zero again.  Both calls take
+ * band: band_cap entries per job; band_ctl: 4 uint32 per job, zero before
+ * the first call -- tpe_band_rescore leaves them zero again; work:
+ * tpe_band_work_bytes(n_jobs) bytes (the cell expansions).  Both calls take
  * the same job list and partial workspace (tpe_table_partials()).
  * out_score / out_x (nullable, tests): the per-candidate fp32 score and value
  * at job.out_off. */
@@ -386,10 +388,12 @@ int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_jobs, int n_jo
                          const float* cells, tpe_band* band, int64_t band_cap,
                          uint32_t* band_ctl, double* out_score, double* out_x, tpe_best* partial,
                          int64_t n_partial, uint64_t* stats, void* stream);
+int64_t tpe_band_work_bytes(int n_jobs);
 int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                      const tpe_seg* segs, const double* coef64, const tpe_table* tables,
-                     const tpe_band* band, int64_t band_cap, uint32_t* band_ctl,
-                     const tpe_best* partial, int64_t n_partial, tpe_best* best, void* stream);
+                     tpe_band* band, int64_t band_cap, uint32_t* band_ctl,
+                     const tpe_best* partial, int64_t n_partial, tpe_best* best, void* work,
+                     void* stream);
 
 /* ---- continuous candidates, exact fp64 with pruning (parity mode) ----------
  * Same results as tpe_score_continuous(precision=64) up to fp64 rounding (a

@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 14
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 15
     sizes = (ctypes.c_int32 * 11)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 11) == 11
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -120,7 +120,7 @@ def test_argument_errors_are_reported():
 
     def rescore(band_cap=1 << 16, ptr=None, n_partial=1 << 20):
         return lib.tpe_band_rescore(ptr, hp_, 1, ptr, ptr, ptr, ptr, band_cap, ptr, ptr,
-                                    n_partial, ptr, None)
+                                    n_partial, ptr, ptr, None)
     assert fast() == -1 and b"sampled jobs only" in lib.tpe_last_error()
     assert rescore() == -1 and b"sampled jobs only" in lib.tpe_last_error()
     jobs["flags"] = 0
@@ -131,6 +131,7 @@ def test_argument_errors_are_reported():
     assert fast(-3, eight) == -1 and b"band_cap" in lib.tpe_last_error()
     assert rescore(0, eight) == -1 and b"band_cap" in lib.tpe_last_error()
     assert rescore(64, eight, n_partial=0) == -1 and b"partial workspace" in lib.tpe_last_error()
+    assert lib.tpe_band_work_bytes(3) > 3 * 64 * 2 * 8 * 25 and lib.tpe_band_work_bytes(-1) == -1
     rc = lib.tpe_table_build(None, hp_, 1, None, None, None, None, 8, *([None] * 8))
     assert rc == -1 and b"null pointer" in lib.tpe_last_error()
     assert lib.tpe_table_scratch_bytes(3, 1000) > 0 and lib.tpe_table_scratch_bytes(-1, 5) == -1
