@@ -34,7 +34,7 @@ namespace {
 constexpr int kSB = 1024;            // block size of every kernel here
 constexpr int kSWaves = kSB / kWave;
 constexpr int kNew = 2048;           // new rows sorted per tpe_history_order call
-constexpr int kRowsPT = 16;          // rows per thread per compaction pass
+constexpr int kRowsPT = 12;          // rows per thread per compaction pass
 constexpr int kPass = kRowsPT * kSB; // rows per compaction pass
 constexpr int kSlots = kRowsPT * kSWaves;
 
@@ -137,27 +137,42 @@ __global__ __launch_bounds__(256) void k_order_copy(const tpe_colspec* __restric
 
 // ---- the fit ------------------------------------------------------------------
 // Block-wide stream compaction over items [0, n) in item order, kRowsPT items
-// per thread per pass (the loads of a pass in flight together): take(i, v)
-// says whether item i is kept (and loads its payload), emit(i, rank, v) gets
+// per thread per pass.  The loads of a pass are issued together, in two
+// dependent rounds: first(i) (e.g. the order entry), then second(first) (the
+// row's fields); take(L) says whether the item is kept, emit(i, rank, L) gets
 // its rank among the kept items.  Returns the number kept.
-template <class Take, class Emit>
-__device__ int64_t block_compact(int64_t n, Take take, Emit emit, int* wsum, int64_t* carry_s) {
+struct RowLoad {
+  int32_t row;
+  uint8_t act, side;
+  double v;
+  int32_t gi;
+};
+template <class First, class Second, class Take, class Emit>
+__device__ int64_t block_compact(int64_t n, First first, Second second, Take take, Emit emit,
+                                 int* wsum, int64_t* carry_s) {
   const int lane = lane_id(), wid = threadIdx.x / kWave;
   const uint64_t lt = (1ull << lane) - 1ull;
   if (threadIdx.x == 0) *carry_s = 0;
   __syncthreads();
   for (int64_t p0 = 0; p0 < n; p0 += kPass) {
-    bool tk[kRowsPT];
-    int64_t pl[kRowsPT];
+    int32_t f[kRowsPT];
 #pragma unroll
     for (int t = 0; t < kRowsPT; ++t) {
       const int64_t i = p0 + (int64_t)t * kSB + threadIdx.x;
-      pl[t] = 0;
-      tk[t] = i < n && take(i, pl[t]);
+      f[t] = i < n ? first(i) : 0;
     }
+    RowLoad L[kRowsPT];
+#pragma unroll
+    for (int t = 0; t < kRowsPT; ++t) {
+      const int64_t i = p0 + (int64_t)t * kSB + threadIdx.x;
+      L[t] = i < n ? second(f[t]) : RowLoad{0, 0, 2, 0.0, 0};
+    }
+    bool tk[kRowsPT];
     int before[kRowsPT];
 #pragma unroll
     for (int t = 0; t < kRowsPT; ++t) {
+      const int64_t i = p0 + (int64_t)t * kSB + threadIdx.x;
+      tk[t] = i < n && take(L[t]);
       const uint64_t bal = __ballot(tk[t]);
       before[t] = __popcll(bal & lt);
       if (lane == 0) wsum[t * kSWaves + wid] = __popcll(bal);
@@ -184,7 +199,7 @@ __device__ int64_t block_compact(int64_t n, Take take, Emit emit, int* wsum, int
 #pragma unroll
     for (int t = 0; t < kRowsPT; ++t)
       if (tk[t]) emit(p0 + (int64_t)t * kSB + threadIdx.x,
-                      carry + wsum[t * kSWaves + wid] + before[t], pl[t]);
+                      carry + wsum[t * kSWaves + wid] + before[t], L[t]);
     __syncthreads();
     if (threadIdx.x == 0) *carry_s = carry + total;
     __syncthreads();
@@ -221,19 +236,16 @@ __global__ __launch_bounds__(kSB) void k_fit_sorted(
   // 1. rows in tid order: position in the segment's list, count below the prior
   int lt = 0;
   const int64_t n = block_compact(
-      n_rows,
-      [&](int64_t r, int64_t& pl) {
-        const bool t = A[r] && is_below[r] == side;
-        if (t) {
-          const double v = obs_transform(V[r], transform, floor_);
-          lt += order_key(v) < kp ? 1 : 0;
-          pl = __double_as_longlong(v);
-        }
+      n_rows, [&](int64_t r) { return (int32_t)r; },
+      [&](int32_t r) { return RowLoad{r, A[r], is_below[r], V[r], 0}; },
+      [&](const RowLoad& L) {
+        const bool t = L.act && L.side == side;
+        lt += (t && order_key(obs_transform(L.v, transform, floor_)) < kp) ? 1 : 0;
         return t;
       },
-      [&](int64_t r, int64_t rank, int64_t pl) {
+      [&](int64_t r, int64_t rank, const RowLoad& L) {
         GI[r] = (int32_t)rank;
-        if (rank == 0) s_x0 = __longlong_as_double(pl);
+        if (rank == 0) s_x0 = obs_transform(L.v, transform, floor_);
       },
       wsum, &carry_s);
   atomicAdd(&s_lt, lt);
@@ -248,16 +260,13 @@ __global__ __launch_bounds__(kSB) void k_fit_sorted(
   const int prior_pos = n >= 2 ? s_lt : (n == 1 ? ((pmu < s_x0) ? 0 : 1) : 0);
   // 2. the column's sorted order compacted to the segment
   block_compact(
-      n_rows,
-      [&](int64_t e, int64_t& pl) {
-        const int32_t row = O[e];
-        pl = row;
-        return A[row] && is_below[row] == side;
-      },
-      [&](int64_t e, int64_t p, int64_t row) {
+      n_rows, [&](int64_t e) { return O[e]; },
+      [&](int32_t row) { return RowLoad{row, A[row], is_below[row], V[row], GI[row]}; },
+      [&](const RowLoad& L) { return L.act && L.side == side; },
+      [&](int64_t e, int64_t p, const RowLoad& L) {
         const int64_t pos = p + (p >= prior_pos ? 1 : 0);
-        mu[coff + pos] = obs_transform(V[row], transform, floor_);
-        w[coff + pos] = lf_weight(GI[row], nn, lf);  // ramp in tid order (tpe.py:441-447)
+        mu[coff + pos] = obs_transform(L.v, transform, floor_);
+        w[coff + pos] = lf_weight(L.gi, nn, lf);  // ramp in tid order (tpe.py:441-447)
       },
       wsum, &carry_s);
   if (threadIdx.x == 0) {

@@ -373,21 +373,6 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
          (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
           __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
 }
-__device__ __forceinline__ double wave_max_dpp(double v) {
-  v = fmax(v, dpp_d<kDppXor1>(v));
-  v = fmax(v, dpp_d<kDppXor2>(v));
-  v = fmax(v, dpp_d<kDppHalfMirror>(v));
-  v = fmax(v, dpp_d<kDppMirror>(v));
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  double r = -INFINITY;
-#pragma unroll
-  for (int row = 0; row < 4; ++row) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, row * 16);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), row * 16);
-    r = fmax(r, __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo));
-  }
-  return r;
-}
 // The nine P_n sums of a wave at once (transposed butterfly).  Per DPP stage
 // each lane keeps half of its live values and adds its partner's copy of
 // them: stage 1 pairs lane i with 15-i of its row (row mirror, bit 3 chooses
@@ -395,9 +380,8 @@ __device__ __forceinline__ double wave_max_dpp(double v) {
 // and 4 with i^2 and i^1 (quad perms); a stage's partner always holds the same
 // subset as the lane, because the mirrors come first.  After four stages lane
 // p of each row holds its row's sum of P_rev4(p) (rev4: the 4-bit reversal);
-// two cross-row exchanges complete the totals.  Returns lane L's total of
-// P_rev4(L) (L < 16; rev4(L) >= 9 gives 0): 11 exchange-adds instead of the
-// 9 x 4 of one wave_sum_dpp per term.
+// (row_sum9_transposed: the build sums each row on its own, one cell per
+// row): 9 exchange-adds instead of the 9 x 4 of one DPP sum per term.
 template <int CTRL, int M>
 __device__ __forceinline__ void fold_stage(float (&w)[16], bool hi) {
 #pragma unroll
@@ -405,22 +389,6 @@ __device__ __forceinline__ void fold_stage(float (&w)[16], bool hi) {
     const float keep = hi ? w[2 * j + 1] : w[2 * j], send = hi ? w[2 * j] : w[2 * j + 1];
     w[j] = keep + dpp_f<CTRL>(send);
   }
-}
-__device__ __forceinline__ float wave_sum9_transposed(const float (&P)[9]) {
-  const int lane = lane_id();
-  float w[16];
-#pragma unroll
-  for (int n = 0; n < 16; ++n) w[n] = n < 9 ? P[n] : 0.0f;
-  fold_stage<kDppMirror, 5>(w, (lane >> 3) & 1);      // 9 live -> 5
-  w[5] = 0.0f;
-  fold_stage<kDppHalfMirror, 3>(w, (lane >> 2) & 1);  // -> 3
-  w[3] = 0.0f;
-  fold_stage<kDppXor2, 2>(w, (lane >> 1) & 1);        // -> 2
-  fold_stage<kDppXor1, 1>(w, lane & 1);               // -> 1
-  float v = w[0];
-  v += __shfl_xor(v, 16, kWave);
-  v += __shfl_xor(v, 32, kWave);
-  return v;
 }
 __device__ __forceinline__ int rev4(int p) {
   return ((p & 1) << 3) | ((p & 2) << 1) | ((p & 4) >> 1) | ((p & 8) >> 3);
@@ -437,10 +405,10 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
-// A cell's two reach windows at once: four searches of wave_first's kind in
-// one pass, one per 16-lane group -- g = 0 / 2: the first k of the below /
-// above mixture with reach_hi[k] >= y0 - h, g = 1 / 3: the first k with
-// reach_lo[k] > y0 + h (the window ends one before it).  16-ary narrowing:
+// The two reach windows of the span [ylo, yhi] (a run of cells) at once: four
+// searches of wave_first's kind in one pass, one per 16-lane group -- g = 0 /
+// 2: the first k of the below / above mixture with reach_hi[k] >= ylo, g = 1 /
+// 3: the first k with reach_lo[k] > yhi (the window ends one before it).  16-ary narrowing:
 // 10^4 components take 4 dependent probes, for all four searches together
 // instead of 3 for each.  Every lane gets all four answers.
 struct Windows {
@@ -448,13 +416,13 @@ struct Windows {
 };
 __device__ __forceinline__ Windows cell_windows(const tpe_seg& SB, const tpe_seg& SA,
                                                 const double* __restrict__ reach_hi,
-                                                const double* __restrict__ reach_lo, double y0,
-                                                double h) {
+                                                const double* __restrict__ reach_lo, double ylo,
+                                                double yhi) {
   const int lane = lane_id(), g = lane >> 4, l = lane & 15;
   const tpe_seg& S = g < 2 ? SB : SA;
   const bool gt = g & 1;
   const double* a = (gt ? reach_lo : reach_hi) + S.comp_off;
-  const double v = gt ? y0 + h : y0 - h;
+  const double v = gt ? yhi : ylo;
   int lo = 0, hi = S.n_obs + 1;  // answer in [lo, hi]
   while (__any(lo < hi)) {
     const bool active = lo < hi;
@@ -478,83 +446,111 @@ __device__ __forceinline__ Windows cell_windows(const tpe_seg& SB, const tpe_seg
                  __builtin_amdgcn_readlane(lo, 32), __builtin_amdgcn_readlane(lo, 48)};
 }
 
-// one wave builds one mixture's expansion on one cell; returns the failed flag
-// (k_lo .. k_hi: the cell's reach window, cell_windows)
-__device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __restrict__ sigma,
-                                          const double* __restrict__ coef64, int k_lo, int k_hi,
+// Row-level reductions (each 16-lane DPP row on its own): max in every lane of
+// the row; the nine P_n sums of the row, lane p holding the sum of P_rev4(p)
+// (wave_sum9_transposed without the cross-row steps).
+__device__ __forceinline__ double row_max_dpp(double v) {
+  v = fmax(v, dpp_d<kDppXor1>(v));
+  v = fmax(v, dpp_d<kDppXor2>(v));
+  v = fmax(v, dpp_d<kDppHalfMirror>(v));
+  v = fmax(v, dpp_d<kDppMirror>(v));
+  return v;
+}
+__device__ __forceinline__ float row_sum9_transposed(const float (&P)[9]) {
+  const int lane = lane_id();
+  float w[16];
+#pragma unroll
+  for (int n = 0; n < 16; ++n) w[n] = n < 9 ? P[n] : 0.0f;
+  fold_stage<kDppMirror, 5>(w, (lane >> 3) & 1);      // 9 live -> 5
+  w[5] = 0.0f;
+  fold_stage<kDppHalfMirror, 3>(w, (lane >> 2) & 1);  // -> 3
+  w[3] = 0.0f;
+  fold_stage<kDppXor2, 2>(w, (lane >> 1) & 1);        // -> 2
+  fold_stage<kDppXor1, 1>(w, lane & 1);               // -> 1
+  return w[0];
+}
+
+// One wave builds one mixture's expansion on four consecutive cells, one per
+// 16-lane row (y0: the row's cell centre); returns the row's failed flag.
+// k_lo .. k_hi: the reach window of the four cells' span (cell_windows) --
+// a superset of each cell's own, whose components the exclusion test below
+// drops -- then the wide list; every row walks the same items.
+__device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __restrict__ coef64,
+                                          int k_lo, int k_hi,
                                           const int32_t* __restrict__ wide_idx, int n_wide,
-                                          double T, double y0, double h, float* cell,
+                                          double T, double y0, double h, float* cell, bool store,
                                           int mix, double& m_out) {
   const int64_t off = S.comp_off;
   const int nwin = max(0, k_hi - k_lo + 1);
   const int items = nwin + n_wide;
-  const int lane = lane_id();
+  const int lane = lane_id(), l = lane & 15;
   // component of work item `it` (window first, then the wide list)
   auto comp = [&](int it) -> int {
     return it < nwin ? k_lo + it : wide_idx[off + (it - nwin)];
   };
-  // One pass: every component inside the cell's reach window (components the
-  // plan's global bound admits; each satisfies the expansion bound by the
-  // choice of h).  The exponent is formed in fp64, the series and the
-  // per-component tests in fp32; each lane keeps its own scale m_l (raised
-  // only when a term would exceed e^8 of it) and the lanes are merged at the
-  // end.  The next item's coefficients are loaded before this item's work.
+  // One pass: every component inside the window (components the plan's
+  // global bound admits; each satisfies the expansion bound by the choice of
+  // h).  The exponent is formed in fp64, the series and the per-component
+  // tests in fp32; each lane keeps its own scale m_l (raised only when a term
+  // would exceed e^8 of it) and the row's lanes are merged at the end.  The
+  // next item's coefficients are loaded before this item's work.
   float P[kP];
 #pragma unroll
   for (int n = 0; n < kP; ++n) P[n] = 0.0f;
   double ml = -INFINITY;
   bool bad = false;
   const float hf = (float)h, Tf = (float)T;
-  int it = lane;
+  int it = l;
   int k = it < items ? comp(it) : 0;
   double4 c = it < items ? ld4(coef64, off + k) : make_double4(0.0, 0.0, 0.0, 0.0);
-  for (; it < items; it += kWave) {
-    const int itn = it + kWave;
+  for (; it < items; it += 16) {
+    const int itn = it + 16;
     const int kn = itn < items ? comp(itn) : 0;
     const double4 cn = itn < items ? ld4(coef64, off + kn) : c;
-    // window items that are wide come from the list instead
+    // window items that are wide come from the list instead; below the
+    // plan's floor on the whole cell: left out.  Branch-free: an excluded
+    // item adds zero terms.
     const bool skip = it < nwin && is_wide(S, k, c.y);
     const double dy = y0 - c.x;
     const float dyf = (float)dy, inv = (float)c.y;
     const float zn = fmaxf(fabsf(dyf) - hf, 0.0f) * inv;
-    // below the plan's floor on the whole cell: left out
-    if (!skip && (float)c.z - 0.5f * zn * zn >= Tf) {
-      const double zc = dy * c.y;
-      const double v = c.z - 0.5 * zc * zc;
-      if (v > ml + 8.0) {  // new scale: rescale this lane's partial sums
-        const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - v));
+    const bool inc = !skip && ((float)c.z - 0.5f * zn * zn >= Tf);
+    const double zc = dy * c.y;
+    const double v = c.z - 0.5 * zc * zc;
+    const bool up = inc && v > ml + 8.0;
+    if (__any(up)) {  // new scale: rescale the raising lanes' partial sums
+      const float r = up ? ((ml == -INFINITY) ? 0.0f : __expf((float)(ml - v))) : 1.0f;
 #pragma unroll
-        for (int n = 0; n < kP; ++n) P[n] *= r;
-        ml = v;
-      }
-      const float hi2 = hf * inv * inv;
-      const float Af = -dyf * hi2, B2 = -hf * hi2;  // A and 2B
-      bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > kRhoLim * (1.0 + 1e-5));
-      const float e = __expf((float)(v - ml));
-      float cm = 0.0f, cc = e;  // e * c_n
-      P[0] += e;
+      for (int n = 0; n < kP; ++n) P[n] *= r;
+      ml = up ? v : ml;
+    }
+    const float hi2 = hf * inv * inv;
+    const float Af = inc ? -dyf * hi2 : 0.0f, B2 = inc ? -hf * hi2 : 0.0f;  // A and 2B
+    bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > (float)(kRhoLim * (1.0 + 1e-5)));
+    const float e = inc ? __expf((float)(v - ml)) : 0.0f;
+    float cm = 0.0f, cc = e;  // e * c_n
+    P[0] += e;
 #pragma unroll
-      for (int n = 0; n + 1 < kP; ++n) {
-        const float cnx = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
-        P[n + 1] += cnx;
-        cm = cc;
-        cc = cnx;
-      }
+    for (int n = 0; n + 1 < kP; ++n) {
+      const float cnx = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
+      P[n + 1] += cnx;
+      cm = cc;
+      cc = cnx;
     }
     k = kn;
     c = cn;
   }
-  const double m0 = wave_max_dpp(ml);
+  const double m0 = row_max_dpp(ml);
   {
     const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - m0));
 #pragma unroll
     for (int n = 0; n < kP; ++n) P[n] *= r;
   }
-  static_assert(kP == 9, "wave_sum9_transposed folds nine terms");
-  const float v = wave_sum9_transposed(P);  // lane L < 16: the total of P_rev4(L)
-  bad = __any(bad);
-  const int n = rev4(lane & 15);
-  if (lane < 16 && n < kP) {
+  static_assert(kP == 9, "row_sum9_transposed folds nine terms");
+  const float v = row_sum9_transposed(P);  // lane p of the row: the row's total of P_rev4(p)
+  bad = ((__ballot(bad) >> (lane & ~15)) & 0xFFFFull) != 0;
+  const int n = rev4(l);
+  if (store && n < kP) {
     if (n < kP32)
       cell[2 * n + mix] = v;
     else
@@ -682,19 +678,25 @@ __global__ __launch_bounds__(kBS) void k_table_build(
     W->slope = 0.0f;  // raised by k_table_score (the next launch)
   }
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
-  const int wid = threadIdx.x / kWave;
-  for (int64_t c = (int64_t)blockIdx.x * (kBS / kWave) + wid; c < g.nb;
-       c += (int64_t)gridDim.x * (kBS / kWave)) {
-    const double y0 = (double)cell_centre((float)g.origin, (float)g.h, (int)c);
-    float* region = cells + J.tbl_off * (kSlotB / 4);
-    float* out = region + c * kCellF;
+  const int wid = threadIdx.x / kWave, row = lane_id() >> 4;
+  float* region = cells + J.tbl_off * (kSlotB / 4);
+  // a wave per four consecutive cells (one per 16-lane row)
+  for (int64_t q = (int64_t)blockIdx.x * (kBS / kWave) + wid; 4 * q < g.nb;
+       q += (int64_t)gridDim.x * (kBS / kWave)) {
+    const int c0 = (int)(4 * q), c1 = min(c0 + 3, g.nb - 1);
+    const int c = c0 + row;
+    const bool mine = c < g.nb;
+    const double y0 = (double)cell_centre((float)g.origin, (float)g.h, min(c, c1));
+    const double ylo = (double)cell_centre((float)g.origin, (float)g.h, c0) - g.h;
+    const double yhi = (double)cell_centre((float)g.origin, (float)g.h, c1) + g.h;
+    float* out = region + (int64_t)min(c, c1) * kCellF;
     double mb, ma;
-    const Windows w = cell_windows(SB, SA, reach_hi, reach_lo, y0, g.h);
-    const bool bb = build_mix(SB, sigma, coef64, w.lo_b, w.end_b - 1, wide_idx, Tb.n_wide_below,
-                              Tb.T_below, y0, g.h, out, 0, mb);
-    const bool ba = build_mix(SA, sigma, coef64, w.lo_a, w.end_a - 1, wide_idx, Tb.n_wide_above,
-                              Tb.T_above, y0, g.h, out, 1, ma);
-    if (lane_id() == 0) {
+    const Windows w = cell_windows(SB, SA, reach_hi, reach_lo, ylo, yhi);
+    const bool bb = build_mix(SB, coef64, w.lo_b, w.end_b - 1, wide_idx, Tb.n_wide_below,
+                              Tb.T_below, y0, g.h, out, mine, 0, mb);
+    const bool ba = build_mix(SA, coef64, w.lo_a, w.end_a - 1, wide_idx, Tb.n_wide_above,
+                              Tb.T_above, y0, g.h, out, mine, 1, ma);
+    if ((lane_id() & 15) == 0 && mine) {
       // dword 15: the score offset m_below - m_above, NaN marks a failed cell
       out[15] = (bb || ba) ? __int_as_float(0x7FC00000) : (float)(mb - ma);
       float* mp = region + (int64_t)J.tbl_cap * kCellF + 2 * c;  // (m_below, m_above)
@@ -1230,6 +1232,9 @@ constexpr double kBandRho = 1.5;     // admissible 1.05 |A| + 1.1025 |B|
 constexpr int kBandCells = 64;       // cells expanded per job (sorted; the rest: direct)
 constexpr int kBandBits = 32768;     // cell bitmap of the select kernel (LDS)
 constexpr int kBandSlots = 16;       // expand blocks per job and mixture (grid-stride over cells)
+constexpr int kBandFinal = 16;       // final blocks per job (grid-stride over survivors)
+constexpr int kSelPT = 16;           // entries per thread and pass of the select kernel
+constexpr int kExpU = 8;             // components loaded ahead per thread in the expansion
 
 struct BandMix {  // one mixture's expansion on one cell
   double P[kBandD + 1];
@@ -1241,9 +1246,14 @@ struct BandMix {  // one mixture's expansion on one cell
 struct BandWork {  // per job (tpe_band_work_bytes)
   int cell[kBandCells];
   BandMix mix[kBandCells][2];
+  BestT part[kBandFinal];  // the final blocks' winners
+  unsigned int done;       // final blocks finished (the last one reduces)
 };
 
-// expansion of mixture S on the cell (y0, h) into E (LDS); all threads
+// expansion of mixture S on the cell (y0, h) into E (LDS); all threads.
+// One pass over the components, kExpU loads in flight per thread; each thread
+// keeps its own scale (raised when a term would exceed e^8 of it) and the
+// threads are merged at the end (fixed order: deterministic).
 __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64, double y0,
                             double h, BandMix& E, double* dred) {
   const int nc = S.n_obs + 1;
@@ -1251,43 +1261,55 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
   const double4 cp = ld4(coef64, off + S.prior_pos);
   const double far = (fabs(y0 - cp.x) + 1.05 * h) * cp.y;
   const double T = cp.z - 0.5 * far * far - (log((double)nc) + kBandTau);
-  // scale: the largest included term at the centre
-  double m = -INFINITY;
-  for (int k = threadIdx.x; k < nc; k += kBS) {
-    const double4 c = ld4(coef64, off + k);
-    const double zn = fmax(fabs(y0 - c.x) - 1.05 * h, 0.0) * c.y;
-    if (c.z - 0.5 * zn * zn >= T) {
-      const double z0 = (y0 - c.x) * c.y;
-      m = fmax(m, c.z - 0.5 * z0 * z0);
-    }
-  }
-  m = block_max<kBS, double>(m, dred);
   if (threadIdx.x == 0) E.n_dir = 0;
   __syncthreads();
   double P[kBandD + 1];
 #pragma unroll
   for (int n = 0; n <= kBandD; ++n) P[n] = 0.0;
-  for (int k = threadIdx.x; k < nc; k += kBS) {
-    const double4 c = ld4(coef64, off + k);
-    const double zn = fmax(fabs(y0 - c.x) - 1.05 * h, 0.0) * c.y;
-    if (!(c.z - 0.5 * zn * zn >= T)) continue;
-    const double hi2 = h * c.y * c.y;
-    const double A = -(y0 - c.x) * hi2, B = -0.5 * h * hi2;
-    if (1.05 * fabs(A) + 1.1025 * fabs(B) > kBandRho) {
-      const int p = atomicAdd(&E.n_dir, 1);
-      if (p < kBandDirect) E.dir[p] = k;
-      continue;
-    }
-    const double z0 = (y0 - c.x) * c.y;
-    double cm = 0.0, cc = exp(c.z - 0.5 * z0 * z0 - m);  // e * c_n
-    P[0] += cc;
+  double ml = -INFINITY;
+  for (int k0 = 0; k0 < nc; k0 += kExpU * kBS) {
+    double4 cs[kExpU];
 #pragma unroll
-    for (int n = 0; n < kBandD; ++n) {
-      const double cn = fma(A, cc, 2.0 * B * cm) * (1.0 / (double)(n + 1));
-      P[n + 1] += cn;
-      cm = cc;
-      cc = cn;
+    for (int u = 0; u < kExpU; ++u) {
+      const int k = k0 + u * kBS + (int)threadIdx.x;
+      cs[u] = k < nc ? ld4(coef64, off + k) : make_double4(0.0, 0.0, -INFINITY, 0.0);
     }
+#pragma unroll
+    for (int u = 0; u < kExpU; ++u) {
+      const double4 c = cs[u];
+      const double zn = fmax(fabs(y0 - c.x) - 1.05 * h, 0.0) * c.y;
+      if (!(c.z - 0.5 * zn * zn >= T)) continue;  // (padding: lc = -inf)
+      const double hi2 = h * c.y * c.y;
+      const double A = -(y0 - c.x) * hi2, B = -0.5 * h * hi2;
+      if (1.05 * fabs(A) + 1.1025 * fabs(B) > kBandRho) {
+        const int p = atomicAdd(&E.n_dir, 1);
+        if (p < kBandDirect) E.dir[p] = k0 + u * kBS + (int)threadIdx.x;
+        continue;
+      }
+      const double z0 = (y0 - c.x) * c.y;
+      const double v = c.z - 0.5 * z0 * z0;
+      if (v > ml + 8.0) {  // new scale: rescale this thread's sums
+        const double r = (ml == -INFINITY) ? 0.0 : exp(ml - v);
+#pragma unroll
+        for (int n = 0; n <= kBandD; ++n) P[n] *= r;
+        ml = v;
+      }
+      double cm = 0.0, cc = exp(v - ml);  // e * c_n
+      P[0] += cc;
+#pragma unroll
+      for (int n = 0; n < kBandD; ++n) {
+        const double cn = fma(A, cc, 2.0 * B * cm) * (1.0 / (double)(n + 1));
+        P[n + 1] += cn;
+        cm = cc;
+        cc = cn;
+      }
+    }
+  }
+  const double m = block_max<kBS, double>(ml, dred);
+  {
+    const double r = (ml == -INFINITY) ? 0.0 : exp(ml - m);
+#pragma unroll
+    for (int n = 0; n <= kBandD; ++n) P[n] *= r;
   }
   // block sums of the kBandD + 1 terms (fixed order: deterministic)
 #pragma unroll
@@ -1363,17 +1385,19 @@ __device__ __forceinline__ int band_cell(const tpe_table& Tb, float y) {
 // (kBandOverflow: the band overflowed), [3] listed cells
 constexpr uint32_t kBandOverflow = 0xFFFFFFFFu;
 
-// Select: keep the entries with hi >= the final G, compacted in place (entry
-// order), and list their distinct cells (ascending, at most kBandCells) in
-// the job's BandWork.  A job whose band overflowed gets the fp32 winner with
-// n_scored = -1.
+// Select (block per job): keep the entries with hi >= the final G, compacted
+// in place, and list their distinct cells (ascending, at most kBandCells) in
+// the job's BandWork.  kSelPT entries per thread per pass, loaded together
+// (C3's bands are a few thousand entries: one pass).  A job whose band
+// overflowed gets the fp32 winner with n_scored = -1.
 __global__ __launch_bounds__(kBS) void k_band_select(
     const tpe_job* __restrict__ jobs, const tpe_table* __restrict__ tables,
     tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
     const tpe_best* __restrict__ partial, int64_t nper, tpe_best* __restrict__ best,
     BandWork* __restrict__ work) {
-  __shared__ BestT red[kBS / kWave];
-  __shared__ int s_scan[kBS / kWave];
+  constexpr int kNW = kBS / kWave;
+  __shared__ BestT red[kNW];
+  __shared__ int s_cnt[kSelPT * kNW], s_scan[kNW];
   __shared__ uint32_t s_bits[kBandBits / 32];
   const int j = blockIdx.x;
   uint32_t* ctl = band_ctl + 4 * (int64_t)j;
@@ -1383,6 +1407,7 @@ __global__ __launch_bounds__(kBS) void k_band_select(
   if (threadIdx.x == 0) {
     ctl[0] = 0u;  // ready for the next scorer call
     ctl[1] = 0u;
+    work[j].done = 0u;
   }
   if (n > band_cap) {
     // the fp32 winner; the caller re-scores the job exactly
@@ -1401,35 +1426,54 @@ __global__ __launch_bounds__(kBS) void k_band_select(
   }
   const tpe_table Tb = tables[j];
   for (int w = threadIdx.x; w < kBandBits / 32; w += kBS) s_bits[w] = 0u;
-  __syncthreads();
   tpe_band* B = band + (int64_t)j * band_cap;
   const int lane = lane_id(), wid = threadIdx.x / kWave;
+  const uint64_t lt = (1ull << lane) - 1ull;
   int64_t kept = 0;
-  for (int64_t e0 = 0; e0 < n; e0 += kBS) {
-    const int64_t e = e0 + threadIdx.x;
-    tpe_band E{};
-    bool keep = false;
-    if (e < n) {
-      E = B[e];
-      keep = !(E.hi < G);  // (NaN bounds stay)
+  for (int64_t e0 = 0; e0 < n; e0 += (int64_t)kSelPT * kBS) {
+    tpe_band E[kSelPT];
+    bool keep[kSelPT];
+#pragma unroll
+    for (int t = 0; t < kSelPT; ++t) {
+      const int64_t e = e0 + (int64_t)t * kBS + threadIdx.x;
+      keep[t] = false;
+      if (e < n) E[t] = B[e];
     }
-    const uint64_t bal = __ballot(keep);
-    if (lane == 0) s_scan[wid] = __popcll(bal);
-    __syncthreads();  // (every entry of the chunk is read before any is written)
-    int64_t p = kept + __popcll(bal & ((1ull << lane) - 1ull));
-    int tot = 0;
-    for (int w = 0; w < kBS / kWave; ++w) {
-      p += (w < wid) ? s_scan[w] : 0;
-      tot += s_scan[w];
+    int before[kSelPT];
+#pragma unroll
+    for (int t = 0; t < kSelPT; ++t) {
+      const int64_t e = e0 + (int64_t)t * kBS + threadIdx.x;
+      keep[t] = e < n && !(E[t].hi < G);  // (NaN bounds stay)
+      const uint64_t bal = __ballot(keep[t]);
+      before[t] = __popcll(bal & lt);
+      if (lane == 0) s_cnt[t * kNW + wid] = __popcll(bal);
     }
-    if (keep) {
-      B[p] = E;
-      const int c = band_cell(Tb, E.y);
+    __syncthreads();  // (every entry of the pass is read before any is written)
+    // exclusive scan of the kSelPT * kNW counts (slot order = entry order)
+    if (threadIdx.x < kWave) {
+      const int c = s_cnt[threadIdx.x];
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int v = __shfl_up(incl, o, kWave);
+        if (lane >= o) incl += v;
+      }
+      s_cnt[threadIdx.x] = incl - c;
+      if (threadIdx.x == kWave - 1) s_scan[0] = incl;
+    }
+    static_assert(kSelPT * kNW == kWave, "one wave scans the pass's slot counts");
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kSelPT; ++t) {
+      if (!keep[t]) continue;
+      B[kept + s_cnt[t * kNW + wid] + before[t]] = E[t];
+      const int c = band_cell(Tb, E[t].y);
       if (c >= 0 && c < kBandBits) atomicOr(&s_bits[c >> 5], 1u << (c & 31));
     }
-    kept += tot;
-    __syncthreads();  // s_scan reused
+    kept += s_scan[0];
+    __syncthreads();  // s_cnt / s_scan reused
   }
+  __syncthreads();  // (the bitmap is complete; also when n == 0)
   // the listed cells: bitmap words in order, kBandBits / 32 / kBS per thread
   constexpr int kPer = kBandBits / 32 / kBS;
   int cnt = 0;
@@ -1437,7 +1481,7 @@ __global__ __launch_bounds__(kBS) void k_band_select(
   for (int i = 0; i < kPer; ++i) cnt += __popc(s_bits[threadIdx.x * kPer + i]);
   int pos = block_scan_sum(cnt, s_scan) - cnt;  // exclusive prefix
   int total = 0;  // (s_scan holds the wave totals)
-  for (int w = 0; w < kBS / kWave; ++w) total += s_scan[w];
+  for (int w = 0; w < kNW; ++w) total += s_scan[w];
   for (int i = 0; i < kPer && pos < kBandCells; ++i) {
     uint32_t b = s_bits[threadIdx.x * kPer + i];
     while (b && pos < kBandCells) {
@@ -1482,59 +1526,82 @@ __global__ __launch_bounds__(kBS) void k_band_expand(
   }
 }
 
-// Final: every survivor scored in fp64 (its cell's expansions, else the
-// direct sum); np.argmax over them -> best[j]; the controls left zero.
+// Final: block (slot, job) scores survivors slot * kBS + t, stride kBandFinal
+// * kBS, in fp64 (its cell's expansions, else the direct sum); the last
+// block of the job to finish takes np.argmax over the blocks' winners ->
+// best[j] and leaves the controls zero.
 __global__ __launch_bounds__(kBS) void k_band_final(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
     const tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
-    tpe_best* __restrict__ best, const BandWork* __restrict__ work) {
+    tpe_best* __restrict__ best, BandWork* __restrict__ work) {
   __shared__ BestT red[kBS / kWave];
   __shared__ int s_cell[kBandCells];
-  const int j = blockIdx.x;
+  __shared__ bool s_last;
+  const int j = blockIdx.y;
   uint32_t* ctl = band_ctl + 4 * (int64_t)j;
   const uint32_t ns = ctl[2];
   const int nc = (int)ctl[3];
   for (int k = threadIdx.x; k < nc; k += kBS) s_cell[k] = work[j].cell[k];
-  __syncthreads();  // (controls read; cells staged)
-  if (threadIdx.x == 0) {
-    ctl[2] = 0u;
-    ctl[3] = 0u;
-  }
-  if (ns == kBandOverflow) return;  // (best[j] written by k_band_select)
+  __syncthreads();
   const tpe_job J = jobs[j];
-  const tpe_seg SB = segs[J.below], SA = segs[J.above];
-  const tpe_table Tb = tables[j];
-  const bool lgmm = J.family == TPE_LGMM1;
-  const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
-  const tpe_band* B = band + (int64_t)j * band_cap;
   BestT bx{0.0, -1, 0.0};
-  for (int64_t p = threadIdx.x; p < (int64_t)ns; p += kBS) {
-    const tpe_band E = B[p];
-    const double y = (double)E.y;
-    const int c = band_cell(Tb, E.y);
-    int k = -1;
-    if (c >= 0) {  // binary search of the listed cells
-      int lo = 0, hi = nc;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (s_cell[mid] < c) lo = mid + 1; else hi = mid;
+  if (ns != kBandOverflow) {
+    const tpe_seg SB = segs[J.below], SA = segs[J.above];
+    const tpe_table Tb = tables[j];
+    const bool lgmm = J.family == TPE_LGMM1;
+    const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
+    const tpe_band* B = band + (int64_t)j * band_cap;
+    for (int64_t p = (int64_t)blockIdx.x * kBS + threadIdx.x; p < (int64_t)ns;
+         p += (int64_t)kBandFinal * kBS) {
+      const tpe_band E = B[p];
+      const double y = (double)E.y;
+      const int c = band_cell(Tb, E.y);
+      int k = -1;
+      if (c >= 0) {  // binary search of the listed cells
+        int lo = 0, hi = nc;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (s_cell[mid] < c) lo = mid + 1; else hi = mid;
+        }
+        k = (lo < nc && s_cell[lo] == c) ? lo : -1;
       }
-      k = (lo < nc && s_cell[lo] == c) ? lo : -1;
+      double lb, la;
+      if (k >= 0 && work[j].mix[k][0].n_dir >= 0 && work[j].mix[k][1].n_dir >= 0) {
+        const double u = (y - (double)cell_centre(g0, h32, c)) / Tb.h;
+        lb = band_eval(work[j].mix[k][0], coef64, SB.comp_off, u, y);
+        la = band_eval(work[j].mix[k][1], coef64, SA.comp_off, u, y);
+      } else {
+        lb = band_direct(SB, coef64, y);
+        la = band_direct(SA, coef64, y);
+      }
+      best_update(bx, lb - la, E.index, cand_value(E.y, lgmm));
     }
-    double lb, la;
-    if (k >= 0 && work[j].mix[k][0].n_dir >= 0 && work[j].mix[k][1].n_dir >= 0) {
-      const double u = (y - (double)cell_centre(g0, h32, c)) / Tb.h;
-      lb = band_eval(work[j].mix[k][0], coef64, SB.comp_off, u, y);
-      la = band_eval(work[j].mix[k][1], coef64, SA.comp_off, u, y);
-    } else {
-      lb = band_direct(SB, coef64, y);
-      la = band_direct(SA, coef64, y);
-    }
-    best_update(bx, lb - la, E.index, cand_value(E.y, lgmm));
   }
   bx = block_best<kBS>(bx, red);
-  if (threadIdx.x == 0) best[j] = tpe_best{bx.score, bx.index, bx.value, J.n_cand};
+  if (threadIdx.x == 0) {
+    work[j].part[blockIdx.x] = bx;
+    __threadfence();  // the winner is visible before the count
+    s_last = atomicAdd(&work[j].done, 1u) == (unsigned)(kBandFinal - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // (acquire: the other blocks' winners)
+  if (threadIdx.x == 0) {
+    if (ns != kBandOverflow) {
+      BestT r = work[j].part[0];
+      for (int b = 1; b < kBandFinal; ++b) {
+        const BestT o = work[j].part[b];
+        if (better(o.score, o.index, r.score, r.index)) r = o;
+      }
+      best[j] = tpe_best{r.score, r.index, r.value, J.n_cand};
+    }
+#ifndef TPE_DIAG_BAND_KEEP  // diagnostic builds: counters left for tools/band_probe.py
+    ctl[2] = 0u;
+    ctl[3] = 0u;
+#endif
+    work[j].done = 0u;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1955,8 +2022,8 @@ extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, i
                      band_ctl, partial, gx, best, W);
   hipLaunchKernelGGL(k_band_expand, dim3(kBandSlots, n_jobs, 2), dim3(kBS), 0, st, jobs, segs,
                      coef64, tables, band_ctl, W);
-  hipLaunchKernelGGL(k_band_final, dim3(n_jobs), dim3(kBS), 0, st, jobs, segs, coef64, tables,
-                     band, band_cap, band_ctl, best, W);
+  hipLaunchKernelGGL(k_band_final, dim3(kBandFinal, n_jobs), dim3(kBS), 0, st, jobs, segs, coef64,
+                     tables, band, band_cap, band_ctl, best, W);
   return check_launch("tpe_band_rescore");
 }
 
