@@ -37,6 +37,7 @@ struct Rccl {
   ErrorStringFn error_string = nullptr;
   AsyncErrorFn async_error = nullptr;
   bool ok = false;
+  char why[256] = "not loaded";  // the loader's error, kept (dlerror() is one-shot)
 };
 
 const Rccl& rccl() {
@@ -46,12 +47,19 @@ const Rccl& rccl() {
     void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
     if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
     if (!h) h = dlopen("librccl.so", RTLD_NOW);
-    if (!h) return;
+    auto keep = [](const char* e, const char* dflt) {
+      snprintf(r.why, sizeof(r.why), "%s", e ? e : dflt);
+    };
+    if (!h) {
+      keep(dlerror(), "dlopen failed");
+      return;
+    }
     r.all_gather = reinterpret_cast<AllGatherFn>(dlsym(h, "ncclAllGather"));
     r.comm_count = reinterpret_cast<CommCountFn>(dlsym(h, "ncclCommCount"));
     r.error_string = reinterpret_cast<ErrorStringFn>(dlsym(h, "ncclGetErrorString"));
     r.async_error = reinterpret_cast<AsyncErrorFn>(dlsym(h, "ncclCommGetAsyncError"));
     r.ok = r.all_gather && r.comm_count;
+    if (!r.ok) keep(dlerror(), "ncclAllGather / ncclCommCount not exported");
   });
   return r;
 }
@@ -120,7 +128,7 @@ extern "C" int tpe_maxloc_allreduce(const tpe_best* local, tpe_best* gathered, t
   if (n_labels == 0) return TPE_OK;
   const Rccl& r = rccl();
   if (!r.ok) {
-    set_error("tpe_maxloc_allreduce: librccl.so.1 not loadable (%s)", dlerror());
+    set_error("tpe_maxloc_allreduce: librccl.so.1 not loadable (%s)", r.why);
     return TPE_E_UNSUPPORTED;
   }
   int world = 0;

@@ -224,11 +224,12 @@ int tpe_history_order(const double* vals, int64_t ld, const tpe_colspec* specs,
 /* The fit of segment i (segs[i]) from the sorted history: gathers[i] names its
  * column, side (below: 1) and observation count (identity row list: row r of
  * the history is position r, is_below[r] its split flag, n_rows of them).
- * One kernel: the segment's rows in tid order (linear-forgetting positions,
- * the prior's searchsorted slot), the column's order compacted to the
- * segment (means and weights in sorted order), then bandwidths, p_accept and
- * the coefficients exactly as tpe_parzen_fit computes them (same bits).  A
- * count other than gathers[i].count sets bit 4 of *err (nothing written).
+ * One compaction block per segment: the segment's rows in tid order
+ * (linear-forgetting positions, the prior's searchsorted slot), then the
+ * column's order compacted to the segment (means and weights in sorted
+ * order); then tpe_parzen_fit's own bandwidth / coefficient launches (same
+ * bits).  A count other than gathers[i].count sets bit 4 of *err (the
+ * segment's means are not written; the call's results are void).
  * scratch: tpe_fit_sorted_scratch_bytes(n_seg, n_rows) bytes. */
 int64_t tpe_fit_sorted_scratch_bytes(int n_seg, int64_t n_rows);
 int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t ld, const int32_t* order,
