@@ -612,6 +612,233 @@ class Engine:
         return (jobs, np.zeros(1), fb_jobs, P["fb_slice"]) + tuple(P["counts"])
 
     # -- main entry ----------------------------------------------------------
+    def _plan_new(self, works, pkey, prior_weight, lf, precision, scorer, outputs, sample_only,
+                  hist_mode, _hmark):
+        """A level's plan built from its works (the path _plan_fast replays
+        from a recorded plan): kernel groups, fit / categorical segments, the
+        gather list of a history level, and the job descriptors ordered so
+        every kernel call takes a contiguous slice.  Records the plan under
+        ``pkey`` when it can be replayed."""
+        cont, quant, cat = [], [], []
+        for i, w in enumerate(works):
+            if w.kind in CONTINUOUS:
+                (quant if w.kind.startswith("q") else cont).append(i)
+            elif w.kind in CATEGORICAL:
+                cat.append(i)
+            else:
+                raise ValueError("unsupported prior %r for label %r" % (w.kind, w.label))
+
+        _hmark('prep')
+        gathers = []  # history mode: (col, below, dst_off, offset, count, to_int, hist)
+        # ---- continuous / quantized segments --------------------------------
+        fit_ids = cont + quant
+        params = {i: _params(works[i].kind, works[i].args) for i in fit_ids}
+        nf = len(fit_ids)
+        segs = np.zeros(2 * nf, L.SEG_DTYPE)
+        obs_pool = None
+        n_obs_total = n_comp = max_obs = 0
+        if nf:
+            if hist_mode:
+                sizes = np.empty(2 * nf, np.int64)
+                for si, i in enumerate(fit_ids):
+                    sizes[2 * si] = np.asarray(works[i].obs_below).size
+                    sizes[2 * si + 1] = int(works[i].n_above)
+            else:
+                parts = [np.asarray(o, dtype=np.float64).reshape(-1) for i in fit_ids
+                         for o in (works[i].obs_below, works[i].obs_above)]
+                sizes = np.fromiter((o.size for o in parts), np.int64, 2 * nf)
+                obs_pool = np.concatenate(parts)
+            ends = np.cumsum(sizes)
+            obs_off = ends - sizes
+            comp_off = np.cumsum(sizes + 1) - (sizes + 1)
+            segs["obs_off"], segs["comp_off"], segs["n_obs"] = obs_off, comp_off, sizes
+            segs["lf"], segs["prior_weight"] = lf, prior_weight
+            pl = [params[i] for i in fit_ids]
+            for name in ("transform", "family", "floor", "prior_mu", "prior_sigma", "low", "high"):
+                segs[name] = np.repeat([p[name] for p in pl], 2)
+            segs["bounded"] = np.repeat([int(p["bounded"]) for p in pl], 2)
+            n_obs_total = int(ends[-1])
+            n_comp = n_obs_total + 2 * nf
+            max_obs = int(sizes.max())
+            if hist_mode:
+                for si, i in enumerate(fit_ids):
+                    for half in (0, 1):
+                        k = 2 * si + half
+                        gathers.append((works[i].col, 1 - half, int(obs_off[k]), 0, int(sizes[k]),
+                                        0, works[i].hist))
+        if obs_pool is None:
+            obs_pool = np.zeros(1)
+
+        _hmark('segs')
+        # ---- categorical segments ------------------------------------------
+        csegs = np.zeros(2 * len(cat), L.CAT_SEG_DTYPE)
+        cobs_parts, p_init = [], []
+        cobs_off = p_off = 0
+        cat_meta = {}
+        ccols = []
+        for ci, i in enumerate(cat):
+            w = works[i]
+            K, offset, mode, prior_p = categorical_params(w.kind, w.args)
+            cat_meta[i] = (K, offset)
+            prior_off = -1
+            if mode == 1:
+                prior_off = p_off
+                p_init.append(prior_p)
+                p_off += K
+            for half in (0, 1):
+                if hist_mode:
+                    n = np.asarray(w.obs_below).size if half == 0 else int(w.n_above)
+                    gathers.append((w.col, 1 - half, cobs_off, offset, n, 1, w.hist))
+                else:
+                    obs = np.asarray(w.obs_below if half == 0 else w.obs_above).reshape(-1)
+                    obs = obs.astype(np.int64) - offset
+                    cobs_parts.append(obs)
+                    n = obs.size
+                ccols.append((cobs_off, p_off, n, K, mode, max(prior_off, 0)))
+                p_init.append(np.zeros(K))
+                cobs_off += n
+                p_off += K
+        if cat:  # one column assignment per field instead of per segment
+            cc = np.array(ccols, dtype=np.int64)
+            (csegs["obs_off"], csegs["p_off"], csegs["n_obs"], csegs["n_cat"], csegs["mode"],
+             csegs["prior_p_off"]) = cc.T
+            csegs["lf"], csegs["prior_weight"] = lf, prior_weight
+        cobs_pool = np.concatenate(cobs_parts) if cobs_parts else np.zeros(1, np.int64)
+        p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
+
+        _hmark('cats')
+        # ---- jobs, ordered so every kernel call takes a contiguous slice -----------
+        inj = lambda i: works[i].cand is not None  # noqa: E731
+        lat_ranges = {}
+        fallback = []
+        for i in quant:
+            if not inj(i):
+                kmin, kmax = _lattice_range(works[i], params[i])
+                if kmax - kmin + 1 > LATTICE_CAP:
+                    fallback.append(i)
+                else:
+                    lat_ranges[i] = (kmin, kmax - kmin + 1)
+        def cont_mode(i):
+            if sample_only:
+                return "cont"
+            if precision != 32:
+                w = works[i]
+                m = int(w.n_above) if w.obs_above is None else np.size(w.obs_above)
+                return "pruned64" if (self.exact64 == "pruned" or (
+                    self.exact64 == "auto" and m >= PRUNED64_MIN_COMP)) else "cont"
+            n = int(np.asarray(works[i].cand).size) if inj(i) else \
+                int(works[i].n_total or works[i].n_cand)
+            mode = scorer
+            if mode == "auto":
+                mode = "cont"
+                if not inj(i):
+                    if n >= TABLE_MIN_CAND:
+                        mode = "table"
+                    elif n >= SORTED_MIN_CAND and not outputs:
+                        mode = "sorted"
+            if mode == "sorted" and (inj(i) or outputs):
+                mode = "cont"
+            return "cont" if mode == "dense" else mode
+        modes = {i: cont_mode(i) for i in cont}
+        groups = [
+            ("cont", [i for i in cont if inj(i) and modes[i] == "cont"]),
+            ("cont", [i for i in cont if not inj(i) and modes[i] == "cont"]),
+            ("sorted", [i for i in cont if modes[i] == "sorted"]),
+            ("pruned64", [i for i in cont if inj(i) and modes[i] == "pruned64"]),
+            ("pruned64", [i for i in cont if not inj(i) and modes[i] == "pruned64"]),
+            ("table", [i for i in cont if inj(i) and modes[i] == "table"]),
+            ("table", [i for i in cont if not inj(i) and modes[i] == "table"]),
+            ("lat", [i for i in quant if i in lat_ranges]),
+            ("qfb", fallback),
+            ("qinj", [i for i in quant if inj(i)]),
+            ("cat", [i for i in cat if inj(i)]),
+            ("cat", [i for i in cat if not inj(i)]),
+        ]
+        order = [i for _, ids in groups for i in ids]
+        nj_all = len(order)
+        jobs = np.zeros(nj_all, L.JOB_DTYPE)
+        J = {name: np.zeros(nj_all, L.JOB_DTYPE[name]) for name in L.JOB_DTYPE.names}
+        cand_parts, cand_off, out_off, lat_off, qfb_off = [], 0, 0, 0, 0
+        sort_off = cnt_off = tbl_off = 0
+        seg_of = {i: si for si, i in enumerate(fit_ids)}
+        cseg_of = {i: ci for ci, i in enumerate(cat)}
+        for pos, i in enumerate(order):
+            w = works[i]
+            J["key"][pos] = int(w.key) & 0xFFFFFFFFFFFFFFFF
+            J["cand_base"][pos] = w.cand_base
+            n = int(np.asarray(w.cand).size) if inj(i) else int(w.n_cand)
+            J["n_cand"][pos] = n
+            J["out_off"][pos] = out_off
+            out_off += n
+            flags = 0
+            if inj(i):
+                # categorical candidates are category indices (0..K-1), as the
+                # reference's randint_via_categorical samples them (tpe.py:590)
+                c = np.asarray(w.cand, dtype=np.float64).reshape(-1)
+                J["cand_off"][pos] = cand_off
+                cand_parts.append(c)
+                cand_off += c.size
+                flags |= L.F_INJECTED
+            if i in cat_meta:
+                J["family"][pos] = L.CAT
+                J["lat_n"][pos] = cat_meta[i][0]  # category count (sizes the sampler's path)
+                J["below"][pos], J["above"][pos] = 2 * cseg_of[i], 2 * cseg_of[i] + 1
+                J["flags"][pos] = flags
+                continue
+            P = params[i]
+            J["family"][pos] = P["family"]
+            J["below"][pos], J["above"][pos] = 2 * seg_of[i], 2 * seg_of[i] + 1
+            if P["bounded"]:
+                flags |= L.F_LOW | L.F_HIGH
+                J["low"][pos], J["high"][pos] = P["low"], P["high"]
+            if P["q"] is not None:
+                flags |= L.F_QUANT
+                J["q"][pos] = P["q"]
+                if i in lat_ranges:
+                    kmin, nk = lat_ranges[i]
+                    J["lat_off"][pos], J["lat_kmin"][pos], J["lat_n"][pos] = lat_off, kmin, nk
+                    if precision == 32 and max(abs(kmin), abs(kmin + nk - 1)) <= DRAW32_MAX_SLOT:
+                        flags |= L.F_DRAW32
+                    flags |= L.F_LATTICE_READY  # cleared below for a large level
+                    lat_off += nk
+                elif i in fallback:
+                    J["cand_off"][pos] = qfb_off
+                    qfb_off += n
+            elif modes[i] == "table":
+                J["tbl_off"][pos], J["tbl_cap"][pos] = tbl_off, TABLE_CAP
+                tbl_off += TABLE_CAP
+                if inj(i):
+                    J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P)
+            elif modes[i] == "pruned64" and inj(i):
+                J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P, fp32=False)
+            elif modes[i] == "sorted":
+                J["bin_lo"][pos], J["bin_hi"][pos] = _support(w, P)
+                J["sort_off"][pos], J["cnt_off"][pos] = sort_off, cnt_off
+                slots = ctypes.c_int64(0)
+                cnt_off += self.lib.tpe_sort_layout(n, ctypes.byref(slots))
+                sort_off += slots.value
+            J["flags"][pos] = flags
+        if lat_off > LAT_PACK_MAX:  # the slots are set by the library's memset instead
+            J["flags"] &= ~L.F_LATTICE_READY
+        for name, col in J.items():
+            jobs[name] = col
+        cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
+        # the dense fallback first materialises its draws: a job copy whose
+        # out_off points into the scratch candidate buffer
+        fb_slice = _slice_of(groups, [k for k, _ in groups].index("qfb"))
+        fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
+        fb_jobs["out_off"] = fb_jobs["cand_off"]
+        if pkey is not None and not any(k == "sorted" and ids for k, ids in groups):
+            self._plans[pkey] = self._plan_record(
+                works, cont, quant, cat, fit_ids, params, segs, csegs, p_pool, cat_meta,
+                lat_ranges, fallback, modes, groups, order, gathers, jobs, fb_slice, out_off,
+                lat_off, qfb_off, sort_off, cnt_off, tbl_off)
+
+        return (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp,
+                max_obs, csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes,
+                groups, order, gathers, inj, jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off,
+                qfb_off, sort_off, cnt_off, tbl_off)
+
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
             outputs=False, stream=None, timers=None, sample_only=False,
             pruned=True, scorer=None, posteriors=False, history=None, rows=None,
@@ -730,226 +957,16 @@ class Engine:
                 inj = lambda i: False  # noqa: E731
             else:
                 inj = lambda i: works[i].cand is not None  # noqa: E731
-        else:
-            cont, quant, cat = [], [], []
-            for i, w in enumerate(works):
-                if w.kind in CONTINUOUS:
-                    (quant if w.kind.startswith("q") else cont).append(i)
-                elif w.kind in CATEGORICAL:
-                    cat.append(i)
-                else:
-                    raise ValueError("unsupported prior %r for label %r" % (w.kind, w.label))
-
-            _hmark('prep')
-            gathers = []  # history mode: (col, below, dst_off, offset, count, to_int, hist)
-            # ---- continuous / quantized segments --------------------------------
-            fit_ids = cont + quant
-            params = {i: _params(works[i].kind, works[i].args) for i in fit_ids}
-            nf = len(fit_ids)
-            segs = np.zeros(2 * nf, L.SEG_DTYPE)
-            obs_pool = None
-            n_obs_total = n_comp = max_obs = 0
-            if nf:
-                if hist_mode:
-                    sizes = np.empty(2 * nf, np.int64)
-                    for si, i in enumerate(fit_ids):
-                        sizes[2 * si] = np.asarray(works[i].obs_below).size
-                        sizes[2 * si + 1] = int(works[i].n_above)
-                else:
-                    parts = [np.asarray(o, dtype=np.float64).reshape(-1) for i in fit_ids
-                             for o in (works[i].obs_below, works[i].obs_above)]
-                    sizes = np.fromiter((o.size for o in parts), np.int64, 2 * nf)
-                    obs_pool = np.concatenate(parts)
-                ends = np.cumsum(sizes)
-                obs_off = ends - sizes
-                comp_off = np.cumsum(sizes + 1) - (sizes + 1)
-                segs["obs_off"], segs["comp_off"], segs["n_obs"] = obs_off, comp_off, sizes
-                segs["lf"], segs["prior_weight"] = lf, prior_weight
-                pl = [params[i] for i in fit_ids]
-                for name in ("transform", "family", "floor", "prior_mu", "prior_sigma", "low", "high"):
-                    segs[name] = np.repeat([p[name] for p in pl], 2)
-                segs["bounded"] = np.repeat([int(p["bounded"]) for p in pl], 2)
-                n_obs_total = int(ends[-1])
-                n_comp = n_obs_total + 2 * nf
-                max_obs = int(sizes.max())
-                if hist_mode:
-                    for si, i in enumerate(fit_ids):
-                        for half in (0, 1):
-                            k = 2 * si + half
-                            gathers.append((works[i].col, 1 - half, int(obs_off[k]), 0, int(sizes[k]),
-                                            0, works[i].hist))
-            if obs_pool is None:
-                obs_pool = np.zeros(1)
-
-            _hmark('segs')
-            # ---- categorical segments ------------------------------------------
-            csegs = np.zeros(2 * len(cat), L.CAT_SEG_DTYPE)
-            cobs_parts, p_init = [], []
-            cobs_off = p_off = 0
-            cat_meta = {}
-            ccols = []
-            for ci, i in enumerate(cat):
-                w = works[i]
-                K, offset, mode, prior_p = categorical_params(w.kind, w.args)
-                cat_meta[i] = (K, offset)
-                prior_off = -1
-                if mode == 1:
-                    prior_off = p_off
-                    p_init.append(prior_p)
-                    p_off += K
-                for half in (0, 1):
-                    if hist_mode:
-                        n = np.asarray(w.obs_below).size if half == 0 else int(w.n_above)
-                        gathers.append((w.col, 1 - half, cobs_off, offset, n, 1, w.hist))
-                    else:
-                        obs = np.asarray(w.obs_below if half == 0 else w.obs_above).reshape(-1)
-                        obs = obs.astype(np.int64) - offset
-                        cobs_parts.append(obs)
-                        n = obs.size
-                    ccols.append((cobs_off, p_off, n, K, mode, max(prior_off, 0)))
-                    p_init.append(np.zeros(K))
-                    cobs_off += n
-                    p_off += K
-            if cat:  # one column assignment per field instead of per segment
-                cc = np.array(ccols, dtype=np.int64)
-                (csegs["obs_off"], csegs["p_off"], csegs["n_obs"], csegs["n_cat"], csegs["mode"],
-                 csegs["prior_p_off"]) = cc.T
-                csegs["lf"], csegs["prior_weight"] = lf, prior_weight
-            cobs_pool = np.concatenate(cobs_parts) if cobs_parts else np.zeros(1, np.int64)
-            p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
-
-            _hmark('cats')
-            # ---- jobs, ordered so every kernel call takes a contiguous slice -----------
-            inj = lambda i: works[i].cand is not None  # noqa: E731
-            lat_ranges = {}
-            fallback = []
-            for i in quant:
-                if not inj(i):
-                    kmin, kmax = _lattice_range(works[i], params[i])
-                    if kmax - kmin + 1 > LATTICE_CAP:
-                        fallback.append(i)
-                    else:
-                        lat_ranges[i] = (kmin, kmax - kmin + 1)
-            def cont_mode(i):
-                if sample_only:
-                    return "cont"
-                if precision != 32:
-                    w = works[i]
-                    m = int(w.n_above) if w.obs_above is None else np.size(w.obs_above)
-                    return "pruned64" if (self.exact64 == "pruned" or (
-                        self.exact64 == "auto" and m >= PRUNED64_MIN_COMP)) else "cont"
-                n = int(np.asarray(works[i].cand).size) if inj(i) else \
-                    int(works[i].n_total or works[i].n_cand)
-                mode = scorer
-                if mode == "auto":
-                    mode = "cont"
-                    if not inj(i):
-                        if n >= TABLE_MIN_CAND:
-                            mode = "table"
-                        elif n >= SORTED_MIN_CAND and not outputs:
-                            mode = "sorted"
-                if mode == "sorted" and (inj(i) or outputs):
-                    mode = "cont"
-                return "cont" if mode == "dense" else mode
-            modes = {i: cont_mode(i) for i in cont}
-            groups = [
-                ("cont", [i for i in cont if inj(i) and modes[i] == "cont"]),
-                ("cont", [i for i in cont if not inj(i) and modes[i] == "cont"]),
-                ("sorted", [i for i in cont if modes[i] == "sorted"]),
-                ("pruned64", [i for i in cont if inj(i) and modes[i] == "pruned64"]),
-                ("pruned64", [i for i in cont if not inj(i) and modes[i] == "pruned64"]),
-                ("table", [i for i in cont if inj(i) and modes[i] == "table"]),
-                ("table", [i for i in cont if not inj(i) and modes[i] == "table"]),
-                ("lat", [i for i in quant if i in lat_ranges]),
-                ("qfb", fallback),
-                ("qinj", [i for i in quant if inj(i)]),
-                ("cat", [i for i in cat if inj(i)]),
-                ("cat", [i for i in cat if not inj(i)]),
-            ]
-            order = [i for _, ids in groups for i in ids]
         if cached is not None:
             (jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off, sort_off, cnt_off,
              tbl_off) = self._jobs_fast(cached, cols[2], cols[3])
         else:
-            nj_all = len(order)
-            jobs = np.zeros(nj_all, L.JOB_DTYPE)
-            J = {name: np.zeros(nj_all, L.JOB_DTYPE[name]) for name in L.JOB_DTYPE.names}
-            cand_parts, cand_off, out_off, lat_off, qfb_off = [], 0, 0, 0, 0
-            sort_off = cnt_off = tbl_off = 0
-            seg_of = {i: si for si, i in enumerate(fit_ids)}
-            cseg_of = {i: ci for ci, i in enumerate(cat)}
-            for pos, i in enumerate(order):
-                w = works[i]
-                J["key"][pos] = int(w.key) & 0xFFFFFFFFFFFFFFFF
-                J["cand_base"][pos] = w.cand_base
-                n = int(np.asarray(w.cand).size) if inj(i) else int(w.n_cand)
-                J["n_cand"][pos] = n
-                J["out_off"][pos] = out_off
-                out_off += n
-                flags = 0
-                if inj(i):
-                    # categorical candidates are category indices (0..K-1), as the
-                    # reference's randint_via_categorical samples them (tpe.py:590)
-                    c = np.asarray(w.cand, dtype=np.float64).reshape(-1)
-                    J["cand_off"][pos] = cand_off
-                    cand_parts.append(c)
-                    cand_off += c.size
-                    flags |= L.F_INJECTED
-                if i in cat_meta:
-                    J["family"][pos] = L.CAT
-                    J["lat_n"][pos] = cat_meta[i][0]  # category count (sizes the sampler's path)
-                    J["below"][pos], J["above"][pos] = 2 * cseg_of[i], 2 * cseg_of[i] + 1
-                    J["flags"][pos] = flags
-                    continue
-                P = params[i]
-                J["family"][pos] = P["family"]
-                J["below"][pos], J["above"][pos] = 2 * seg_of[i], 2 * seg_of[i] + 1
-                if P["bounded"]:
-                    flags |= L.F_LOW | L.F_HIGH
-                    J["low"][pos], J["high"][pos] = P["low"], P["high"]
-                if P["q"] is not None:
-                    flags |= L.F_QUANT
-                    J["q"][pos] = P["q"]
-                    if i in lat_ranges:
-                        kmin, nk = lat_ranges[i]
-                        J["lat_off"][pos], J["lat_kmin"][pos], J["lat_n"][pos] = lat_off, kmin, nk
-                        if precision == 32 and max(abs(kmin), abs(kmin + nk - 1)) <= DRAW32_MAX_SLOT:
-                            flags |= L.F_DRAW32
-                        flags |= L.F_LATTICE_READY  # cleared below for a large level
-                        lat_off += nk
-                    elif i in fallback:
-                        J["cand_off"][pos] = qfb_off
-                        qfb_off += n
-                elif modes[i] == "table":
-                    J["tbl_off"][pos], J["tbl_cap"][pos] = tbl_off, TABLE_CAP
-                    tbl_off += TABLE_CAP
-                    if inj(i):
-                        J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P)
-                elif modes[i] == "pruned64" and inj(i):
-                    J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P, fp32=False)
-                elif modes[i] == "sorted":
-                    J["bin_lo"][pos], J["bin_hi"][pos] = _support(w, P)
-                    J["sort_off"][pos], J["cnt_off"][pos] = sort_off, cnt_off
-                    slots = ctypes.c_int64(0)
-                    cnt_off += lib.tpe_sort_layout(n, ctypes.byref(slots))
-                    sort_off += slots.value
-                J["flags"][pos] = flags
-            if lat_off > LAT_PACK_MAX:  # the slots are set by the library's memset instead
-                J["flags"] &= ~L.F_LATTICE_READY
-            for name, col in J.items():
-                jobs[name] = col
-            cand_pool = np.concatenate(cand_parts) if cand_parts else np.zeros(1)
-            # the dense fallback first materialises its draws: a job copy whose
-            # out_off points into the scratch candidate buffer
-            fb_slice = _slice_of(groups, [k for k, _ in groups].index("qfb"))
-            fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
-            fb_jobs["out_off"] = fb_jobs["cand_off"]
-            if pkey is not None and not any(k == "sorted" and ids for k, ids in groups):
-                self._plans[pkey] = self._plan_record(
-                    works, cont, quant, cat, fit_ids, params, segs, csegs, p_pool, cat_meta,
-                    lat_ranges, fallback, modes, groups, order, gathers, jobs, fb_slice, out_off,
-                    lat_off, qfb_off, sort_off, cnt_off, tbl_off)
-
+            (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp, max_obs,
+             csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes, groups,
+             order, gathers, inj, jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off,
+             sort_off, cnt_off, tbl_off) = self._plan_new(
+                works, pkey, prior_weight, lf, precision, scorer, outputs, sample_only, hist_mode,
+                _hmark)
         _hmark('plan')
         # ---- upload (descriptors, jobs, injected candidates: one copy) -----------
         o_segs = pack.add(segs) if segs.size else None
