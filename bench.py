@@ -402,16 +402,23 @@ def self_launch(n):
 
 def drawn_per_step(eng, space, units):
     """Candidates this rank drew in its last level: every candidate of a
-    table or categorical unit; of a quantized unit, eng.lat_prefix when the
-    prefix-first lattice argmax settled it (need flag 0), else all."""
-    quant = [c for j, _, c in units if space[j][1].startswith("q")]
-    drawn = sum(c for j, _, c in units if not space[j][1].startswith("q"))
-    buf = eng._bufs.get("lat_need")
+    table unit; of a quantized or categorical unit, eng.lat_prefix when the
+    prefix-first argmax settled it (need flag 0: tpe_lattice_suggest,
+    tpe_categorical_suggest), else all."""
     prefix = eng.lat_prefix
-    if not quant or buf is None or not prefix or max(quant) <= prefix:
-        return drawn + sum(quant)
-    need = buf[:4 * len(quant)].cpu().numpy().view(np.int32)
-    return drawn + sum(c if (n or c <= prefix) else prefix for c, n in zip(quant, need.tolist()))
+    drawn = 0
+    for kinds, buf_name in ((lambda k: k.startswith("q"), "lat_need"),
+                            (lambda k: k in ("randint", "categorical"), "cat_need")):
+        cnt = [c for j, _, c in units if kinds(space[j][1])]
+        buf = eng._bufs.get(buf_name)
+        if not cnt or buf is None or not prefix or max(cnt) <= prefix:
+            drawn += sum(cnt)
+            continue
+        need = buf[:4 * len(cnt)].cpu().numpy().view(np.int32)
+        drawn += sum(c if (n or c <= prefix) else prefix for c, n in zip(cnt, need.tolist()))
+    drawn += sum(c for j, _, c in units
+                 if not space[j][1].startswith("q") and space[j][1] not in ("randint", "categorical"))
+    return drawn
 
 
 def main():

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -71,6 +71,7 @@ OP_CODES["tpe_lattice_suggest"] = OP_STREAM_SYNC + 3
 OP_CODES["tpe_band_rescore"] = OP_STREAM_SYNC + 4
 OP_CODES["tpe_fit_sorted"] = OP_STREAM_SYNC + 5
 OP_CODES["tpe_history_order"] = OP_STREAM_SYNC + 6
+OP_CODES["tpe_categorical_suggest"] = OP_STREAM_SYNC + 7
 PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
     PRIOR_CATEGORICAL = range(6)
 
@@ -103,6 +104,7 @@ _SIGNATURES = {
                                   _P, _I64, _P, _P]),
     "tpe_band_rescore": (_I, [_P, _P, _I, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P]),
     "tpe_band_work_bytes": (_I64, [_I]),
+    "tpe_categorical_suggest": (_I, [_P, _P, _I, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "tpe_history_order_scratch_bytes": (_I64, [_I, _I64]),
     "tpe_history_order": (_I, [_P, _I64, _P, _P, _I, _I64, _I64, _P, _P, _P]),
     "tpe_fit_sorted_scratch_bytes": (_I64, [_I, _I64]),

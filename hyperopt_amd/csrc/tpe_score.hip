@@ -1184,19 +1184,23 @@ __device__ __forceinline__ uint32_t word_of(const U4& q, int sel) {
   return sel == 0 ? q.x : sel == 1 ? q.y : sel == 2 ? q.z : q.w;
 }
 
+// Candidates [lo + blockIdx.x * kBS * kRC, ...) of job blockIdx.y; the
+// block's winner goes to partial[job * nper + blockIdx.x].  need (nullable):
+// jobs whose flag is 0 are skipped (the prefix-first path's second pass).
 template <int KR>
 __global__ __launch_bounds__(kBS) void k_score_cat(
     const tpe_job* __restrict__ jobs, const tpe_cat_seg* __restrict__ csegs,
     const double* __restrict__ logp, const double* __restrict__ cdf,
     double* __restrict__ out_bl, double* __restrict__ out_al, double* __restrict__ out_x,
-    tpe_best* __restrict__ partial) {
+    tpe_best* __restrict__ partial, int64_t lo, int64_t nper, const int32_t* __restrict__ need) {
   __shared__ double s_sc[kCatKey];
   __shared__ uint64_t s_key[kCatKey];
   __shared__ uint32_t s_thr[KR];
   __shared__ uint64_t red[kBS / kWave];
+  if (need && !need[blockIdx.y]) return;  // block-uniform
   const tpe_job J = jobs[blockIdx.y];
-  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * (kBS * kRC);
+  tpe_best* P = partial + (int64_t)blockIdx.y * nper + blockIdx.x;
+  const int64_t base = lo + (int64_t)blockIdx.x * (kBS * kRC);
   if (base >= J.n_cand) {
     if (threadIdx.x == 0) *P = empty_best();
     return;
@@ -1303,6 +1307,48 @@ __global__ __launch_bounds__(kBS) void k_score_cat(
       const int64_t g = (int64_t)((b >> 8) & ((1ull << 40) - 1));
       *P = tpe_best{s_sc[k], g, (double)k, 0};
     }
+  }
+}
+
+// The prefix-first decision for categorical jobs (tpe_categorical_suggest).
+// Pass 0: the winner of the first `prefix` candidates (partials [0, n1)); a
+// later candidate can only beat it with a strictly better score (its index is
+// larger), i.e. with a category that scores better -- and every such category
+// is absent from the prefix (else it would have won there).  need[j] = 1 when
+// one of them can be drawn at all (a non-empty inverse-CDF interval) and the
+// stream is longer than the prefix.  Pass 1 (jobs with need): the rest's
+// partials [0, n2) folded into best[j].
+__global__ __launch_bounds__(kBS) void k_cat_decide(
+    const tpe_job* __restrict__ jobs, const tpe_cat_seg* __restrict__ csegs,
+    const double* __restrict__ logp, const double* __restrict__ cdf,
+    const tpe_best* __restrict__ partial, int64_t nper, int64_t n_use, int64_t prefix, int pass,
+    int32_t* __restrict__ need, tpe_best* __restrict__ best) {
+  __shared__ BestT red[kBS / kWave];
+  const int j = blockIdx.x;
+  if (pass == 1 && !need[j]) return;  // block-uniform
+  const tpe_job J = jobs[j];
+  const tpe_best* P = partial + (int64_t)j * nper;
+  BestT b{0.0, -1, 0.0};
+  if (pass == 1 && threadIdx.x == 0) b = BestT{best[j].score, best[j].index, best[j].value};
+  for (int64_t i = threadIdx.x; i < n_use; i += kBS) best_update(b, P[i].score, P[i].index, P[i].value);
+  b = block_best<kBS>(b, red);
+  int open = 0;
+  if (pass == 0 && J.n_cand > prefix) {
+    const tpe_cat_seg CB = csegs[J.below], CA = csegs[J.above];
+    const int K = CB.n_cat;
+    for (int k = threadIdx.x; k < K && !open; k += kBS) {
+      const double sk = logp[CB.p_off + k] - logp[CA.p_off + k];
+      // category k takes the words [thr[k-1], thr[k]) (thr[-1] = 0, the last one
+      // up to 2^32)
+      const uint64_t t0 = k > 0 ? cat_thr(cdf + CB.p_off, K, k - 1) : 0ull;
+      const uint64_t t1 = k < K - 1 ? (uint64_t)cat_thr(cdf + CB.p_off, K, k) : (1ull << 32);
+      open = better(sk, INT64_MAX, b.score, b.index) && t1 > t0;
+    }
+    open = __syncthreads_or(open);
+  }
+  if (threadIdx.x == 0) {
+    best[j] = tpe_best{b.score, b.index, b.value, J.n_cand};
+    if (pass == 0) need[j] = open;
   }
 }
 
@@ -1702,15 +1748,76 @@ extern "C" int tpe_score_categorical(const tpe_job* jobs, const tpe_job* host_jo
                        out_bl, out_al, out_x, partial);
   else if (kmax <= 4)
     hipLaunchKernelGGL(k_score_cat<4>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool, cdf_pool,
-                       out_bl, out_al, out_x, partial);
+                       out_bl, out_al, out_x, partial, (int64_t)0, gx, nullptr);
   else if (kmax <= 8)
     hipLaunchKernelGGL(k_score_cat<8>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool, cdf_pool,
-                       out_bl, out_al, out_x, partial);
+                       out_bl, out_al, out_x, partial, (int64_t)0, gx, nullptr);
   else
     hipLaunchKernelGGL(k_score_cat<16>, grid, dim3(kBS), 0, st, jobs, csegs, logp_pool, cdf_pool,
-                       out_bl, out_al, out_x, partial);
+                       out_bl, out_al, out_x, partial, (int64_t)0, gx, nullptr);
   hipLaunchKernelGGL(k_reduce, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
   return check_launch("tpe_score_categorical");
+}
+
+// prefix-first categorical argmax (the suggest path; see k_cat_decide)
+static void launch_cat(int kmax, dim3 grid, hipStream_t st, const tpe_job* jobs,
+                       const tpe_cat_seg* csegs, const double* logp, const double* cdf,
+                       tpe_best* partial, int64_t lo, int64_t nper, const int32_t* need) {
+  if (kmax <= 4)
+    hipLaunchKernelGGL(k_score_cat<4>, grid, dim3(kBS), 0, st, jobs, csegs, logp, cdf, nullptr,
+                       nullptr, nullptr, partial, lo, nper, need);
+  else if (kmax <= 8)
+    hipLaunchKernelGGL(k_score_cat<8>, grid, dim3(kBS), 0, st, jobs, csegs, logp, cdf, nullptr,
+                       nullptr, nullptr, partial, lo, nper, need);
+  else
+    hipLaunchKernelGGL(k_score_cat<16>, grid, dim3(kBS), 0, st, jobs, csegs, logp, cdf, nullptr,
+                       nullptr, nullptr, partial, lo, nper, need);
+}
+
+extern "C" int tpe_categorical_suggest(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                                       const tpe_cat_seg* csegs, const double* logp_pool,
+                                       const double* cdf_pool, int64_t prefix, tpe_best* partial,
+                                       int64_t n_partial, int32_t* need, tpe_best* best,
+                                       void* stream) {
+  if (!check_jobs("tpe_categorical_suggest", host_jobs, n_jobs)) return TPE_E_ARG;
+  if (n_jobs == 0) return TPE_OK;
+  for (int i = 0; i < n_jobs; ++i)
+    if (host_jobs[i].family != TPE_CAT || (host_jobs[i].flags & TPE_F_INJECTED)) {
+      set_error("tpe_categorical_suggest: job %d is not a sampled categorical job", i);
+      return TPE_E_ARG;
+    }
+  if (!jobs || !csegs || !logp_pool || !cdf_pool || !partial || !need || !best) {
+    set_error("tpe_categorical_suggest: null pointer");
+    return TPE_E_ARG;
+  }
+  constexpr int64_t kT = (int64_t)kBS * kRC;
+  if (prefix <= 0 || prefix % kT != 0) {
+    set_error("tpe_categorical_suggest: prefix %lld is not a positive multiple of %lld",
+              (long long)prefix, (long long)kT);
+    return TPE_E_ARG;
+  }
+  const int64_t gx = max_blocks(host_jobs, n_jobs, kT, -1);
+  if (gx * n_jobs > n_partial) {
+    set_error("tpe_categorical_suggest: partial workspace %lld < %lld", (long long)n_partial,
+              (long long)(gx * n_jobs));
+    return TPE_E_ARG;
+  }
+  int kmax = 1;
+  for (int i = 0; i < n_jobs; ++i)
+    kmax = std::max(kmax, host_jobs[i].lat_n > 0 ? (int)host_jobs[i].lat_n : kCatKey);
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t g1 = std::min(gx, prefix / kT);  // prefix blocks per job
+  launch_cat(kmax, dim3((unsigned)g1, (unsigned)n_jobs), st, jobs, csegs, logp_pool, cdf_pool,
+             partial, 0, gx, nullptr);
+  hipLaunchKernelGGL(k_cat_decide, dim3(n_jobs), dim3(kBS), 0, st, jobs, csegs, logp_pool,
+                     cdf_pool, partial, gx, g1, prefix, 0, need, best);
+  if (gx > g1) {  // the rest of the streams that need it (blocks of the others exit at once)
+    launch_cat(kmax, dim3((unsigned)(gx - g1), (unsigned)n_jobs), st, jobs, csegs, logp_pool,
+               cdf_pool, partial, prefix, gx, need);
+    hipLaunchKernelGGL(k_cat_decide, dim3(n_jobs), dim3(kBS), 0, st, jobs, csegs, logp_pool,
+                       cdf_pool, partial, gx, gx - g1, prefix, 1, need, best);
+  }
+  return check_launch("tpe_categorical_suggest");
 }
 
 extern "C" int tpe_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,

@@ -1357,9 +1357,18 @@ class Engine:
                 else:
                     npart = lib.tpe_categorical_partials(hjp, nj)
                     d_part = self._buf(pname, 32 * max(npart, 1))
-                    L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf, d_cand,
-                                                      d_bl, d_al, d_x, d_part, npart, db, ks),
-                            "tpe_score_categorical")
+                    if self.lat_prefix and not inj(ids[0]) and d_bl is None and d_x is None and \
+                            int(hj["n_cand"].max()) > self.lat_prefix:
+                        # prefix first: the rest of a stream only where an unseen
+                        # better category could still be drawn (tpe_categorical_suggest)
+                        d_need = self._buf("cat_need", 4 * nj)
+                        L.check(lib.tpe_categorical_suggest(dj, hjp, nj, d_csegs, d_logp, d_ccdf,
+                                                            self.lat_prefix, d_part, npart, d_need,
+                                                            db, ks), "tpe_categorical_suggest")
+                    else:
+                        L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf,
+                                                          d_cand, d_bl, d_al, d_x, d_part, npart,
+                                                          db, ks), "tpe_score_categorical")
                 tock(kind, e0, kst)
 
             # categorical labels need only the gathered lists: with cat_early

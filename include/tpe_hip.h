@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 15
+#define TPE_ABI_VERSION 16
 
 enum {
   TPE_OK = 0,
@@ -465,6 +465,18 @@ int tpe_score_categorical(const tpe_job* jobs, const tpe_job* host_jobs, int n_j
                           const double* cdf_pool, const double* cand, double* out_bl, double* out_al,
                           double* out_x, tpe_best* partial, int64_t n_partial,
                           tpe_best* best, void* stream);
+/* The suggest path's categorical argmax, prefix first (sampled jobs without
+ * per-candidate outputs; the same tpe_best as tpe_score_categorical).  Draws
+ * the first `prefix` candidates of every job (a positive multiple of 4096);
+ * a later candidate can only win with a strictly better-scoring category, all
+ * of which are then absent from the prefix -- a job where one of them can be
+ * drawn at all (non-empty inverse-CDF interval) draws the rest of its stream
+ * and decides again.  partial: >= tpe_categorical_partials(); need: int32
+ * per job (written: 1 = the rest was drawn). */
+int tpe_categorical_suggest(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
+                            const tpe_cat_seg* csegs, const double* logp_pool,
+                            const double* cdf_pool, int64_t prefix, tpe_best* partial,
+                            int64_t n_partial, int32_t* need, tpe_best* best, void* stream);
 
 /* ---- sampler only (KS tests, debugging): n_cand draws of job.below ------- */
 int tpe_sample(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
@@ -554,6 +566,7 @@ enum {
   TPE_OP_BAND_RESCORE,         /* tpe_band_rescore                           */
   TPE_OP_FIT_SORTED,           /* tpe_fit_sorted                             */
   TPE_OP_HISTORY_ORDER,        /* tpe_history_order                          */
+  TPE_OP_CATEGORICAL_SUGGEST,  /* tpe_categorical_suggest                    */
   TPE_OP_COUNT
 };
 #define TPE_OP_ARGS 23
