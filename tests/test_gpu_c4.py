@@ -113,3 +113,38 @@ def test_suggest_many_chunked_mixed_spaces(monkeypatch, chunk):
         one = tpe.suggest(rq.new_ids, rq.domain, rq.trials, rq.seed, n_EI_candidates=512,
                           verbose=False)
         assert m[0]["misc"]["vals"] == one[0]["misc"]["vals"], s
+
+
+def test_c4_4096_studies_rank_by_rank(monkeypatch):
+    """C4 at its stated size: 4096 studies through suggest_many(shard_studies=
+    True), rehearsed rank by rank on one GPU (hdist.world() patched to (r, 8)):
+    rank r returns exactly studies r::8, each equal to the unsharded batched
+    call's suggestion, and a sample equals its own tpe.suggest.  64 distinct
+    20-dim spaces / 2k-trial histories are shared round-robin by the 4096
+    studies (each with its own seed, so its own Philox keys)."""
+    from hyperopt_amd import dist as hdist
+    from hyperopt_amd import tpe
+    from hyperopt_amd.base import Domain
+    from tools import scale_configs as S
+    n_hist, n_studies, world = 64, 4096, 8
+    doms = [Domain(lambda p: 0.0, S.c4_space(s)) for s in range(n_hist)]
+    trs = [S.flat_trials(d, T, s) for s, d in enumerate(doms)]
+
+    def reqs():
+        return [tpe.SuggestRequest([T], doms[q % n_hist], trs[q % n_hist], 5000 + q,
+                                   n_EI_candidates=N_EI) for q in range(n_studies)]
+    whole = tpe.suggest_many(reqs())
+    assert all(w is not None and len(w) == 1 for w in whole)
+    for r in range(world):
+        monkeypatch.setattr(hdist, "world", lambda r=r: (r, world))
+        part = tpe.suggest_many(reqs(), shard_studies=True)
+        for q in range(n_studies):
+            if q % world == r:
+                assert part[q][0]["misc"]["vals"] == whole[q][0]["misc"]["vals"], (r, q)
+            else:
+                assert part[q] is None
+    monkeypatch.undo()
+    for q in np.random.RandomState(3).choice(n_studies, 16, replace=False):
+        one = tpe.suggest([T], doms[q % n_hist], trs[q % n_hist], 5000 + q,
+                          n_EI_candidates=N_EI, verbose=False)
+        assert one[0]["misc"]["vals"] == whole[q][0]["misc"]["vals"], q

@@ -135,7 +135,7 @@ def c4(studies=512, T=2000, n_ei=1 << 12):
         reqs = [tpe.SuggestRequest([T + k], d, t, s + k, n_EI_candidates=n_ei)
                 for s, (d, t) in enumerate(zip(doms, trs))]
         return tpe.suggest_many(reqs)
-    out, ms = timed(call, 3, 1)
+    out, ms = timed(call, 10, 2)  # p50 over 10 warm calls
     assert all(len(o) == 1 for o in out)
     return {"config": "C4 (one GPU's share)", "studies": studies, "history": T, "dims": 20,
             "n_EI_candidates": n_ei, "suggest_many_p50_ms": float(np.median(ms)),
