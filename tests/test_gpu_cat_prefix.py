@@ -68,6 +68,9 @@ def test_rare_best_category_draws_the_rest(engine):
     full, _ = out[0]
     pre, need = out[4096]
     assert pre == full
-    assert need is not None and need.all()  # category 7 scores best and stays open
+    # category 7 scores best: a job stays open unless its prefix drew it
+    assert need is not None
+    assert need.tolist() == [int(not (r[2] == K - 1 and r[1] < 4096)) for r in full]
+    assert need.sum() >= 4
     assert any(r[2] == K - 1 for r in full)
     assert any(r[1] >= 4096 for r in full)  # a winner past the prefix
