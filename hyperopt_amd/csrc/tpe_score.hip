@@ -956,37 +956,21 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
   const int nc = S.n_obs + 1;
   double acc = 0.0;
   const double xu = lg ? lub : ub, xl = lg ? llb : lb;
-  // each thread's components in index order (k = t, t + kBS, ...), kQU
-  // loaded ahead: a chain of ~40 dependent L2 round trips per block otherwise
-  constexpr int kQU = 4;
-  for (int k0 = threadIdx.x; k0 < nc; k0 += kQU * kBS) {
-    double wq[kQU], mq[kQU], sq[kQU];
-#pragma unroll
-    for (int u = 0; u < kQU; ++u) {
-      const int k = k0 + u * kBS;
-      const bool in = k < nc;
-      wq[u] = in ? w[S.comp_off + k] : 0.0;
-      mq[u] = in ? mu[S.comp_off + k] : 0.0;
-      sq[u] = in ? sigma[S.comp_off + k] : 0.0;
+  for (int k = threadIdx.x; k < nc; k += kBS) {
+    const double wk = w[S.comp_off + k], m = mu[S.comp_off + k], s = sigma[S.comp_off + k];
+    // both erf arguments beyond +-6.5 (erf exactly +-1 in fp64): the two cdf
+    // values are equal and the term w*cu - w*cl is exactly 0 -- skip it
+    const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
+    if (xl - m >= b65 || xu - m <= -b65) continue;
+    double cu, cl;
+    if (lg) {
+      cu = lognormal_cdf_logx(lub, m, s);
+      cl = lognormal_cdf_logx(llb, m, s);
+    } else {
+      cu = normal_cdf(ub, m, s);
+      cl = normal_cdf(lb, m, s);
     }
-#pragma unroll
-    for (int u = 0; u < kQU; ++u) {
-      if (k0 + u * kBS >= nc) break;
-      const double wk = wq[u], m = mq[u], s = sq[u];
-      // both erf arguments beyond +-6.5 (erf exactly +-1 in fp64): the two cdf
-      // values are equal and the term w*cu - w*cl is exactly 0 -- skip it
-      const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
-      if (xl - m >= b65 || xu - m <= -b65) continue;
-      double cu, cl;
-      if (lg) {
-        cu = lognormal_cdf_logx(lub, m, s);
-        cl = lognormal_cdf_logx(llb, m, s);
-      } else {
-        cu = normal_cdf(ub, m, s);
-        cl = normal_cdf(lb, m, s);
-      }
-      acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
-    }
+    acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
   }
   acc = block_sum<kBS, double>(acc, sh);
   return log(acc) - log(S.p_accept);
