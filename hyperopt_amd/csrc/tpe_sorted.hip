@@ -7,8 +7,9 @@
 // its rows sorted by (transformed value, row) -- updated when trials are
 // appended (tpe_history_order: the new rows sorted in LDS, then merged into
 // the existing order, O(T) per append instead of O(T log T) per suggest) --
-// and a suggest's fit (tpe_fit_sorted) is one compaction block per segment,
-// then the fit's bandwidth / coefficient launches:
+// and a suggest's fit (tpe_fit_sorted) is a chunked compaction (three
+// launches over (chunk, segment) blocks), then the fit's bandwidth /
+// coefficient launches:
 //
 //   1. rows in row (tid) order: which belong to the segment (active for the
 //      label, on its side of the split), each one's position in the segment's
@@ -32,11 +33,7 @@
 namespace tpe {
 namespace {
 constexpr int kSB = 1024;            // block size of every kernel here
-constexpr int kSWaves = kSB / kWave;
 constexpr int kNew = 2048;           // new rows sorted per tpe_history_order call
-constexpr int kRowsPT = 12;          // rows per thread per compaction pass
-constexpr int kPass = kRowsPT * kSB; // rows per compaction pass
-constexpr int kSlots = kRowsPT * kSWaves;
 
 __device__ __forceinline__ uint64_t row_key(const double* __restrict__ V, int64_t row,
                                             const tpe_colspec& C) {
@@ -136,141 +133,209 @@ __global__ __launch_bounds__(256) void k_order_copy(const tpe_colspec* __restric
 }
 
 // ---- the fit ------------------------------------------------------------------
-// Block-wide stream compaction over items [0, n) in item order, kRowsPT items
-// per thread per pass.  The loads of a pass are issued together, in two
-// dependent rounds: first(i) (e.g. the order entry), then second(first) (the
-// row's fields); take(L) says whether the item is kept, emit(i, rank, L) gets
-// its rank among the kept items.  Returns the number kept.
-struct RowLoad {
-  int32_t row;
-  uint8_t act, side;
-  double v;
-  int32_t gi;
+// ---- the fit: chunked compaction ---------------------------------------------
+// Rows (tid order) and order entries (sorted order) are cut into chunks of
+// kChunk; every (chunk, segment) pair is a 256-thread block, so a segment's
+// random gathers through its column's order (the rows' flags, values and list
+// positions) are spread over many CUs instead of one CU's load pipeline.
+// Three launches: counts per chunk, then the tid-order emit (list positions),
+// then the sorted-order emit (means and ramp weights); each block re-reduces
+// the few counts of the chunks before it (fixed order).
+constexpr int kCB = 256;                 // block size of the compaction kernels
+constexpr int kCR = 4;                   // items per thread
+constexpr int kChunk = kCB * kCR;        // items per chunk (item u * kCB + t of a chunk)
+constexpr int kCnt = 4;                  // per (segment, chunk): members tid / lt / first row / members sorted
+
+struct SegView {
+  const double* V;
+  const uint8_t* A;
+  const int32_t* O;
+  uint8_t side;
+  int transform;
+  double floor_;
+  uint64_t kp;
 };
-template <class First, class Second, class Take, class Emit>
-__device__ int64_t block_compact(int64_t n, First first, Second second, Take take, Emit emit,
-                                 int* wsum, int64_t* carry_s) {
-  const int lane = lane_id(), wid = threadIdx.x / kWave;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  if (threadIdx.x == 0) *carry_s = 0;
-  __syncthreads();
-  for (int64_t p0 = 0; p0 < n; p0 += kPass) {
-    int32_t f[kRowsPT];
-#pragma unroll
-    for (int t = 0; t < kRowsPT; ++t) {
-      const int64_t i = p0 + (int64_t)t * kSB + threadIdx.x;
-      f[t] = i < n ? first(i) : 0;
-    }
-    RowLoad L[kRowsPT];
-#pragma unroll
-    for (int t = 0; t < kRowsPT; ++t) {
-      const int64_t i = p0 + (int64_t)t * kSB + threadIdx.x;
-      L[t] = i < n ? second(f[t]) : RowLoad{0, 0, 2, 0.0, 0};
-    }
-    bool tk[kRowsPT];
-    int before[kRowsPT];
-#pragma unroll
-    for (int t = 0; t < kRowsPT; ++t) {
-      const int64_t i = p0 + (int64_t)t * kSB + threadIdx.x;
-      tk[t] = i < n && take(L[t]);
-      const uint64_t bal = __ballot(tk[t]);
-      before[t] = __popcll(bal & lt);
-      if (lane == 0) wsum[t * kSWaves + wid] = __popcll(bal);
-    }
-    __syncthreads();
-    // exclusive scan of the kSlots (tile, wave) counts, slot order = item order
-    const int c = threadIdx.x < kSlots ? wsum[threadIdx.x] : 0;
-    int incl = c;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-      const int o = __shfl_up(incl, off, kWave);
-      if (lane >= off) incl += o;
-    }
-    __syncthreads();
-    if (threadIdx.x < kSlots && lane == kWave - 1) wsum[kSlots + wid] = incl;
-    __syncthreads();
-    int wave_base = 0;
-    for (int q = 0; q < wid && q < kSlots / kWave; ++q) wave_base += wsum[kSlots + q];
-    const int64_t carry = *carry_s;
-    if (threadIdx.x < kSlots) wsum[threadIdx.x] = wave_base + incl - c;
-    int total = 0;
-    for (int q = 0; q < kSlots / kWave; ++q) total += wsum[kSlots + q];
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < kRowsPT; ++t)
-      if (tk[t]) emit(p0 + (int64_t)t * kSB + threadIdx.x,
-                      carry + wsum[t * kSWaves + wid] + before[t], L[t]);
-    __syncthreads();
-    if (threadIdx.x == 0) *carry_s = carry + total;
-    __syncthreads();
-  }
-  return *carry_s;
+__device__ __forceinline__ SegView seg_view(const double* vals, const uint8_t* active,
+                                            const int32_t* order, int64_t ld,
+                                            const tpe_gather& G, const tpe_seg& S) {
+  const int64_t col = G.col;
+  return SegView{vals + col * ld, active + col * ld, order + col * ld,
+                 (uint8_t)(G.below ? 1 : 0), S.transform, S.floor, order_key(S.prior_mu)};
 }
 
-__global__ __launch_bounds__(kSB) void k_fit_sorted(
+// exclusive ranks of the kept items of a chunk (item order u * kCB + t) and
+// the chunk's total; sh: >= kCR * kCB / kWave ints
+__device__ __forceinline__ int chunk_ranks(const bool (&tk)[kCR], int (&rank)[kCR], int* sh) {
+  constexpr int kNW = kCB / kWave;
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int before[kCR];
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) {
+    const uint64_t bal = __ballot(tk[u]);
+    before[u] = __popcll(bal & lt);
+    if (lane == 0) sh[u * kNW + wid] = __popcll(bal);
+  }
+  __syncthreads();
+  int total = 0, mine[kCR];
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) mine[u] = 0;
+  for (int q = 0; q < kCR * kNW; ++q) {  // 16 slot counts, slot order = item order
+    const int c = sh[q];
+#pragma unroll
+    for (int u = 0; u < kCR; ++u) mine[u] += (q < u * kNW + wid) ? c : 0;
+    total += c;
+  }
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) rank[u] = mine[u] + before[u];
+  __syncthreads();  // sh reused
+  return total;
+}
+
+// K1: per (chunk, segment): members in the tid-order chunk, how many of them
+// lie below the prior mean, the first member row; members in the sorted chunk
+__global__ __launch_bounds__(kCB) void k_fit_count(
+    const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
+    const int32_t* __restrict__ order, int64_t n_rows, const uint8_t* __restrict__ is_below,
+    const tpe_gather* __restrict__ gathers, const tpe_seg* __restrict__ segs,
+    int32_t* __restrict__ cnt) {
+  __shared__ int sh[4 * (kCB / kWave)];
+  const int sg = blockIdx.y;
+  const SegView Q = seg_view(vals, active, order, ld, gathers[sg], segs[sg]);
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  int32_t rows[kCR];
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) {
+    const int64_t e = c0 + u * kCB + threadIdx.x;
+    rows[u] = e < n_rows ? Q.O[e] : -1;
+  }
+  int n1 = 0, nlt = 0, n2 = 0, first = INT32_MAX;
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) {
+    const int64_t r = c0 + u * kCB + threadIdx.x;
+    if (r < n_rows && Q.A[r] && is_below[r] == Q.side) {
+      ++n1;
+      nlt += order_key(obs_transform(Q.V[r], Q.transform, Q.floor_)) < Q.kp ? 1 : 0;
+      first = min(first, (int)r);
+    }
+    const int32_t row = rows[u];
+    if (row >= 0 && Q.A[row] && is_below[row] == Q.side) ++n2;
+  }
+  n1 = block_sum<kCB, int>(n1, sh);
+  nlt = block_sum<kCB, int>(nlt, sh + kCB / kWave);
+  n2 = block_sum<kCB, int>(n2, sh + 2 * (kCB / kWave));
+  first = -block_max<kCB, int>(-first, sh + 3 * (kCB / kWave));
+  if (threadIdx.x == 0) {
+    int32_t* C = cnt + ((int64_t)sg * gridDim.x + blockIdx.x) * kCnt;
+    C[0] = n1;
+    C[1] = nlt;
+    C[2] = first;
+    C[3] = n2;
+  }
+}
+
+// sum of field f over chunks [0, c) (all threads; fixed order)
+__device__ __forceinline__ int64_t chunks_before(const int32_t* C, int c, int f, int64_t* sh) {
+  int64_t v = 0;
+  for (int q = threadIdx.x; q < c; q += kCB) v += C[q * kCnt + f];
+  return block_sum<kCB, int64_t>(v, sh);
+}
+
+// K2: tid-order emit -- each member row's position in the segment's list
+__global__ __launch_bounds__(kCB) void k_fit_emit_tid(
+    const uint8_t* __restrict__ active, int64_t ld, int64_t n_rows,
+    const uint8_t* __restrict__ is_below, const tpe_gather* __restrict__ gathers,
+    const int32_t* __restrict__ cnt, int32_t* __restrict__ gi_scr) {
+  __shared__ int sh[kCR * (kCB / kWave)];
+  __shared__ int64_t sh64[kCB / kWave];
+  const int sg = blockIdx.y;
+  const tpe_gather G = gathers[sg];
+  const uint8_t* A = active + (int64_t)G.col * ld;
+  const uint8_t side = G.below ? 1 : 0;
+  const int32_t* C = cnt + (int64_t)sg * gridDim.x * kCnt;
+  const int64_t base = chunks_before(C, blockIdx.x, 0, sh64);
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  bool tk[kCR];
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) {
+    const int64_t r = c0 + u * kCB + threadIdx.x;
+    tk[u] = r < n_rows && A[r] && is_below[r] == side;
+  }
+  int rk[kCR];
+  chunk_ranks(tk, rk, sh);
+  int32_t* GI = gi_scr + (int64_t)sg * n_rows;
+#pragma unroll
+  for (int u = 0; u < kCR; ++u)
+    if (tk[u]) GI[c0 + u * kCB + threadIdx.x] = (int32_t)(base + rk[u]);
+}
+
+// K3: sorted-order emit -- means and ramp weights in sorted order, the prior
+// at its slot: searchsorted(obs, prior_mu, 'left') (tpe.py:427), or the
+// len == 1 rule (tpe.py:414-421).  A count other than gathers[sg].count sets
+// bit 4 of *err and writes nothing.
+__global__ __launch_bounds__(kCB) void k_fit_emit_sorted(
     const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
     const int32_t* __restrict__ order, int64_t n_rows, const uint8_t* __restrict__ is_below,
     const tpe_gather* __restrict__ gathers, tpe_seg* __restrict__ segs,
-    int32_t* __restrict__ gi_scr, double* __restrict__ w, double* __restrict__ mu,
-    int32_t* __restrict__ err) {
-  __shared__ int wsum[kSlots + kSlots / kWave];
-  __shared__ int64_t carry_s;
-  __shared__ int s_lt;
-  __shared__ double s_x0;
-  tpe_seg* S = segs + blockIdx.x;
-  const tpe_gather G = gathers[blockIdx.x];
-  const int64_t col = G.col;
-  const uint8_t side = G.below ? 1 : 0;
-  const double* V = vals + col * ld;
-  const uint8_t* A = active + col * ld;
-  const int32_t* O = order + col * ld;
-  int32_t* GI = gi_scr + (int64_t)blockIdx.x * n_rows;
-  const int transform = S->transform;
-  const double floor_ = S->floor, pmu = S->prior_mu;
-  const uint64_t kp = order_key(pmu);
-  const int64_t coff = S->comp_off;
-  if (threadIdx.x == 0) {
-    s_lt = 0;
-    s_x0 = 0.0;
-  }
-  // 1. rows in tid order: position in the segment's list, count below the prior
-  int lt = 0;
-  const int64_t n = block_compact(
-      n_rows, [&](int64_t r) { return (int32_t)r; },
-      [&](int32_t r) { return RowLoad{r, A[r], is_below[r], V[r], 0}; },
-      [&](const RowLoad& L) {
-        const bool t = L.act && L.side == side;
-        lt += (t && order_key(obs_transform(L.v, transform, floor_)) < kp) ? 1 : 0;
-        return t;
-      },
-      [&](int64_t r, int64_t rank, const RowLoad& L) {
-        GI[r] = (int32_t)rank;
-        if (rank == 0) s_x0 = obs_transform(L.v, transform, floor_);
-      },
-      wsum, &carry_s);
-  atomicAdd(&s_lt, lt);
+    const int32_t* __restrict__ cnt, const int32_t* __restrict__ gi_scr,
+    double* __restrict__ w, double* __restrict__ mu, int32_t* __restrict__ err) {
+  __shared__ int sh[kCR * (kCB / kWave)];
+  __shared__ int64_t sh64[kCB / kWave];
+  const int sg = blockIdx.y;
+  tpe_seg* S = segs + sg;
+  const tpe_gather G = gathers[sg];
+  const SegView Q = seg_view(vals, active, order, ld, G, *S);
+  const int nch = gridDim.x;
+  const int32_t* C = cnt + (int64_t)sg * nch * kCnt;
+  const int64_t n = chunks_before(C, nch, 0, sh64);
   if (n != G.count) {  // the segment was sized for another count: nothing written
-    if (threadIdx.x == 0 && err) atomicOr(err, 4);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && err) atomicOr(err, 4);
     return;
   }
-  __syncthreads();
+  const int64_t n_lt = chunks_before(C, nch, 1, sh64);
+  const int64_t base = chunks_before(C, blockIdx.x, 3, sh64);
+  int prior_pos = 0;
+  if (n >= 2) {
+    prior_pos = (int)n_lt;
+  } else if (n == 1) {
+    int first = INT32_MAX;
+    for (int q = 0; q < nch; ++q) first = min(first, C[q * kCnt + 2]);
+    const double x0 = obs_transform(Q.V[first], Q.transform, Q.floor_);
+    prior_pos = (S->prior_mu < x0) ? 0 : 1;
+  }
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  int32_t rows[kCR];
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) {
+    const int64_t e = c0 + u * kCB + threadIdx.x;
+    rows[u] = e < n_rows ? Q.O[e] : -1;
+  }
+  bool tk[kCR];
+  double v[kCR];
+  int32_t gi[kCR];
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) {
+    const int32_t row = rows[u];
+    const bool in = row >= 0;
+    const uint8_t a = in ? Q.A[row] : 0, b = in ? is_below[row] : 2;
+    v[u] = in ? Q.V[row] : 0.0;
+    gi[u] = in ? gi_scr[(int64_t)sg * n_rows + row] : 0;
+    tk[u] = a && b == Q.side;
+  }
+  int rk[kCR];
+  chunk_ranks(tk, rk, sh);
+  const int64_t coff = S->comp_off;
   const int nn = (int)n, lf = S->lf;
-  // the prior's slot: searchsorted(obs, prior_mu, 'left') (tpe.py:427), or the
-  // len == 1 rule (tpe.py:414-421)
-  const int prior_pos = n >= 2 ? s_lt : (n == 1 ? ((pmu < s_x0) ? 0 : 1) : 0);
-  // 2. the column's sorted order compacted to the segment
-  block_compact(
-      n_rows, [&](int64_t e) { return O[e]; },
-      [&](int32_t row) { return RowLoad{row, A[row], is_below[row], V[row], GI[row]}; },
-      [&](const RowLoad& L) { return L.act && L.side == side; },
-      [&](int64_t e, int64_t p, const RowLoad& L) {
-        const int64_t pos = p + (p >= prior_pos ? 1 : 0);
-        mu[coff + pos] = obs_transform(L.v, transform, floor_);
-        w[coff + pos] = lf_weight(L.gi, nn, lf);  // ramp in tid order (tpe.py:441-447)
-      },
-      wsum, &carry_s);
-  if (threadIdx.x == 0) {
-    mu[coff + prior_pos] = pmu;
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) {
+    if (!tk[u]) continue;
+    const int64_t p = base + rk[u];
+    const int64_t pos = p + (p >= prior_pos ? 1 : 0);
+    mu[coff + pos] = obs_transform(v[u], Q.transform, Q.floor_);
+    w[coff + pos] = lf_weight(gi[u], nn, lf);  // ramp in tid order (tpe.py:441-447)
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    mu[coff + prior_pos] = S->prior_mu;
     w[coff + prior_pos] = S->prior_weight;
     S->prior_pos = prior_pos;
   }
@@ -320,14 +385,18 @@ extern "C" int tpe_history_order(const double* vals, int64_t ld, const tpe_colsp
   return check_launch("tpe_history_order");
 }
 
-// scratch: the per-row list positions (int32 per segment and row), then the
-// fit tail's tile partials (counts are <= n_rows)
+// scratch: the per-row list positions (int32 per segment and row), the chunk
+// counts, then the fit tail's tile partials (counts are <= n_rows)
 static int64_t gi_bytes(int n_seg, int64_t n_rows) {
   return (4 * (int64_t)std::max(n_seg, 1) * std::max<int64_t>(n_rows, 1) + 255) / 256 * 256;
 }
+static int64_t n_chunks(int64_t n_rows) { return std::max<int64_t>(1, (n_rows + kChunk - 1) / kChunk); }
+static int64_t cnt_bytes(int n_seg, int64_t n_rows) {
+  return (4 * kCnt * (int64_t)std::max(n_seg, 1) * n_chunks(n_rows) + 255) / 256 * 256;
+}
 extern "C" int64_t tpe_fit_sorted_scratch_bytes(int n_seg, int64_t n_rows) {
   if (n_seg < 0 || n_rows < 0 || n_rows > INT32_MAX) return -1;
-  return gi_bytes(n_seg, n_rows) +
+  return gi_bytes(n_seg, n_rows) + cnt_bytes(n_seg, n_rows) +
          8 * (int64_t)std::max(n_seg, 1) * fit_part_doubles((int)n_rows);
 }
 
@@ -359,9 +428,17 @@ extern "C" int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t
   int max_obs = 0;
   for (int i = 0; i < n_seg; ++i) max_obs = std::max(max_obs, (int)host_gathers[i].count);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_fit_sorted, dim3(n_seg), dim3(kSB), 0, st, vals, active, ld, order, n_rows,
-                     is_below, gathers, segs, reinterpret_cast<int32_t*>(scratch), w, mu, err);
-  double* part = reinterpret_cast<double*>(static_cast<char*>(scratch) + gi_bytes(n_seg, n_rows));
+  char* p = static_cast<char*>(scratch);
+  int32_t* gi = reinterpret_cast<int32_t*>(p);
+  int32_t* cnt = reinterpret_cast<int32_t*>(p + gi_bytes(n_seg, n_rows));
+  double* part = reinterpret_cast<double*>(p + gi_bytes(n_seg, n_rows) + cnt_bytes(n_seg, n_rows));
+  const dim3 grid((unsigned)n_chunks(n_rows), (unsigned)n_seg);
+  hipLaunchKernelGGL(k_fit_count, grid, dim3(kCB), 0, st, vals, active, ld, order, n_rows,
+                     is_below, gathers, segs, cnt);
+  hipLaunchKernelGGL(k_fit_emit_tid, grid, dim3(kCB), 0, st, active, ld, n_rows, is_below,
+                     gathers, cnt, gi);
+  hipLaunchKernelGGL(k_fit_emit_sorted, grid, dim3(kCB), 0, st, vals, active, ld, order, n_rows,
+                     is_below, gathers, segs, cnt, gi, w, mu, err);
   fit_tail(segs, n_seg, max_obs, part, w, mu, sigma, wcdf, coef64, coef32, st);
   return check_launch("tpe_fit_sorted");
 }
