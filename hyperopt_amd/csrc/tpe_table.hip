@@ -766,6 +766,36 @@ __device__ __forceinline__ float lse_exact32(const float4* __restrict__ coef, co
   return (m + __builtin_amdgcn_logf(s) + (float)S.cmax) * kLn2T;
 }
 
+// The same log-sum-exp with the whole wave on one candidate (y wave-uniform,
+// every lane active): lane l sums components l, l + 64, ... online, then the
+// 64 partial sums are merged at the wave's maximum.  A per-lane serial sum over
+// 10^4 components is ~10^5 instructions in one lane -- a tail of ~100 us for
+// the wave that holds such a candidate.  Rounding: <= M/64 + 8 sequential
+// steps per term, inside the bound taken for the serial sum (kEpsLse).
+__device__ __forceinline__ float lse_wave32(const float4* __restrict__ coef, const tpe_seg& S,
+                                            float y) {
+  const float xc = y - (float)S.center;
+  float m = -INFINITY, s = 0.0f;
+  for (int k = lane_id(); k < S.n_obs + 1; k += kWave) {
+    const float4 c = coef[k];
+    const float t = fmaf(xc, c.x, c.y);
+    const float v = fmaf(-t, t, c.z);
+    if (v > m) {
+      s = s * __builtin_amdgcn_exp2f(m - v) + 1.0f;
+      m = v;
+    } else {
+      s += __builtin_amdgcn_exp2f(v - m);
+    }
+  }
+  float M = m;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, kWave));
+  float t = (m == -INFINITY) ? 0.0f : s * __builtin_amdgcn_exp2f(m - M);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, kWave);
+  return (M + __builtin_amdgcn_logf(t) + (float)S.cmax) * kLn2T;
+}
+
 template <bool INJ>
 __global__ __launch_bounds__(kBS) void k_score_table(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
@@ -1132,22 +1162,7 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
       if (fb & (1u << r)) stage[r * kWave + lane] = x[r];
     __builtin_amdgcn_wave_barrier();
     const f4* cell4 = reinterpret_cast<const f4*>(region);
-    while (fb) {
-      const int r = __builtin_ctz(fb);
-      fb &= fb - 1;
-      const float y = stage[r * kWave + lane];
-      const int c = cell_of(y);
-      const float u = (y - cell_centre(g0, h32, c)) * inv_h;
-      const f4 q0 = cell4[4 * c], q1 = cell4[4 * c + 1], q2 = cell4[4 * c + 2],
-               q3 = cell4[4 * c + 3];
-      float pb, pa, s;
-      horner9x2(q0, q1, q2, q3, u, pb, pa);
-      if ((q3.w == q3.w) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f)) {
-        s = q3.w + (__builtin_amdgcn_logf(pb) - __builtin_amdgcn_logf(pa)) * kLn2T;
-      } else {
-        s = lse_exact32(coef32 + SB.comp_off, SB, y) - lse_exact32(coef32 + SA.comp_off, SA, y);
-        lsem |= 1u << r;
-      }
+    auto fold = [&](int r, float s, float y) __attribute__((always_inline)) {
       stage[r * kWave + lane] = s;
       if (out_score) out_score[J.out_off + t0 + r] = (double)s;
       const bool na = s != s, nbn = bs != bs;
@@ -1159,6 +1174,37 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
         by = y;
       }
       ++n_fb;
+    };
+    while (fb) {
+      const int r = __builtin_ctz(fb);
+      fb &= fb - 1;
+      const float y = stage[r * kWave + lane];
+      const int c = cell_of(y);
+      const float u = (y - cell_centre(g0, h32, c)) * inv_h;
+      const f4 q0 = cell4[4 * c], q1 = cell4[4 * c + 1], q2 = cell4[4 * c + 2],
+               q3 = cell4[4 * c + 3];
+      float pb, pa;
+      horner9x2(q0, q1, q2, q3, u, pb, pa);
+      if ((q3.w == q3.w) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f))
+        fold(r, q3.w + (__builtin_amdgcn_logf(pb) - __builtin_amdgcn_logf(pa)) * kLn2T, y);
+      else
+        lsem |= 1u << r;  // the exact log-sum-exp, below, the wave together
+    }
+    // the exact fp32 log-sum-exp over every component, one candidate at a
+    // time with the whole wave (its y still waits in the stage)
+    uint32_t ex = lsem;
+    for (;;) {
+      const uint64_t lanes = __ballot(ex != 0);
+      if (!lanes) break;
+      const int L = __builtin_ctzll(lanes);
+      const int r = __shfl(ex ? __builtin_ctz(ex) : 0, L, kWave);
+      const float y = stage[r * kWave + L];
+      const float s = lse_wave32(coef32 + SB.comp_off, SB, y) -
+                      lse_wave32(coef32 + SA.comp_off, SA, y);
+      if (lane == L) {
+        fold(r, s, y);
+        ex &= ex - 1;
+      }
     }
   }
   BestT run{0.0, -1, 0.0};
