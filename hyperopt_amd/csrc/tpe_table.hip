@@ -1059,7 +1059,7 @@ __device__ __forceinline__ double cand_value(float y, bool lgmm) {
 // reaches the G known at that point is appended to the job's band list for
 // the band kernels (k_band_select / k_band_expand / k_band_final).
 // out_score / out_x (nullable, tests): per-candidate fp32 score and value.
-__global__ __launch_bounds__(kBS) void k_score_table_fast(
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k_score_table_fast(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, const float4* __restrict__ coef32,
@@ -1239,15 +1239,26 @@ __global__ __launch_bounds__(kBS) void k_score_table_fast(
   // NaN scores and fallback candidates are checked one by one
   const float hi_t = br >= 0 ? bs + ea + kEpsRel * fabsf(bs) : -INFINITY;
   if (fbm != 0u || !(hi_t < G)) {
-    tpe_band* B = band + (int64_t)job * band_cap;
+    uint32_t em = 0;  // this lane's candidates in the band
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
       if (r >= nvalid) break;
       const float s = stage[r * kWave + lane];
       const float hi = s + eps(r, s);
-      if (hi < G) continue;  // (NaN scores go on)
-      const uint32_t p = atomicAdd(ctl + 1, 1u);
-      if ((int64_t)p < band_cap) B[p] = tpe_band{J.cand_base + t0 + r, x[r], hi};
+      stage[r * kWave + lane] = hi;
+      if (!(hi < G)) em |= 1u << r;  // (NaN scores go on)
+    }
+    if (em) {
+      // one slot reservation per lane, not per entry: a label's band can be a
+      // few thousand entries, and an atomic per entry serialises them
+      int64_t p = atomicAdd(ctl + 1, (uint32_t)__popc(em));
+      tpe_band* B = band + (int64_t)job * band_cap;
+#pragma unroll
+      for (int r = 0; r < kTR; ++r) {
+        if (!((em >> r) & 1u)) continue;
+        if (p < band_cap) B[p] = tpe_band{J.cand_base + t0 + r, x[r], stage[r * kWave + lane]};
+        ++p;
+      }
     }
   }
 }
