@@ -80,6 +80,7 @@ constexpr int kTR = TPE_TR;          // candidates per thread and tile in the sc
 constexpr int kTiles = TPE_TILES;    // tiles (kBS * kTR candidates) per scorer block
 constexpr int64_t kTile = (int64_t)kBS * kTR;
 constexpr int kBuildBlocks = 512;    // build blocks per job (grid-stride over cells)
+constexpr int kCoopCells = 4096;     // labels with at most this many cells build a quad per block
 constexpr float kLn2T = 0.6931471805599453f;
 
 __device__ __forceinline__ double4 ld4(const double* coef64, int64_t k) {
@@ -475,11 +476,21 @@ __device__ __forceinline__ float row_sum9_transposed(const float (&P)[9]) {
 // k_lo .. k_hi: the reach window of the four cells' span (cell_windows) --
 // a superset of each cell's own, whose components the exclusion test below
 // drops -- then the wide list; every row walks the same items.
+struct BuildLds {  // the block's four waves' partial expansions of one mixture
+  double m[kBS / kWave][4];   // per wave and row: its scale
+  float p[kBS / kWave][kWave];  // per wave and lane: its row's sum of P_rev4(lane & 15)
+  int bad[kBS / kWave][4];
+};
 __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __restrict__ coef64,
                                           int k_lo, int k_hi,
                                           const int32_t* __restrict__ wide_idx, int n_wide,
                                           double T, double y0, double h, float* cell, bool store,
-                                          int mix, double& m_out) {
+                                          int mix, double& m_out, BuildLds& X, bool coop) {
+  // coop (block-uniform): the block's four waves build the same four cells
+  // and split the items; otherwise every wave builds its own four cells
+  constexpr int kNW = kBS / kWave;
+  const int wv = coop ? (int)threadIdx.x / kWave : 0;
+  const int stride = coop ? 16 * kNW : 16;
   const int64_t off = S.comp_off;
   const int nwin = max(0, k_hi - k_lo + 1);
   const int items = nwin + n_wide;
@@ -500,11 +511,11 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   double ml = -INFINITY;
   bool bad = false;
   const float hf = (float)h, Tf = (float)T;
-  int it = l;
+  int it = wv * 16 + l;  // the block's four waves split the items, 16 lanes per cell each
   int k = it < items ? comp(it) : 0;
   double4 c = it < items ? ld4(coef64, off + k) : make_double4(0.0, 0.0, 0.0, 0.0);
-  for (; it < items; it += 16) {
-    const int itn = it + 16;
+  for (; it < items; it += stride) {
+    const int itn = it + stride;
     const int kn = itn < items ? comp(itn) : 0;
     const double4 cn = itn < items ? ld4(coef64, off + kn) : c;
     // window items that are wide come from the list instead; below the
@@ -549,15 +560,39 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   static_assert(kP == 9, "row_sum9_transposed folds nine terms");
   const float v = row_sum9_transposed(P);  // lane p of the row: the row's total of P_rev4(p)
   bad = ((__ballot(bad) >> (lane & ~15)) & 0xFFFFull) != 0;
-  const int n = rev4(l);
-  if (store && n < kP) {
-    if (n < kP32)
-      cell[2 * n + mix] = v;
-    else
-      reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (n - kP32) + mix] = (_Float16)v;
+  // the four waves' partial sums of each row (cell), merged at their largest
+  // scale; wave 0 holds the result
+  double M = m0;
+  float tot = v;
+  bool anybad = bad;
+  if (coop) {
+    const int row = lane >> 4;
+    if (l == 0) {
+      X.m[wv][row] = m0;
+      X.bad[wv][row] = bad;
+    }
+    X.p[wv][lane] = v;
+    __syncthreads();
+    M = X.m[0][row];
+    for (int w = 1; w < kNW; ++w) M = fmax(M, X.m[w][row]);
+    tot = 0.0f;
+    anybad = false;
+    for (int w = 0; w < kNW; ++w) {
+      const double mw = X.m[w][row];
+      tot += (mw == -INFINITY) ? 0.0f : X.p[w][lane] * __expf((float)(mw - M));
+      anybad = anybad || X.bad[w][row];
+    }
+    __syncthreads();  // (X is reused by the next call)
   }
-  m_out = m0;
-  return bad;
+  const int n = rev4(l);
+  if (store && wv == 0 && n < kP) {
+    if (n < kP32)
+      cell[2 * n + mix] = tot;
+    else
+      reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (n - kP32) + mix] = (_Float16)tot;
+  }
+  m_out = M;
+  return anybad;
 }
 
 // ---------------------------------------------------------------------------
@@ -680,9 +715,15 @@ __global__ __launch_bounds__(kBS) void k_table_build(
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const int wid = threadIdx.x / kWave, row = lane_id() >> 4;
   float* region = cells + J.tbl_off * (kSlotB / 4);
-  // a wave per four consecutive cells (one per 16-lane row)
-  for (int64_t q = (int64_t)blockIdx.x * (kBS / kWave) + wid; 4 * q < g.nb;
-       q += (int64_t)gridDim.x * (kBS / kWave)) {
+  __shared__ BuildLds X;
+  // four consecutive cells (a "quad", one per 16-lane row) per wave; a label
+  // with few cells (wide windows: many components per cell) gives each quad
+  // the whole block, whose four waves split the components -- so it still
+  // spreads over many waves when it is one of a rank's few labels
+  const bool coop = g.nb <= kCoopCells;  // block-uniform
+  const int64_t q0 = coop ? blockIdx.x : (int64_t)blockIdx.x * (kBS / kWave) + wid;
+  const int64_t qs = coop ? gridDim.x : (int64_t)gridDim.x * (kBS / kWave);
+  for (int64_t q = q0; 4 * q < g.nb; q += qs) {
     const int c0 = (int)(4 * q), c1 = min(c0 + 3, g.nb - 1);
     const int c = c0 + row;
     const bool mine = c < g.nb;
@@ -693,10 +734,10 @@ __global__ __launch_bounds__(kBS) void k_table_build(
     double mb, ma;
     const Windows w = cell_windows(SB, SA, reach_hi, reach_lo, ylo, yhi);
     const bool bb = build_mix(SB, coef64, w.lo_b, w.end_b - 1, wide_idx, Tb.n_wide_below,
-                              Tb.T_below, y0, g.h, out, mine, 0, mb);
+                              Tb.T_below, y0, g.h, out, mine, 0, mb, X, coop);
     const bool ba = build_mix(SA, coef64, w.lo_a, w.end_a - 1, wide_idx, Tb.n_wide_above,
-                              Tb.T_above, y0, g.h, out, mine, 1, ma);
-    if ((lane_id() & 15) == 0 && mine) {
+                              Tb.T_above, y0, g.h, out, mine, 1, ma, X, coop);
+    if ((!coop || wid == 0) && (lane_id() & 15) == 0 && mine) {
       // dword 15: the score offset m_below - m_above, NaN marks a failed cell
       out[15] = (bb || ba) ? __int_as_float(0x7FC00000) : (float)(mb - ma);
       float* mp = region + (int64_t)J.tbl_cap * kCellF + 2 * c;  // (m_below, m_above)
@@ -1242,11 +1283,12 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k
     uint32_t em = 0;  // this lane's candidates in the band
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
-      if (r >= nvalid) break;
-      const float s = stage[r * kWave + lane];
-      const float hi = s + eps(r, s);
-      stage[r * kWave + lane] = hi;
-      if (!(hi < G)) em |= 1u << r;  // (NaN scores go on)
+      if (r < nvalid) {
+        const float s = stage[r * kWave + lane];
+        const float hi = s + eps(r, s);
+        stage[r * kWave + lane] = hi;
+        if (!(hi < G)) em |= 1u << r;  // (NaN scores go on)
+      }
     }
     if (em) {
       // one slot reservation per lane, not per entry: a label's band can be a
@@ -1255,9 +1297,10 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k
       tpe_band* B = band + (int64_t)job * band_cap;
 #pragma unroll
       for (int r = 0; r < kTR; ++r) {
-        if (!((em >> r) & 1u)) continue;
-        if (p < band_cap) B[p] = tpe_band{J.cand_base + t0 + r, x[r], stage[r * kWave + lane]};
-        ++p;
+        if ((em >> r) & 1u) {
+          if (p < band_cap) B[p] = tpe_band{J.cand_base + t0 + r, x[r], stage[r * kWave + lane]};
+          ++p;
+        }
       }
     }
   }
