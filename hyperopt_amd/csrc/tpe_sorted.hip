@@ -264,9 +264,13 @@ __global__ __launch_bounds__(kCB) void k_fit_emit_tid(
   int rk[kCR];
   chunk_ranks(tk, rk, sh);
   int32_t* GI = gi_scr + (int64_t)sg * n_rows;
+  // every row gets its word: the list position of a member, -1 otherwise
+  // (so the sorted-order emit gathers this word alone for membership)
 #pragma unroll
-  for (int u = 0; u < kCR; ++u)
-    if (tk[u]) GI[c0 + u * kCB + threadIdx.x] = (int32_t)(base + rk[u]);
+  for (int u = 0; u < kCR; ++u) {
+    const int64_t r = c0 + u * kCB + threadIdx.x;
+    if (r < n_rows) GI[r] = tk[u] ? (int32_t)(base + rk[u]) : -1;
+  }
 }
 
 // K3: sorted-order emit -- means and ramp weights in sorted order, the prior
@@ -317,10 +321,9 @@ __global__ __launch_bounds__(kCB) void k_fit_emit_sorted(
   for (int u = 0; u < kCR; ++u) {
     const int32_t row = rows[u];
     const bool in = row >= 0;
-    const uint8_t a = in ? Q.A[row] : 0, b = in ? is_below[row] : 2;
     v[u] = in ? Q.V[row] : 0.0;
-    gi[u] = in ? gi_scr[(int64_t)sg * n_rows + row] : 0;
-    tk[u] = a && b == Q.side;
+    gi[u] = in ? gi_scr[(int64_t)sg * n_rows + row] : -1;  // -1: not a member
+    tk[u] = gi[u] >= 0;
   }
   int rk[kCR];
   chunk_ranks(tk, rk, sh);
