@@ -1334,7 +1334,6 @@ constexpr int kBandBits = 32768;     // cell bitmap of the select kernel (LDS)
 constexpr int kBandSlots = 16;       // expand blocks per job and mixture (grid-stride over cells)
 constexpr int kBandFinal = 16;       // final blocks per job (grid-stride over survivors)
 constexpr int kSelPT = 16;           // entries per thread and pass of the select kernel
-constexpr int kExpU = 8;             // components loaded ahead per thread in the expansion
 
 struct BandMix {  // one mixture's expansion on one cell
   double P[kBandD + 1];
@@ -1351,9 +1350,10 @@ struct BandWork {  // per job (tpe_band_work_bytes)
 };
 
 // expansion of mixture S on the cell (y0, h) into E (LDS); all threads.
-// One pass over the components, kExpU loads in flight per thread; each thread
+// One pass over the components, U loads in flight per thread; each thread
 // keeps its own scale (raised when a term would exceed e^8 of it) and the
 // threads are merged at the end (fixed order: deterministic).
+template <int BX, int U>
 __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64, double y0,
                             double h, BandMix& E, double* dred) {
   const int nc = S.n_obs + 1;
@@ -1367,15 +1367,15 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
 #pragma unroll
   for (int n = 0; n <= kBandD; ++n) P[n] = 0.0;
   double ml = -INFINITY;
-  for (int k0 = 0; k0 < nc; k0 += kExpU * kBS) {
-    double4 cs[kExpU];
+  for (int k0 = 0; k0 < nc; k0 += U * BX) {
+    double4 cs[U];
 #pragma unroll
-    for (int u = 0; u < kExpU; ++u) {
-      const int k = k0 + u * kBS + (int)threadIdx.x;
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * BX + (int)threadIdx.x;
       cs[u] = k < nc ? ld4(coef64, off + k) : make_double4(0.0, 0.0, -INFINITY, 0.0);
     }
 #pragma unroll
-    for (int u = 0; u < kExpU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const double4 c = cs[u];
       const double zn = fmax(fabs(y0 - c.x) - 1.05 * h, 0.0) * c.y;
       if (!(c.z - 0.5 * zn * zn >= T)) continue;  // (padding: lc = -inf)
@@ -1383,7 +1383,7 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
       const double A = -(y0 - c.x) * hi2, B = -0.5 * h * hi2;
       if (1.05 * fabs(A) + 1.1025 * fabs(B) > kBandRho) {
         const int p = atomicAdd(&E.n_dir, 1);
-        if (p < kBandDirect) E.dir[p] = k0 + u * kBS + (int)threadIdx.x;
+        if (p < kBandDirect) E.dir[p] = k0 + u * BX + (int)threadIdx.x;
         continue;
       }
       const double z0 = (y0 - c.x) * c.y;
@@ -1405,7 +1405,7 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
       }
     }
   }
-  const double m = block_max<kBS, double>(ml, dred);
+  const double m = block_max<BX, double>(ml, dred);
   {
     const double r = (ml == -INFINITY) ? 0.0 : exp(ml - m);
 #pragma unroll
@@ -1428,7 +1428,7 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
   __syncthreads();
   if (threadIdx.x <= kBandD) {
     double t = 0.0;
-    for (int w = 0; w < kBS / kWave; ++w) t += dred[w * (kBandD + 1) + threadIdx.x];
+    for (int w = 0; w < BX / kWave; ++w) t += dred[w * (kBandD + 1) + threadIdx.x];
     E.P[threadIdx.x] = t;
   }
   if (threadIdx.x == 0) {
@@ -1597,11 +1597,12 @@ __global__ __launch_bounds__(kBS) void k_band_select(
 
 // Expand: block (slot, job, mixture) expands its mixture on listed cells
 // slot, slot + kBandSlots, ... into the job's BandWork.
-__global__ __launch_bounds__(kBS) void k_band_expand(
+constexpr int kBX = 512;  // expansion block: ~20 components per thread at 10^4
+__global__ __launch_bounds__(kBX) void k_band_expand(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
     const uint32_t* __restrict__ band_ctl, BandWork* __restrict__ work) {
-  __shared__ double dred[(kBS / kWave) * (kBandD + 1)];
+  __shared__ double dred[(kBX / kWave) * (kBandD + 1)];
   __shared__ BandMix s_e;
   const int j = blockIdx.y;
   const uint32_t ns = band_ctl[4 * (int64_t)j + 2];
@@ -1613,7 +1614,7 @@ __global__ __launch_bounds__(kBS) void k_band_expand(
   const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
   for (int k = blockIdx.x; k < nc; k += kBandSlots) {
     const int c = work[j].cell[k];
-    band_expand(S, coef64, (double)cell_centre(g0, h32, c), Tb.h, s_e, dred);
+    band_expand<kBX, 4>(S, coef64, (double)cell_centre(g0, h32, c), Tb.h, s_e, dred);
     BandMix& G = work[j].mix[k][blockIdx.z];
     if (threadIdx.x <= kBandD) G.P[threadIdx.x] = s_e.P[threadIdx.x];
     const int nd = s_e.n_dir;
@@ -1621,7 +1622,7 @@ __global__ __launch_bounds__(kBS) void k_band_expand(
       G.m = s_e.m;
       G.n_dir = nd;
     }
-    for (int i = threadIdx.x; i < nd; i += kBS) G.dir[i] = s_e.dir[i];
+    for (int i = threadIdx.x; i < nd; i += kBX) G.dir[i] = s_e.dir[i];
     __syncthreads();  // s_e reused
   }
 }
@@ -2120,7 +2121,7 @@ extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, i
   BandWork* W = static_cast<BandWork*>(work);
   hipLaunchKernelGGL(k_band_select, dim3(n_jobs), dim3(kBS), 0, st, jobs, tables, band, band_cap,
                      band_ctl, partial, gx, best, W);
-  hipLaunchKernelGGL(k_band_expand, dim3(kBandSlots, n_jobs, 2), dim3(kBS), 0, st, jobs, segs,
+  hipLaunchKernelGGL(k_band_expand, dim3(kBandSlots, n_jobs, 2), dim3(kBX), 0, st, jobs, segs,
                      coef64, tables, band_ctl, W);
   hipLaunchKernelGGL(k_band_final, dim3(kBandFinal, n_jobs), dim3(kBS), 0, st, jobs, segs, coef64,
                      tables, band, band_cap, band_ctl, best, W);
