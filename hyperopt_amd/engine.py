@@ -1128,10 +1128,26 @@ class Engine:
                             "hipStreamWaitEvent")
 
         def launch_level(lib=lib):
+            side = None
+            if self.side_stream != "0" and not sample_only and not posteriors and any(
+                    ids for k, ids in groups if k in SIDE_KINDS):
+                if self._side is None:
+                    self._side = torch.cuda.Stream(self.device)
+                side = self._side
+            side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
+            # with the sorted fit the gather only lists the categorical labels'
+            # observations, which only their posterior (side stream) reads: it
+            # runs there, behind an event after the upload, and the main
+            # stream starts with the fit
+            gather_side = hist_mode and histories is None and sorted_fit and \
+                side is not None and bool(cat) and self.cat_early
             if hist_mode:
                 d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
                 d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
-                e0 = tick("gather")
+                gs, gsp = (side, side_p) if gather_side else (None, sp)
+                if gather_side:
+                    stream_order("uploaded", sp, side_p)
+                e0 = tick("gather", gs)
                 g0 = nfs if sorted_fit else 0  # (the sorted fit reads the history itself)
                 if histories is None:
                     if len(g_arr) > g0:
@@ -1141,7 +1157,7 @@ class Engine:
                                                    _V("n_rows", n_rows), base + o_isb,
                                                    base + o_g + g0 * L.GATHER_DTYPE.itemsize,
                                                    g_arr.ctypes.data + g0 * L.GATHER_DTYPE.itemsize,
-                                                   len(g_arr) - g0, d_obs, d_cobs, d_err, sp),
+                                                   len(g_arr) - g0, d_obs, d_cobs, d_err, gsp),
                                 "tpe_gather_obs")
                 else:
                     L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
@@ -1149,7 +1165,7 @@ class Engine:
                                                      g_arr.ctypes.data_as(ctypes.c_void_p),
                                                      len(g_arr), d_obs, d_cobs, d_err, sp),
                             "tpe_gather_obs_multi")
-                tock("gather", e0)
+                tock("gather", e0, gs)
             else:
                 d_obs, d_cobs = base + o_obs, base + o_cobs
 
@@ -1157,13 +1173,6 @@ class Engine:
             # side stream (TPE_SIDE_STREAM != "0"): quantized and categorical work
             # overlaps the continuous pipeline; the categorical posterior starts on
             # it as soon as the lists are gathered (it needs nothing else)
-            side = None
-            if self.side_stream != "0" and not sample_only and not posteriors and any(
-                    ids for k, ids in groups if k in SIDE_KINDS):
-                if self._side is None:
-                    self._side = torch.cuda.Stream(self.device)
-                side = self._side
-            side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
             # main-stream issue order: gather, fit, table build, scorers; the
             # side stream's launches are issued after the table build (host
             # launches cost a few us each: at a one-eighth label share the main
@@ -1203,7 +1212,8 @@ class Engine:
                     return
                 if cat_early and kind == "cat" and not cat_started:
                     cat_started = True  # the categorical work needs only the gather
-                    stream_wait("gathered", side_p)
+                    if not gather_side:  # (else the gather ran on the side stream)
+                        stream_wait("gathered", side_p)
                     cat_fit()
                 if not side_started and kind in SIDE_KINDS and not (cat_early and kind == "cat"):
                     side_started = True  # the side stream's groups that need the fit
@@ -1380,7 +1390,8 @@ class Engine:
             # fit ends)
             cat_early = side is not None and bool(cat) and self.cat_early
             if cat_early:
-                stream_rec("gathered", sp)
+                if not gather_side:
+                    stream_rec("gathered", sp)
                 if self.cat_issue == "pre":  # issued before the fit's launches
                     for g, (k, ids) in enumerate(groups):
                         if k == "cat" and ids:
