@@ -1572,7 +1572,20 @@ class Engine:
                         (list(band_jobs), d_segs, sp.value, exchange is not None))
                     self._staged_sig = sig[:-1]
             return p if defer else p.result()
-        if ops is None:
+        return self._read_results(stream, sp, ops is None, after, pin, nbytes, n_jobs, fix, jobs,
+                                  xbytes, groups, table_calls, outputs, table_scores, out_off,
+                                  works, order, cont, modes, _hmark)
+
+
+    def _read_results(self, stream, sp, sync, after, pin, nbytes, n_jobs, fix, jobs, xbytes,
+                      groups, table_calls, outputs, table_scores, out_off, works, order, cont,
+                      modes, _hmark):
+        """The level's synchronous readback: the result block (error bits, table
+        stats, one tpe_best per job, the exchange's label records) from the
+        pinned copy, the overflowed bands' exact re-score, per-candidate
+        outputs of the test hooks; one LabelResult per work."""
+        BS = L.BEST_DTYPE.itemsize
+        if sync:
             L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
         if after is not None:
             after()
@@ -1582,7 +1595,7 @@ class Engine:
             fix(best_h, jobs)
         self.last_exchange = res_h[64 + n_jobs * BS:].view(L.BEST_DTYPE).copy() if xbytes \
             else None
-        with torch.cuda.stream(stream):
+        with self.torch.cuda.stream(stream):
             err = int(res_h[:4].view(np.int32)[0])
             self.last_pairs = None
             if any(k == "sorted" and ids for k, ids in groups):
@@ -1619,7 +1632,6 @@ class Engine:
             results[i] = r
         _hmark("results")
         return results
-
 
     def _band_fix(self, band_jobs, d_segs, max_comp, n_comp, stream, exchanged, best_h, jobs):
         """Jobs of the table path whose band overflowed (n_scored == -1: more
