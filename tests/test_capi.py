@@ -209,3 +209,32 @@ def test_lattice_suggest_argument_errors():
     jobs["flags"] = L.F_QUANT | L.F_INJECTED
     assert call(1 << 16, 1 << 10) == -1
     assert b"not a sampled quantized job" in lib.tpe_last_error()
+
+
+def test_categorical_suggest_argument_errors():
+    """tpe_categorical_suggest (the prefix-first categorical argmax)
+    validates its jobs, pointers, prefix and workspace before any launch."""
+    lib = L.load()
+    jobs = np.zeros(1, L.JOB_DTYPE)
+    jobs["n_cand"] = 1 << 20
+    jobs["lat_n"] = 8
+    hp_ = jobs.ctypes.data_as(ctypes.c_void_p)
+    one = ctypes.c_void_p(8)  # a non-null stand-in: validation fails before any launch
+    ptrs = [one] * 3
+
+    def call(prefix, n_partial, need=one, n_jobs=1):
+        return lib.tpe_categorical_suggest(one, hp_, n_jobs, *ptrs, prefix, one, n_partial,
+                                           need, one, None)
+    assert call(1 << 16, 1 << 10, n_jobs=0) == 0  # nothing to do
+    assert call(1 << 16, 1 << 10) == -1  # family 0: not categorical
+    assert b"not a sampled categorical job" in lib.tpe_last_error()
+    jobs["family"] = L.CAT
+    assert call(1 << 16, 1 << 10, need=None) == -1
+    assert b"null pointer" in lib.tpe_last_error()
+    assert call(1000, 1 << 10) == -1
+    assert b"prefix" in lib.tpe_last_error()
+    assert call(1 << 16, 10) == -1
+    assert b"partial workspace" in lib.tpe_last_error()
+    jobs["flags"] = L.F_INJECTED
+    assert call(1 << 16, 1 << 10) == -1
+    assert b"not a sampled categorical job" in lib.tpe_last_error()
