@@ -614,7 +614,6 @@ def main():
 
     per_rank = sum(c for _, _, c in units)
     total_cand = (len(space) * n_cand if strong else per_rank * world) * args.steps
-    value = total_cand / elapsed
     # candidates actually drawn: a quantized label's prefix-first lattice
     # argmax (tpe_lattice_suggest) decides most labels from the first
     # eng.lat_prefix draws of its stream (exact by construction);
@@ -624,6 +623,11 @@ def main():
         t = torch.tensor([float(drawn)], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)
         drawn = int(t.item())
+    # the headline counts candidates actually drawn and scored (VERDICT r03
+    # weak #2); the decided count (every label's full 2^22-candidate argmax,
+    # settled from a prefix for the quantized / categorical labels) is reported
+    # beside it as value_decided
+    value = drawn * args.steps / elapsed
     # per-launch HBM bytes / VALU figures of the dominant kernel, from the PMC
     # passes of tools/profile_round.sh (tools/make_traffic.py)
     traffic, prof = None, {}
@@ -669,9 +673,11 @@ def main():
         "metric": "EI candidates scored/sec (50-dim, 10k trials)",
         "value": value,
         "unit": "EI candidates/s",
+        "value_note": "candidates drawn and scored per second (value_decided: every "
+                      "label's full candidate count, prefix-settled labels included)",
         "candidates_drawn_per_step": drawn,
         "candidates_decided_per_step": total_cand // args.steps,
-        "value_drawn": drawn * args.steps / elapsed,
+        "value_decided": total_cand / elapsed,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -41,7 +41,8 @@ JOB_DTYPE = np.dtype([
 TABLE_DTYPE = np.dtype([
     ("lo", "<f8"), ("hi", "<f8"), ("h_below", "<f8"), ("h_above", "<f8"), ("origin", "<f8"),
     ("h", "<f8"), ("inv_h", "<f4"), ("inv_w", "<f4"), ("nb", "<i4"), ("n_wide_below", "<i4"),
-    ("n_wide_above", "<i4"), ("slope", "<f4"), ("T_below", "<f8"), ("T_above", "<f8")],
+    ("n_wide_above", "<i4"), ("slope", "<f4"), ("eps_cubic", "<f4"), ("eps_mix", "<f4"),
+    ("build_items", "<i4"), ("build_ab", "<f4"), ("T_below", "<f8"), ("T_above", "<f8")],
     align=True)
 GATHER_DTYPE = np.dtype([
     ("col", "<i4"), ("below", "<i4"), ("dst_off", "<i8"), ("offset", "<i8"), ("count", "<i8"),
@@ -100,10 +101,10 @@ _SIGNATURES = {
     "tpe_table_build": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_score_table": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
                              _P, _P, _P]),
-    "tpe_score_table_fast": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P,
-                                  _P, _I64, _P, _P]),
-    "tpe_band_rescore": (_I, [_P, _P, _I, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P]),
-    "tpe_band_work_bytes": (_I64, [_I]),
+    "tpe_score_table_fast": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                  _P, _I64, _I, _P, _P]),
+    "tpe_band_rescore": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P]),
+    "tpe_band_bytes": (_I64, [_P, _I, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "tpe_categorical_suggest": (_I, [_P, _P, _I, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "tpe_history_order_scratch_bytes": (_I64, [_I, _I64]),
     "tpe_history_order": (_I, [_P, _I64, _P, _P, _I, _I64, _I64, _P, _P, _P]),
@@ -131,6 +132,7 @@ _SIGNATURES = {
     "tpe_best_scatter": (_I, [_P, _P, _I, _P, _I, _P]),
     "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
     "tpe_run_ops": (_I, [_P, _I, ctypes.POINTER(_I)]),
+    "tpe_check_transcendentals": (_I, [_P, _P]),
     "tpe_smallest_rows": (_I64, [_P, _I64, _I64, _P]),
     "tpe_last_error": (ctypes.c_char_p, []),
     "tpe_abi_version": (_I, []),

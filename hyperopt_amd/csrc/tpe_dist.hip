@@ -93,13 +93,15 @@ __global__ void k_scatter_best(const tpe_best* __restrict__ by_job,
   b.index = -1;
   b.value = 0.0;
   int64_t n = 0;
+  bool inexact = false;  // a job whose band overflowed (n_scored -1): the label is owed
   for (int j = 0; j < n_jobs; ++j) {
     if (slot[j] != s) continue;
     const tpe_best o = by_job[j];
     n += o.n_scored;
+    inexact = inexact || o.n_scored < 0;
     if (better(o.score, o.index, b.score, b.index)) b = o;
   }
-  b.n_scored = n;
+  b.n_scored = inexact ? -1 : n;
   out[s] = b;
 }
 }  // namespace

@@ -1410,12 +1410,14 @@ __global__ void k_combine(const tpe_best* __restrict__ sets, int n_sets, int n_l
   if (l >= n_labels) return;
   tpe_best b = sets[l];
   int64_t n = b.n_scored;
+  bool inexact = n < 0;  // a set whose exact decision is still owed (band overflow)
   for (int s = 1; s < n_sets; ++s) {
     const tpe_best o = sets[(int64_t)s * n_labels + l];
     n += o.n_scored;
+    inexact = inexact || o.n_scored < 0;
     if (better(o.score, o.index, b.score, b.index)) b = o;
   }
-  b.n_scored = n;
+  b.n_scored = inexact ? -1 : n;  // -1 travels: every rank sees the label is owed
   out[l] = b;
 }
 

@@ -284,6 +284,11 @@ __global__ __launch_bounds__(kBS) void k_table_plan2(
     if (half == 0) {
       tables[job].h_below = hmin;
       tables[job].n_wide_below = ntot;
+      // raised by k_table_build (build_items, build_ab) and k_table_score
+      // (eps_cubic) with atomics: zeroed here, one launch before
+      tables[job].build_items = 0;
+      tables[job].build_ab = 0.0f;
+      tables[job].eps_cubic = 0.0f;
     } else {
       tables[job].h_above = hmin;
       tables[job].n_wide_above = ntot;
@@ -340,6 +345,19 @@ __device__ __forceinline__ int last_le(const double* a, int n, double v) {
   return lo - 1;
 }
 
+// e^x as fp32 for x <= 0 with a relative error <= 2^-22 + 2^-25 (v_exp_f32
+// on the fractional part of x log2 e, formed in fp64): the build's rescale and
+// merge factors (mix_eps counts two roundings per factor)
+__device__ __forceinline__ float exp_acc(double x) {
+  const double t = x * kLog2e;
+  const double n = floor(t);
+  return ldexpf(__builtin_amdgcn_exp2f((float)(t - n)), (int)n);
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
 __device__ __forceinline__ double wave_max_d(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
@@ -384,11 +402,11 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
 // (row_sum9_transposed: the build sums each row on its own, one cell per
 // row): 9 exchange-adds instead of the 9 x 4 of one DPP sum per term.
 template <int CTRL, int M>
-__device__ __forceinline__ void fold_stage(float (&w)[16], bool hi) {
+__device__ __forceinline__ void fold_stage(double (&w)[16], bool hi) {
 #pragma unroll
   for (int j = 0; j < M; ++j) {
-    const float keep = hi ? w[2 * j + 1] : w[2 * j], send = hi ? w[2 * j] : w[2 * j + 1];
-    w[j] = keep + dpp_f<CTRL>(send);
+    const double keep = hi ? w[2 * j + 1] : w[2 * j], send = hi ? w[2 * j] : w[2 * j + 1];
+    w[j] = keep + dpp_d<CTRL>(send);
   }
 }
 __device__ __forceinline__ int rev4(int p) {
@@ -457,15 +475,15 @@ __device__ __forceinline__ double row_max_dpp(double v) {
   v = fmax(v, dpp_d<kDppMirror>(v));
   return v;
 }
-__device__ __forceinline__ float row_sum9_transposed(const float (&P)[9]) {
+__device__ __forceinline__ double row_sum9_transposed(const double (&P)[9]) {
   const int lane = lane_id();
-  float w[16];
+  double w[16];
 #pragma unroll
-  for (int n = 0; n < 16; ++n) w[n] = n < 9 ? P[n] : 0.0f;
+  for (int n = 0; n < 16; ++n) w[n] = n < 9 ? P[n] : 0.0;
   fold_stage<kDppMirror, 5>(w, (lane >> 3) & 1);      // 9 live -> 5
-  w[5] = 0.0f;
+  w[5] = 0.0;
   fold_stage<kDppHalfMirror, 3>(w, (lane >> 2) & 1);  // -> 3
-  w[3] = 0.0f;
+  w[3] = 0.0;
   fold_stage<kDppXor2, 2>(w, (lane >> 1) & 1);        // -> 2
   fold_stage<kDppXor1, 1>(w, lane & 1);               // -> 1
   return w[0];
@@ -478,14 +496,15 @@ __device__ __forceinline__ float row_sum9_transposed(const float (&P)[9]) {
 // drops -- then the wide list; every row walks the same items.
 struct BuildLds {  // the block's four waves' partial expansions of one mixture
   double m[kBS / kWave][4];   // per wave and row: its scale
-  float p[kBS / kWave][kWave];  // per wave and lane: its row's sum of P_rev4(lane & 15)
+  double p[kBS / kWave][kWave];  // per wave and lane: its row's sum of P_rev4(lane & 15)
   int bad[kBS / kWave][4];
 };
 __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __restrict__ coef64,
                                           int k_lo, int k_hi,
                                           const int32_t* __restrict__ wide_idx, int n_wide,
                                           double T, double y0, double h, float* cell, bool store,
-                                          int mix, double& m_out, BuildLds& X, bool coop) {
+                                          int mix, double& m_out, BuildLds& X, bool coop,
+                                          int& itm) {
   // coop (block-uniform): the block's four waves build the same four cells
   // and split the items; otherwise every wave builds its own four cells
   constexpr int kNW = kBS / kWave;
@@ -494,6 +513,7 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   const int64_t off = S.comp_off;
   const int nwin = max(0, k_hi - k_lo + 1);
   const int items = nwin + n_wide;
+  itm = max(itm, items);  // (the error bound's summation depth, mix_eps)
   const int lane = lane_id(), l = lane & 15;
   // component of work item `it` (window first, then the wide list)
   auto comp = [&](int it) -> int {
@@ -502,12 +522,14 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   // One pass: every component inside the window (components the plan's
   // global bound admits; each satisfies the expansion bound by the choice of
   // h).  The exponent is formed in fp64, the series and the per-component
-  // tests in fp32; each lane keeps its own scale m_l (raised only when a term
-  // would exceed e^8 of it) and the row's lanes are merged at the end.  The
-  // next item's coefficients are loaded before this item's work.
-  float P[kP];
+  // tests in fp32, the nine P_n sums in fp64 (a sum of ~10^3 fp32 terms would
+  // carry ~10^3 roundings into the error bound, mix_eps); each lane keeps its
+  // own scale m_l (raised only when a term would exceed e^8 of it) and the
+  // row's lanes are merged at the end.  The next item's coefficients are
+  // loaded before this item's work.
+  double P[kP];
 #pragma unroll
-  for (int n = 0; n < kP; ++n) P[n] = 0.0f;
+  for (int n = 0; n < kP; ++n) P[n] = 0.0;
   double ml = -INFINITY;
   bool bad = false;
   const float hf = (float)h, Tf = (float)T;
@@ -530,7 +552,7 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     const double v = c.z - 0.5 * zc * zc;
     const bool up = inc && v > ml + 8.0;
     if (__any(up)) {  // new scale: rescale the raising lanes' partial sums
-      const float r = up ? ((ml == -INFINITY) ? 0.0f : __expf((float)(ml - v))) : 1.0f;
+      const double r = up ? ((ml == -INFINITY) ? 0.0 : exp(ml - v)) : 1.0;
 #pragma unroll
       for (int n = 0; n < kP; ++n) P[n] *= r;
       ml = up ? v : ml;
@@ -538,13 +560,14 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     const float hi2 = hf * inv * inv;
     const float Af = inc ? -dyf * hi2 : 0.0f, B2 = inc ? -hf * hi2 : 0.0f;  // A and 2B
     bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > (float)(kRhoLim * (1.0 + 1e-5)));
-    const float e = inc ? __expf((float)(v - ml)) : 0.0f;
+    // the term: exponent (v - ml) log2 e formed in fp64, rounded once to fp32
+    const float e = inc ? __builtin_amdgcn_exp2f((float)((v - ml) * kLog2e)) : 0.0f;
     float cm = 0.0f, cc = e;  // e * c_n
-    P[0] += e;
+    P[0] += (double)e;
 #pragma unroll
     for (int n = 0; n + 1 < kP; ++n) {
       const float cnx = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
-      P[n + 1] += cnx;
+      P[n + 1] += (double)cnx;
       cm = cc;
       cc = cnx;
     }
@@ -553,17 +576,17 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   }
   const double m0 = row_max_dpp(ml);
   {
-    const float r = (ml == -INFINITY) ? 0.0f : __expf((float)(ml - m0));
+    const double r = (ml == -INFINITY) ? 0.0 : exp(ml - m0);
 #pragma unroll
     for (int n = 0; n < kP; ++n) P[n] *= r;
   }
   static_assert(kP == 9, "row_sum9_transposed folds nine terms");
-  const float v = row_sum9_transposed(P);  // lane p of the row: the row's total of P_rev4(p)
+  const double v = row_sum9_transposed(P);  // lane p of the row: the row's total of P_rev4(p)
   bad = ((__ballot(bad) >> (lane & ~15)) & 0xFFFFull) != 0;
   // the four waves' partial sums of each row (cell), merged at their largest
   // scale; wave 0 holds the result
   double M = m0;
-  float tot = v;
+  double tot = v;
   bool anybad = bad;
   if (coop) {
     const int row = lane >> 4;
@@ -575,11 +598,15 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     __syncthreads();
     M = X.m[0][row];
     for (int w = 1; w < kNW; ++w) M = fmax(M, X.m[w][row]);
-    tot = 0.0f;
+    // the four waves' scale factors: lane l of the row takes wave l & 3's
+    // (one fp64 exp per lane), the row's lanes read them by shuffle
+    static_assert(kNW == 4, "one factor per row lane quad");
+    const double mq = X.m[l & 3][row];
+    const double fq = (mq == -INFINITY) ? 0.0 : exp(mq - M);
+    tot = 0.0;
     anybad = false;
     for (int w = 0; w < kNW; ++w) {
-      const double mw = X.m[w][row];
-      tot += (mw == -INFINITY) ? 0.0f : X.p[w][lane] * __expf((float)(mw - M));
+      tot += X.p[w][lane] * __shfl(fq, (lane & ~15) + w, kWave);
       anybad = anybad || X.bad[w][row];
     }
     __syncthreads();  // (X is reused by the next call)
@@ -587,9 +614,9 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   const int n = rev4(l);
   if (store && wv == 0 && n < kP) {
     if (n < kP32)
-      cell[2 * n + mix] = tot;
+      cell[2 * n + mix] = (float)tot;
     else
-      reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (n - kP32) + mix] = (_Float16)tot;
+      reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (n - kP32) + mix] = (_Float16)(float)tot;
   }
   m_out = M;
   return anybad;
@@ -602,25 +629,137 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
 // difference of two log-densities, sampled at half-widths of ~0.06 of the
 // narrowest bandwidth): a cubic interpolant at four Chebyshev nodes of
 // [-1.05, 1.05] reproduces it to ~1e-7 on C3's histories.
-// k_table_score gives each cell 16 lanes: lanes 0-3 evaluate f at the
-// nodes, lanes 4-15 at 12 check points, from the cell's STORED coefficients
-// (what the two-polynomial scorer evaluates; fp32 Horner, the log of the
-// ratio as exponent + v_log_f32 of the mantissa, < 3e-7 in all); the nodes'
-// values are broadcast, every lane forms the same cubic (fp64 divided
-// differences), rounds it to fp32 and checks it at its point.  A cell whose
-// cubic misses f by more than kScoreTol (absolute, + 2^-22 relative), or
-// whose P is not positive, is flagged (NaN c0) and its candidates take the
-// two-polynomial cell.  16 B per cell, after the job's cells and m pairs in
-// its 128-B-per-cell region.
+// k_table_score gives each cell kScoreLanes = 8 lanes: lanes 0-3 evaluate f
+// at the nodes from the cell's STORED coefficients (fp32 Horner, the log of
+// the ratio as exponent + v_log_f32 of the mantissa); the nodes' values are
+// broadcast, every lane forms the same cubic (fp64 divided differences) and
+// rounds it to fp32.  Then the cubic's error is BOUNDED, not sampled: lane i
+// takes the sub-interval of [-1.0501, 1.0501] centred at c_i (half-width
+// r = 1.0501 / 8) and encloses
+//     e(c_i + t) = f^(c_i + t) - q(c_i + t),   |t| <= r,
+// f^ = off + ln P^_b - ln P^_a being the score of the stored polynomials
+// (exact reals).  Per mixture: the Taylor coefficients T_k of P^ at c_i (a
+// Horner shift), a_k = T_k / T_0, the log series ln P^(c+t) = ln T_0 +
+// sum_k l_k t^k with l_k = a_k - (1/k) sum_{j<k} j l_j a_{k-j} (exact up to
+// fp64 rounding) for k <= kLogD, and the rest bounded by the majorant
+// -ln(1 - w~(t)), w~ = sum |a_k| t^k: its coefficients m_k >= |l_k| (same
+// recurrence on |a_k|, all terms positive), summed for kLogD < k <= kLogM,
+// and past kLogM by Cauchy's estimate on the radius 4r (m_k (4r)^k <=
+// -ln(1 - w~(4r)) <= ln 2 when w~(4r) <= 1/2; otherwise the cell is flagged).
+// So |e| <= |E_0| + sum_{k<=kLogD} |E_k| r^k + rem_b + rem_a + rounding, E_k
+// the coefficients of the difference polynomial; the cell's bound is the
+// largest of its lanes'.  A cell whose bound exceeds kFitTol (or whose P is
+// not positive, or whose cubic is not finite) is flagged (NaN c0) and its
+// candidates take the two-polynomial cell.  The job's tpe_table gets
+//   slope     = max |c1| + 2.11 |c2| + 3.31 |c3|  (>= |q'(u)| on |u| <= 1.0501)
+//   eps_cubic = max over unflagged cells of  fit + 2^-21 sum_k |c_k| 1.0501^k
+//               + 4.5 2^-24 slope_cell + 2^-24 |off| (1 + 1e-4)
+// (the cubic's fp32 Horner beyond its 2^-22 |s| part, u's fp32 rounding, the
+// fp32 score offset) and eps_mix, the per-mixture polynomial bound
+// (mix_eps).  16 B per cell, after the job's cells and m pairs in its
+// 128-B-per-cell region.
 // ---------------------------------------------------------------------------
-constexpr double kScoreTol = 1.0e-6;  // absolute fit error allowed (nats)
-constexpr int kScoreLanes = 16;       // lanes per cell: 4 nodes + 12 check points
-constexpr int kScoreChecks = kScoreLanes - 4;
+constexpr double kFitTol = 1.0e-6;   // cubic-vs-polynomial bound allowed (nats)
+constexpr int kScoreLanes = 8;       // lanes per cell: 4 nodes, 8 sub-intervals
 constexpr int kScoreCellsPerBlock = kBS / kScoreLanes;
-constexpr int kScoreBlocks = 256;     // per job (grid-stride over cells)
+constexpr int kScoreBlocks = 256;    // per job (grid-stride over cells)
+constexpr double kUFit = 1.0501;     // |u| the bounds cover (u's fp32 rounding: <= 1.05 (1 + 5 2^-24))
+constexpr int kLogD = 8;             // log-series terms carried exactly
+constexpr int kLogM = 14;            // majorant terms summed (then Cauchy's tail)
+constexpr double kU32 = 0x1.0p-24;   // fp32 unit roundoff
+// max of a + b = 1.0501|A| + 1.1028|B| over the admissible set 9|A| + 65|B| <=
+// 5.8 (1 + 2e-5) (the build's test with its fp32 slack): at |A| = 0.64446
+constexpr double kAbMax = 0.6768;
+
+// Per-mixture relative error bound of a stored cell polynomial against its
+// mixture, |P^(u) - S(y) e^-m| <= eps_mix S(y) e^-m on |u| <= kUFit, from the
+// build's worst case over the job's cells (DESIGN.md 3.1 derives each term):
+// items = most components one cell summed, coop = the cooperative build (64
+// lanes per row), ab = max 1.0501|A| + 1.1028|B| of a summed component (also
+// >= a + 2b).  Terms relative to a component's value carry e^ab (its
+// majorant over its value at u); those of the P_n sums carry E2 = e^2ab.
+__host__ __device__ inline double mix_eps(int items, bool coop, double ab) {
+  const double u = kU32, ud = 0x1.0p-53;
+  const int stride = coop ? 64 : 16;
+  const int K = (items + stride - 1) / stride + 5 + (coop ? 5 : 0);  // fp64 adds into one P_n
+  const double E1 = exp(ab), E2 = E1 * E1;
+  return 4.4e-7                         // series truncation (tools/table_bounds.py)
+         + 1.0e-10                      // components below the exclusion floor
+         + (10.0 + 4.6e-4 * items) * u  // each term's exponent rounded to fp32
+         + 0x1.0p-22                    // v_exp_f32 (checked exhaustively, tpe_check_transcendentals)
+         + 5.5 * u * ab                 // A, B rounded to fp32
+         + 4.0 * u * ab * E2            // the fp32 series recurrence (4 roundings per step)
+         + u * E2                       // P_0..P_5 stored in fp32
+         + 1.5e-7 + 0x1.0p-25 * 4.2 * E1  // P_6..P_8 in fp16 (+ subnormal spacing)
+         + (K + 8) * 2.0 * ud * E2;     // fp64 sums, rescale and merge factors of the P_n
+}
 
 __device__ __forceinline__ const float4* score_cells_of(const char* region, int64_t cap) {
   return reinterpret_cast<const float4*>(region + ((cap * (int64_t)(kCellF * 4 + 8) + 15) & ~15ll));
+}
+
+// one mixture's stored coefficients as doubles (exact)
+__device__ __forceinline__ void cell_coefs(const float* cell, int mix, double (&p)[kP]) {
+  const _Float16* tail = reinterpret_cast<const _Float16*>(cell + 2 * kP32);
+#pragma unroll
+  for (int n = 0; n < kP32; ++n) p[n] = (double)cell[2 * n + mix];
+#pragma unroll
+  for (int n = kP32; n < kP; ++n) p[n] = (double)(float)tail[2 * (n - kP32) + mix];
+}
+
+// ln P^(c + t) = lnT0 + sum_{k=1..kLogD} l[k] t^k + R, |R| <= rem on |t| <= r;
+// false when P^(c) <= 0 or the majorant's radius check fails
+__device__ __forceinline__ bool log_taylor(const double (&p)[kP], double c, double r, double& lnT0,
+                                           double (&l)[kLogD + 1], double& rem) {
+  double T[kP];
+#pragma unroll
+  for (int n = 0; n < kP; ++n) T[n] = p[n];
+#pragma unroll
+  for (int i = 0; i < kP - 1; ++i)
+#pragma unroll
+    for (int j = kP - 2; j >= i; --j) T[j] = fma(c, T[j + 1], T[j]);
+  if (!(T[0] > 0.0) || !isfinite(T[0])) return false;
+  lnT0 = log(T[0]);
+  const double inv0 = 1.0 / T[0];
+  double a[kP];
+  a[0] = 1.0;
+#pragma unroll
+  for (int k = 1; k < kP; ++k) a[k] = T[k] * inv0;
+  l[0] = 0.0;
+#pragma unroll
+  for (int k = 1; k <= kLogD; ++k) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 1; j < k; ++j) s = fma((double)j * l[j], a[k - j], s);
+    l[k] = a[k] - s * (1.0 / (double)k);
+  }
+  // majorant of the log series (fp32: a bound, inflated by 1e-3 below)
+  float aa[kP], m[kLogM + 1];
+  float w4 = 0.0f, rr = 1.0f;
+  const float r4 = (float)(4.0 * r);
+#pragma unroll
+  for (int k = 1; k < kP; ++k) {
+    aa[k] = (float)fabs(a[k]);
+    rr *= r4;
+    w4 = fmaf(aa[k], rr, w4);
+  }
+  w4 *= 1.001f;
+  if (!(w4 <= 0.5f)) return false;
+  float tail = 0.0f, rk = 1.0f;
+  const float rf = (float)r;
+#pragma unroll
+  for (int k = 1; k <= kLogM; ++k) {
+    float s = k < kP ? aa[k] : 0.0f;
+#pragma unroll
+    for (int j = 1; j < k; ++j)
+      if (k - j < kP) s = fmaf((float)j * m[j] * (1.0f / (float)k), aa[k - j], s);
+    m[k] = s;
+    rk *= rf;
+    if (k > kLogD) tail = fmaf(s, rk, tail);
+  }
+  // past kLogM: m_k (4r)^k <= ln 2, so sum_{k > kLogM} m_k r^k <= ln2 4^-(M+1) / (3/4)
+  rem = (double)tail * 1.001 + 0.6931471805599453 * ldexp(1.0, -2 * (kLogM + 1)) / 0.75;
+  return true;
 }
 
 __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__ jobs,
@@ -629,7 +768,14 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
                                                      unsigned long long* __restrict__ stats) {
   __shared__ float fred[kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
-  const int nb = tables[blockIdx.y].nb;
+  const tpe_table Tb = tables[blockIdx.y];
+  const int nb = Tb.nb;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the per-mixture bound from the build's worst case (k_table_build's atomics)
+    tables[blockIdx.y].build_ab = (float)kAbMax;
+    tables[blockIdx.y].eps_mix =
+        (float)(mix_eps(Tb.build_items, nb <= kCoopCells, kAbMax) * (1.0 + 1e-6));
+  }
   char* region = reinterpret_cast<char*>(cells) + J.tbl_off * kSlotB;
   float4* outs = const_cast<float4*>(score_cells_of(region, J.tbl_cap));
   const int sub = threadIdx.x / kScoreLanes, l = threadIdx.x % kScoreLanes;
@@ -637,10 +783,11 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
   constexpr double kU = (double)kULim;
   const double nd0 = kU * 0.92387953251128674, nd1 = kU * 0.38268343236508978, nd2 = -nd1,
                nd3 = -nd0;
-  const double u = l == 0 ? nd0 : l == 1 ? nd1 : l == 2 ? nd2 : l == 3 ? nd3
-                 : -kU + 2.0 * kU * (double)(l - 4) / (kScoreChecks - 1);
-  const float uf = (float)u;
-  float slope = 0.0f;  // max |f'(u)| bound over this thread's unflagged cells (lane 0 of a group)
+  const double un = l == 0 ? nd0 : l == 1 ? nd1 : l == 2 ? nd2 : nd3;  // (lanes >= 4: unused)
+  const float uf = (float)un;
+  constexpr double r = kUFit / kScoreLanes;
+  const double cI = -kUFit + (2 * l + 1) * r;  // this lane's sub-interval centre
+  float slope = 0.0f, epsc = 0.0f;  // over this thread's unflagged cells (lane 0 of a group)
   // group-uniform trip count: every lane of a group runs the shuffles
   for (int64_t c = (int64_t)blockIdx.x * kScoreCellsPerBlock + sub; c < nb;
        c += (int64_t)gridDim.x * kScoreCellsPerBlock) {
@@ -661,10 +808,11 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
     const bool ok_pt = (pb > 0.0f) && (pa > 0.0f) && isfinite(pb) && isfinite(pa);
     // log(pb / pa) = ln2 * (e + log2(m)), m = the ratio's mantissa in [0.5, 1)
     int e = 0;
-    const float m = ok_pt ? frexpf(pb / pa, &e) : 1.0f;
-    const double f = off + kLn2 * ((double)e + (double)__builtin_amdgcn_logf(m));
+    const float mt = ok_pt ? frexpf(pb / pa, &e) : 1.0f;
+    const double f = off + kLn2 * ((double)e + (double)__builtin_amdgcn_logf(mt));
     const double f0 = __shfl(f, gbase + 0, kWave), f1 = __shfl(f, gbase + 1, kWave),
                  f2 = __shfl(f, gbase + 2, kWave), f3 = __shfl(f, gbase + 3, kWave);
+    const bool nodes_ok = ((__ballot(!ok_pt) >> gbase) & 0xFull) == 0;
     // Newton divided differences -> monomial coefficients of the cubic
     const double d01 = (f1 - f0) / (nd1 - nd0), d12 = (f2 - f1) / (nd2 - nd1),
                  d23 = (f3 - f2) / (nd3 - nd2);
@@ -675,23 +823,64 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
     const double c1 = d01 - d012 * (nd0 + nd1) + d0123 * (nd0 * nd1 + nd0 * nd2 + nd1 * nd2);
     const double c0 = f0 - d01 * nd0 + d012 * nd0 * nd1 - d0123 * nd0 * nd1 * nd2;
     const float4 q = make_float4((float)c0, (float)c1, (float)c2, (float)c3);
-    const double p = (((double)q.w * u + (double)q.z) * u + (double)q.y) * u + (double)q.x;
-    bool fail = !ok_pt || (l >= 4 && !(fabs(p - f) <= kScoreTol + fabs(f) * 0x1.0p-22));
-    fail = fail || !(off == off) || !isfinite(q.x) || !isfinite(q.y) || !isfinite(q.z) ||
-           !isfinite(q.w);
-    const uint64_t mk = __ballot(fail) >> gbase;
+    // the bound of |f^ - q| on this lane's sub-interval
+    const double q0 = q.x, q1 = q.y, q2 = q.z, q3 = q.w;
+    bool fail = !nodes_ok || !(off == off) || !isfinite(q0) || !isfinite(q1) || !isfinite(q2) ||
+                !isfinite(q3);
+    double bound = INFINITY;
+    if (!fail) {
+      double pbv[kP], pav[kP], lb[kLogD + 1], la[kLogD + 1], lnb = 0.0, lna = 0.0, rb = 0.0,
+             ra = 0.0;
+      cell_coefs(cell, 0, pbv);
+      cell_coefs(cell, 1, pav);
+      const bool okb = log_taylor(pbv, cI, r, lnb, lb, rb);
+      const bool oka = log_taylor(pav, cI, r, lna, la, ra);
+      if (okb && oka) {
+        // the cubic's Taylor coefficients at cI
+        const double qc = ((q3 * cI + q2) * cI + q1) * cI + q0;
+        const double qk[4] = {qc, (3.0 * q3 * cI + 2.0 * q2) * cI + q1, 3.0 * q3 * cI + q2, q3};
+        const double E0 = off + lnb - lna - qc;
+        double sum = fabs(E0), rk = 1.0;
+#pragma unroll
+        for (int k = 1; k <= kLogD; ++k) {
+          rk *= r;
+          const double Ek = lb[k] - la[k] - (k < 4 ? qk[k] : 0.0);
+          sum = fma(fabs(Ek), rk, sum);
+        }
+        // fp64 rounding of the whole computation (magnitudes ~|off| + |ln T0|)
+        const double slack = 1e-13 * (1.0 + fabs(off) + fabs(lnb) + fabs(lna) + fabs(qc));
+        bound = sum + rb + ra + slack;
+      }
+    }
+    // the cell's bound: the largest of its 8 lanes'
+    float bmax = (float)(bound * (1.0 + 1e-6));
+#pragma unroll
+    for (int o = 1; o < kScoreLanes; o <<= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, kWave));
+    if (!(bmax == bmax)) bmax = INFINITY;
+    fail = fail || !(bmax <= (float)kFitTol);
+    const bool bad = ((__ballot(fail) >> gbase) & ((1ull << kScoreLanes) - 1)) != 0;
     if (l == 0) {
-      const bool bad = (mk & ((1ull << kScoreLanes) - 1)) != 0;
       outs[c] = bad ? make_float4(__int_as_float(0x7FC00000), 0.0f, 0.0f, 0.0f) : q;
       if (bad && stats) atomicAdd(stats + 2, 1ull);
-      // |f'(u)| <= |c1| + 2|c2||u| + 3|c3|u^2 on |u| <= 1.05: the slope term of the
-      // scorer's error bound (u is rounded to fp32 there)
-      if (!bad) slope = fmaxf(slope, fabsf(q.y) + 2.1f * fabsf(q.z) + 3.31f * fabsf(q.w));
+      if (!bad) {
+        // |q'(u)| <= |c1| + 2|c2||u| + 3|c3|u^2 on |u| <= 1.0501
+        const float sl = fabsf(q.y) + 2.11f * fabsf(q.z) + 3.31f * fabsf(q.w);
+        slope = fmaxf(slope, sl);
+        const float ev = 0x1.0p-21f * (1.0501f * fabsf(q.y) + 1.1028f * fabsf(q.z) +
+                                        1.1581f * fabsf(q.w));
+        const float ec = bmax + ev + 4.5f * 0x1.0p-24f * sl + 0x1.0p-24f * 1.0001f * (float)fabs(off);
+        epsc = fmaxf(epsc, ec * 1.0001f);
+      }
     }
   }
   slope = block_max<kBS, float>(slope, fred);
-  if (threadIdx.x == 0 && slope > 0.0f)  // non-negative floats order as their bits
+  epsc = block_max<kBS, float>(epsc, fred);
+  // non-negative floats order as their bits
+  if (threadIdx.x == 0 && slope > 0.0f)
     atomicMax(reinterpret_cast<unsigned int*>(&tables[blockIdx.y].slope), __float_as_uint(slope));
+  if (threadIdx.x == 0 && epsc > 0.0f)
+    atomicMax(reinterpret_cast<unsigned int*>(&tables[blockIdx.y].eps_cubic),
+              __float_as_uint(epsc));
 }
 
 __global__ __launch_bounds__(kBS) void k_table_build(
@@ -723,6 +912,7 @@ __global__ __launch_bounds__(kBS) void k_table_build(
   const bool coop = g.nb <= kCoopCells;  // block-uniform
   const int64_t q0 = coop ? blockIdx.x : (int64_t)blockIdx.x * (kBS / kWave) + wid;
   const int64_t qs = coop ? gridDim.x : (int64_t)gridDim.x * (kBS / kWave);
+  int itm = 0;       // most items a cell of this wave summed
   for (int64_t q = q0; 4 * q < g.nb; q += qs) {
     const int c0 = (int)(4 * q), c1 = min(c0 + 3, g.nb - 1);
     const int c = c0 + row;
@@ -734,9 +924,9 @@ __global__ __launch_bounds__(kBS) void k_table_build(
     double mb, ma;
     const Windows w = cell_windows(SB, SA, reach_hi, reach_lo, ylo, yhi);
     const bool bb = build_mix(SB, coef64, w.lo_b, w.end_b - 1, wide_idx, Tb.n_wide_below,
-                              Tb.T_below, y0, g.h, out, mine, 0, mb, X, coop);
+                              Tb.T_below, y0, g.h, out, mine, 0, mb, X, coop, itm);
     const bool ba = build_mix(SA, coef64, w.lo_a, w.end_a - 1, wide_idx, Tb.n_wide_above,
-                              Tb.T_above, y0, g.h, out, mine, 1, ma, X, coop);
+                              Tb.T_above, y0, g.h, out, mine, 1, ma, X, coop, itm);
     if ((!coop || wid == 0) && (lane_id() & 15) == 0 && mine) {
       // dword 15: the score offset m_below - m_above, NaN marks a failed cell
       out[15] = (bb || ba) ? __int_as_float(0x7FC00000) : (float)(mb - ma);
@@ -746,6 +936,9 @@ __global__ __launch_bounds__(kBS) void k_table_build(
       if ((bb || ba) && stats) atomicAdd(stats + 1, 1ull);
     }
   }
+  // the job's worst case for the polynomial bound (mix_eps, k_table_score):
+  // one atomic per wave (itm is wave-uniform)
+  if (lane_id() == 0 && itm > 0) atomicMax(&tables[blockIdx.y].build_items, itm);
 }
 
 // ---------------------------------------------------------------------------
@@ -1057,17 +1250,23 @@ __global__ __launch_bounds__(kBS) void k_score_table(
   if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
 }
 
-// fp32 score error bound of the fast path, per candidate:
-//   |s32 - s64| <= kEpsAbs + kEpsSlope * slope + kEpsRel * |s32|
-// for a candidate scored by its cell's cubic or two-polynomial cell: each
-// mixture's polynomial 1.0e-6 (relative, so 1.0e-6 in its log), the stored
-// polynomial's fp32 evaluation at the build's check points 3e-7, the cubic's
-// fit (checked at 16 points against 1e-6 + 2^-22 |f|, taken twice) and its
-// fp32 rounding (offset 2^-24 |m_b - m_a|, three FMAs ~2^-22 (|f| + slope)),
-// and u's rounding (slope 2^-23), `slope` = tpe_table.slope.  A candidate of
-// the exact fp32 log-sum-exp fallback adds kEpsLse * (M_b + M_a + 4) (two
-// sequential fp32 sums of M terms).
-constexpr float kEpsAbs = 5.0e-6f, kEpsSlope = 4.0e-7f, kEpsRel = 1.0e-6f, kEpsLse = 1.2e-7f;
+// fp32 score error bound of the fast path.  A candidate
+// scored by its cell's cubic has
+//     |s32 - s64| <= eps_cubic + 2.0001 eps_mix + 2^-22 |s32|
+// (tpe_table: eps_cubic bounds the cubic against the stored polynomials, its
+// fp32 evaluation beyond the |s| part, u's rounding and the fp32 offset;
+// eps_mix the stored polynomial against its mixture, whose log then moves by
+// at most eps_mix / (1 - eps_mix)).  A candidate of the two-polynomial cell
+// carries its own bound (eps_2poly); one of the exact fp32 log-sum-exp
+// fallback is always re-scored in fp64 (its hi is +inf).
+constexpr float kEpsRel = 0x1.0p-22f;  // >= gamma_3 of the cubic's three fp32 FMAs
+
+// outward rounding of a round-to-nearest fp32 result x (|exact - x| <= ulp/2
+// <= 2^-24 |x|): up(x) >= exact >= dn(x) (the fma adds at least one ulp; the
+// 1e-30 covers x = 0)
+__device__ __forceinline__ float up(float x) { return fmaf(fabsf(x), 0x1.0p-23f, x) + 1e-30f; }
+__device__ __forceinline__ float dn(float x) { return fmaf(-fabsf(x), 0x1.0p-23f, x) - 1e-30f; }
+constexpr float kEtaLog2 = 0x1.0p-22f;  // v_log_f32 error, absolute or relative to |log2 p| (checked exhaustively)
 
 // order-preserving float -> uint32 code (larger float, larger code; code 0 is
 // below every float: "no value yet")
@@ -1087,6 +1286,60 @@ __device__ __forceinline__ double cand_value(float y, bool lgmm) {
   return lgmm ? exp((double)y) : (double)y;
 }
 
+// relative error bound of one mixture's two-polynomial value p (fp32 Horner
+// from the fp16 tail, horner9x2) at u against the stored polynomial at the
+// exact u: gamma_6 times the absolute polynomial, the fp16 tail's rounding
+// (u to fp16, two fp16 FMAs, subnormal spacing), and u's fp32 rounding times
+// a bound of |P'|; +inf when it is not below p
+__device__ __forceinline__ float poly_rel_err(const float (&P)[kP], float u, float p) {
+  const float au = fabsf(u);
+  float pabs = 0.0f, pd = 0.0f;
+#pragma unroll
+  for (int n = kP - 1; n >= 0; --n) {
+    pabs = fmaf(pabs, au, fabsf(P[n]));
+    if (n >= 1) pd = fmaf(pd, 1.0501f, (float)n * fabsf(P[n]));
+  }
+  const float dt = 0x1.0p-9f * 1.16f * (fabsf(P[6]) + fabsf(P[7]) + fabsf(P[8])) + 0x1.0p-23f;
+  const float dp = (6.1f * 0x1.0p-24f * pabs + 1.35f * dt + 4.5f * 0x1.0p-24f * pd) * 1.001f;
+  return dp < p ? dp / (p - dp) : INFINITY;
+}
+
+// bound of |s - s64| for a two-polynomial score s = off + (lb2 - la2) ln2,
+// beyond the polynomials' own 2.0001 eps_mix
+__device__ __forceinline__ float eps_2poly(const f4 q0, const f4 q1, const f4 q2, const f4 q3,
+                                           float u, float pb, float pa, float lb2, float la2,
+                                           float s) {
+  float Pb[kP], Pa[kP];
+  const float c[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+#pragma unroll
+  for (int n = 0; n < kP32; ++n) {
+    Pb[n] = c[2 * n];
+    Pa[n] = c[2 * n + 1];
+  }
+  const h2_t t6 = __builtin_bit_cast(h2_t, q3.x), t7 = __builtin_bit_cast(h2_t, q3.y),
+             t8 = __builtin_bit_cast(h2_t, q3.z);
+  Pb[6] = (float)t6.x; Pa[6] = (float)t6.y;
+  Pb[7] = (float)t7.x; Pa[7] = (float)t7.y;
+  Pb[8] = (float)t8.x; Pa[8] = (float)t8.y;
+  const float rb = poly_rel_err(Pb, u, pb), ra = poly_rel_err(Pa, u, pa);
+  const float off = fabsf(q3.w);
+  return (0x1.0p-24f * off + rb + ra +
+          kLn2T * kEtaLog2 * (fmaxf(1.0f, fabsf(lb2)) + fmaxf(1.0f, fabsf(la2))) +
+          0x1.0p-21f * (fabsf(s) + off + kLn2T * (fabsf(lb2) + fabsf(la2)))) * 1.001f;
+}
+
+// Band tiles: every scorer block (tile of kTile candidates) writes a header
+// {lo, hi_max, n} into band_ctl and its band entries into its own kTileSlots
+// slots -- plain stores, no atomics (one returning atomic per block on a job
+// word contended when a job's ~10^3 blocks ran together).  lo = the tile's
+// best lower bound s - eps (a lower bound of G), hi_max = its largest upper
+// bound (+inf with a NaN or log-sum-exp candidate), entries = its candidates
+// with s + eps >= lo (a superset of the band's: G >= lo); a tile with more
+// than kTileSlots such candidates writes n = kTileFull and no entries.
+constexpr int kTileSlots = 64;
+constexpr uint32_t kTileFull = 0xFFFFFFFFu;
+constexpr int kHdrWords = 4;  // per tile: lo, hi_max (float bits), n, unused
+
 // Fast path for sampled candidates (the suggest path: no per-candidate
 // log-densities asked for).  Same draws as k_score_table (draw32_pairs), same
 // cell index; the score comes from the cell's 16-B cubic (k_table_score):
@@ -1094,28 +1347,25 @@ __device__ __forceinline__ double cand_value(float y, bool lgmm) {
 // FMAs instead of two degree-8 polynomials and two logs.  Loads run four
 // candidates ahead.  Candidates on a flagged score cell (or off the grid)
 // take the two-polynomial cell, then the exact log-sum-exp, after the loop.
-// Then the band (tpe_hip.h, tpe_score_table_fast): the block's best lower
-// bound s32 - eps goes into the job's running maximum G (atomic max on its
-// order code), and every candidate of the block whose upper bound s32 + eps
-// reaches the G known at that point is appended to the job's band list for
-// the band kernels (k_band_select / k_band_expand / k_band_final).
-// out_score / out_x (nullable, tests): per-candidate fp32 score and value.
+// out_score / out_x / out_eps (nullable, tests): per-candidate fp32 score,
+// value and the bound eps the band used (+inf: always re-scored).
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k_score_table_fast(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, const float4* __restrict__ coef32,
     const tpe_table* __restrict__ tables, const float* __restrict__ cells,
-    tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
-    double* __restrict__ out_score, double* __restrict__ out_x, tpe_best* __restrict__ partial,
-    unsigned long long* __restrict__ stats, int n_tiles, int n_jobs) {
+    tpe_band* __restrict__ band, uint32_t* __restrict__ band_ctl,
+    double* __restrict__ out_score, double* __restrict__ out_x, double* __restrict__ out_eps,
+    tpe_best* __restrict__ partial, unsigned long long* __restrict__ stats, int n_tiles,
+    int n_jobs, int tile_cap) {
   __shared__ MixLds s_mix;
   // retry staging, then each lane's scores (slot r of lane l at r * 64 + l)
   __shared__ float s_stage[(kBS / kWave) * kTR * kWave];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   __shared__ BestT red[kBS / kWave];
-  __shared__ int nred[kBS / kWave];
-  __shared__ float fred[kBS / kWave];
-  __shared__ float s_g;
+  __shared__ float s_lo[kBS / kWave], s_hi[kBS / kWave];
+  __shared__ int s_cnt[kBS / kWave];
+  __shared__ int s_n;
   int job, bx;
   {  // XCD-aware work order (see k_score_table)
     const int64_t W = (int64_t)n_tiles * n_jobs, per = (W + 7) / 8;
@@ -1126,9 +1376,15 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   }
   const tpe_job J = jobs[job];
   tpe_best* P = partial + (int64_t)job * n_tiles + bx;
+  uint32_t* hdr = band_ctl + ((int64_t)job * n_tiles + bx) * kHdrWords;
   const int64_t base = (int64_t)bx * kTile;
   if (base >= J.n_cand) {
-    if (threadIdx.x == 0) *P = empty_best();
+    if (threadIdx.x == 0) {
+      *P = empty_best();
+      hdr[0] = __float_as_uint(-INFINITY);
+      hdr[1] = __float_as_uint(-INFINITY);
+      hdr[2] = 0u;
+    }
     return;
   }
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
@@ -1190,21 +1446,31 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k
     if (out_x && valid) out_x[J.out_off + t0 + r] = cand_value(y, lgmm);
   }
 #endif
+  // the lane's best cubic-scored candidate (its bounds are monotone in s)
+  const float bs_cubic = bs;
+  const float ea = (Tb.eps_cubic + 2.0001f * Tb.eps_mix) * 1.000001f;  // (covers its rounding)
+  // eps(s) = ea + 2^-22 |s| of a cubic-scored candidate; bounds s -/+ eps are
+  // rounded outwards (up / dn)
+  auto eps_of = [&](float v) __attribute__((always_inline)) -> float {
+    return fmaf(kEpsRel, fabsf(v), ea) * 1.000001f;
+  };
+  float lo_fb = -INFINITY, hi_fb = -INFINITY;  // the lane's fallback candidates' bounds
   int n_fb = 0;
   uint32_t lsem = 0;  // candidates scored by the exact fp32 log-sum-exp
   const uint32_t fbm = fb;
   if (__any(fb != 0)) {
     // fallback: the two-polynomial cell, else the exact fp32 log-sum-exp;
     // the lane's candidates wait in its own column of the wave's stage, and
-    // their scores replace them there
+    // their UPPER BOUNDS (two-polynomial) or scores (log-sum-exp) replace
+    // them there
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < kTR; ++r)
       if (fb & (1u << r)) stage[r * kWave + lane] = x[r];
     __builtin_amdgcn_wave_barrier();
     const f4* cell4 = reinterpret_cast<const f4*>(region);
-    auto fold = [&](int r, float s, float y) __attribute__((always_inline)) {
-      stage[r * kWave + lane] = s;
+    auto fold = [&](int r, float s, float y, float keep) __attribute__((always_inline)) {
+      stage[r * kWave + lane] = keep;
       if (out_score) out_score[J.out_off + t0 + r] = (double)s;
       const bool na = s != s, nbn = bs != bs;
       const bool take =
@@ -1226,13 +1492,26 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k
                q3 = cell4[4 * c + 3];
       float pb, pa;
       horner9x2(q0, q1, q2, q3, u, pb, pa);
-      if ((q3.w == q3.w) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f))
-        fold(r, q3.w + (__builtin_amdgcn_logf(pb) - __builtin_amdgcn_logf(pa)) * kLn2T, y);
-      else
-        lsem |= 1u << r;  // the exact log-sum-exp, below, the wave together
+      bool done = false;
+      if ((q3.w == q3.w) && (fabsf(u) <= kULim) && (pb > 0.0f) && (pa > 0.0f) &&
+          isfinite(pb) && isfinite(pa)) {
+        const float lb2 = __builtin_amdgcn_logf(pb), la2 = __builtin_amdgcn_logf(pa);
+        const float s = q3.w + (lb2 - la2) * kLn2T;
+        const float e2 = eps_2poly(q0, q1, q2, q3, u, pb, pa, lb2, la2, s) + 2.0001f * Tb.eps_mix;
+        if (s == s && e2 < INFINITY) {
+          const float hi = up(s + e2);
+          fold(r, s, y, hi);
+          lo_fb = fmaxf(lo_fb, dn(s - e2));
+          hi_fb = fmaxf(hi_fb, hi);
+          if (out_eps) out_eps[J.out_off + t0 + r] = (double)hi - (double)s;
+          done = true;
+        }
+      }
+      if (!done) lsem |= 1u << r;  // the exact log-sum-exp, below, the wave together
     }
     // the exact fp32 log-sum-exp over every component, one candidate at a
-    // time with the whole wave (its y still waits in the stage)
+    // time with the whole wave (its y still waits in the stage); always in
+    // the band (hi = +inf: its bound is not tracked)
     uint32_t ex = lsem;
     for (;;) {
       const uint64_t lanes = __ballot(ex != 0);
@@ -1243,120 +1522,198 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k
       const float s = lse_wave32(coef32 + SB.comp_off, SB, y) -
                       lse_wave32(coef32 + SA.comp_off, SA, y);
       if (lane == L) {
-        fold(r, s, y);
+        fold(r, s, y, INFINITY);
+        hi_fb = INFINITY;
+        if (out_eps) out_eps[J.out_off + t0 + r] = INFINITY;
         ex &= ex - 1;
       }
     }
   }
-  BestT run{0.0, -1, 0.0};
-  if (br >= 0) run = BestT{(double)bs, J.cand_base + t0 + br, cand_value(by, lgmm)};
-  const BestT best = block_best<kBS>(run, red);
-  if (stats) {
-    const int ne = block_sum<kBS, int>(n_fb, nred);
-    if (threadIdx.x == 0 && ne) atomicAdd(stats, (unsigned long long)ne);
+  // the lane's best lower bound and largest upper bound
+  float lo_t = lo_fb, hi_t = hi_fb;
+  if (bs_cubic > -INFINITY) {
+    const float e = eps_of(bs_cubic);
+    lo_t = fmaxf(lo_t, dn(bs_cubic - e));
+    hi_t = fmaxf(hi_t, up(bs_cubic + e));
   }
-  if (threadIdx.x == 0) *P = tpe_best{best.score, best.index, best.value, 0};
-
-  // ---- the band: candidates that can still be the exact winner --------------
+  // one LDS round: the tile's fp32 winner, lo and hi_max (and the fallback count)
+  const int wid = threadIdx.x / kWave;
+  {
+    BestT run{0.0, -1, 0.0};
+    if (br >= 0) run = BestT{(double)bs, J.cand_base + t0 + br, cand_value(by, lgmm)};
+    run = wave_best(run);
+    const float a = wave_max_f(lo_t), b = wave_max_f(hi_t);
+    int nf = n_fb;
+    if (stats) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) nf += __shfl_xor(nf, o, kWave);
+    }
+    if (lane == 0) {
+      red[wid] = run;
+      s_lo[wid] = a;
+      s_hi[wid] = b;
+      s_cnt[wid] = nf;
+    }
+    if (threadIdx.x == 0) s_n = 0;
+  }
+  __syncthreads();
+  float lo_blk = s_lo[0], hi_blk = s_hi[0];
+  if (threadIdx.x == 0) {
+    BestT r = red[0];
+    int ne = s_cnt[0];
+#pragma unroll
+    for (int w = 1; w < kBS / kWave; ++w) {
+      if (better(red[w].score, red[w].index, r.score, r.index)) r = red[w];
+      ne += s_cnt[w];
+    }
+    *P = tpe_best{r.score, r.index, r.value, 0};
+    if (stats && ne) atomicAdd(stats, (unsigned long long)ne);
+  }
+#pragma unroll
+  for (int w = 1; w < kBS / kWave; ++w) {
+    lo_blk = fmaxf(lo_blk, s_lo[w]);
+    hi_blk = fmaxf(hi_blk, s_hi[w]);
+  }
+  if (out_eps) {  // (test hook) the bound of every cubic-scored candidate
+#pragma unroll
+    for (int r = 0; r < kTR; ++r)
+      if (r < nvalid && !((fbm >> r) & 1u)) {
+        const float v = stage[r * kWave + lane];
+        out_eps[J.out_off + t0 + r] = (double)up(v + eps_of(v)) - (double)v;
+      }
+  }
 #ifdef TPE_DIAG_NO_BAND  // diagnostic builds only: the fp32 winner alone
   return;
 #endif
-  const float ea = kEpsAbs + kEpsSlope * Tb.slope;
-  const float el = ea + kEpsLse * (float)(SB.n_obs + SA.n_obs + 4);
-  auto eps = [&](int r, float s) __attribute__((always_inline)) -> float {
-    return (((lsem >> r) & 1u) ? el : ea) + kEpsRel * fabsf(s);
-  };
-  // the thread's best candidate's lower bound (a lower bound of G); NaN: none
-  const float lo_t = (br >= 0 && bs == bs) ? bs - eps(br, bs) : -INFINITY;
-  const float blo = block_max<kBS, float>(lo_t, fred);
-  uint32_t* ctl = band_ctl + 4 * (int64_t)job;
-  if (threadIdx.x == 0) {
-    const uint32_t old = atomicMax(ctl, blo > -INFINITY ? ord_enc(blo) : 0u);
-    s_g = fmaxf(blo, ord_dec(old));
-  }
-  __syncthreads();
-  const float G = s_g;
-  // upper bound of the thread's candidates scored on the table (monotone in s);
-  // NaN scores and fallback candidates are checked one by one
-  const float hi_t = br >= 0 ? bs + ea + kEpsRel * fabsf(bs) : -INFINITY;
-  if (fbm != 0u || !(hi_t < G)) {
-    uint32_t em = 0;  // this lane's candidates in the band
+  // ---- the band tile: its candidates with hi >= lo_blk (NaN hi included);
+  // only a lane whose largest upper bound reaches lo_blk holds any
+  uint32_t em = 0;
+  if (!(hi_t < lo_blk)) {
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
       if (r < nvalid) {
-        const float s = stage[r * kWave + lane];
-        const float hi = s + eps(r, s);
+        const float v = stage[r * kWave + lane];
+        const float hi = ((lsem >> r) & 1u) ? INFINITY
+                         : ((fbm >> r) & 1u) ? v : up(v + eps_of(v));
         stage[r * kWave + lane] = hi;
-        if (!(hi < G)) em |= 1u << r;  // (NaN scores go on)
+        if (!(hi < lo_blk)) em |= 1u << r;
       }
     }
-    if (em) {
-      // one slot reservation per lane, not per entry: a label's band can be a
-      // few thousand entries, and an atomic per entry serialises them
-      int64_t p = atomicAdd(ctl + 1, (uint32_t)__popc(em));
-      tpe_band* B = band + (int64_t)job * band_cap;
+  }
+  const int cnt = __popc(em);
+  const int pos0 = cnt ? atomicAdd(&s_n, cnt) : 0;  // (LDS; the entries' order is free)
+  __syncthreads();
+  const int total = s_n;
+  if (total <= tile_cap && em) {
+    tpe_band* B = band + ((int64_t)job * n_tiles + bx) * kTileSlots;
+    int pos = pos0;
 #pragma unroll
-      for (int r = 0; r < kTR; ++r) {
-        if ((em >> r) & 1u) {
-          if (p < band_cap) B[p] = tpe_band{J.cand_base + t0 + r, x[r], stage[r * kWave + lane]};
-          ++p;
-        }
+    for (int r = 0; r < kTR; ++r) {
+      if ((em >> r) & 1u) {
+        // (its value drawn again -- draw32 gives candidate g exactly what
+        // draw32_pairs gave it -- so x[] need not live through the tail)
+        const float yv = draw32(M, J.key, J.cand_base + t0 + r, lo_on, hi_on, (float)J.low,
+                                (float)J.high);
+        B[pos] = tpe_band{J.cand_base + t0 + r, yv, stage[r * kWave + lane]};
+        ++pos;
       }
     }
+  }
+  if (threadIdx.x == 0) {
+    hdr[0] = __float_as_uint(lo_blk);
+    hdr[1] = __float_as_uint(hi_blk == hi_blk ? hi_blk : INFINITY);
+    hdr[2] = total <= tile_cap ? (uint32_t)total : kTileFull;
   }
 }
 
 // ---------------------------------------------------------------------------
-// exact re-score of the band: select (block per job), expand (block per
-// cell and mixture), final (block per job)
+// exact re-score of the band: one kernel (k_band), kBandBlocks blocks per job
 // ---------------------------------------------------------------------------
-// A band candidate y is scored in fp64 through the table cell c that holds it
-// (the fp32 cell index, a function of y alone): both mixtures are expanded
-// around the cell centre y0 as e^m sum_{n<=kBandD} P_n u^n, u = (y - y0)/h,
-// over every component whose largest term on the cell reaches e^-45 / M of
-// the prior component's smallest one there (a lower bound of the sum): the
-// rest add < e^-45 of it.  A component's series exp(A u + B u^2) converges
-// like rho^n / n!, rho = 1.05|A| + 1.1025|B|; with rho <= kBandRho the tail
-// past degree 24 is < 1e-20 of its term, and components with a larger rho (far
-// out relative to their bandwidth) are summed term by term instead.  Rounding
-// of the P_n sums is ~1e-14 relative: the fp64 accuracy of a direct sum over
-// 10^4 terms.  Survivors off the grid, of a cell past the kBandCells listed,
-// or of a cell with more slow components than fit the list, take the direct
-// online log-sum-exp over every component (k_score64's arithmetic).  Every
-// survivor's score depends on its y alone, so the winner does not depend on
-// how candidates are sharded over ranks.
+// Every survivor's two log-densities are summed in fp64 over EVERY component
+// (within e^-45 of the sum) -- GMM1_lpdf / LGMM1_lpdf's sums (tpe.py:117-180,
+// 265-307; LGMM1's -log x cancels in the score) -- and its score is a
+// function of its y alone, whatever the sharding of the candidates, within
+// fp64 rounding of the reference's.  Two ways, per job:
+//  * few survivors (<= kBandSurv; a peaked score): directly -- the components
+//    split into kBandBlocks chunks, one block each, every survivor's partial
+//    log-sum-exp per chunk (per thread an online sum in a fixed order, then a
+//    fixed reduction tree), the chunks combined in order by the job's last
+//    block;
+//  * many (a flat score: thousands within the band, in a few cells): per
+//    table cell holding survivors, both mixtures expanded around the cell
+//    centre to degree kBandD (band_expand; components whose series would
+//    converge slowly summed term by term), the cells dealt to the job's
+//    blocks; survivors off the grid or past the kBandCells listed take the
+//    direct sum (band_direct).
+// Steps of every block:
+//  1. G = max over the job's tiles of their lo; a tile whose entries did not
+//     fit (kTileFull) with hi_max >= G makes the job "overflowed": block 0
+//     gives the fp32 winner with n_scored = -1 (the caller re-scores the job
+//     exactly).
+//  2. The survivors -- entries with hi >= G of the tiles with hi_max >= G, in
+//     flat entry order, the same in every block.  The exact winner i* is
+//     among them: lo_k <= s64_k <= s64_i* <= hi_i* for every k, so hi_i* >=
+//     G, and i* is in its tile's entries (hi_i* >= G >= that tile's lo);
+//     every other candidate has s64 <= hi < G <= s64_i*.
+//  3. The block's share of the sums (above).
+//  4. The last block of the job to finish takes np.argmax over the
+//     survivors (largest score, then smallest index, NaN first): best[j] =
+//     {fp64 score, index, value, n_cand}, and re-arms the counter.
+constexpr int kBandBlocks = 16;      // blocks per job
+constexpr int kBandSurv = 128;       // survivors scored directly (more: the cell expansions)
+constexpr int kSurvBatch = 4;        // survivors summed together per pass
+constexpr int kBX = 256;             // band block
+constexpr int kBandTiles = 4096;     // tiles of a job the kernel's LDS prefix holds (2^24 candidates;
+                                     // a larger job takes the exact fallback)
+constexpr int kTilesPT = kBandTiles / kBX;  // tile headers per thread (prefix pass)
 constexpr int kBandD = 24;           // expansion degree
-constexpr int kBandDirect = 128;     // slow components summed term by term, per mixture
 constexpr double kBandTau = 45.0;    // exclusion margin (nats) on top of log(M)
 constexpr double kBandRho = 1.5;     // admissible 1.05 |A| + 1.1025 |B|
 constexpr int kBandCells = 64;       // cells expanded per job (sorted; the rest: direct)
-constexpr int kBandBits = 32768;     // cell bitmap of the select kernel (LDS)
-constexpr int kBandSlots = 16;       // expand blocks per job and mixture (grid-stride over cells)
-constexpr int kBandFinal = 16;       // final blocks per job (grid-stride over survivors)
-constexpr int kSelPT = 16;           // entries per thread and pass of the select kernel
+constexpr int kBandBits = 32768;     // cell bitmap (LDS)
 
-struct BandMix {  // one mixture's expansion on one cell
+constexpr int kChunkDir = 16;        // slow components listed per (cell, chunk, mixture)
+struct BandMix {  // one mixture's expansion on one cell (or one chunk of its components)
   double P[kBandD + 1];
   double m;
-  int n_dir;  // -1: too many slow components (the cell's survivors take the direct sum)
+  int n_dir;  // slow components listed; -1: more than fit (the job takes the exact fallback)
   int pad;
-  int dir[kBandDirect];
+  int dir[kChunkDir];
 };
-struct BandWork {  // per job (tpe_band_work_bytes)
-  int cell[kBandCells];
-  BandMix mix[kBandCells][2];
-  BestT part[kBandFinal];  // the final blocks' winners
-  unsigned int done;       // final blocks finished (the last one reduces)
+struct BandWork {  // per job (tpe_band_bytes)
+  double part[kBandBlocks][kBandSurv][4];         // direct: per chunk and survivor {m, s} b, a
+  BandMix cpart[kBandCells][kBandBlocks][2];      // cells: per cell, chunk and mixture
+  BestT win[kBandCells];                          // cells: each cell's survivors' winner
+  unsigned int cell_done[kBandCells];             // chunks finished per cell
+  unsigned int cells_done;                        // cells finished (the last one reduces)
+  unsigned int done;                              // direct: blocks finished
+  unsigned int pad[2];
 };
+
+// (m, s): e^m s; combined in a fixed order
+__device__ __forceinline__ void lse_merge(double& m, double& s, double m2, double s2) {
+  if (m2 == -INFINITY) return;
+  if (m2 > m) {
+    s = s * exp(m - m2) + s2;
+    m = m2;
+  } else {
+    s += s2 * exp(m2 - m);
+  }
+}
 
 // expansion of mixture S on the cell (y0, h) into E (LDS); all threads.
 // One pass over the components, U loads in flight per thread; each thread
 // keeps its own scale (raised when a term would exceed e^8 of it) and the
-// threads are merged at the end (fixed order: deterministic).
+// threads are merged at the end (fixed order: deterministic).  A component's
+// series exp(A u + B u^2) converges like rho^n / n!, rho = 1.05|A| +
+// 1.1025|B|: with rho <= kBandRho the tail past degree 24 is < 1e-20 of its
+// term; components with a larger rho are summed term by term (band_eval).
+// Components whose largest term on the cell is below e^-45 / M of the prior
+// component's smallest one there are left out (< e^-45 of the sum).
 template <int BX, int U>
 __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64, double y0,
-                            double h, BandMix& E, double* dred) {
-  const int nc = S.n_obs + 1;
+                            double h, BandMix& E, double* dred, int k_begin, int k_end) {
+  const int nc = S.n_obs + 1;  // (the floor is the whole mixture's)
   const int64_t off = S.comp_off;
   const double4 cp = ld4(coef64, off + S.prior_pos);
   const double far = (fabs(y0 - cp.x) + 1.05 * h) * cp.y;
@@ -1367,12 +1724,12 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
 #pragma unroll
   for (int n = 0; n <= kBandD; ++n) P[n] = 0.0;
   double ml = -INFINITY;
-  for (int k0 = 0; k0 < nc; k0 += U * BX) {
+  for (int k0 = k_begin; k0 < k_end; k0 += U * BX) {
     double4 cs[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = k0 + u * BX + (int)threadIdx.x;
-      cs[u] = k < nc ? ld4(coef64, off + k) : make_double4(0.0, 0.0, -INFINITY, 0.0);
+      cs[u] = k < k_end ? ld4(coef64, off + k) : make_double4(0.0, 0.0, -INFINITY, 0.0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1383,7 +1740,7 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
       const double A = -(y0 - c.x) * hi2, B = -0.5 * h * hi2;
       if (1.05 * fabs(A) + 1.1025 * fabs(B) > kBandRho) {
         const int p = atomicAdd(&E.n_dir, 1);
-        if (p < kBandDirect) E.dir[p] = k0 + u * BX + (int)threadIdx.x;
+        if (p < kChunkDir) E.dir[p] = k0 + u * BX + (int)threadIdx.x;
         continue;
       }
       const double z0 = (y0 - c.x) * c.y;
@@ -1433,20 +1790,20 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
   }
   if (threadIdx.x == 0) {
     E.m = m;
-    if (E.n_dir > kBandDirect) E.n_dir = -1;
+    if (E.n_dir > kChunkDir) E.n_dir = -1;
   }
   __syncthreads();
 }
 
 // log of the mixture at y from its cell expansion (u = (y - y0) / h)
-__device__ __forceinline__ double band_eval(const BandMix& E, const double* __restrict__ coef64,
-                                            int64_t off, double u, double y) {
+__device__ __forceinline__ double band_eval(const BandMix& E, const int* dir, int nd,
+                                            const double* __restrict__ coef64, int64_t off,
+                                            double u, double y) {
   double p = E.P[kBandD];
 #pragma unroll
   for (int n = kBandD - 1; n >= 0; --n) p = fma(p, u, E.P[n]);
-  const int nd = E.n_dir;
   for (int i = 0; i < nd; ++i) {
-    const double4 c = ld4(coef64, off + E.dir[i]);
+    const double4 c = ld4(coef64, off + dir[i]);
     const double t = (y - c.x) * c.y;
     p += exp(c.z - 0.5 * t * t - E.m);
   }
@@ -1481,227 +1838,378 @@ __device__ __forceinline__ int band_cell(const tpe_table& Tb, float y) {
   return (fabs(u) <= (double)kULim && y == y) ? c : -2;
 }
 
-// band_ctl words per job: [0] G (order code), [1] entries, [2] survivors
-// (kBandOverflow: the band overflowed), [3] listed cells
-constexpr uint32_t kBandOverflow = 0xFFFFFFFFu;
-
-// Select (block per job): keep the entries with hi >= the final G, compacted
-// in place, and list their distinct cells (ascending, at most kBandCells) in
-// the job's BandWork.  kSelPT entries per thread per pass, loaded together
-// (C3's bands are a few thousand entries: one pass).  A job whose band
-// overflowed gets the fp32 winner with n_scored = -1.
-__global__ __launch_bounds__(kBS) void k_band_select(
-    const tpe_job* __restrict__ jobs, const tpe_table* __restrict__ tables,
-    tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
-    const tpe_best* __restrict__ partial, int64_t nper, tpe_best* __restrict__ best,
+__global__ __launch_bounds__(kBX) void k_band(
+    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
+    const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
+    const tpe_band* __restrict__ band, const uint32_t* __restrict__ band_ctl,
+    const tpe_best* __restrict__ partial, int n_tiles, tpe_best* __restrict__ best,
     BandWork* __restrict__ work) {
-  constexpr int kNW = kBS / kWave;
+  constexpr int kNW = kBX / kWave;
   __shared__ BestT red[kNW];
-  __shared__ int s_cnt[kSelPT * kNW], s_scan[kNW];
+  __shared__ int s_end[kBandTiles];  // inclusive prefix of the tiles' counted entries
   __shared__ uint32_t s_bits[kBandBits / 32];
-  const int j = blockIdx.x;
-  uint32_t* ctl = band_ctl + 4 * (int64_t)j;
-  const float G = ord_dec(ctl[0]);
-  const int64_t n = (int64_t)ctl[1];
-  __syncthreads();  // every thread has read the controls
-  if (threadIdx.x == 0) {
-    ctl[0] = 0u;  // ready for the next scorer call
-    ctl[1] = 0u;
-    work[j].done = 0u;
-  }
-  if (n > band_cap) {
-    // the fp32 winner; the caller re-scores the job exactly
-    BestT b32{0.0, -1, 0.0};
-    for (int64_t i = threadIdx.x; i < nper; i += kBS) {
-      const tpe_best p = partial[(int64_t)j * nper + i];
-      best_update(b32, p.score, p.index, p.value);
+  __shared__ int s_cell[kBandCells];
+  __shared__ float s_y[kBandSurv];
+  __shared__ int64_t s_idx[kBandSurv];
+  __shared__ int s_wt[kNW];
+  __shared__ float s_g[kNW];
+  __shared__ double s_red[kNW][kSurvBatch][2];
+  __shared__ double dred[kNW * (kBandD + 1)];
+  __shared__ BandMix s_eb, s_ea;
+  __shared__ int s_dirb[kBandBlocks * kChunkDir], s_dira[kBandBlocks * kChunkDir];
+  __shared__ int s_over, s_off;
+  __shared__ bool s_last, s_lastc;
+  const int j = blockIdx.y, kb = blockIdx.x;
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+  const tpe_job J = jobs[j];
+  const uint32_t* H = band_ctl + (int64_t)j * n_tiles * kHdrWords;
+  const tpe_band* Bj = band + (int64_t)j * n_tiles * kTileSlots;
+  // exclusive block scan of one int per thread (wave scan + wave totals)
+  auto block_excl = [&](int v, int& total) -> int {
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int w = __shfl_up(incl, o, kWave);
+      if (lane >= o) incl += w;
     }
-    b32 = block_best<kBS>(b32, red);
-    if (threadIdx.x == 0) {
-      best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
-      ctl[2] = kBandOverflow;
-      ctl[3] = 0u;
+    __syncthreads();
+    if (lane == kWave - 1) s_wt[wid] = incl;
+    __syncthreads();
+    int pos = incl - v;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) {
+      pos += w < wid ? s_wt[w] : 0;
+      total += s_wt[w];
+    }
+    return pos;
+  };
+  // ---- 1. G, overflow, the tiles' counts ----
+  float g = -INFINITY;
+  for (int t = threadIdx.x; t < n_tiles; t += kBX) g = fmaxf(g, __uint_as_float(H[t * kHdrWords]));
+  g = wave_max_f(g);
+  if (lane == 0) s_g[wid] = g;
+  if (threadIdx.x == 0) s_over = n_tiles > kBandTiles;
+  for (int w = threadIdx.x; w < kBandBits / 32; w += kBX) s_bits[w] = 0u;
+  __syncthreads();
+  float G = s_g[0];
+#pragma unroll
+  for (int w = 1; w < kNW; ++w) G = fmaxf(G, s_g[w]);
+  // the relevant tiles' counts in LDS, then their inclusive prefix in place
+  for (int t = threadIdx.x; t < kBandTiles; t += kBX) {
+    int c = 0;
+    if (t < n_tiles) {
+      const float hm = __uint_as_float(H[t * kHdrWords + 1]);
+      const uint32_t n = H[t * kHdrWords + 2];
+      if (!(hm < G) && n != 0u) {
+        if (n == kTileFull) s_over = 1;
+        else c = (int)n;
+      }
+    }
+    s_end[t] = c;
+  }
+  __syncthreads();
+  int tot = 0;
+  for (int i = 0; i < kTilesPT; ++i) tot += s_end[threadIdx.x * kTilesPT + i];
+  int n_ent = 0;
+  int run = block_excl(tot, n_ent);
+  for (int i = 0; i < kTilesPT; ++i) {
+    run += s_end[threadIdx.x * kTilesPT + i];
+    s_end[threadIdx.x * kTilesPT + i] = run;
+  }
+  __syncthreads();
+  if (s_over) {  // the fp32 winner; the caller re-scores the job exactly
+    if (kb == 0) {
+      BestT b32{0.0, -1, 0.0};
+      for (int i = threadIdx.x; i < n_tiles; i += kBX) {
+        const tpe_best p = partial[(int64_t)j * n_tiles + i];
+        best_update(b32, p.score, p.index, p.value);
+      }
+      b32 = block_best<kBX>(b32, red);
+      if (threadIdx.x == 0) best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
+    }
+    return;  // (every block: the counter is untouched)
+  }
+  const int nt = min(n_tiles, kBandTiles);
+  const tpe_table Tb = tables[j];
+  // every entry once, kEPT consecutive ones per thread loaded together;
+  // fn(entry, flat position) for the survivors, every thread taking part
+  constexpr int kEPT = 4;
+  auto for_survivors = [&](auto&& fn) {
+    for (int f0 = 0; f0 < n_ent; f0 += kEPT * kBX) {
+      tpe_band E[kEPT];
+#pragma unroll
+      for (int u = 0; u < kEPT; ++u) {
+        const int f = f0 + threadIdx.x * kEPT + u;
+        E[u].hi = -INFINITY;
+        if (f < n_ent) {
+          int lo = 0, hi = nt - 1;  // the first tile whose inclusive end passes f
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_end[mid] > f) hi = mid; else lo = mid + 1;
+          }
+          const int e = f - (s_end[lo] - (int)H[lo * kHdrWords + 2]);
+          E[u] = Bj[(int64_t)lo * kTileSlots + e];
+        }
+      }
+      uint32_t keep = 0;
+#pragma unroll
+      for (int u = 0; u < kEPT; ++u)
+        if (f0 + threadIdx.x * kEPT + u < n_ent && !(E[u].hi < G)) keep |= 1u << u;
+      fn(E, keep);
+    }
+  };
+  // ---- 2. the survivors: their number, their cells; the first kBandSurv in
+  // flat order listed ----
+  int ns = 0;
+  if (threadIdx.x == 0) s_off = 0;
+  for_survivors([&](const tpe_band (&E)[kEPT], uint32_t keep) {
+    int total = 0;
+    int pos = ns + block_excl(__popc(keep), total);
+#pragma unroll
+    for (int u = 0; u < kEPT; ++u) {
+      if ((keep >> u) & 1u) {
+        if (pos < kBandSurv) {
+          s_y[pos] = E[u].y;
+          s_idx[pos] = E[u].index;
+        }
+        ++pos;
+        const int c = band_cell(Tb, E[u].y);
+        if (c >= 0 && c < kBandBits) atomicOr(&s_bits[c >> 5], 1u << (c & 31));
+        else s_off = 1;
+      }
+    }
+    ns += total;
+  });
+  __syncthreads();
+  // the listed cells (ascending)
+  constexpr int kPer = kBandBits / 32 / kBX;  // bitmap words per thread
+  int ncell = 0;
+  {
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) c += __popc(s_bits[threadIdx.x * kPer + i]);
+    int pos = block_excl(c, ncell);
+    for (int i = 0; i < kPer && pos < kBandCells; ++i) {
+      uint32_t b = s_bits[threadIdx.x * kPer + i];
+      while (b && pos < kBandCells) {
+        s_cell[pos++] = (threadIdx.x * kPer + i) * 32 + __builtin_ctz(b);
+        b &= b - 1;
+      }
+    }
+  }
+  __syncthreads();
+  BandWork& W = work[j];
+  const bool lgmm = J.family == TPE_LGMM1;
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  if (ns > kBandSurv && (ncell > kBandCells || s_off)) {
+    // many survivors, off the grid or over too many cells: the exact fallback
+    if (kb == 0) {
+      BestT b32{0.0, -1, 0.0};
+      for (int i = threadIdx.x; i < n_tiles; i += kBX) {
+        const tpe_best p = partial[(int64_t)j * n_tiles + i];
+        best_update(b32, p.score, p.index, p.value);
+      }
+      b32 = block_best<kBX>(b32, red);
+      if (threadIdx.x == 0) best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
     }
     return;
   }
-  const tpe_table Tb = tables[j];
-  for (int w = threadIdx.x; w < kBandBits / 32; w += kBS) s_bits[w] = 0u;
-  tpe_band* B = band + (int64_t)j * band_cap;
-  const int lane = lane_id(), wid = threadIdx.x / kWave;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  int64_t kept = 0;
-  for (int64_t e0 = 0; e0 < n; e0 += (int64_t)kSelPT * kBS) {
-    tpe_band E[kSelPT];
-    bool keep[kSelPT];
+  if (ns <= kBandSurv) {
+    // ---- 3a. direct: this block's component chunk, for every survivor ----
+    for (int mix = 0; mix < 2; ++mix) {
+      const tpe_seg& S = mix ? SA : SB;
+      const int nc = S.n_obs + 1;
+      const int per = (nc + kBandBlocks - 1) / kBandBlocks;
+      const int k0 = kb * per, k1 = min(nc, k0 + per);
+      const double4* C = reinterpret_cast<const double4*>(coef64) + S.comp_off;
+      for (int b0 = 0; b0 < ns; b0 += kSurvBatch) {
+        double m[kSurvBatch], sm[kSurvBatch], y[kSurvBatch];
 #pragma unroll
-    for (int t = 0; t < kSelPT; ++t) {
-      const int64_t e = e0 + (int64_t)t * kBS + threadIdx.x;
-      keep[t] = false;
-      if (e < n) E[t] = B[e];
-    }
-    int before[kSelPT];
-#pragma unroll
-    for (int t = 0; t < kSelPT; ++t) {
-      const int64_t e = e0 + (int64_t)t * kBS + threadIdx.x;
-      keep[t] = e < n && !(E[t].hi < G);  // (NaN bounds stay)
-      const uint64_t bal = __ballot(keep[t]);
-      before[t] = __popcll(bal & lt);
-      if (lane == 0) s_cnt[t * kNW + wid] = __popcll(bal);
-    }
-    __syncthreads();  // (every entry of the pass is read before any is written)
-    // exclusive scan of the kSelPT * kNW counts (slot order = entry order)
-    if (threadIdx.x < kWave) {
-      const int c = s_cnt[threadIdx.x];
-      int incl = c;
-#pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) {
-        const int v = __shfl_up(incl, o, kWave);
-        if (lane >= o) incl += v;
-      }
-      s_cnt[threadIdx.x] = incl - c;
-      if (threadIdx.x == kWave - 1) s_scan[0] = incl;
-    }
-    static_assert(kSelPT * kNW == kWave, "one wave scans the pass's slot counts");
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < kSelPT; ++t) {
-      if (!keep[t]) continue;
-      B[kept + s_cnt[t * kNW + wid] + before[t]] = E[t];
-      const int c = band_cell(Tb, E[t].y);
-      if (c >= 0 && c < kBandBits) atomicOr(&s_bits[c >> 5], 1u << (c & 31));
-    }
-    kept += s_scan[0];
-    __syncthreads();  // s_cnt / s_scan reused
-  }
-  __syncthreads();  // (the bitmap is complete; also when n == 0)
-  // the listed cells: bitmap words in order, kBandBits / 32 / kBS per thread
-  constexpr int kPer = kBandBits / 32 / kBS;
-  int cnt = 0;
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) cnt += __popc(s_bits[threadIdx.x * kPer + i]);
-  int pos = block_scan_sum(cnt, s_scan) - cnt;  // exclusive prefix
-  int total = 0;  // (s_scan holds the wave totals)
-  for (int w = 0; w < kNW; ++w) total += s_scan[w];
-  for (int i = 0; i < kPer && pos < kBandCells; ++i) {
-    uint32_t b = s_bits[threadIdx.x * kPer + i];
-    while (b && pos < kBandCells) {
-      work[j].cell[pos++] = (threadIdx.x * kPer + i) * 32 + __builtin_ctz(b);
-      b &= b - 1;
-    }
-  }
-  if (threadIdx.x == 0) {
-    ctl[2] = (uint32_t)kept;
-    ctl[3] = (uint32_t)min(total, kBandCells);
-  }
-}
-
-// Expand: block (slot, job, mixture) expands its mixture on listed cells
-// slot, slot + kBandSlots, ... into the job's BandWork.
-constexpr int kBX = 512;  // expansion block: ~20 components per thread at 10^4
-__global__ __launch_bounds__(kBX) void k_band_expand(
-    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
-    const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
-    const uint32_t* __restrict__ band_ctl, BandWork* __restrict__ work) {
-  __shared__ double dred[(kBX / kWave) * (kBandD + 1)];
-  __shared__ BandMix s_e;
-  const int j = blockIdx.y;
-  const uint32_t ns = band_ctl[4 * (int64_t)j + 2];
-  const int nc = (int)band_ctl[4 * (int64_t)j + 3];
-  if (ns == kBandOverflow || ns == 0u || (int)blockIdx.x >= nc) return;
-  const tpe_job J = jobs[j];
-  const tpe_seg S = segs[blockIdx.z ? J.above : J.below];
-  const tpe_table Tb = tables[j];
-  const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
-  for (int k = blockIdx.x; k < nc; k += kBandSlots) {
-    const int c = work[j].cell[k];
-    band_expand<kBX, 4>(S, coef64, (double)cell_centre(g0, h32, c), Tb.h, s_e, dred);
-    BandMix& G = work[j].mix[k][blockIdx.z];
-    if (threadIdx.x <= kBandD) G.P[threadIdx.x] = s_e.P[threadIdx.x];
-    const int nd = s_e.n_dir;
-    if (threadIdx.x == 0) {
-      G.m = s_e.m;
-      G.n_dir = nd;
-    }
-    for (int i = threadIdx.x; i < nd; i += kBX) G.dir[i] = s_e.dir[i];
-    __syncthreads();  // s_e reused
-  }
-}
-
-// Final: block (slot, job) scores survivors slot * kBS + t, stride kBandFinal
-// * kBS, in fp64 (its cell's expansions, else the direct sum); the last
-// block of the job to finish takes np.argmax over the blocks' winners ->
-// best[j] and leaves the controls zero.
-__global__ __launch_bounds__(kBS) void k_band_final(
-    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
-    const double* __restrict__ coef64, const tpe_table* __restrict__ tables,
-    const tpe_band* __restrict__ band, int64_t band_cap, uint32_t* __restrict__ band_ctl,
-    tpe_best* __restrict__ best, BandWork* __restrict__ work) {
-  __shared__ BestT red[kBS / kWave];
-  __shared__ int s_cell[kBandCells];
-  __shared__ bool s_last;
-  const int j = blockIdx.y;
-  uint32_t* ctl = band_ctl + 4 * (int64_t)j;
-  const uint32_t ns = ctl[2];
-  const int nc = (int)ctl[3];
-  for (int k = threadIdx.x; k < nc; k += kBS) s_cell[k] = work[j].cell[k];
-  __syncthreads();
-  const tpe_job J = jobs[j];
-  BestT bx{0.0, -1, 0.0};
-  if (ns != kBandOverflow) {
-    const tpe_seg SB = segs[J.below], SA = segs[J.above];
-    const tpe_table Tb = tables[j];
-    const bool lgmm = J.family == TPE_LGMM1;
-    const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
-    const tpe_band* B = band + (int64_t)j * band_cap;
-    for (int64_t p = (int64_t)blockIdx.x * kBS + threadIdx.x; p < (int64_t)ns;
-         p += (int64_t)kBandFinal * kBS) {
-      const tpe_band E = B[p];
-      const double y = (double)E.y;
-      const int c = band_cell(Tb, E.y);
-      int k = -1;
-      if (c >= 0) {  // binary search of the listed cells
-        int lo = 0, hi = nc;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (s_cell[mid] < c) lo = mid + 1; else hi = mid;
+        for (int i = 0; i < kSurvBatch; ++i) {
+          m[i] = -INFINITY;
+          sm[i] = 0.0;
+          y[i] = (double)s_y[min(b0 + i, ns - 1)];
         }
-        k = (lo < nc && s_cell[lo] == c) ? lo : -1;
+        for (int k = k0 + (int)threadIdx.x; k < k1; k += kBX) {
+          const double4 c = C[k];
+#pragma unroll
+          for (int i = 0; i < kSurvBatch; ++i) {
+            const double t = (y[i] - c.x) * c.y;
+            const double v = -0.5 * (t * t) + c.z;  // (log coefficient c.z: GMM1_lpdf's terms)
+            const bool upv = v > m[i];
+            const double e = exp(upv ? m[i] - v : v - m[i]);
+            sm[i] = upv ? sm[i] * e + 1.0 : sm[i] + e;
+            m[i] = upv ? v : m[i];
+          }
+        }
+        // fixed reduction tree: the wave (both partners combine the lower
+        // lane's pair first), then the block's waves in order
+#pragma unroll
+        for (int i = 0; i < kSurvBatch; ++i) {
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) {
+            const double m2 = __shfl_xor(m[i], o, kWave), s2 = __shfl_xor(sm[i], o, kWave);
+            double ma = m[i], sa = sm[i], mb = m2, sb = s2;
+            if (lane & o) {
+              ma = m2;
+              sa = s2;
+              mb = m[i];
+              sb = sm[i];
+            }
+            lse_merge(ma, sa, mb, sb);
+            m[i] = ma;
+            sm[i] = sa;
+          }
+          if (lane == 0) {
+            s_red[wid][i][0] = m[i];
+            s_red[wid][i][1] = sm[i];
+          }
+        }
+        __syncthreads();
+        if (threadIdx.x < kSurvBatch && b0 + (int)threadIdx.x < ns) {
+          const int i = threadIdx.x;
+          double mm = s_red[0][i][0], ss = s_red[0][i][1];
+          for (int w = 1; w < kNW; ++w) lse_merge(mm, ss, s_red[w][i][0], s_red[w][i][1]);
+          W.part[kb][b0 + i][2 * mix] = mm;
+          W.part[kb][b0 + i][2 * mix + 1] = ss;
+        }
+        __syncthreads();  // (s_red reused)
       }
-      double lb, la;
-      if (k >= 0 && work[j].mix[k][0].n_dir >= 0 && work[j].mix[k][1].n_dir >= 0) {
-        const double u = (y - (double)cell_centre(g0, h32, c)) / Tb.h;
-        lb = band_eval(work[j].mix[k][0], coef64, SB.comp_off, u, y);
-        la = band_eval(work[j].mix[k][1], coef64, SA.comp_off, u, y);
-      } else {
-        lb = band_direct(SB, coef64, y);
-        la = band_direct(SA, coef64, y);
-      }
-      best_update(bx, lb - la, E.index, cand_value(E.y, lgmm));
     }
+  } else {
+    // ---- 3b. cells: this block expands chunk kb of every listed cell's
+    // components (both mixtures); the last chunk of a cell to finish merges
+    // the chunks and scores the cell's survivors; the last cell reduces ----
+    const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
+    auto listed = [&](int c) -> int {  // listed position of cell c, -1 if none
+      if (c < 0) return -1;
+      int lo = 0, hi = ncell;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_cell[mid] < c) lo = mid + 1; else hi = mid;
+      }
+      return (lo < ncell && s_cell[lo] == c) ? lo : -1;
+    };
+    for (int k = 0; k < ncell; ++k) {
+      const int cell = s_cell[k];
+      const double y0 = (double)cell_centre(g0, h32, cell);
+      for (int mix = 0; mix < 2; ++mix) {
+        const tpe_seg& S = mix ? SA : SB;
+        const int nc = S.n_obs + 1;
+        const int per = (nc + kBandBlocks - 1) / kBandBlocks;
+        const int k0 = min(nc, kb * per), k1 = min(nc, k0 + per);
+        band_expand<kBX, 2>(S, coef64, y0, Tb.h, s_eb, dred, k0, k1);
+        BandMix& Q = W.cpart[k][kb][mix];
+        if (threadIdx.x <= kBandD) Q.P[threadIdx.x] = s_eb.P[threadIdx.x];
+        if (threadIdx.x == 0) {
+          Q.m = s_eb.m;
+          Q.n_dir = s_eb.n_dir;
+        }
+        if (threadIdx.x < kChunkDir) Q.dir[threadIdx.x] = s_eb.dir[threadIdx.x];
+        __syncthreads();  // (s_eb reused)
+      }
+      if (threadIdx.x == 0) {
+        __threadfence();  // this chunk's expansions are visible before the count
+        s_last = atomicAdd(&W.cell_done[k], 1u) == (unsigned)(kBandBlocks - 1);
+      }
+      __syncthreads();
+      if (!s_last) continue;
+      __threadfence();  // (acquire: the other chunks)
+      // this block merges cell k (one thread per mixture: 16 x 25 terms, in
+      // chunk order) and scores its survivors
+      if (threadIdx.x < 2) {
+        const int mix = threadIdx.x;
+        double mm = -INFINITY;
+        bool ok = true;
+        int nd = 0;
+        for (int c = 0; c < kBandBlocks; ++c) {
+          mm = fmax(mm, W.cpart[k][c][mix].m);
+          ok = ok && W.cpart[k][c][mix].n_dir >= 0;
+        }
+        BandMix& E = mix ? s_ea : s_eb;
+        int* dir = mix ? s_dira : s_dirb;
+        for (int n = 0; n <= kBandD; ++n) E.P[n] = 0.0;
+        for (int c = 0; c < kBandBlocks && ok; ++c) {
+          const BandMix& q = W.cpart[k][c][mix];
+          const double f = q.m == -INFINITY ? 0.0 : exp(q.m - mm);
+          for (int n = 0; n <= kBandD; ++n) E.P[n] += q.P[n] * f;
+          for (int i = 0; i < q.n_dir; ++i) dir[nd++] = q.dir[i];
+        }
+        E.m = mm;
+        E.n_dir = ok ? nd : -1;
+      }
+      __syncthreads();
+      const bool direct_cell = s_eb.n_dir < 0 || s_ea.n_dir < 0;
+      BestT bx{0.0, -1, 0.0};
+      for_survivors([&](const tpe_band (&E)[kEPT], uint32_t keep) {
+#pragma unroll
+        for (int u = 0; u < kEPT; ++u) {
+          if (!((keep >> u) & 1u)) continue;
+          if (listed(band_cell(Tb, E[u].y)) != k) continue;
+          const double y = (double)E[u].y;
+          double lb, la;
+          if (!direct_cell) {
+            const double uu = (y - y0) / Tb.h;
+            lb = band_eval(s_eb, s_dirb, s_eb.n_dir, coef64, SB.comp_off, uu, y);
+            la = band_eval(s_ea, s_dira, s_ea.n_dir, coef64, SA.comp_off, uu, y);
+          } else {
+            lb = band_direct(SB, coef64, y);
+            la = band_direct(SA, coef64, y);
+          }
+          best_update(bx, lb - la, E[u].index, cand_value(E[u].y, lgmm));
+        }
+      });
+      bx = block_best<kBX>(bx, red);
+      if (threadIdx.x == 0) {
+        W.win[k] = bx;
+        W.cell_done[k] = 0u;  // (re-armed: every chunk of this cell has counted)
+        __threadfence();      // the cell's winner is visible before the count
+        s_lastc = atomicAdd(&W.cells_done, 1u) == (unsigned)(ncell - 1);
+      }
+      __syncthreads();
+      if (s_lastc) {  // every cell is decided: the job's winner
+        __threadfence();
+        BestT r{0.0, -1, 0.0};
+        if (threadIdx.x == 0) {
+          r = W.win[0];
+          for (int c = 1; c < ncell; ++c)
+            if (better(W.win[c].score, W.win[c].index, r.score, r.index)) r = W.win[c];
+          best[j] = tpe_best{r.score, r.index, r.value, J.n_cand};
+          W.cells_done = 0u;
+        }
+      }
+      __syncthreads();  // (s_eb / s_ea / s_last reused)
+    }
+    return;
   }
-  bx = block_best<kBS>(bx, red);
+  // ---- 4. the job's winner: the last block to finish ----
   if (threadIdx.x == 0) {
-    work[j].part[blockIdx.x] = bx;
-    __threadfence();  // the winner is visible before the count
-    s_last = atomicAdd(&work[j].done, 1u) == (unsigned)(kBandFinal - 1);
+    __threadfence();  // this block's sums / winner are visible before the count
+    s_last = atomicAdd(&W.done, 1u) == (unsigned)(kBandBlocks - 1);
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();  // (acquire: the other blocks' winners)
-  if (threadIdx.x == 0) {
-    if (ns != kBandOverflow) {
-      BestT r = work[j].part[0];
-      for (int b = 1; b < kBandFinal; ++b) {
-        const BestT o = work[j].part[b];
-        if (better(o.score, o.index, r.score, r.index)) r = o;
+  __threadfence();  // (acquire: the other blocks' results)
+  BestT bx{0.0, -1, 0.0};
+  if (ns <= kBandSurv) {
+    for (int i = threadIdx.x; i < ns; i += kBX) {
+      double l2[2];
+      for (int mix = 0; mix < 2; ++mix) {
+        double mm = W.part[0][i][2 * mix], ss = W.part[0][i][2 * mix + 1];
+        for (int c = 1; c < kBandBlocks; ++c)
+          lse_merge(mm, ss, W.part[c][i][2 * mix], W.part[c][i][2 * mix + 1]);
+        l2[mix] = log(ss) + mm;
       }
-      best[j] = tpe_best{r.score, r.index, r.value, J.n_cand};
+      best_update(bx, l2[0] - l2[1], s_idx[i], cand_value(s_y[i], lgmm));
     }
-#ifndef TPE_DIAG_BAND_KEEP  // diagnostic builds: counters left for tools/band_probe.py
-    ctl[2] = 0u;
-    ctl[3] = 0u;
-#endif
-    work[j].done = 0u;
+  } else if (threadIdx.x < kBandBlocks) {
+    bx = W.win[threadIdx.x];
+  }
+  bx = block_best<kBX>(bx, red);
+  if (threadIdx.x == 0) {
+    best[j] = tpe_best{bx.score, bx.index, bx.value, J.n_cand};
+    W.done = 0u;
   }
 }
 
@@ -2044,13 +2552,22 @@ extern "C" int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, in
   return check_launch("tpe_score_table");
 }
 
+extern "C" int64_t tpe_band_bytes(const tpe_job* host_jobs, int n_jobs, int64_t* ctl_bytes,
+                                  int64_t* work_bytes) {
+  if (n_jobs < 0 || (n_jobs > 0 && !host_jobs)) return -1;
+  const int64_t tiles = n_jobs > 0 ? tpe_table_fast_tiles(host_jobs, n_jobs) * n_jobs : 1;
+  if (ctl_bytes) *ctl_bytes = tiles * kHdrWords * (int64_t)sizeof(uint32_t);
+  if (work_bytes) *work_bytes = (int64_t)sizeof(BandWork) * std::max(n_jobs, 1);
+  return tiles * kTileSlots * (int64_t)sizeof(tpe_band);
+}
+
 extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                                     const tpe_seg* segs, const double* mu, const double* sigma,
                                     const double* wcdf, const float* coef32,
                                     const tpe_table* tables, const float* cells, tpe_band* band,
-                                    int64_t band_cap, uint32_t* band_ctl, double* out_score,
-                                    double* out_x, tpe_best* partial, int64_t n_partial,
-                                    uint64_t* stats, void* stream) {
+                                    uint32_t* band_ctl, double* out_score, double* out_x,
+                                    double* out_eps, tpe_best* partial, int64_t n_partial,
+                                    int tile_cap, uint64_t* stats, void* stream) {
   bool inj = false;
   if (!check_table_jobs("tpe_score_table_fast", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
   if (n_jobs == 0) return TPE_OK;
@@ -2063,8 +2580,8 @@ extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_job
     set_error("tpe_score_table_fast: null pointer");
     return TPE_E_ARG;
   }
-  if (band_cap < 1 || band_cap > ((int64_t)1 << 31)) {
-    set_error("tpe_score_table_fast: band_cap=%lld", (long long)band_cap);
+  if (tile_cap < 0 || tile_cap > kTileSlots) {
+    set_error("tpe_score_table_fast: tile_cap=%d (0..%d)", tile_cap, kTileSlots);
     return TPE_E_ARG;
   }
   const int64_t gx = tpe_table_fast_tiles(host_jobs, n_jobs);
@@ -2081,21 +2598,16 @@ extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_job
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_score_table_fast, dim3((unsigned)(8 * per)), dim3(kBS), 0, st, jobs, segs,
                      mu, sigma, wcdf, reinterpret_cast<const float4*>(coef32), tables, cells, band,
-                     band_cap, band_ctl, out_score, out_x, partial, (unsigned long long*)stats,
-                     (int)gx, n_jobs);
+                     band_ctl, out_score, out_x, out_eps, partial, (unsigned long long*)stats,
+                     (int)gx, n_jobs, tile_cap);
   return check_launch("tpe_score_table_fast");
-}
-
-extern "C" int64_t tpe_band_work_bytes(int n_jobs) {
-  if (n_jobs < 0) return -1;
-  return (int64_t)sizeof(BandWork) * std::max(n_jobs, 1);
 }
 
 extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                                 const tpe_seg* segs, const double* coef64,
-                                const tpe_table* tables, tpe_band* band, int64_t band_cap,
-                                uint32_t* band_ctl, const tpe_best* partial, int64_t n_partial,
-                                tpe_best* best, void* work, void* stream) {
+                                const tpe_table* tables, const tpe_band* band,
+                                const uint32_t* band_ctl, const tpe_best* partial,
+                                int64_t n_partial, tpe_best* best, void* work, void* stream) {
   bool inj = false;
   if (!check_table_jobs("tpe_band_rescore", host_jobs, n_jobs, &inj)) return TPE_E_ARG;
   if (n_jobs == 0) return TPE_OK;
@@ -2107,24 +2619,15 @@ extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, i
     set_error("tpe_band_rescore: null pointer");
     return TPE_E_ARG;
   }
-  if (band_cap < 1 || band_cap > ((int64_t)1 << 31)) {
-    set_error("tpe_band_rescore: band_cap=%lld", (long long)band_cap);
-    return TPE_E_ARG;
-  }
   const int64_t gx = tpe_table_fast_tiles(host_jobs, n_jobs);
   if (gx * n_jobs > n_partial) {
     set_error("tpe_band_rescore: partial workspace %lld < %lld", (long long)n_partial,
               (long long)(gx * n_jobs));
     return TPE_E_ARG;
   }
-  hipStream_t st = (hipStream_t)stream;
-  BandWork* W = static_cast<BandWork*>(work);
-  hipLaunchKernelGGL(k_band_select, dim3(n_jobs), dim3(kBS), 0, st, jobs, tables, band, band_cap,
-                     band_ctl, partial, gx, best, W);
-  hipLaunchKernelGGL(k_band_expand, dim3(kBandSlots, n_jobs, 2), dim3(kBX), 0, st, jobs, segs,
-                     coef64, tables, band_ctl, W);
-  hipLaunchKernelGGL(k_band_final, dim3(kBandFinal, n_jobs), dim3(kBS), 0, st, jobs, segs, coef64,
-                     tables, band, band_cap, band_ctl, best, W);
+  hipLaunchKernelGGL(k_band, dim3(kBandBlocks, n_jobs), dim3(kBX), 0, (hipStream_t)stream, jobs,
+                     segs, coef64, tables, band, band_ctl, partial, (int)gx, best,
+                     static_cast<BandWork*>(work));
   return check_launch("tpe_band_rescore");
 }
 

@@ -113,3 +113,58 @@ extern "C" int64_t tpe_smallest_rows(const double* losses, int64_t n, int64_t k,
   std::copy(ki.begin(), ki.end(), out);
   return k;
 }
+
+// ---------------------------------------------------------------------------
+// The hardware transcendentals the fp32 error bounds lean on,
+// measured exhaustively: v_exp_f32 (the build's terms, mix_eps' 2^-22) over
+// every fp32 x in [-126, 12] (results >= 2^-126: no subnormal outputs), as the
+// relative error against exp2 in fp64; v_log_f32 (the two-polynomial
+// fallback's kEtaLog2 = 2^-22) over every positive normal fp32 p, as
+// |log2f(p) - log2(p)| / max(1, |log2 p|).  Device-side fp64 references (each
+// within 1 fp64 ulp).  out[0], out[1]: the two maxima (device, 2 doubles).
+// ---------------------------------------------------------------------------
+namespace tpe {
+namespace {
+__global__ __launch_bounds__(256) void k_ulp_check(unsigned long long* out) {
+  double ee = 0.0, el = 0.0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32);
+       i += stride) {
+    const float x = __uint_as_float((uint32_t)i);
+    if (x >= -126.0f && x <= 12.0f) {
+      const double r = exp2((double)x);
+      const double g = (double)__builtin_amdgcn_exp2f(x);
+      ee = fmax(ee, fabs(g - r) / r);
+    }
+    if (x > 0.0f && x >= 0x1.0p-126f && isfinite(x)) {
+      const double r = log2((double)x);
+      const double g = (double)__builtin_amdgcn_logf(x);
+      el = fmax(el, fabs(g - r) / fmax(1.0, fabs(r)));
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    ee = fmax(ee, __shfl_xor(ee, o, 64));
+    el = fmax(el, __shfl_xor(el, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {  // non-negative doubles order as their bits
+    atomicMax(out, (unsigned long long)__double_as_longlong(ee));
+    atomicMax(out + 1, (unsigned long long)__double_as_longlong(el));
+  }
+}
+}  // namespace
+}  // namespace tpe
+
+extern "C" int tpe_check_transcendentals(double* out, void* stream) {
+  if (!out) {
+    tpe::set_error("tpe_check_transcendentals: null pointer");
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(out, 0, 2 * sizeof(double), st) != hipSuccess) {
+    tpe::set_error("tpe_check_transcendentals: hipMemsetAsync failed");
+    return TPE_E_LAUNCH;
+  }
+  hipLaunchKernelGGL(tpe::k_ulp_check, dim3(8192), dim3(256), 0, st,
+                     reinterpret_cast<unsigned long long*>(out));
+  return tpe::check_launch("tpe_check_transcendentals");
+}

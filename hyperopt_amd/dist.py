@@ -211,7 +211,8 @@ def combine_host(records):
     out = sets[0].copy()
     for s in sets[1:]:
         for k in range(out.size):
-            out["n_scored"][k] += s["n_scored"][k]
+            owed = out["n_scored"][k] < 0 or s["n_scored"][k] < 0  # (an inexact record)
+            out["n_scored"][k] = -1 if owed else out["n_scored"][k] + s["n_scored"][k]
             if better(s["score"][k], s["index"][k], out["score"][k], out["index"][k]):
                 n = out["n_scored"][k]
                 out[k] = s[k]

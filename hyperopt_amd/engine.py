@@ -41,7 +41,7 @@ LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense 
 LAT_PACK_MAX = 1 << 16  # lattice slots of a level initialised through the upload (else memset)
 TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
-BAND_CAP = 1 << 16  # per job: candidates the table path re-scores exactly (tpe_score_table_fast)
+BAND_TILE_CAP = 64  # per scorer tile: band entries kept (tpe_score_table_fast's tile_cap, <= 64)
 LAT_PREFIX = 1 << 16  # lattice argmax: candidates drawn before the early decision
 LAT_SUGGEST_MAX_SLOTS = 1 << 10  # ... for lattices of at most this many slots (all scored)
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
@@ -1044,8 +1044,11 @@ class Engine:
         # the fit from the history's sorted orders (tpe_fit_sorted): one kernel
         # instead of gather + sort + merge ranks + three coefficient kernels;
         # needs the single history with its identity row list (row = tid order)
+        # (it walks the history's sorted order, a permutation of rows [0, rows):
+        # the split flags must cover exactly those rows -- tpe_fit_sorted reads
+        # is_below[row] for every one of them)
         sorted_fit = bool(fit_ids) and self.sorted_fit and history is not None and \
-            histories is None and rows is None and not prune
+            histories is None and rows is None and not prune and n_rows == history.rows
         tjobs = max([b - a for a, b in (_slice_of(groups, g) for g, (k, ids) in enumerate(groups)
                                         if k in ("table", "pruned64") and ids)], default=0)
         self._presize(n_comp, n_obs_total, max_obs, cobs_off, len(segs), tjobs,
@@ -1182,7 +1185,7 @@ class Engine:
             # stream has the slack and the fork costs two more host calls)
             d_cand = base + o_cand
             d_bl = d_al = d_x = None
-            d_sc = None
+            d_sc = d_eps = None
             if outputs:
                 d_bl = self._buf("out_bl", 8 * max(out_off, 1))
                 d_al = self._buf("out_al", 8 * max(out_off, 1))
@@ -1190,6 +1193,7 @@ class Engine:
             elif table_scores:
                 d_sc = self._buf("out_sc", 8 * max(out_off, 1))
                 d_x = self._buf("out_x", 8 * max(out_off, 1))
+                d_eps = self._buf("out_eps", 8 * max(out_off, 1))
             table_calls = []
             band_jobs.clear()
             jobs_ptr = jobs.__array_interface__["data"][0]
@@ -1289,19 +1293,22 @@ class Engine:
                                                     d_tab, d_cells, d_cand, d_bl, d_al, d_x, d_part,
                                                     npart, db, d_stats, sp), "tpe_score_table")
                     else:  # the suggest path: one score cubic per candidate, exact argmax
-                        d_band = self._buf("band", L.BAND_DTYPE.itemsize * BAND_CAP * nj)
-                        d_bctl = self._zbuf("band_ctl", 16 * nj)
-                        d_bwork = self._buf("band_work", lib.tpe_band_work_bytes(nj))
+                        ctl_b, work_b = ctypes.c_int64(0), ctypes.c_int64(0)
+                        nbb = lib.tpe_band_bytes(hjp, nj, ctypes.byref(ctl_b),
+                                                 ctypes.byref(work_b))
+                        d_band = self._buf("band", nbb)
+                        d_bctl = self._buf("band_ctl", ctl_b.value)
+                        d_bwork = self._zbuf("band_work", work_b.value)
                         L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
-                                                         d_c32, d_tab, d_cells, d_band, BAND_CAP,
-                                                         d_bctl, d_sc, d_x, d_part, npart,
-                                                         d_stats, sp),
+                                                         d_c32, d_tab, d_cells, d_band, d_bctl,
+                                                         d_sc, d_x, d_eps, d_part, npart,
+                                                         BAND_TILE_CAP, d_stats, sp),
                                 "tpe_score_table_fast")
                         tock("table", e0)
+                        self._tables_slice = (a, b)  # (the test hook reads these tables back)
                         e0 = tick("band")
                         L.check(lib.tpe_band_rescore(dj, hjp, nj, d_segs, d_c64, d_tab, d_band,
-                                                     BAND_CAP, d_bctl, d_part, npart, db,
-                                                     d_bwork, sp),
+                                                     d_bctl, d_part, npart, db, d_bwork, sp),
                                 "tpe_band_rescore")
                         tock("band", e0)
                         e0 = None
@@ -1537,6 +1544,10 @@ class Engine:
         if band_jobs:
             fix = functools.partial(self._band_fix, list(band_jobs), d_segs, max_obs + 1, n_comp,
                                     sp.value, exchange is not None)
+        xinfo = None
+        if exchange is not None:  # (comm, labels, world, slot per job in launch order, stream)
+            xinfo = (int(x_comm), int(x_labels), int(x_world),
+                     x_slots[np.asarray(order, np.int64)].copy(), sp.value)
         # ---- results: one device->host copy of the result block into pinned memory
         # (issued by the records themselves on the native path)
         pin = self._res_pinned(nbytes)
@@ -1552,7 +1563,7 @@ class Engine:
                 L.hip_check(self._hip.hipEventRecord(ev, sp), "hipEventRecord")
             p = self._inflight = _Pending(self, ev, pin, nbytes, np.asarray(order, np.int64),
                                           64 + n_jobs * BS if xbytes else None,
-                                          bool(table_calls), after, fix, jobs)
+                                          bool(table_calls), after, fix, jobs, xinfo)
             if ops is not None and self._oplists.get(gkey) is ops and history is not None:
                 # a recorded level: the next call with the same signature only
                 # rewrites its keys and split flags in the staged pack (_Replay)
@@ -1569,17 +1580,17 @@ class Engine:
                         sig, self._gen, ops, self._pinned[0], pkey, p, pin,
                         dict(segs=o_segs, csegs=o_csegs, g=o_g, jobs=o_jobs, fb=o_fb, isb=o_isb),
                         history if sorted_fit else None, tjobs,
-                        (list(band_jobs), d_segs, sp.value, exchange is not None))
+                        (list(band_jobs), d_segs, sp.value, exchange is not None, xinfo))
                     self._staged_sig = sig[:-1]
             return p if defer else p.result()
         return self._read_results(stream, sp, ops is None, after, pin, nbytes, n_jobs, fix, jobs,
                                   xbytes, groups, table_calls, outputs, table_scores, out_off,
-                                  works, order, cont, modes, _hmark)
+                                  works, order, cont, modes, _hmark, xinfo)
 
 
     def _read_results(self, stream, sp, sync, after, pin, nbytes, n_jobs, fix, jobs, xbytes,
                       groups, table_calls, outputs, table_scores, out_off, works, order, cont,
-                      modes, _hmark):
+                      modes, _hmark, xinfo=None):
         """The level's synchronous readback: the result block (error bits, table
         stats, one tpe_best per job, the exchange's label records) from the
         pinned copy, the overflowed bands' exact re-score, per-candidate
@@ -1595,6 +1606,8 @@ class Engine:
             fix(best_h, jobs)
         self.last_exchange = res_h[64 + n_jobs * BS:].view(L.BEST_DTYPE).copy() if xbytes \
             else None
+        if xbytes:
+            self.last_exchange = self._exchange_fix(best_h, self.last_exchange, xinfo)
         with self.torch.cuda.stream(stream):
             err = int(res_h[:4].view(np.int32)[0])
             self.last_pairs = None
@@ -1611,7 +1624,10 @@ class Engine:
                         for k in ("out_bl", "out_al", "out_x")]
             elif table_scores:
                 outs = [self._bufs[k][:8 * max(out_off, 1)].to("cpu").numpy().view(np.float64)
-                        for k in ("out_sc", "out_x")]
+                        for k in ("out_sc", "out_x", "out_eps")]
+                ta, tb = self._tables_slice
+                tabs = self._bufs["tables"][:L.TABLE_DTYPE.itemsize * (tb - ta)].to("cpu") \
+                    .numpy().view(L.TABLE_DTYPE)
         _raise_errors(err)
         _hmark('readback')
         results = [None] * len(works)
@@ -1628,6 +1644,8 @@ class Engine:
             elif table_scores and i in cont and modes[i] == "table":
                 o, n = int(jobs[pos]["out_off"]), int(jobs[pos]["n_cand"])
                 r.extra["score"] = outs[0][o:o + n].copy()
+                r.extra["eps"] = outs[2][o:o + n].copy()  # the band's bound per candidate
+                r.extra["table"] = tabs[pos - ta].copy()  # (slope, eps_cubic, eps_mix, ...)
                 r.cand = outs[1][o:o + n].copy()
             results[i] = r
         _hmark("results")
@@ -1635,16 +1653,13 @@ class Engine:
 
     def _band_fix(self, band_jobs, d_segs, max_comp, n_comp, stream, exchanged, best_h, jobs):
         """Jobs of the table path whose band overflowed (n_scored == -1: more
-        than BAND_CAP candidates within the fp32 error bound of the maximum --
+        than BAND_TILE_CAP candidates of one scorer tile within the fp32 error bound of the maximum --
         a plateau of equal scores) are re-scored exactly: their fp32 candidate
         stream (TPE_F_DRAW32) through tpe_score_pruned64, every candidate in
         fp64.  Patches ``best_h`` (launch order) in place."""
         pos = [p for a, b in band_jobs for p in range(a, b) if best_h["n_scored"][p] < 0]
         if not pos:
             return
-        if exchanged:
-            raise L.TpeHipError("band overflow on %d label(s) of a level with an in-level "
-                                "exchange: run the level without exchange=" % len(pos))
         torch, lib = self.torch, self.lib
         hj = np.ascontiguousarray(jobs[np.asarray(pos)].copy())
         hj["flags"] |= L.F_DRAW32
@@ -1667,6 +1682,40 @@ class Engine:
         for k, p in enumerate(pos):
             best_h[p] = res[k]
         self.band_overflows = getattr(self, "band_overflows", 0) + len(pos)
+
+    def _exchange_fix(self, best_h, xrec, xinfo):
+        """The exchange of a label-sharded level carries n_scored = -1 for a
+        label whose band overflowed on some rank (tpe_best_scatter /
+        tpe_best_combine propagate it), and every rank holds the same combined
+        records -- so every rank, and only when one is owed, comes here
+        together.  By now ``best_h`` holds this rank's exact records (its
+        overflowed jobs were re-scored by _band_fix before the exchange was
+        read), so the exchange is run once more on them: a second all-gather
+        on the same communicator, in the same order on every rank (no rank
+        leaves the level early and none takes an inexact winner)."""
+        if xinfo is None or not (xrec["n_scored"] < 0).any():
+            return xrec
+        torch, lib = self.torch, self.lib
+        comm, n_labels, world, slots, stream = xinfo
+        if (best_h["n_scored"] < 0).any():
+            raise L.TpeHipError("exchange fix: a local record is still inexact")
+        sp = ctypes.c_void_p(stream)
+        BS = L.BEST_DTYPE.itemsize
+        dev = self.device
+        d_by = torch.from_numpy(np.ascontiguousarray(best_h).view(np.uint8).copy()).to(dev)
+        d_slot = torch.from_numpy(np.ascontiguousarray(slots, np.int32)).to(dev)
+        d_xl = torch.empty(n_labels * BS, dtype=torch.uint8, device=dev)
+        d_xg = torch.empty(world * n_labels * BS, dtype=torch.uint8, device=dev)
+        d_out = torch.empty(n_labels * BS, dtype=torch.uint8, device=dev)
+        torch.cuda.current_stream(dev).synchronize()  # (the uploads above, on torch's stream)
+        L.check(lib.tpe_best_scatter(d_by.data_ptr(), d_slot.data_ptr(), best_h.size,
+                                     d_xl.data_ptr(), n_labels, sp), "tpe_best_scatter (fix)")
+        L.check(lib.tpe_maxloc_allreduce(d_xl.data_ptr(), d_xg.data_ptr(), d_out.data_ptr(),
+                                         n_labels, comm, sp), "tpe_maxloc_allreduce (fix)")
+        L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
+        out = d_out.cpu().numpy().view(L.BEST_DTYPE).copy()
+        self.exchange_fixes = getattr(self, "exchange_fixes", 0) + 1
+        return out
 
     def _read_posteriors(self, works, fit_ids, cat, segs, csegs, n_comp, n_p, d_segs, stream,
                          o_p):
@@ -1711,11 +1760,12 @@ class _Pending(object):
     and returns the BatchResult (cached)."""
 
     def __init__(self, eng, event, pin, nbytes, order, xoff, table, after=None, fix=None,
-                 jobs=None):
+                 jobs=None, xinfo=None):
         self.eng, self.event, self.pin, self.nbytes = eng, event, pin, nbytes
         self.order, self.table, self.after = order, table, after
         self.fix, self.jobs = fix, jobs  # band overflow re-score (Engine._band_fix)
         self.xoff = xoff  # offset of the exchanged label records (Engine.run exchange=)
+        self.xinfo = xinfo  # what Engine._exchange_fix needs to redo an owed exchange
         self._res = None
 
     def result(self):
@@ -1743,6 +1793,8 @@ class _Pending(object):
             self.fix(best_h, self.jobs)
         eng.last_exchange = res_h[self.xoff:].view(L.BEST_DTYPE).copy() \
             if self.xoff is not None else None
+        if self.xoff is not None:
+            eng.last_exchange = eng._exchange_fix(best_h, eng.last_exchange, self.xinfo)
         by = np.empty(n, L.BEST_DTYPE)
         by[self.order] = best_h[:n]
         self._res = BatchResult(by["index"].copy(), by["value"].copy(), by["score"].copy(),
@@ -1779,6 +1831,7 @@ class _Replay(object):
         self.counts = None  # (n_below, n_above, rows) the staged pack holds
         self.hist_rows = None
         self.fix = None
+        self.xinfo = fix_args[4]
 
     @staticmethod
     def signature(eng, works, prior_weight, lf, precision, outputs, stream, sample_only, pruned,
@@ -1855,7 +1908,7 @@ class _Replay(object):
                                 max_comp=max_obs + 1, pack_size=pack_size))
         self.counts = counts
         self.hist_rows = self.history.rows if self.history is not None else None
-        band_jobs, d_segs, stream, exchanged = self.fix_args
+        band_jobs, d_segs, stream, exchanged, self.xinfo = self.fix_args
         self.fix = None
         if band_jobs:
             self.fix = functools.partial(eng._band_fix, band_jobs, d_segs, max_obs + 1, n_comp,
@@ -1879,7 +1932,8 @@ class _Replay(object):
         if self.ops.timed and timers is not None:
             after = functools.partial(self.ops.read_timers, eng._hip, timers)
         p = eng._inflight = _Pending(eng, eng._event("result"), self.res_pin, self.nbytes,
-                                     self.order, self.xoff, self.table, after, self.fix, jobs)
+                                     self.order, self.xoff, self.table, after, self.fix, jobs,
+                                     self.xinfo)
         return p if defer else p.result()
 
 

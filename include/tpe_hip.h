@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 16
+#define TPE_ABI_VERSION 17
 
 enum {
   TPE_OK = 0,
@@ -230,6 +230,9 @@ int tpe_history_order(const double* vals, int64_t ld, const tpe_colspec* specs,
  * order); then tpe_parzen_fit's own bandwidth / coefficient launches (same
  * bits).  A count other than gathers[i].count sets bit 4 of *err (the
  * segment's means are not written; the call's results are void).
+ * Precondition: `order` holds, per column, a permutation of the rows
+ * [0, n_rows) -- n_rows must be the history's row count (tpe_history_order's
+ * n_rows), so is_below must hold exactly one flag per history row.
  * scratch: tpe_fit_sorted_scratch_bytes(n_seg, n_rows) bytes. */
 int64_t tpe_fit_sorted_scratch_bytes(int n_seg, int64_t n_rows);
 int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t ld, const int32_t* order,
@@ -297,15 +300,20 @@ int tpe_score_sorted(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
  * as exp(m) * sum_{n<9} P_n u^n, u = (y - y0)/h: a degree-8 polynomial whose
  * P_0..P_5 are stored in fp32 and P_6..P_8 in fp16 (tpe_table_build).  Each
  * component's factor exp(A u + B u^2) is expanded only where 9|A| + 65|B| <=
- * 5.8, which bounds the relative error of the stored, fp32-evaluated
- * polynomial by 1.0e-6 (truncation 4.3e-7 + fp32/fp16 storage 1.4e-7 + fp16
- * tail evaluation 4.4e-7; DESIGN.md section 3.1, tools/table_bounds.py);
- * components whose largest term on the whole range is below e^-25 / M of the
- * prior component's smallest term are left out (< 1.4e-11 of the sum).
+ * 5.8 (series truncation <= 4.4e-7 relative on |u| <= 1.0501,
+ * tools/table_bounds.py); the stored polynomial's whole error against its
+ * mixture -- truncation, the build's fp32 terms, series, sums and merges,
+ * fp32/fp16 storage -- is bounded per job from the build's worst case
+ * (tpe_table.eps_mix); components whose largest term
+ * on the whole range is below e^-25 / M of the prior component's smallest
+ * term are left out (< 1.4e-11 of the sum).
  * From those two polynomials the build also fits, per cell, a cubic of the
  * score f(u) = (m_b - m_a) + log P_b(u) - log P_a(u) at four Chebyshev nodes
- * of [-1.05, 1.05], rounds it to fp32 and checks it against f at 12 more
- * points: a cell whose error exceeds 1e-6 + 2^-22 |f| is flagged.
+ * of [-1.05, 1.05], rounds it to fp32 and BOUNDS its error against f on
+ * |u| <= 1.0501 (per sub-interval, the log series of both polynomials and a
+ * majorant of its remainder): a cell whose bound exceeds 1e-6 is flagged;
+ * the largest bound of the others (with the cubic's evaluation terms) is
+ * tpe_table.eps_cubic.
  * A candidate whose cell fails the bound, or that lies outside the grid, is
  * scored by the exact fp32 log-sum-exp over all components instead.
  * tables: one tpe_table per job (device); cells: byte pool, 128 B per cell
@@ -326,9 +334,21 @@ typedef struct tpe_table {
   float inv_h, inv_w;   /* 1/h and 1/(2h)                                    */
   int32_t nb;           /* cells used (<= job.tbl_cap)                       */
   int32_t n_wide_below, n_wide_above;
-  float slope;          /* max over unflagged cells of |c1| + 2.1|c2| + 3.31|c3|:
-                           a bound of |df/du| on |u| <= 1.05 (score cubics),
+  float slope;          /* max over unflagged cells of |c1| + 2.11|c2| + 3.31|c3|:
+                           a bound of |df/du| on |u| <= 1.0501 (score cubics),
                            written by tpe_table_build                        */
+  float eps_cubic;      /* max over unflagged cells of the proven bound of
+                           |s32 - f^(u)| for a cubic-scored candidate, less its
+                           2^-22 |s32| part: the cubic's fit to the stored
+                           polynomials' score f^ (interval remainder, DESIGN.md
+                           3.1), its fp32 evaluation and u's rounding, and the
+                           fp32 score offset                                  */
+  float eps_mix;        /* proven bound of the relative error of one stored
+                           polynomial against its mixture on |u| <= 1.0501
+                           (truncation, exclusion, the build's fp32 terms,
+                           series, sums and merges, fp32/fp16 storage)       */
+  int32_t build_items;  /* most components one cell's expansion summed       */
+  float build_ab;       /* max over summed components of 1.0501|A| + 1.1028|B| */
   double T_below, T_above; /* log-term floor: components whose term stays
                               below it on a cell are left out               */
 } tpe_table;
@@ -353,48 +373,56 @@ int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
  * tpe_score_table_fast: the same draws as tpe_score_table; each candidate is
  * scored by its cell's score cubic -- one 16-B load and three FMAs -- or, on a
  * flagged cubic, by the two-polynomial cell, then the exact fp32
- * log-sum-exp.  Writes the per-block fp32 winners to `partial` and the band.
- * tpe_band_rescore: the winner decided EXACTLY -- np.argmax (tpe.py:649-658)
- * over the fp64 scores of every candidate that can still be the maximum.
+ * log-sum-exp.  Writes the per-block fp32 winners to `partial` and the band
+ * tiles.  tpe_band_rescore: the winner decided EXACTLY -- np.argmax
+ * (tpe.py:649-658) over the fp64 scores of every candidate that can still be
+ * the maximum.
  *
- * Band.  With eps(s) the bound of |s32 - s64| (polynomial
- * 1.0e-6 per mixture, cubic fit, fp32 rounding), candidate i can be the exact
- * winner only if s32_i + eps_i >= G := max_k (s32_k - eps_k).  Each scorer
- * block publishes its best s32_k - eps_k into band_ctl (atomic max) and
- * appends its candidates with s32 + eps >= the maximum known so far to
- * `band`; tpe_band_rescore keeps those with s32 + eps >= the final G
- * (compacted in place) and re-scores them in fp64 -- per table cell, a
- * degree-24 expansion of both mixtures around the cell centre over every
- * component within e^-45 of the sum (components whose series would converge
- * slowly summed term by term; one block per cell and mixture) -- and takes
- * the np.argmax winner (largest score, then smallest index):
- * best[j] = {fp64 score, index, value (x, or exp(y) in fp64 for LGMM1),
- * n_cand}.  A job whose band got more than band_cap entries (a plateau of
- * near-equal scores) keeps the fp32 winner with n_scored = -1: the caller
- * re-scores it exactly (tpe_score_pruned64 with TPE_F_DRAW32).
- * band: band_cap entries per job; band_ctl: 4 uint32 per job, zero before
- * the first call -- tpe_band_rescore leaves them zero again; work:
- * tpe_band_work_bytes(n_jobs) bytes (the cell expansions).  Both calls take
- * the same job list and partial workspace (tpe_table_partials()).
- * out_score / out_x (nullable, tests): the per-candidate fp32 score and value
- * at job.out_off. */
+ * Band.  With eps(s) a proven bound of |s32 - s64| (for a
+ * cubic-scored candidate eps = table.eps_cubic + 2.0001 table.eps_mix +
+ * 2^-22 |s32|; a two-polynomial candidate carries its own; a log-sum-exp
+ * candidate is always re-scored), candidate i can be the exact winner only if
+ * s32_i + eps_i >= G := max_k (s32_k - eps_k).  Each scorer block (tile of
+ * 4096 candidates) writes, without atomics, a header {lo = its best
+ * s32 - eps, hi_max = its largest s32 + eps, n} (4 uint32 per tile in
+ * band_ctl) and its candidates with s32 + eps >= lo (a superset: G >= lo)
+ * into its own 64 entries of `band` (n = 0xFFFFFFFF: more than tile_cap,
+ * <= 64, did not fit; tests shrink tile_cap to force the overflow path).
+ * tpe_band_rescore (one launch, 4 blocks per job) takes G from the headers,
+ * keeps the entries with s32 + eps >= G and re-scores them in fp64 -- per
+ * table cell, a degree-24 expansion of both mixtures around the cell centre
+ * over every component within e^-45 of the sum (components whose series
+ * would converge slowly summed term by term) -- and takes the np.argmax
+ * winner (largest score, then smallest index): best[j] = {fp64 score, index,
+ * value (x, or exp(y) in fp64 for LGMM1), n_cand}.  A job with a full tile
+ * that can still hold the winner (hi_max >= G) keeps the fp32 winner with
+ * n_scored = -1: the caller re-scores it exactly (tpe_score_pruned64 with
+ * TPE_F_DRAW32).
+ * band / band_ctl / work: tpe_band_bytes(host_jobs, n_jobs, &ctl, &work),
+ * ctl and work bytes (work: zeroed once before its first use; the rescore
+ * leaves it zero).  No state carries from one call to the next in band or
+ * band_ctl: every tile rewrites its header.  Both calls take the same job
+ * list and partial workspace (tpe_table_partials()).
+ * out_score / out_x / out_eps (nullable, tests): per candidate at
+ * job.out_off, the fp32 score, the value and the bound eps used (+inf for
+ * a log-sum-exp candidate). */
 typedef struct tpe_band {
   int64_t index;        /* global candidate index                            */
   float y;              /* candidate in the scoring coordinate (fp32 draw)   */
   float hi;             /* s32 + eps: upper bound of its exact score          */
 } tpe_band;
+int64_t tpe_band_bytes(const tpe_job* host_jobs, int n_jobs, int64_t* ctl_bytes,
+                       int64_t* work_bytes);
 int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                          const tpe_seg* segs, const double* mu, const double* sigma,
                          const double* wcdf, const float* coef32, const tpe_table* tables,
-                         const float* cells, tpe_band* band, int64_t band_cap,
-                         uint32_t* band_ctl, double* out_score, double* out_x, tpe_best* partial,
-                         int64_t n_partial, uint64_t* stats, void* stream);
-int64_t tpe_band_work_bytes(int n_jobs);
+                         const float* cells, tpe_band* band, uint32_t* band_ctl,
+                         double* out_score, double* out_x, double* out_eps, tpe_best* partial,
+                         int64_t n_partial, int tile_cap, uint64_t* stats, void* stream);
 int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                      const tpe_seg* segs, const double* coef64, const tpe_table* tables,
-                     tpe_band* band, int64_t band_cap, uint32_t* band_ctl,
-                     const tpe_best* partial, int64_t n_partial, tpe_best* best, void* work,
-                     void* stream);
+                     const tpe_band* band, const uint32_t* band_ctl, const tpe_best* partial,
+                     int64_t n_partial, tpe_best* best, void* work, void* stream);
 
 /* ---- continuous candidates, exact fp64 with pruning (parity mode) ----------
  * Same results as tpe_score_continuous(precision=64) up to fp64 rounding (a
@@ -585,6 +613,13 @@ int64_t tpe_smallest_rows(const double* losses, int64_t n, int64_t k, int64_t* o
 
 const char* tpe_last_error(void);
 int tpe_abi_version(void);
+/* Self-check of the hardware transcendentals the fp32 error bounds assume
+ * (DESIGN.md 3.1): out[0] = max relative error of v_exp_f32 over every fp32
+ * x in [-126, 12]; out[1] = max over positive normal fp32 p of
+ * |v_log_f32(p) - log2 p| / max(1, |log2 p|).  Exhaustive (2^32 inputs, a
+ * few ms); out: 2 doubles (device), asynchronous on `stream`. */
+int tpe_check_transcendentals(double* out, void* stream);
+
 /* host: writes sizeof(tpe_seg, tpe_cat_seg, tpe_job, tpe_best, tpe_table, tpe_gather,
  * tpe_history, tpe_prior, tpe_op, tpe_band, tpe_colspec) to out[0..n); returns 11 */
 int tpe_struct_sizes(int32_t* out, int n);

@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 16
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 17
     sizes = (ctypes.c_int32 * 11)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 11) == 11
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -113,25 +113,29 @@ def test_argument_errors_are_reported():
     jobs["tbl_cap"] = 64
     jobs["flags"] = L.F_INJECTED
 
-    def fast(band_cap=1 << 16, ptr=None):
+    def fast(tile_cap=64, ptr=None, n_partial=1 << 20):
         p = [ptr] * 8
-        return lib.tpe_score_table_fast(p[0], hp_, 1, *p[:7], ptr, band_cap, ptr, None, None, ptr,
-                                        1 << 20, None, None)
+        return lib.tpe_score_table_fast(p[0], hp_, 1, *p[:7], ptr, ptr, None, None, None, ptr,
+                                        n_partial, tile_cap, None, None)
 
-    def rescore(band_cap=1 << 16, ptr=None, n_partial=1 << 20):
-        return lib.tpe_band_rescore(ptr, hp_, 1, ptr, ptr, ptr, ptr, band_cap, ptr, ptr,
-                                    n_partial, ptr, ptr, None)
+    def rescore(ptr=None, n_partial=1 << 20):
+        return lib.tpe_band_rescore(ptr, hp_, 1, ptr, ptr, ptr, ptr, ptr, ptr, n_partial, ptr, ptr,
+                                    None)
     assert fast() == -1 and b"sampled jobs only" in lib.tpe_last_error()
     assert rescore() == -1 and b"sampled jobs only" in lib.tpe_last_error()
     jobs["flags"] = 0
     assert fast() == -1 and b"null pointer" in lib.tpe_last_error()
     assert rescore() == -1 and b"null pointer" in lib.tpe_last_error()
     eight = ctypes.c_void_p(8)
-    assert fast(0, eight) == -1 and b"band_cap" in lib.tpe_last_error()
-    assert fast(-3, eight) == -1 and b"band_cap" in lib.tpe_last_error()
-    assert rescore(0, eight) == -1 and b"band_cap" in lib.tpe_last_error()
-    assert rescore(64, eight, n_partial=0) == -1 and b"partial workspace" in lib.tpe_last_error()
-    assert lib.tpe_band_work_bytes(3) > 3 * 64 * 2 * 8 * 25 and lib.tpe_band_work_bytes(-1) == -1
+    assert fast(65, eight) == -1 and b"tile_cap" in lib.tpe_last_error()
+    assert fast(-3, eight) == -1 and b"tile_cap" in lib.tpe_last_error()
+    assert fast(64, eight, n_partial=0) == -1 and b"partial workspace" in lib.tpe_last_error()
+    assert rescore(eight, n_partial=0) == -1 and b"partial workspace" in lib.tpe_last_error()
+    ctl, work = ctypes.c_int64(0), ctypes.c_int64(0)
+    jobs["n_cand"] = 1 << 22  # 1024 tiles of 4096 candidates
+    nb = lib.tpe_band_bytes(hp_, 1, ctypes.byref(ctl), ctypes.byref(work))
+    assert nb == 1024 * 64 * L.BAND_DTYPE.itemsize and ctl.value == 1024 * 16 and work.value > 0
+    assert lib.tpe_band_bytes(hp_, -1, None, None) == -1
     rc = lib.tpe_table_build(None, hp_, 1, None, None, None, None, 8, *([None] * 8))
     assert rc == -1 and b"null pointer" in lib.tpe_last_error()
     assert lib.tpe_table_scratch_bytes(3, 1000) > 0 and lib.tpe_table_scratch_bytes(-1, 5) == -1

@@ -25,10 +25,18 @@ def majorant(a, b, n_terms=60):
     return np.array(c)
 
 
-def bounds(P=10, n32=6, lim=5.8, ulim=1.05, steps=801):
+def bounds(P=10, n32=6, lim=5.8 * (1 + 2e-5), ulim=1.0501, steps=4001):
+    """Maxima over the admissible boundary 9|A| + 65|B| = lim (every bound is
+    increasing in |A| and in |B|, so the boundary holds the maximum).  Rigorous
+    over the whole boundary, not only at the sample points: on the piece
+    between t_i and t_i+1 the bound is at most its value at (A(t_i+1), B(t_i)),
+    the piece's largest A and largest B.  lim carries the build's fp32
+    admissibility-test slack (5.8 (1 + 1e-5) plus rounding), ulim the scorer's
+    |u| range after u's fp32 rounding."""
     trunc = fp16 = horner = 0.0
-    for t in np.linspace(0.0, 1.0, steps):
-        A, B = t * lim / 9.0, (1.0 - t) * lim / 65.0
+    ts = np.linspace(0.0, 1.0, steps)
+    for t0, t1 in zip(ts[:-1], ts[1:]):
+        A, B = t1 * lim / 9.0, (1.0 - t0) * lim / 65.0
         a, b = A * ulim, B * ulim * ulim
         c = majorant(a, b)
         e = np.exp(a + b)
