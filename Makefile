@@ -8,7 +8,9 @@ LIB := hyperopt_amd/libtpe_hip.so
 # -ffp-contract=off: no implicit FMA fusion, so expressions written to
 # follow numpy's operation order (linspace ramps, normal_cdf, erf-pair sums)
 # round exactly as numpy does; hot loops spell their FMAs out (fmaf).
-FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -ffp-contract=off
+# EXTRA: diagnostic defines for A/B variant builds (tools/mkvariant.sh); empty in the product
+EXTRA ?=
+FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -ffp-contract=off $(EXTRA)
 
 all: $(LIB)
 

@@ -26,7 +26,7 @@ SEG_DTYPE = np.dtype([
     ("transform", "<i4"), ("family", "<i4"), ("floor", "<f8"), ("prior_weight", "<f8"),
     ("prior_mu", "<f8"), ("prior_sigma", "<f8"), ("low", "<f8"), ("high", "<f8"),
     ("bounded", "<i4"), ("prior_pos", "<i4"), ("p_accept", "<f8"), ("cmax", "<f8"),
-    ("center", "<f8"), ("lglob", "<f8"), ("n_wide", "<i4"), ("pad", "<i4")], align=True)
+    ("center", "<f8"), ("lglob", "<f8"), ("n_wide", "<i4"), ("given", "<i4")], align=True)
 CAT_SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("p_off", "<i8"), ("n_obs", "<i4"), ("n_cat", "<i4"),
     ("lf", "<i4"), ("mode", "<i4"), ("prior_weight", "<f8"), ("prior_p_off", "<i8")],
@@ -133,6 +133,8 @@ _SIGNATURES = {
     "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
     "tpe_run_ops": (_I, [_P, _I, ctypes.POINTER(_I)]),
     "tpe_check_transcendentals": (_I, [_P, _P]),
+    "tpe_mixture_scratch_bytes": (_I64, [_I, _I]),
+    "tpe_mixture_prepare": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_smallest_rows": (_I64, [_P, _I64, _I64, _P]),
     "tpe_last_error": (ctypes.c_char_p, []),
     "tpe_abi_version": (_I, []),

@@ -243,7 +243,9 @@ __global__ __launch_bounds__(kFitBS) void k_fit_comp(const tpe_seg* __restrict__
   double wk = 0.0, dphi = 0.0;
   if (k < nc) {
     double s;
-    if (n == 0) {
+    if (S.given) {  // an explicit mixture: its sigmas as given (tpe_mixture_prepare)
+      s = sigma[off + k];
+    } else if (n == 0) {
       s = ps;
     } else if (n == 1) {
       s = (k == pos) ? ps : ps * 0.5;
@@ -254,10 +256,12 @@ __global__ __launch_bounds__(kFitBS) void k_fit_comp(const tpe_seg* __restrict__
     } else {
       s = fmax(mu[off + k] - mu[off + k - 1], mu[off + k + 1] - mu[off + k]);
     }
-    const double lo_clip = ps / fmin(100.0, 1.0 + (double)nc);  // tpe.py:455
-    s = fmin(fmax(s, lo_clip), ps);
-    if (k == pos) s = ps;
-    sigma[off + k] = s;
+    if (!S.given) {
+      const double lo_clip = ps / fmin(100.0, 1.0 + (double)nc);  // tpe.py:455
+      s = fmin(fmax(s, lo_clip), ps);
+      if (k == pos) s = ps;
+      sigma[off + k] = s;
+    }
     wk = w[off + k];
     if (S.bounded) {
       const double m = mu[off + k];
@@ -558,4 +562,26 @@ extern "C" int tpe_parzen_fit(const double* obs, void* scratch, tpe_seg* segs, i
     hipLaunchKernelGGL(k_fit_prune, dim3(n_seg), dim3(kFitBS), 0, st, segs, mu, sigma, coef64,
                        coef32, coef32n, wide32, pm, sm);
   return check_launch("tpe_parzen_fit");
+}
+
+extern "C" int64_t tpe_mixture_scratch_bytes(int n_seg, int max_comp) {
+  if (n_seg < 0 || max_comp < 1) return -1;
+  return 8 * (int64_t)std::max(n_seg, 1) * fit_part_doubles(max_comp - 1);
+}
+
+extern "C" int tpe_mixture_prepare(tpe_seg* segs, int n_seg, int max_comp, void* scratch,
+                                   double* w, const double* mu, double* sigma, double* wcdf,
+                                   double* coef64, float* coef32, void* stream) {
+  if (n_seg < 0 || max_comp < 1 || n_seg > 65535 || max_comp >= (1 << 30)) {
+    set_error("tpe_mixture_prepare: n_seg=%d max_comp=%d", n_seg, max_comp);
+    return TPE_E_ARG;
+  }
+  if (n_seg == 0) return TPE_OK;
+  if (!segs || !scratch || !w || !mu || !sigma || !wcdf || !coef64 || !coef32) {
+    set_error("tpe_mixture_prepare: null pointer");
+    return TPE_E_ARG;
+  }
+  fit_tail(segs, n_seg, max_comp - 1, static_cast<double*>(scratch), w, mu, sigma, wcdf, coef64,
+           coef32, (hipStream_t)stream);
+  return check_launch("tpe_mixture_prepare");
 }

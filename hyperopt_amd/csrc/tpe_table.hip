@@ -62,6 +62,9 @@ constexpr int kCellF = 16;           // floats per cell (64 B: four 16-B chunks)
 constexpr int kSlotB = 128;          // bytes per cell slot of a job's region (cells + m pairs)
 constexpr int kChunks = 4;           // 16-B chunks of a cell the scorer reads
 constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
+#ifndef TPE_SCORE_WPE  // waves per SIMD the fast scorer is compiled for (its VGPR budget)
+#define TPE_SCORE_WPE 6
+#endif
 #ifndef TPE_TAU_TABLE
 #define TPE_TAU_TABLE 25.0
 #endif
@@ -664,8 +667,8 @@ constexpr int kScoreLanes = 8;       // lanes per cell: 4 nodes, 8 sub-intervals
 constexpr int kScoreCellsPerBlock = kBS / kScoreLanes;
 constexpr int kScoreBlocks = 256;    // per job (grid-stride over cells)
 constexpr double kUFit = 1.0501;     // |u| the bounds cover (u's fp32 rounding: <= 1.05 (1 + 5 2^-24))
-constexpr int kLogD = 8;             // log-series terms carried exactly
-constexpr int kLogM = 14;            // majorant terms summed (then Cauchy's tail)
+constexpr int kLogD = 7;             // log-series terms carried exactly
+constexpr int kLogM = 12;            // majorant terms summed (then Cauchy's tail)
 constexpr double kU32 = 0x1.0p-24;   // fp32 unit roundoff
 // max of a + b = 1.0501|A| + 1.1028|B| over the admissible set 9|A| + 65|B| <=
 // 5.8 (1 + 2e-5) (the build's test with its fp32 slack): at |A| = 0.64446
@@ -883,7 +886,10 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
               __float_as_uint(epsc));
 }
 
-__global__ __launch_bounds__(kBS) void k_table_build(
+#ifndef TPE_BUILD_WPE  // diagnostic builds: waves-per-EU target of the build kernel
+#define TPE_BUILD_WPE 1
+#endif
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_BUILD_WPE))) void k_table_build(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ sigma, const double* __restrict__ coef64,
     const double* __restrict__ reach_hi, const double* __restrict__ reach_lo,
@@ -1349,7 +1355,7 @@ constexpr int kHdrWords = 4;  // per tile: lo, hi_max (float bits), n, unused
 // take the two-polynomial cell, then the exact log-sum-exp, after the loop.
 // out_score / out_x / out_eps (nullable, tests): per-candidate fp32 score,
 // value and the bound eps the band used (+inf: always re-scored).
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k_score_table_fast(
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_WPE))) void k_score_table_fast(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, const float4* __restrict__ coef32,
@@ -1586,17 +1592,22 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   return;
 #endif
   // ---- the band tile: its candidates with hi >= lo_blk (NaN hi included);
-  // only a lane whose largest upper bound reaches lo_blk holds any
+  // only a lane whose largest upper bound reaches lo_blk holds any.  A
+  // cubic-scored candidate's hi = up(s + eps(s)) is monotone in s, so it is
+  // tested as s >= s_thr, s_thr = a value below every s with hi >= lo_blk
+  // (s + eps(s) < lo_blk whenever s < s_thr: eps(s) <= ea' + 2^-22 |s|, the
+  // 2^-20 |lo_blk| slack covers the outward roundings); its hi is formed
+  // only for the entries written.  Fallback candidates carry their hi in the
+  // stage (two-polynomial) or are always in (log-sum-exp: +inf).
+  const float s_thr = lo_blk - fmaf(0x1.0p-20f, fabsf(lo_blk), ea * 1.0001f) - 1e-30f;
   uint32_t em = 0;
   if (!(hi_t < lo_blk)) {
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
       if (r < nvalid) {
         const float v = stage[r * kWave + lane];
-        const float hi = ((lsem >> r) & 1u) ? INFINITY
-                         : ((fbm >> r) & 1u) ? v : up(v + eps_of(v));
-        stage[r * kWave + lane] = hi;
-        if (!(hi < lo_blk)) em |= 1u << r;
+        const bool in = ((fbm >> r) & 1u) ? (((lsem >> r) & 1u) || !(v < lo_blk)) : !(v < s_thr);
+        if (in) em |= 1u << r;
       }
     }
   }
@@ -1614,7 +1625,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(6))) void k
         // draw32_pairs gave it -- so x[] need not live through the tail)
         const float yv = draw32(M, J.key, J.cand_base + t0 + r, lo_on, hi_on, (float)J.low,
                                 (float)J.high);
-        B[pos] = tpe_band{J.cand_base + t0 + r, yv, stage[r * kWave + lane]};
+        const float v = stage[r * kWave + lane];
+        const float hi = ((lsem >> r) & 1u) ? INFINITY : ((fbm >> r) & 1u) ? v : up(v + eps_of(v));
+        B[pos] = tpe_band{J.cand_base + t0 + r, yv, hi};
         ++pos;
       }
     }
@@ -1666,7 +1679,7 @@ constexpr int kBX = 256;             // band block
 constexpr int kBandTiles = 4096;     // tiles of a job the kernel's LDS prefix holds (2^24 candidates;
                                      // a larger job takes the exact fallback)
 constexpr int kTilesPT = kBandTiles / kBX;  // tile headers per thread (prefix pass)
-constexpr int kBandD = 24;           // expansion degree
+constexpr int kBandD = 20;           // expansion degree
 constexpr double kBandTau = 45.0;    // exclusion margin (nats) on top of log(M)
 constexpr double kBandRho = 1.5;     // admissible 1.05 |A| + 1.1025 |B|
 constexpr int kBandCells = 64;       // cells expanded per job (sorted; the rest: direct)
@@ -1680,14 +1693,19 @@ struct BandMix {  // one mixture's expansion on one cell (or one chunk of its co
   int pad;
   int dir[kChunkDir];
 };
+constexpr int kEPT = 8;              // band entries per thread per window (k_band)
+constexpr int kBandSurvMax = 16384;  // survivors a job may have (more: the exact fallback)
 struct BandWork {  // per job (tpe_band_bytes)
   double part[kBandBlocks][kBandSurv][4];         // direct: per chunk and survivor {m, s} b, a
   BandMix cpart[kBandCells][kBandBlocks][2];      // cells: per cell, chunk and mixture
-  BestT win[kBandCells];                          // cells: each cell's survivors' winner
-  unsigned int cell_done[kBandCells];             // chunks finished per cell
-  unsigned int cells_done;                        // cells finished (the last one reduces)
-  unsigned int done;                              // direct: blocks finished
-  unsigned int pad[2];
+  float sy[kBandSurvMax];                         // the survivors (flat entry order): y ...
+  int64_t sidx[kBandSurvMax];                     // ... and candidate index
+  int cells[kBandCells];                          // the listed cells (ascending)
+  int ns, ncell, over, pad0;                      // survivors, cells, job overflowed
+  long long tmark[8];                             // (TPE_BAND_TIMING diagnostic builds)
+  BestT win[kBandBlocks];                         // k_band_final: per block, its winner
+  unsigned int done;                              // k_band_final: blocks finished
+  unsigned int pad[3];
 };
 
 // (m, s): e^m s; combined in a fixed order
@@ -1706,8 +1724,9 @@ __device__ __forceinline__ void lse_merge(double& m, double& s, double m2, doubl
 // keeps its own scale (raised when a term would exceed e^8 of it) and the
 // threads are merged at the end (fixed order: deterministic).  A component's
 // series exp(A u + B u^2) converges like rho^n / n!, rho = 1.05|A| +
-// 1.1025|B|: with rho <= kBandRho the tail past degree 24 is < 1e-20 of its
-// term; components with a larger rho are summed term by term (band_eval).
+// 1.1025|B|: with rho <= kBandRho the tail past degree 20 is < 1.1e-16 of
+// its term (1.5^21 / 21!; a component the table admitted has rho <= 0.68:
+// < 4e-23); components with a larger rho are summed term by term.
 // Components whose largest term on the cell is below e^-45 / M of the prior
 // component's smallest one there are left out (< e^-45 of the sum).
 template <int BX, int U>
@@ -1855,10 +1874,10 @@ __global__ __launch_bounds__(kBX) void k_band(
   __shared__ float s_g[kNW];
   __shared__ double s_red[kNW][kSurvBatch][2];
   __shared__ double dred[kNW * (kBandD + 1)];
-  __shared__ BandMix s_eb, s_ea;
-  __shared__ int s_dirb[kBandBlocks * kChunkDir], s_dira[kBandBlocks * kChunkDir];
+  __shared__ BandMix s_eb;
   __shared__ int s_over, s_off;
-  __shared__ bool s_last, s_lastc;
+  __shared__ int s_tile[kEPT * kBX];
+  __shared__ int s_wm[kNW];
   const int j = blockIdx.y, kb = blockIdx.x;
   const int lane = lane_id(), wid = threadIdx.x / kWave;
   const tpe_job J = jobs[j];
@@ -1884,6 +1903,13 @@ __global__ __launch_bounds__(kBX) void k_band(
     }
     return pos;
   };
+#ifdef TPE_BAND_TIMING
+#define TMARK(i) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) work[blockIdx.y].tmark[i] = wall_clock64();
+#else
+#define TMARK(i)
+#endif
+  TMARK(0)
   // ---- 1. G, overflow, the tiles' counts ----
   float g = -INFINITY;
   for (int t = threadIdx.x; t < n_tiles; t += kBX) g = fmaxf(g, __uint_as_float(H[t * kHdrWords]));
@@ -1926,30 +1952,58 @@ __global__ __launch_bounds__(kBX) void k_band(
         best_update(b32, p.score, p.index, p.value);
       }
       b32 = block_best<kBX>(b32, red);
-      if (threadIdx.x == 0) best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
+      if (threadIdx.x == 0) {
+        best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
+        work[j].over = 1;  // (k_band_final leaves the job alone)
+      }
     }
-    return;  // (every block: the counter is untouched)
+    return;
   }
   const int nt = min(n_tiles, kBandTiles);
   const tpe_table Tb = tables[j];
   // every entry once, kEPT consecutive ones per thread loaded together;
-  // fn(entry, flat position) for the survivors, every thread taking part
-  constexpr int kEPT = 4;
+  // fn(entry, flat position) for the survivors, every thread taking part.
+  // A window's flat positions find their tile without a search: each tile
+  // marks its first position in the window with its id, and a running max
+  // over the window (thread, then wave and block prefix) fills the rest.
+  constexpr int kWin = kEPT * kBX;
   auto for_survivors = [&](auto&& fn) {
-    for (int f0 = 0; f0 < n_ent; f0 += kEPT * kBX) {
+    for (int f0 = 0; f0 < n_ent; f0 += kWin) {
+      for (int i = threadIdx.x; i < kWin; i += kBX) s_tile[i] = -1;
+      __syncthreads();
+      for (int t = threadIdx.x; t < nt; t += kBX) {
+        const int st = t > 0 ? s_end[t - 1] : 0, en = s_end[t];
+        if (en > st && en > f0 && st < f0 + kWin) s_tile[max(st, f0) - f0] = t;
+      }
+      __syncthreads();
+      int tl[kEPT];
+      int run = -1;
+#pragma unroll
+      for (int u = 0; u < kEPT; ++u) {
+        run = max(run, s_tile[threadIdx.x * kEPT + u]);
+        tl[u] = run;
+      }
+      int incl = run;  // inclusive max-scan over the wave, then the waves before
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int w = __shfl_up(incl, o, kWave);
+        if (lane >= o) incl = max(incl, w);
+      }
+      int carry = __shfl_up(incl, 1, kWave);
+      if (lane == 0) carry = -1;
+      if (lane == kWave - 1) s_wm[wid] = incl;
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < kNW; ++w) carry = w < wid ? max(carry, s_wm[w]) : carry;
       tpe_band E[kEPT];
 #pragma unroll
       for (int u = 0; u < kEPT; ++u) {
         const int f = f0 + threadIdx.x * kEPT + u;
         E[u].hi = -INFINITY;
         if (f < n_ent) {
-          int lo = 0, hi = nt - 1;  // the first tile whose inclusive end passes f
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_end[mid] > f) hi = mid; else lo = mid + 1;
-          }
-          const int e = f - (s_end[lo] - (int)H[lo * kHdrWords + 2]);
-          E[u] = Bj[(int64_t)lo * kTileSlots + e];
+          const int t = max(tl[u], carry);
+          const int e = f - (t > 0 ? s_end[t - 1] : 0);
+          E[u] = Bj[(int64_t)t * kTileSlots + e];
         }
       }
       uint32_t keep = 0;
@@ -1959,8 +2013,10 @@ __global__ __launch_bounds__(kBX) void k_band(
       fn(E, keep);
     }
   };
-  // ---- 2. the survivors: their number, their cells; the first kBandSurv in
-  // flat order listed ----
+  TMARK(1)
+  // ---- 2. the survivors: their number and cells; block 0 lists them (flat
+  // entry order) for k_band_final ----
+  BandWork& W = work[j];
   int ns = 0;
   if (threadIdx.x == 0) s_off = 0;
   for_survivors([&](const tpe_band (&E)[kEPT], uint32_t keep) {
@@ -1973,10 +2029,19 @@ __global__ __launch_bounds__(kBX) void k_band(
           s_y[pos] = E[u].y;
           s_idx[pos] = E[u].index;
         }
+        if (kb == 0 && pos < kBandSurvMax) {
+          W.sy[pos] = E[u].y;
+          W.sidx[pos] = E[u].index;
+        }
         ++pos;
         const int c = band_cell(Tb, E[u].y);
-        if (c >= 0 && c < kBandBits) atomicOr(&s_bits[c >> 5], 1u << (c & 31));
-        else s_off = 1;
+        // (read first: a band's thousands of survivors share a few cells,
+        // and same-word LDS atomics serialise)
+        if (c >= 0 && c < kBandBits) {
+          if (!(s_bits[c >> 5] & (1u << (c & 31)))) atomicOr(&s_bits[c >> 5], 1u << (c & 31));
+        } else {
+          s_off = 1;
+        }
       }
     }
     ns += total;
@@ -1993,16 +2058,23 @@ __global__ __launch_bounds__(kBX) void k_band(
     for (int i = 0; i < kPer && pos < kBandCells; ++i) {
       uint32_t b = s_bits[threadIdx.x * kPer + i];
       while (b && pos < kBandCells) {
-        s_cell[pos++] = (threadIdx.x * kPer + i) * 32 + __builtin_ctz(b);
+        const int cell = (threadIdx.x * kPer + i) * 32 + __builtin_ctz(b);
+        s_cell[pos] = cell;
+        if (kb == 0) W.cells[pos] = cell;
+        ++pos;
         b &= b - 1;
       }
     }
   }
   __syncthreads();
-  BandWork& W = work[j];
-  const bool lgmm = J.family == TPE_LGMM1;
-  const tpe_seg SB = segs[J.below], SA = segs[J.above];
-  if (ns > kBandSurv && (ncell > kBandCells || s_off)) {
+  TMARK(2)
+  const bool over = ns > kBandSurv && (ncell > kBandCells || s_off || ns > kBandSurvMax);
+  if (kb == 0 && threadIdx.x == 0) {
+    W.ns = ns;
+    W.ncell = min(ncell, kBandCells);
+    W.over = over;
+  }
+  if (over) {
     // many survivors, off the grid or over too many cells: the exact fallback
     if (kb == 0) {
       BestT b32{0.0, -1, 0.0};
@@ -2015,6 +2087,7 @@ __global__ __launch_bounds__(kBX) void k_band(
     }
     return;
   }
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
   if (ns <= kBandSurv) {
     // ---- 3a. direct: this block's component chunk, for every survivor ----
     for (int mix = 0; mix < 2; ++mix) {
@@ -2043,27 +2116,17 @@ __global__ __launch_bounds__(kBX) void k_band(
             m[i] = upv ? v : m[i];
           }
         }
-        // fixed reduction tree: the wave (both partners combine the lower
-        // lane's pair first), then the block's waves in order
+        // fixed reduction tree: the wave's largest scale (DPP max), each lane's
+        // sum brought to it once, a plain wave sum; then the block's waves in
+        // order (lse_merge)
 #pragma unroll
         for (int i = 0; i < kSurvBatch; ++i) {
-#pragma unroll
-          for (int o = 32; o >= 1; o >>= 1) {
-            const double m2 = __shfl_xor(m[i], o, kWave), s2 = __shfl_xor(sm[i], o, kWave);
-            double ma = m[i], sa = sm[i], mb = m2, sb = s2;
-            if (lane & o) {
-              ma = m2;
-              sa = s2;
-              mb = m[i];
-              sb = sm[i];
-            }
-            lse_merge(ma, sa, mb, sb);
-            m[i] = ma;
-            sm[i] = sa;
-          }
+          const double mw = wave_max_d(m[i]);
+          double v = (m[i] == -INFINITY) ? 0.0 : sm[i] * exp(m[i] - mw);
+          v = wave_sum_d(v);
           if (lane == 0) {
-            s_red[wid][i][0] = m[i];
-            s_red[wid][i][1] = sm[i];
+            s_red[wid][i][0] = mw;
+            s_red[wid][i][1] = v;
           }
         }
         __syncthreads();
@@ -2078,29 +2141,22 @@ __global__ __launch_bounds__(kBX) void k_band(
       }
     }
   } else {
-    // ---- 3b. cells: this block expands chunk kb of every listed cell's
-    // components (both mixtures); the last chunk of a cell to finish merges
-    // the chunks and scores the cell's survivors; the last cell reduces ----
+    // ---- 3b. cells: (cell, chunk) units, kBandBlocks of them when the cells
+    // are fewer (each cell's components in nch chunks), else one cell each;
+    // block kb takes units kb, kb + kBandBlocks, ... (k_band_final merges
+    // a cell's chunks in order) ----
     const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
-    auto listed = [&](int c) -> int {  // listed position of cell c, -1 if none
-      if (c < 0) return -1;
-      int lo = 0, hi = ncell;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (s_cell[mid] < c) lo = mid + 1; else hi = mid;
-      }
-      return (lo < ncell && s_cell[lo] == c) ? lo : -1;
-    };
-    for (int k = 0; k < ncell; ++k) {
-      const int cell = s_cell[k];
-      const double y0 = (double)cell_centre(g0, h32, cell);
+    const int nch = max(1, kBandBlocks / max(ncell, 1));
+    for (int unit = kb; unit < ncell * nch; unit += kBandBlocks) {
+      const int k = unit / nch, ch = unit % nch;
+      const double y0 = (double)cell_centre(g0, h32, s_cell[k]);
       for (int mix = 0; mix < 2; ++mix) {
         const tpe_seg& S = mix ? SA : SB;
         const int nc = S.n_obs + 1;
-        const int per = (nc + kBandBlocks - 1) / kBandBlocks;
-        const int k0 = min(nc, kb * per), k1 = min(nc, k0 + per);
+        const int per = (nc + nch - 1) / nch;
+        const int k0 = min(nc, ch * per), k1 = min(nc, k0 + per);
         band_expand<kBX, 2>(S, coef64, y0, Tb.h, s_eb, dred, k0, k1);
-        BandMix& Q = W.cpart[k][kb][mix];
+        BandMix& Q = W.cpart[k][ch][mix];
         if (threadIdx.x <= kBandD) Q.P[threadIdx.x] = s_eb.P[threadIdx.x];
         if (threadIdx.x == 0) {
           Q.m = s_eb.m;
@@ -2109,91 +2165,45 @@ __global__ __launch_bounds__(kBX) void k_band(
         if (threadIdx.x < kChunkDir) Q.dir[threadIdx.x] = s_eb.dir[threadIdx.x];
         __syncthreads();  // (s_eb reused)
       }
-      if (threadIdx.x == 0) {
-        __threadfence();  // this chunk's expansions are visible before the count
-        s_last = atomicAdd(&W.cell_done[k], 1u) == (unsigned)(kBandBlocks - 1);
-      }
-      __syncthreads();
-      if (!s_last) continue;
-      __threadfence();  // (acquire: the other chunks)
-      // this block merges cell k (one thread per mixture: 16 x 25 terms, in
-      // chunk order) and scores its survivors
-      if (threadIdx.x < 2) {
-        const int mix = threadIdx.x;
-        double mm = -INFINITY;
-        bool ok = true;
-        int nd = 0;
-        for (int c = 0; c < kBandBlocks; ++c) {
-          mm = fmax(mm, W.cpart[k][c][mix].m);
-          ok = ok && W.cpart[k][c][mix].n_dir >= 0;
-        }
-        BandMix& E = mix ? s_ea : s_eb;
-        int* dir = mix ? s_dira : s_dirb;
-        for (int n = 0; n <= kBandD; ++n) E.P[n] = 0.0;
-        for (int c = 0; c < kBandBlocks && ok; ++c) {
-          const BandMix& q = W.cpart[k][c][mix];
-          const double f = q.m == -INFINITY ? 0.0 : exp(q.m - mm);
-          for (int n = 0; n <= kBandD; ++n) E.P[n] += q.P[n] * f;
-          for (int i = 0; i < q.n_dir; ++i) dir[nd++] = q.dir[i];
-        }
-        E.m = mm;
-        E.n_dir = ok ? nd : -1;
-      }
-      __syncthreads();
-      const bool direct_cell = s_eb.n_dir < 0 || s_ea.n_dir < 0;
-      BestT bx{0.0, -1, 0.0};
-      for_survivors([&](const tpe_band (&E)[kEPT], uint32_t keep) {
-#pragma unroll
-        for (int u = 0; u < kEPT; ++u) {
-          if (!((keep >> u) & 1u)) continue;
-          if (listed(band_cell(Tb, E[u].y)) != k) continue;
-          const double y = (double)E[u].y;
-          double lb, la;
-          if (!direct_cell) {
-            const double uu = (y - y0) / Tb.h;
-            lb = band_eval(s_eb, s_dirb, s_eb.n_dir, coef64, SB.comp_off, uu, y);
-            la = band_eval(s_ea, s_dira, s_ea.n_dir, coef64, SA.comp_off, uu, y);
-          } else {
-            lb = band_direct(SB, coef64, y);
-            la = band_direct(SA, coef64, y);
-          }
-          best_update(bx, lb - la, E[u].index, cand_value(E[u].y, lgmm));
-        }
-      });
-      bx = block_best<kBX>(bx, red);
-      if (threadIdx.x == 0) {
-        W.win[k] = bx;
-        W.cell_done[k] = 0u;  // (re-armed: every chunk of this cell has counted)
-        __threadfence();      // the cell's winner is visible before the count
-        s_lastc = atomicAdd(&W.cells_done, 1u) == (unsigned)(ncell - 1);
-      }
-      __syncthreads();
-      if (s_lastc) {  // every cell is decided: the job's winner
-        __threadfence();
-        BestT r{0.0, -1, 0.0};
-        if (threadIdx.x == 0) {
-          r = W.win[0];
-          for (int c = 1; c < ncell; ++c)
-            if (better(W.win[c].score, W.win[c].index, r.score, r.index)) r = W.win[c];
-          best[j] = tpe_best{r.score, r.index, r.value, J.n_cand};
-          W.cells_done = 0u;
-        }
-      }
-      __syncthreads();  // (s_eb / s_ea / s_last reused)
     }
-    return;
   }
-  // ---- 4. the job's winner: the last block to finish ----
-  if (threadIdx.x == 0) {
-    __threadfence();  // this block's sums / winner are visible before the count
-    s_last = atomicAdd(&W.done, 1u) == (unsigned)(kBandBlocks - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();  // (acquire: the other blocks' results)
+  TMARK(3)
+}
+
+// The band's decision (blocks (k, j), k < kBandBlocks; after k_band): the
+// survivors [k ns / B, (k + 1) ns / B) of job j, one per thread -- direct:
+// its chunks' partial sums combined in chunk order; cells: its cell's chunk
+// expansions merged in chunk order (into LDS, every listed cell) and
+// evaluated -- then np.argmax over the block's survivors into work[j].win[k];
+// the job's last block folds the blocks' winners into best[j] = {fp64
+// score, index, value, n_cand} and re-arms the counter.
+__global__ __launch_bounds__(kBX) void k_band_final(const tpe_job* __restrict__ jobs,
+                                                    const tpe_seg* __restrict__ segs,
+                                                    const double* __restrict__ coef64,
+                                                    const tpe_table* __restrict__ tables,
+                                                    tpe_best* __restrict__ best,
+                                                    BandWork* __restrict__ work) {
+  constexpr int kNW = kBX / kWave;
+  __shared__ BestT red[kNW];
+  __shared__ double s_P[kBandCells][2][kBandD + 2];  // merged expansions: P_0..P_24, m
+  __shared__ int s_nd[kBandCells][2];
+  __shared__ int s_ndu[kBandCells][2];             // per (cell, chunk) unit: slow components ...
+  __shared__ int s_dir[kBandCells][2][kChunkDir];  // ... and their indices (units <= kBandCells)
+  __shared__ int s_cells[kBandCells];
+  __shared__ bool s_last;
+  const int j = blockIdx.y, kb = blockIdx.x;
+  BandWork& W = work[j];
+  if (W.over) return;  // (k_band gave the fp32 winner with n_scored = -1)
+  const tpe_job J = jobs[j];
+  const int ns = W.ns, ncell = W.ncell;
+  const int nch = max(1, kBandBlocks / max(ncell, 1));  // (k_band's chunks per cell)
+  const bool lgmm = J.family == TPE_LGMM1;
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const tpe_table Tb = tables[j];
+  const int i0 = (int)((int64_t)kb * ns / kBandBlocks), i1 = (int)((int64_t)(kb + 1) * ns / kBandBlocks);
   BestT bx{0.0, -1, 0.0};
   if (ns <= kBandSurv) {
-    for (int i = threadIdx.x; i < ns; i += kBX) {
+    for (int i = i0 + (int)threadIdx.x; i < i1; i += kBX) {
       double l2[2];
       for (int mix = 0; mix < 2; ++mix) {
         double mm = W.part[0][i][2 * mix], ss = W.part[0][i][2 * mix + 1];
@@ -2201,14 +2211,96 @@ __global__ __launch_bounds__(kBX) void k_band(
           lse_merge(mm, ss, W.part[c][i][2 * mix], W.part[c][i][2 * mix + 1]);
         l2[mix] = log(ss) + mm;
       }
-      best_update(bx, l2[0] - l2[1], s_idx[i], cand_value(s_y[i], lgmm));
+      best_update(bx, l2[0] - l2[1], W.sidx[i], cand_value(W.sy[i], lgmm));
     }
-  } else if (threadIdx.x < kBandBlocks) {
-    bx = W.win[threadIdx.x];
+  } else {
+    // merge: thread t takes (cell, mixture, term) items; every term summed
+    // over the chunks in order at the cell's largest scale
+    for (int t = threadIdx.x; t < ncell * 2 * (kBandD + 1); t += kBX) {
+      const int k = t / (2 * (kBandD + 1)), r = t % (2 * (kBandD + 1));
+      const int mix = r / (kBandD + 1), n = r % (kBandD + 1);
+      double mm = -INFINITY;
+      for (int c = 0; c < nch; ++c) mm = fmax(mm, W.cpart[k][c][mix].m);
+      double acc = 0.0;
+      for (int c = 0; c < nch; ++c) {
+        const BandMix& q = W.cpart[k][c][mix];
+        acc += q.m == -INFINITY ? 0.0 : q.P[n] * exp(q.m - mm);
+      }
+      s_P[k][mix][n] = acc;
+      if (n == 0) s_P[k][mix][kBandD + 1] = mm;
+    }
+    // the slow-component lists (one thread per cell and mixture); -1: a
+    // chunk's list overflowed (that cell's survivors take the direct sum)
+    for (int t = threadIdx.x; t < ncell * nch * 2; t += kBX) {
+      const int u = t >> 1, mix = t & 1;
+      s_ndu[u][mix] = W.cpart[u / nch][u % nch][mix].n_dir;
+    }
+    for (int t = threadIdx.x; t < ncell * nch * 2 * kChunkDir; t += kBX) {
+      const int d = t % kChunkDir, r = t / kChunkDir, u = r >> 1, mix = r & 1;
+      s_dir[u][mix][d] = W.cpart[u / nch][u % nch][mix].dir[d];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < ncell * 2; t += kBX) {
+      const int k = t >> 1, mix = t & 1;
+      int nd = 0;
+      for (int c = 0; c < nch; ++c) {
+        const int q = s_ndu[k * nch + c][mix];
+        nd = (nd < 0 || q < 0) ? -1 : nd + q;
+      }
+      s_nd[k][mix] = nd;
+    }
+    for (int t = threadIdx.x; t < ncell; t += kBX) s_cells[t] = W.cells[t];
+    __syncthreads();
+    const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
+    for (int i = i0 + (int)threadIdx.x; i < i1; i += kBX) {
+      const float yf = W.sy[i];
+      const int c = band_cell(Tb, yf);
+      int lo = 0, hi = ncell;  // its listed position (k_band listed every survivor's cell)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_cells[mid] < c) lo = mid + 1; else hi = mid;
+      }
+      const int k = lo;
+      const double y = (double)yf;
+      double l2[2];
+      for (int mix = 0; mix < 2; ++mix) {
+        const tpe_seg& S = mix ? SA : SB;
+        if (s_nd[k][mix] < 0) {
+          l2[mix] = band_direct(S, coef64, y);
+          continue;
+        }
+        const double u = (y - (double)cell_centre(g0, h32, c)) / Tb.h;
+        double p = s_P[k][mix][kBandD];
+#pragma unroll
+        for (int n = kBandD - 1; n >= 0; --n) p = fma(p, u, s_P[k][mix][n]);
+        const double m = s_P[k][mix][kBandD + 1];
+        for (int cc = 0; cc < nch; ++cc) {  // the slow components, term by term
+          const int u = k * nch + cc, nd = s_ndu[u][mix];
+          for (int d = 0; d < nd; ++d) {
+            const double4 cf = ld4(coef64, S.comp_off + s_dir[u][mix][d]);
+            const double t = (y - cf.x) * cf.y;
+            p += exp(cf.z - 0.5 * t * t - m);
+          }
+        }
+        l2[mix] = log(p) + m;
+      }
+      best_update(bx, l2[0] - l2[1], W.sidx[i], cand_value(yf, lgmm));
+    }
   }
   bx = block_best<kBX>(bx, red);
   if (threadIdx.x == 0) {
-    best[j] = tpe_best{bx.score, bx.index, bx.value, J.n_cand};
+    W.win[kb] = bx;
+    __threadfence();  // this block's winner is visible before the count
+    s_last = atomicAdd(&W.done, 1u) == (unsigned)(kBandBlocks - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // (acquire: the other blocks' winners)
+  if (threadIdx.x == 0) {
+    BestT r = W.win[0];
+    for (int b = 1; b < kBandBlocks; ++b)
+      if (better(W.win[b].score, W.win[b].index, r.score, r.index)) r = W.win[b];
+    best[j] = tpe_best{r.score, r.index, r.value, J.n_cand};
     W.done = 0u;
   }
 }
@@ -2628,6 +2720,8 @@ extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, i
   hipLaunchKernelGGL(k_band, dim3(kBandBlocks, n_jobs), dim3(kBX), 0, (hipStream_t)stream, jobs,
                      segs, coef64, tables, band, band_ctl, partial, (int)gx, best,
                      static_cast<BandWork*>(work));
+  hipLaunchKernelGGL(k_band_final, dim3(kBandBlocks, n_jobs), dim3(kBX), 0, (hipStream_t)stream,
+                     jobs, segs, coef64, tables, best, static_cast<BandWork*>(work));
   return check_launch("tpe_band_rescore");
 }
 

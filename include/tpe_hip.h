@@ -89,7 +89,8 @@ typedef struct tpe_seg {
   double center;        /* fp32 scoring origin (float-rounded prior_mu)      */
   double lglob;         /* lower bound of log2(sum)-cmax over the support    */
   int32_t n_wide;       /* wide components (prior + sigma >= sigma_p/4)      */
-  int32_t pad;
+  int32_t given;        /* 1: an explicit mixture (tpe_mixture_prepare): its
+                           w / mu / sigma are the caller's, not fitted       */
 } tpe_seg;
 
 /*
@@ -241,6 +242,22 @@ int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t ld, const 
                    double* w, double* mu, double* sigma, double* wcdf, double* coef64,
                    float* coef32, int32_t* err, void* stream);
 
+/* ---- explicit mixtures (GMM1 / LGMM1 with given parameters) -------------
+ * The reference's GMM1 / GMM1_lpdf / LGMM1 / LGMM1_lpdf (tpe.py:79-180,
+ * 229-307) take the mixture directly (weights, mus, sigmas, low, high, q).
+ * tpe_mixture_prepare readies such mixtures for tpe_sample and the scorers:
+ * every segment (given = 1) holds its K = n_obs + 1 components at comp_off in
+ * w (raw weights) / mu / sigma, prior_pos any component index, prior_mu a
+ * point near the mixture (the fp32 coefficients' origin), low / high /
+ * bounded its truncation.  Writes the normalised weights, p_accept (GMM1),
+ * the cumulative weights and the fp64 / fp32 coefficients exactly as the fit
+ * does for a fitted mixture (the sigmas are kept as given).
+ * scratch: tpe_mixture_scratch_bytes(n_seg, max_comp) bytes. */
+int64_t tpe_mixture_scratch_bytes(int n_seg, int max_comp);
+int tpe_mixture_prepare(tpe_seg* segs, int n_seg, int max_comp, void* scratch, double* w,
+                        const double* mu, double* sigma, double* wcdf, double* coef64,
+                        float* coef32, void* stream);
+
 /* ---- categorical posterior (tpe.py:578-615) ------------------------------ */
 /* p_pool: probabilities (mode 1 also reads the prior p from it at
  * prior_p_off); logp_pool / cdf_pool: log p and cumulative p at p_off.
@@ -390,7 +407,7 @@ int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
  * <= 64, did not fit; tests shrink tile_cap to force the overflow path).
  * tpe_band_rescore (one launch, 4 blocks per job) takes G from the headers,
  * keeps the entries with s32 + eps >= G and re-scores them in fp64 -- per
- * table cell, a degree-24 expansion of both mixtures around the cell centre
+ * table cell, a degree-20 expansion of both mixtures around the cell centre
  * over every component within e^-45 of the sum (components whose series
  * would converge slowly summed term by term) -- and takes the np.argmax
  * winner (largest score, then smallest index): best[j] = {fp64 score, index,
