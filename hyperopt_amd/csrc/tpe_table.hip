@@ -66,7 +66,7 @@ constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
 #define TPE_SCORE_WPE 6
 #endif
 #ifndef TPE_TAU_TABLE
-#define TPE_TAU_TABLE 25.0
+#define TPE_TAU_TABLE 17.0
 #endif
 constexpr double kTauExtra = TPE_TAU_TABLE;  // exclusion margin (nats) on top of log(M)
 constexpr double kDrawZ = 5.8;       // |z| of an fp32 Box-Muller draw is < 5.77
@@ -468,16 +468,9 @@ __device__ __forceinline__ Windows cell_windows(const tpe_seg& SB, const tpe_seg
                  __builtin_amdgcn_readlane(lo, 32), __builtin_amdgcn_readlane(lo, 48)};
 }
 
-// Row-level reductions (each 16-lane DPP row on its own): max in every lane of
-// the row; the nine P_n sums of the row, lane p holding the sum of P_rev4(p)
-// (wave_sum9_transposed without the cross-row steps).
-__device__ __forceinline__ double row_max_dpp(double v) {
-  v = fmax(v, dpp_d<kDppXor1>(v));
-  v = fmax(v, dpp_d<kDppXor2>(v));
-  v = fmax(v, dpp_d<kDppHalfMirror>(v));
-  v = fmax(v, dpp_d<kDppMirror>(v));
-  return v;
-}
+// Row-level reduction (each 16-lane DPP row on its own): the nine P_n sums
+// of the row, lane p holding the sum of P_rev4(p) (wave_sum9_transposed
+// without the cross-row steps).
 __device__ __forceinline__ double row_sum9_transposed(const double (&P)[9]) {
   const int lane = lane_id();
   double w[16];
@@ -498,7 +491,7 @@ __device__ __forceinline__ double row_sum9_transposed(const double (&P)[9]) {
 // a superset of each cell's own, whose components the exclusion test below
 // drops -- then the wide list; every row walks the same items.
 struct BuildLds {  // the block's four waves' partial expansions of one mixture
-  double m[kBS / kWave][4];   // per wave and row: its scale
+  float m[kBS / kWave][4];       // per wave and row: its share's largest log term (the scale pass)
   double p[kBS / kWave][kWave];  // per wave and lane: its row's sum of P_rev4(lane & 15)
   int bad[kBS / kWave][4];
 };
@@ -517,25 +510,52 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   const int nwin = max(0, k_hi - k_lo + 1);
   const int items = nwin + n_wide;
   itm = max(itm, items);  // (the error bound's summation depth, mix_eps)
-  const int lane = lane_id(), l = lane & 15;
+  const int lane = lane_id(), l = lane & 15, row = lane >> 4;
   // component of work item `it` (window first, then the wide list)
   auto comp = [&](int it) -> int {
     return it < nwin ? k_lo + it : wide_idx[off + (it - nwin)];
   };
-  // One pass: every component inside the window (components the plan's
-  // global bound admits; each satisfies the expansion bound by the choice of
-  // h).  The exponent is formed in fp64, the series and the per-component
-  // tests in fp32, the nine P_n sums in fp64 (a sum of ~10^3 fp32 terms would
-  // carry ~10^3 roundings into the error bound, mix_eps); each lane keeps its
-  // own scale m_l (raised only when a term would exceed e^8 of it) and the
-  // row's lanes are merged at the end.  The next item's coefficients are
-  // loaded before this item's work.
+  const float hf = (float)h, Tf = (float)T;
+  // an item's largest log term over the cell (fp32) and whether it is summed:
+  // window items that are wide come from the list instead; an item below the
+  // plan's floor on the whole cell is left out
+  auto item_max = [&](int it, const double4& c, float& tmax) -> bool {
+    const bool skip = it < nwin && is_wide(S, comp(it), c.y);
+    const float zn = fmaxf(fabsf((float)(y0 - c.x)) - hf, 0.0f) * (float)c.y;
+    tmax = (float)c.z - 0.5f * zn * zn;
+    return !skip && tmax >= Tf;
+  };
+  // Pass 1: the row's scale ml, the largest log term of a summed item over
+  // the cell (all of the cell's items, across the block's waves in coop), so
+  // every summed term e^(v - ml) at the cell centre is <= ~1 and no partial
+  // sum is ever rescaled.  Terms that can matter are >= T >= ml - ~60 (the
+  // plan's floor) and a centre value lies within ~11 of its cell maximum
+  // (admissible h): e^-71 at least, far inside fp32's normal range.
+  float mf = -INFINITY;
+  for (int it = wv * 16 + l; it < items; it += stride) {
+    const double4 c = ld4(coef64, off + comp(it));
+    float t;
+    if (item_max(it, c, t)) mf = fmaxf(mf, t);
+  }
+  mf = fmaxf(mf, dpp_f<kDppXor1>(mf));
+  mf = fmaxf(mf, dpp_f<kDppXor2>(mf));
+  mf = fmaxf(mf, dpp_f<kDppHalfMirror>(mf));
+  mf = fmaxf(mf, dpp_f<kDppMirror>(mf));  // the row's max in every lane of the row
+  if (coop) {
+    if (l == 0) X.m[wv][row] = mf;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) mf = fmaxf(mf, X.m[w][row]);
+  }
+  const double ml = mf == -INFINITY ? 0.0 : (double)mf;
+  // Pass 2: every summed component.  The exponent is formed in fp64, the
+  // series and the per-component tests in fp32, the nine P_n sums in fp64 (a
+  // sum of ~10^3 fp32 terms would carry ~10^3 roundings into the error bound,
+  // mix_eps).  The next item's coefficients are loaded before this item's work.
   double P[kP];
 #pragma unroll
   for (int n = 0; n < kP; ++n) P[n] = 0.0;
-  double ml = -INFINITY;
   bool bad = false;
-  const float hf = (float)h, Tf = (float)T;
   int it = wv * 16 + l;  // the block's four waves split the items, 16 lanes per cell each
   int k = it < items ? comp(it) : 0;
   double4 c = it < items ? ld4(coef64, off + k) : make_double4(0.0, 0.0, 0.0, 0.0);
@@ -543,23 +563,12 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     const int itn = it + stride;
     const int kn = itn < items ? comp(itn) : 0;
     const double4 cn = itn < items ? ld4(coef64, off + kn) : c;
-    // window items that are wide come from the list instead; below the
-    // plan's floor on the whole cell: left out.  Branch-free: an excluded
-    // item adds zero terms.
-    const bool skip = it < nwin && is_wide(S, k, c.y);
+    float tmax;
+    const bool inc = item_max(it, c, tmax);  // (branch-free: an excluded item adds zero terms)
     const double dy = y0 - c.x;
     const float dyf = (float)dy, inv = (float)c.y;
-    const float zn = fmaxf(fabsf(dyf) - hf, 0.0f) * inv;
-    const bool inc = !skip && ((float)c.z - 0.5f * zn * zn >= Tf);
     const double zc = dy * c.y;
     const double v = c.z - 0.5 * zc * zc;
-    const bool up = inc && v > ml + 8.0;
-    if (__any(up)) {  // new scale: rescale the raising lanes' partial sums
-      const double r = up ? ((ml == -INFINITY) ? 0.0 : exp(ml - v)) : 1.0;
-#pragma unroll
-      for (int n = 0; n < kP; ++n) P[n] *= r;
-      ml = up ? v : ml;
-    }
     const float hi2 = hf * inv * inv;
     const float Af = inc ? -dyf * hi2 : 0.0f, B2 = inc ? -hf * hi2 : 0.0f;  // A and 2B
     bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > (float)(kRhoLim * (1.0 + 1e-5)));
@@ -577,39 +586,20 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     k = kn;
     c = cn;
   }
-  const double m0 = row_max_dpp(ml);
-  {
-    const double r = (ml == -INFINITY) ? 0.0 : exp(ml - m0);
-#pragma unroll
-    for (int n = 0; n < kP; ++n) P[n] *= r;
-  }
   static_assert(kP == 9, "row_sum9_transposed folds nine terms");
   const double v = row_sum9_transposed(P);  // lane p of the row: the row's total of P_rev4(p)
   bad = ((__ballot(bad) >> (lane & ~15)) & 0xFFFFull) != 0;
-  // the four waves' partial sums of each row (cell), merged at their largest
-  // scale; wave 0 holds the result
-  double M = m0;
+  // the four waves' partial sums of each row (cell), all at the row's scale
   double tot = v;
   bool anybad = bad;
   if (coop) {
-    const int row = lane >> 4;
-    if (l == 0) {
-      X.m[wv][row] = m0;
-      X.bad[wv][row] = bad;
-    }
+    if (l == 0) X.bad[wv][row] = bad;
     X.p[wv][lane] = v;
     __syncthreads();
-    M = X.m[0][row];
-    for (int w = 1; w < kNW; ++w) M = fmax(M, X.m[w][row]);
-    // the four waves' scale factors: lane l of the row takes wave l & 3's
-    // (one fp64 exp per lane), the row's lanes read them by shuffle
-    static_assert(kNW == 4, "one factor per row lane quad");
-    const double mq = X.m[l & 3][row];
-    const double fq = (mq == -INFINITY) ? 0.0 : exp(mq - M);
     tot = 0.0;
     anybad = false;
     for (int w = 0; w < kNW; ++w) {
-      tot += X.p[w][lane] * __shfl(fq, (lane & ~15) + w, kWave);
+      tot += X.p[w][lane];
       anybad = anybad || X.bad[w][row];
     }
     __syncthreads();  // (X is reused by the next call)
@@ -621,7 +611,7 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     else
       reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (n - kP32) + mix] = (_Float16)(float)tot;
   }
-  m_out = M;
+  m_out = mf == -INFINITY ? -INFINITY : ml;
   return anybad;
 }
 
@@ -663,7 +653,8 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
 // 128-B-per-cell region.
 // ---------------------------------------------------------------------------
 constexpr double kFitTol = 1.0e-6;   // cubic-vs-polynomial bound allowed (nats)
-constexpr int kScoreLanes = 8;       // lanes per cell: 4 nodes, 8 sub-intervals
+constexpr int kScoreLanes = 16;      // lanes per cell: 4 nodes; 8 sub-intervals x 2 mixtures
+constexpr int kSubInt = 8;           // sub-intervals of [-1.0501, 1.0501] the bound covers
 constexpr int kScoreCellsPerBlock = kBS / kScoreLanes;
 constexpr int kScoreBlocks = 256;    // per job (grid-stride over cells)
 constexpr double kUFit = 1.0501;     // |u| the bounds cover (u's fp32 rounding: <= 1.05 (1 + 5 2^-24))
@@ -687,14 +678,14 @@ __host__ __device__ inline double mix_eps(int items, bool coop, double ab) {
   const int K = (items + stride - 1) / stride + 5 + (coop ? 5 : 0);  // fp64 adds into one P_n
   const double E1 = exp(ab), E2 = E1 * E1;
   return 4.4e-7                         // series truncation (tools/table_bounds.py)
-         + 1.0e-10                      // components below the exclusion floor
+         + exp(-kTauExtra) * 1.0001     // components below the exclusion floor (e^-tau of the sum)
          + (10.0 + 4.6e-4 * items) * u  // each term's exponent rounded to fp32
          + 0x1.0p-22                    // v_exp_f32 (checked exhaustively, tpe_check_transcendentals)
          + 5.5 * u * ab                 // A, B rounded to fp32
          + 4.0 * u * ab * E2            // the fp32 series recurrence (4 roundings per step)
          + u * E2                       // P_0..P_5 stored in fp32
          + 1.5e-7 + 0x1.0p-25 * 4.2 * E1  // P_6..P_8 in fp16 (+ subnormal spacing)
-         + (K + 8) * 2.0 * ud * E2;     // fp64 sums, rescale and merge factors of the P_n
+         + (K + 8) * 2.0 * ud * E2;     // fp64 sums of the P_n (one scale per cell: no rescaling)
 }
 
 __device__ __forceinline__ const float4* score_cells_of(const char* region, int64_t cap) {
@@ -765,7 +756,10 @@ __device__ __forceinline__ bool log_taylor(const double (&p)[kP], double c, doub
   return true;
 }
 
-__global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__ jobs,
+#ifndef TPE_TSCORE_WPE  // waves-per-EU target of k_table_score (1: the compiler's choice)
+#define TPE_TSCORE_WPE 1
+#endif
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_TSCORE_WPE))) void k_table_score(const tpe_job* __restrict__ jobs,
                                                      tpe_table* __restrict__ tables,
                                                      float* __restrict__ cells,
                                                      unsigned long long* __restrict__ stats) {
@@ -783,13 +777,14 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
   float4* outs = const_cast<float4*>(score_cells_of(region, J.tbl_cap));
   const int sub = threadIdx.x / kScoreLanes, l = threadIdx.x % kScoreLanes;
   const int gbase = lane_id() & ~(kScoreLanes - 1);  // first lane of this cell's group
+  const int mixl = l / kSubInt, si = l % kSubInt;  // this lane's mixture and sub-interval
   constexpr double kU = (double)kULim;
   const double nd0 = kU * 0.92387953251128674, nd1 = kU * 0.38268343236508978, nd2 = -nd1,
                nd3 = -nd0;
   const double un = l == 0 ? nd0 : l == 1 ? nd1 : l == 2 ? nd2 : nd3;  // (lanes >= 4: unused)
   const float uf = (float)un;
-  constexpr double r = kUFit / kScoreLanes;
-  const double cI = -kUFit + (2 * l + 1) * r;  // this lane's sub-interval centre
+  constexpr double r = kUFit / kSubInt;
+  const double cI = -kUFit + (2 * si + 1) * r;  // this lane's sub-interval centre
   float slope = 0.0f, epsc = 0.0f;  // over this thread's unflagged cells (lane 0 of a group)
   // group-uniform trip count: every lane of a group runs the shuffles
   for (int64_t c = (int64_t)blockIdx.x * kScoreCellsPerBlock + sub; c < nb;
@@ -830,32 +825,43 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
     const double q0 = q.x, q1 = q.y, q2 = q.z, q3 = q.w;
     bool fail = !nodes_ok || !(off == off) || !isfinite(q0) || !isfinite(q1) || !isfinite(q2) ||
                 !isfinite(q3);
-    double bound = INFINITY;
-    if (!fail) {
-      double pbv[kP], pav[kP], lb[kLogD + 1], la[kLogD + 1], lnb = 0.0, lna = 0.0, rb = 0.0,
-             ra = 0.0;
-      cell_coefs(cell, 0, pbv);
-      cell_coefs(cell, 1, pav);
-      const bool okb = log_taylor(pbv, cI, r, lnb, lb, rb);
-      const bool oka = log_taylor(pav, cI, r, lna, la, ra);
-      if (okb && oka) {
-        // the cubic's Taylor coefficients at cI
-        const double qc = ((q3 * cI + q2) * cI + q1) * cI + q0;
-        const double qk[4] = {qc, (3.0 * q3 * cI + 2.0 * q2) * cI + q1, 3.0 * q3 * cI + q2, q3};
-        const double E0 = off + lnb - lna - qc;
-        double sum = fabs(E0), rk = 1.0;
+    // each lane: its mixture's log series on its sub-interval; the partner
+    // lane (l ^ kSubInt) holds the other mixture's on the same sub-interval
+    double lv[kLogD + 1], lnT0 = 0.0, rem = 0.0;
 #pragma unroll
-        for (int k = 1; k <= kLogD; ++k) {
-          rk *= r;
-          const double Ek = lb[k] - la[k] - (k < 4 ? qk[k] : 0.0);
-          sum = fma(fabs(Ek), rk, sum);
-        }
-        // fp64 rounding of the whole computation (magnitudes ~|off| + |ln T0|)
-        const double slack = 1e-13 * (1.0 + fabs(off) + fabs(lnb) + fabs(lna) + fabs(qc));
-        bound = sum + rb + ra + slack;
-      }
+    for (int k = 0; k <= kLogD; ++k) lv[k] = 0.0;
+    bool ok2 = false;
+    if (!fail) {
+      double pv[kP];
+      cell_coefs(cell, mixl, pv);
+      ok2 = log_taylor(pv, cI, r, lnT0, lv, rem);
     }
-    // the cell's bound: the largest of its 8 lanes'
+    const int partner = lane_id() ^ kSubInt;
+    ok2 = ok2 && __shfl(ok2 ? 1 : 0, partner, kWave) != 0;
+    const double sgn = mixl ? -1.0 : 1.0;  // E_k = l_below - l_above - q_k in both lanes
+    const double lno = __shfl(lnT0, partner, kWave), remo = __shfl(rem, partner, kWave);
+    double E[kLogD + 1];
+#pragma unroll
+    for (int k = 1; k <= kLogD; ++k) E[k] = sgn * (lv[k] - __shfl(lv[k], partner, kWave));
+    double bound = INFINITY;
+    if (!fail && ok2) {
+      const double lnb = mixl ? lno : lnT0, lna = mixl ? lnT0 : lno;
+      // the cubic's Taylor coefficients at cI
+      const double qc = ((q3 * cI + q2) * cI + q1) * cI + q0;
+      const double qk[4] = {qc, (3.0 * q3 * cI + 2.0 * q2) * cI + q1, 3.0 * q3 * cI + q2, q3};
+      const double E0 = off + lnb - lna - qc;
+      double sum = fabs(E0), rk = 1.0;
+#pragma unroll
+      for (int k = 1; k <= kLogD; ++k) {
+        rk *= r;
+        const double Ek = E[k] - (k < 4 ? qk[k] : 0.0);
+        sum = fma(fabs(Ek), rk, sum);
+      }
+      // fp64 rounding of the whole computation (magnitudes ~|off| + |ln T0|)
+      const double slack = 1e-13 * (1.0 + fabs(off) + fabs(lnb) + fabs(lna) + fabs(qc));
+      bound = sum + rem + remo + slack;
+    }
+    // the cell's bound: the largest of its lanes'
     float bmax = (float)(bound * (1.0 + 1e-6));
 #pragma unroll
     for (int o = 1; o < kScoreLanes; o <<= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, kWave));

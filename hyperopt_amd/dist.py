@@ -236,3 +236,27 @@ def allreduce_best(results, group=None):
         r.value = float(comb["value"][k])
         r.n_scored = int(comb["n_scored"][k])
     return results
+
+
+def settle_exchange(combined, local_exact, exchange):
+    """The exact-argmax rule of a label-sharded level's exchange.  A rank
+    whose band overflowed (more near-ties than its band tiles hold) sends its
+    fp32 winner with n_scored = -1; the combine propagates the -1 (a label
+    owed an exact decision), so ``combined`` -- the same records on every
+    rank -- shows it to EVERY rank at once.  Then every rank, together and in
+    the same order, runs ``exchange`` once more on ``local_exact()`` (its
+    records after the exact re-score of its overflowed jobs): no rank leaves
+    the level early, none takes the inexact winner, and a level without an
+    overflow costs nothing extra.  ``exchange(records) -> combined records``
+    is the collective (the engine's RCCL max-loc, or an all-gather + combine
+    on gloo)."""
+    if not (np.asarray(combined)["n_scored"] < 0).any():
+        return combined
+    exact = local_exact()
+    if (np.asarray(exact)["n_scored"] < 0).any():
+        raise L.TpeHipError("settle_exchange: a local record is still inexact")
+    out = exchange(exact)
+    if (np.asarray(out)["n_scored"] < 0).any():
+        raise L.TpeHipError("settle_exchange: the second exchange is still inexact")
+    return out
+

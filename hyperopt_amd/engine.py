@@ -33,6 +33,7 @@ from typing import List, Optional
 import numpy as np
 
 from . import _lib as L
+from . import dist as hdist
 
 EPS = 1e-12  # tpe.py:32
 DEFAULT_LF = 25  # tpe.py:36
@@ -45,7 +46,6 @@ BAND_TILE_CAP = 64  # per scorer tile: band entries kept (tpe_score_table_fast's
 LAT_PREFIX = 1 << 16  # lattice argmax: candidates drawn before the early decision
 LAT_SUGGEST_MAX_SLOTS = 1 << 10  # ... for lattices of at most this many slots (all scored)
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
-SORTED_MIN_CAND = 1 << 12  # auto scorer: sorted/pruned path from this many (below: dense)
 SCORERS = ("auto", "dense", "sorted", "table")
 SIDE_KINDS = ("lat", "qfb", "qinj", "cat")  # groups scored on the side stream
 HOST_EVENTS = ("result",)  # events the host waits on (system-scope release kept)
@@ -733,9 +733,12 @@ class Engine:
                 mode = "cont"
                 if not inj(i):
                     if n >= TABLE_MIN_CAND:
-                        mode = "table"
-                    elif n >= SORTED_MIN_CAND and not outputs:
-                        mode = "sorted"
+                        mode = "table"  # fp32 scores, exact argmax (the band re-score)
+                    elif not outputs:
+                        # fp32 draws, exact decision: the fp32 stream scored in
+                        # fp64 (tpe_score_pruned64 with TPE_F_DRAW32), so an
+                        # explicit precision=32 suggest is exact at every size
+                        mode = "pruned64"
             if mode == "sorted" and (inj(i) or outputs):
                 mode = "cont"
             return "cont" if mode == "dense" else mode
@@ -811,6 +814,8 @@ class Engine:
                     J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P)
             elif modes[i] == "pruned64" and inj(i):
                 J["bin_lo"][pos], J["bin_hi"][pos] = _injected_range(w, P, fp32=False)
+            elif modes[i] == "pruned64" and precision == 32:
+                flags |= L.F_DRAW32  # the fp32 stream (the table path's draws)
             elif modes[i] == "sorted":
                 J["bin_lo"][pos], J["bin_hi"][pos] = _support(w, P)
                 J["sort_off"][pos], J["cnt_off"][pos] = sort_off, cnt_off
@@ -854,8 +859,10 @@ class Engine:
         (k_score32, every component), "sorted" (bucketed candidates +
         component pruning; sampled labels without per-candidate outputs),
         "table" (per-cell expansions, tpe_table_build + tpe_score_table) or
-        "auto" (table from TABLE_MIN_CAND candidates, sorted from
-        SORTED_MIN_CAND, dense below; injected candidates dense).
+        "auto" (sampled labels: the table path from TABLE_MIN_CAND candidates,
+        below it the fp32 stream scored exactly in fp64 by tpe_score_pruned64
+        -- so the argmax is exact at every size; with per-candidate outputs or
+        injected candidates: dense).
         ``pruned=False`` is the old spelling of scorer="dense".  fp64 always
         runs the exact dense kernel.  ``posteriors``: fit only, and return the
         fitted mixtures in ``LabelResult.extra`` ("below" / "above" as
@@ -1693,29 +1700,29 @@ class Engine:
         read), so the exchange is run once more on them: a second all-gather
         on the same communicator, in the same order on every rank (no rank
         leaves the level early and none takes an inexact winner)."""
-        if xinfo is None or not (xrec["n_scored"] < 0).any():
+        if xinfo is None:
             return xrec
         torch, lib = self.torch, self.lib
         comm, n_labels, world, slots, stream = xinfo
-        if (best_h["n_scored"] < 0).any():
-            raise L.TpeHipError("exchange fix: a local record is still inexact")
         sp = ctypes.c_void_p(stream)
         BS = L.BEST_DTYPE.itemsize
         dev = self.device
-        d_by = torch.from_numpy(np.ascontiguousarray(best_h).view(np.uint8).copy()).to(dev)
-        d_slot = torch.from_numpy(np.ascontiguousarray(slots, np.int32)).to(dev)
-        d_xl = torch.empty(n_labels * BS, dtype=torch.uint8, device=dev)
-        d_xg = torch.empty(world * n_labels * BS, dtype=torch.uint8, device=dev)
-        d_out = torch.empty(n_labels * BS, dtype=torch.uint8, device=dev)
-        torch.cuda.current_stream(dev).synchronize()  # (the uploads above, on torch's stream)
-        L.check(lib.tpe_best_scatter(d_by.data_ptr(), d_slot.data_ptr(), best_h.size,
-                                     d_xl.data_ptr(), n_labels, sp), "tpe_best_scatter (fix)")
-        L.check(lib.tpe_maxloc_allreduce(d_xl.data_ptr(), d_xg.data_ptr(), d_out.data_ptr(),
-                                         n_labels, comm, sp), "tpe_maxloc_allreduce (fix)")
-        L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
-        out = d_out.cpu().numpy().view(L.BEST_DTYPE).copy()
-        self.exchange_fixes = getattr(self, "exchange_fixes", 0) + 1
-        return out
+
+        def exchange(local):
+            d_by = torch.from_numpy(np.ascontiguousarray(local).view(np.uint8).copy()).to(dev)
+            d_slot = torch.from_numpy(np.ascontiguousarray(slots, np.int32)).to(dev)
+            d_xl = torch.empty(n_labels * BS, dtype=torch.uint8, device=dev)
+            d_xg = torch.empty(world * n_labels * BS, dtype=torch.uint8, device=dev)
+            d_out = torch.empty(n_labels * BS, dtype=torch.uint8, device=dev)
+            torch.cuda.current_stream(dev).synchronize()  # (the uploads above, on torch's stream)
+            L.check(lib.tpe_best_scatter(d_by.data_ptr(), d_slot.data_ptr(), local.size,
+                                         d_xl.data_ptr(), n_labels, sp), "tpe_best_scatter (fix)")
+            L.check(lib.tpe_maxloc_allreduce(d_xl.data_ptr(), d_xg.data_ptr(), d_out.data_ptr(),
+                                             n_labels, comm, sp), "tpe_maxloc_allreduce (fix)")
+            L.hip_check(self._hip.hipStreamSynchronize(sp), "hipStreamSynchronize")
+            self.exchange_fixes = getattr(self, "exchange_fixes", 0) + 1
+            return d_out.cpu().numpy().view(L.BEST_DTYPE).copy()
+        return hdist.settle_exchange(xrec, lambda: best_h, exchange)
 
     def _read_posteriors(self, works, fit_ids, cat, segs, csegs, n_comp, n_p, d_segs, stream,
                          o_p):

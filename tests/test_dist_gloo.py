@@ -203,3 +203,62 @@ def test_rank_without_units_joins_the_gather():
     assert [out[r][0] for r in range(world)] == [1, 1, 1, 0]
     for r in range(world):  # the highest-scoring shard (start 16) wins everywhere
         assert out[r][1] == [(16.0, 17, 0.1 * 17, 24)]
+
+
+def _overflow_worker(rank, world, port, q):
+    """a band overflow on ONE rank of a label-sharded level.  Rank
+    1's first record for label 0 is its fp32 winner with n_scored = -1 (its
+    band tiles overflowed; BAND_TILE_CAP shrunk to 0 gives exactly this on the
+    GPU).  The combine shows the -1 to every rank, every rank settles with a
+    second exchange of its exact records, and all end on the same exact
+    winner -- no rank leaves early, nobody takes the inexact one."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = [0]
+
+    def exchange(rec):
+        calls[0] += 1
+        return hdist._allgather_combine(rec, world)
+
+    first = hdist.empty_records(3)
+    exact = hdist.empty_records(3)
+    if rank == 0:
+        first[0] = exact[0] = (2.0, 10, 0.5, 100)
+        first[1] = exact[1] = (1.0, 11, 0.6, 100)
+    else:
+        first[0] = (2.5, 110, 1.5, -1)       # fp32 winner, owed an exact decision
+        exact[0] = (1.9999, 117, 1.7, 100)   # the exact re-score picks another candidate
+        first[1] = exact[1] = (0.5, 111, 1.6, 100)
+        first[2] = exact[2] = (3.0, 112, 1.8, 100)
+    combined = exchange(first)
+    owed = bool(combined["n_scored"][0] < 0)
+    settled = hdist.settle_exchange(combined, lambda: exact, exchange)
+    # a level without an overflow settles at once (no second collective)
+    clean = exchange(exact)
+    n_before = calls[0]
+    again = hdist.settle_exchange(clean, lambda: exact, exchange)
+    q.put((rank, owed, settled.tolist(), again.tolist(), calls[0] - n_before))
+    dist.destroy_process_group()
+
+
+def test_band_overflow_on_one_rank_settles_everywhere():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overflow_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        owed, settled, again, extra = out[r]
+        assert owed  # every rank saw the -1
+        assert settled == out[0][1]  # the same records everywhere
+        assert settled[0][:3] == (2.0, 10, 0.5) and settled[0][3] == 200  # exact winner
+        assert settled[1][:3] == (1.0, 11, 0.6) and settled[2][:3] == (3.0, 112, 1.8)
+        assert again == settled and extra == 0
