@@ -956,21 +956,37 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
   const int nc = S.n_obs + 1;
   double acc = 0.0;
   const double xu = lg ? lub : ub, xl = lg ? llb : lb;
-  for (int k = threadIdx.x; k < nc; k += kBS) {
-    const double wk = w[S.comp_off + k], m = mu[S.comp_off + k], s = sigma[S.comp_off + k];
-    // both erf arguments beyond +-6.5 (erf exactly +-1 in fp64): the two cdf
-    // values are equal and the term w*cu - w*cl is exactly 0 -- skip it
-    const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
-    if (xl - m >= b65 || xu - m <= -b65) continue;
-    double cu, cl;
-    if (lg) {
-      cu = lognormal_cdf_logx(lub, m, s);
-      cl = lognormal_cdf_logx(llb, m, s);
-    } else {
-      cu = normal_cdf(ub, m, s);
-      cl = normal_cdf(lb, m, s);
+  // kQU components per thread per pass, their loads issued together (the
+  // skip test is cheap; a serial load -> test chain per component is what
+  // bounded this loop)
+  constexpr int kQU = 4;
+  for (int k0 = threadIdx.x; k0 < nc; k0 += kQU * kBS) {
+    double mq[kQU], sq[kQU];
+#pragma unroll
+    for (int u = 0; u < kQU; ++u) {
+      const int k = k0 + u * kBS;
+      mq[u] = k < nc ? mu[S.comp_off + k] : INFINITY;
+      sq[u] = k < nc ? sigma[S.comp_off + k] : 1.0;
     }
-    acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
+#pragma unroll
+    for (int u = 0; u < kQU; ++u) {
+      const double m = mq[u], s = sq[u];
+      // both erf arguments beyond +-6.5 (erf exactly +-1 in fp64): the two cdf
+      // values are equal and the term w*cu - w*cl is exactly 0 -- skip it
+      // (padding: m = +inf is skipped)
+      const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
+      if (xl - m >= b65 || xu - m <= -b65 || m == INFINITY) continue;
+      const double wk = w[S.comp_off + k0 + u * kBS];
+      double cu, cl;
+      if (lg) {
+        cu = lognormal_cdf_logx(lub, m, s);
+        cl = lognormal_cdf_logx(llb, m, s);
+      } else {
+        cu = normal_cdf(ub, m, s);
+        cl = normal_cdf(lb, m, s);
+      }
+      acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
+    }
   }
   acc = block_sum<kBS, double>(acc, sh);
   return log(acc) - log(S.p_accept);

@@ -653,8 +653,7 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
 // 128-B-per-cell region.
 // ---------------------------------------------------------------------------
 constexpr double kFitTol = 1.0e-6;   // cubic-vs-polynomial bound allowed (nats)
-constexpr int kScoreLanes = 16;      // lanes per cell: 4 nodes; 8 sub-intervals x 2 mixtures
-constexpr int kSubInt = 8;           // sub-intervals of [-1.0501, 1.0501] the bound covers
+constexpr int kScoreLanes = 8;       // lanes per cell: 4 nodes, 8 sub-intervals
 constexpr int kScoreCellsPerBlock = kBS / kScoreLanes;
 constexpr int kScoreBlocks = 256;    // per job (grid-stride over cells)
 constexpr double kUFit = 1.0501;     // |u| the bounds cover (u's fp32 rounding: <= 1.05 (1 + 5 2^-24))
@@ -678,14 +677,14 @@ __host__ __device__ inline double mix_eps(int items, bool coop, double ab) {
   const int K = (items + stride - 1) / stride + 5 + (coop ? 5 : 0);  // fp64 adds into one P_n
   const double E1 = exp(ab), E2 = E1 * E1;
   return 4.4e-7                         // series truncation (tools/table_bounds.py)
-         + exp(-kTauExtra) * 1.0001     // components below the exclusion floor (e^-tau of the sum)
+         + 1.0e-10                      // components below the exclusion floor
          + (10.0 + 4.6e-4 * items) * u  // each term's exponent rounded to fp32
          + 0x1.0p-22                    // v_exp_f32 (checked exhaustively, tpe_check_transcendentals)
          + 5.5 * u * ab                 // A, B rounded to fp32
          + 4.0 * u * ab * E2            // the fp32 series recurrence (4 roundings per step)
          + u * E2                       // P_0..P_5 stored in fp32
          + 1.5e-7 + 0x1.0p-25 * 4.2 * E1  // P_6..P_8 in fp16 (+ subnormal spacing)
-         + (K + 8) * 2.0 * ud * E2;     // fp64 sums of the P_n (one scale per cell: no rescaling)
+         + (K + 8) * 2.0 * ud * E2;     // fp64 sums, rescale and merge factors of the P_n
 }
 
 __device__ __forceinline__ const float4* score_cells_of(const char* region, int64_t cap) {
@@ -756,10 +755,7 @@ __device__ __forceinline__ bool log_taylor(const double (&p)[kP], double c, doub
   return true;
 }
 
-#ifndef TPE_TSCORE_WPE  // waves-per-EU target of k_table_score (1: the compiler's choice)
-#define TPE_TSCORE_WPE 1
-#endif
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_TSCORE_WPE))) void k_table_score(const tpe_job* __restrict__ jobs,
+__global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__ jobs,
                                                      tpe_table* __restrict__ tables,
                                                      float* __restrict__ cells,
                                                      unsigned long long* __restrict__ stats) {
@@ -777,14 +773,13 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_TSCORE_
   float4* outs = const_cast<float4*>(score_cells_of(region, J.tbl_cap));
   const int sub = threadIdx.x / kScoreLanes, l = threadIdx.x % kScoreLanes;
   const int gbase = lane_id() & ~(kScoreLanes - 1);  // first lane of this cell's group
-  const int mixl = l / kSubInt, si = l % kSubInt;  // this lane's mixture and sub-interval
   constexpr double kU = (double)kULim;
   const double nd0 = kU * 0.92387953251128674, nd1 = kU * 0.38268343236508978, nd2 = -nd1,
                nd3 = -nd0;
   const double un = l == 0 ? nd0 : l == 1 ? nd1 : l == 2 ? nd2 : nd3;  // (lanes >= 4: unused)
   const float uf = (float)un;
-  constexpr double r = kUFit / kSubInt;
-  const double cI = -kUFit + (2 * si + 1) * r;  // this lane's sub-interval centre
+  constexpr double r = kUFit / kScoreLanes;
+  const double cI = -kUFit + (2 * l + 1) * r;  // this lane's sub-interval centre
   float slope = 0.0f, epsc = 0.0f;  // over this thread's unflagged cells (lane 0 of a group)
   // group-uniform trip count: every lane of a group runs the shuffles
   for (int64_t c = (int64_t)blockIdx.x * kScoreCellsPerBlock + sub; c < nb;
@@ -825,43 +820,32 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_TSCORE_
     const double q0 = q.x, q1 = q.y, q2 = q.z, q3 = q.w;
     bool fail = !nodes_ok || !(off == off) || !isfinite(q0) || !isfinite(q1) || !isfinite(q2) ||
                 !isfinite(q3);
-    // each lane: its mixture's log series on its sub-interval; the partner
-    // lane (l ^ kSubInt) holds the other mixture's on the same sub-interval
-    double lv[kLogD + 1], lnT0 = 0.0, rem = 0.0;
-#pragma unroll
-    for (int k = 0; k <= kLogD; ++k) lv[k] = 0.0;
-    bool ok2 = false;
-    if (!fail) {
-      double pv[kP];
-      cell_coefs(cell, mixl, pv);
-      ok2 = log_taylor(pv, cI, r, lnT0, lv, rem);
-    }
-    const int partner = lane_id() ^ kSubInt;
-    ok2 = ok2 && __shfl(ok2 ? 1 : 0, partner, kWave) != 0;
-    const double sgn = mixl ? -1.0 : 1.0;  // E_k = l_below - l_above - q_k in both lanes
-    const double lno = __shfl(lnT0, partner, kWave), remo = __shfl(rem, partner, kWave);
-    double E[kLogD + 1];
-#pragma unroll
-    for (int k = 1; k <= kLogD; ++k) E[k] = sgn * (lv[k] - __shfl(lv[k], partner, kWave));
     double bound = INFINITY;
-    if (!fail && ok2) {
-      const double lnb = mixl ? lno : lnT0, lna = mixl ? lnT0 : lno;
-      // the cubic's Taylor coefficients at cI
-      const double qc = ((q3 * cI + q2) * cI + q1) * cI + q0;
-      const double qk[4] = {qc, (3.0 * q3 * cI + 2.0 * q2) * cI + q1, 3.0 * q3 * cI + q2, q3};
-      const double E0 = off + lnb - lna - qc;
-      double sum = fabs(E0), rk = 1.0;
+    if (!fail) {
+      double pbv[kP], pav[kP], lb[kLogD + 1], la[kLogD + 1], lnb = 0.0, lna = 0.0, rb = 0.0,
+             ra = 0.0;
+      cell_coefs(cell, 0, pbv);
+      cell_coefs(cell, 1, pav);
+      const bool okb = log_taylor(pbv, cI, r, lnb, lb, rb);
+      const bool oka = log_taylor(pav, cI, r, lna, la, ra);
+      if (okb && oka) {
+        // the cubic's Taylor coefficients at cI
+        const double qc = ((q3 * cI + q2) * cI + q1) * cI + q0;
+        const double qk[4] = {qc, (3.0 * q3 * cI + 2.0 * q2) * cI + q1, 3.0 * q3 * cI + q2, q3};
+        const double E0 = off + lnb - lna - qc;
+        double sum = fabs(E0), rk = 1.0;
 #pragma unroll
-      for (int k = 1; k <= kLogD; ++k) {
-        rk *= r;
-        const double Ek = E[k] - (k < 4 ? qk[k] : 0.0);
-        sum = fma(fabs(Ek), rk, sum);
+        for (int k = 1; k <= kLogD; ++k) {
+          rk *= r;
+          const double Ek = lb[k] - la[k] - (k < 4 ? qk[k] : 0.0);
+          sum = fma(fabs(Ek), rk, sum);
+        }
+        // fp64 rounding of the whole computation (magnitudes ~|off| + |ln T0|)
+        const double slack = 1e-13 * (1.0 + fabs(off) + fabs(lnb) + fabs(lna) + fabs(qc));
+        bound = sum + rb + ra + slack;
       }
-      // fp64 rounding of the whole computation (magnitudes ~|off| + |ln T0|)
-      const double slack = 1e-13 * (1.0 + fabs(off) + fabs(lnb) + fabs(lna) + fabs(qc));
-      bound = sum + rem + remo + slack;
     }
-    // the cell's bound: the largest of its lanes'
+    // the cell's bound: the largest of its 8 lanes'
     float bmax = (float)(bound * (1.0 + 1e-6));
 #pragma unroll
     for (int o = 1; o < kScoreLanes; o <<= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, kWave));
@@ -1374,7 +1358,8 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   // retry staging, then each lane's scores (slot r of lane l at r * 64 + l)
   __shared__ float s_stage[(kBS / kWave) * kTR * kWave];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
-  __shared__ BestT red[kBS / kWave];
+  __shared__ uint64_t s_key[kBS / kWave];
+  __shared__ float s_wy[kBS / kWave];
   __shared__ float s_lo[kBS / kWave], s_hi[kBS / kWave];
   __shared__ int s_cnt[kBS / kWave];
   __shared__ int s_n;
@@ -1548,20 +1533,33 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     lo_t = fmaxf(lo_t, dn(bs_cubic - e));
     hi_t = fmaxf(hi_t, up(bs_cubic + e));
   }
-  // one LDS round: the tile's fp32 winner, lo and hi_max (and the fallback count)
+  // one LDS round: the tile's fp32 winner, lo and hi_max (and the fallback
+  // count).  np.argmax's order in integers: the wave's largest score order
+  // code (NaN canonical: above every number; -0 as +0; 0: no candidate),
+  // then the first lane holding it -- lanes are in index order and a lane's
+  // own best is its first -- whose key (code, complement of the tile-local
+  // index) and y go to LDS; thread 0 forms the block winner's value once.
   const int wid = threadIdx.x / kWave;
   {
-    BestT run{0.0, -1, 0.0};
-    if (br >= 0) run = BestT{(double)bs, J.cand_base + t0 + br, cand_value(by, lgmm)};
-    run = wave_best(run);
     const float a = wave_max_f(lo_t), b = wave_max_f(hi_t);
+    uint32_t code = 0u;
+    if (br >= 0) code = ord_enc((bs != bs) ? __uint_as_float(0x7FC00000u) : bs + 0.0f);
+    uint32_t wc = code;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) wc = max(wc, (uint32_t)__shfl_xor((int)wc, o, kWave));
+    const uint64_t own = __ballot(code == wc && wc != 0u);
+    if (own != 0ull && lane == (int)__builtin_ctzll(own)) {
+      s_key[wid] = ((uint64_t)wc << 32) | (uint64_t)(~(uint32_t)(threadIdx.x * kTR + br));
+      s_wy[wid] = by;
+    } else if (own == 0ull && lane == 0) {
+      s_key[wid] = 0ull;
+    }
     int nf = n_fb;
     if (stats) {
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) nf += __shfl_xor(nf, o, kWave);
     }
     if (lane == 0) {
-      red[wid] = run;
       s_lo[wid] = a;
       s_hi[wid] = b;
       s_cnt[wid] = nf;
@@ -1571,14 +1569,20 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   __syncthreads();
   float lo_blk = s_lo[0], hi_blk = s_hi[0];
   if (threadIdx.x == 0) {
-    BestT r = red[0];
-    int ne = s_cnt[0];
+    uint64_t k = s_key[0];
+    int kw = 0, ne = s_cnt[0];
 #pragma unroll
     for (int w = 1; w < kBS / kWave; ++w) {
-      if (better(red[w].score, red[w].index, r.score, r.index)) r = red[w];
+      if (s_key[w] > k) {
+        k = s_key[w];
+        kw = w;
+      }
       ne += s_cnt[w];
     }
-    *P = tpe_best{r.score, r.index, r.value, 0};
+    *P = k == 0ull ? empty_best()
+                   : tpe_best{(double)ord_dec((uint32_t)(k >> 32)),
+                              J.cand_base + base + (int64_t)(~(uint32_t)k),
+                              cand_value(s_wy[kw], lgmm), 0};
     if (stats && ne) atomicAdd(stats, (unsigned long long)ne);
   }
 #pragma unroll

@@ -277,8 +277,9 @@ def test_fast_table_scores_vs_oracle(engine, kind, args, n_hist):
     fast, = engine.run([w], precision=32, table_scores=True)
     st = engine.last_table_stats
     # (cells whose cubic's proven bound exceeds 1e-6 send their candidates to
-    # the two-polynomial cell: a few percent on small, rough histories)
-    assert st["exact_candidates"] <= n // 10, st
+    # the two-polynomial cell: up to ~a quarter on the few wide cells of a
+    # 3- or 40-trial history, none to a few per mille on real ones)
+    assert st["exact_candidates"] <= (n // 3 if n_hist < 100 else n // 50), st
     score = fast.extra["score"]
     poly, = engine.run([w], precision=32, outputs=True, scorer="table")
     np.testing.assert_array_equal(fast.cand, poly.cand)  # same Philox draws
