@@ -124,7 +124,7 @@ __device__ __forceinline__ double draw64(const Mix& M, uint64_t key, int64_t g, 
 // 4m, sin -> 4m+1), words 2 / 3 those of (4m+2, 4m+3).  Four candidates per
 // call, so the sampler spends half as many Philox rounds (quarter-rate
 // v_mad_u64_u32) per candidate as a pair-per-call scheme.  Retries (bounded
-// labels) take four attempts per call at counter (g, c) in a stream of their
+// labels) take two attempts per call at counter (g, c) in a stream of their
 // own (retry32).  Candidate g's value depends on g alone, whichever kernel
 // draws it.
 __device__ __forceinline__ int comp_of(const Mix& M, uint32_t word) {
@@ -238,34 +238,30 @@ __device__ __forceinline__ float clamp32(float y, bool lo_on, bool hi_on, float 
 }
 
 // Retries of candidate g (bounded labels, attempt 0 rejected): call c >= 1
-// of the retry stream, at counter (g, c), gives attempts 4c-3 .. 4c the way a
-// quad gives attempt 0 of four candidates (each word a component and a
-// residual, the residual pairs Box-Muller); the first accepted one is the
-// draw.  Four attempts per call: at C3's ~7% rejection a rejected candidate
-// almost never needs a second call, so a wave's retry pass is one call deep
-// instead of the longest of its lanes' geometric runs.  After kMaxRetryCalls
-// calls (acceptance below ~1e-77) the last attempt is clamped.
-constexpr uint32_t kMaxRetryCalls = kMaxAttempts / 4;
+// of the retry stream, at counter (g, c), gives attempts 2c-1 and 2c -- words
+// 0 / 1 pick their components, the two words' residuals are the Box-Muller
+// pair's radius / angle -- and the first accepted one is the draw.  Two
+// attempts per call: at C3's ~7% rejection a rejected candidate needs a
+// second call 0.5% of the time, and a wave's retry pass costs one Philox,
+// two component lookups and one Box-Muller pair instead of four lookups and
+// two pairs.  After kMaxRetryCalls calls (acceptance below ~1e-77) the last
+// attempt is clamped.
+constexpr uint32_t kMaxRetryCalls = kMaxAttempts / 2;
 
 __device__ __forceinline__ float retry32(const Mix& M, uint64_t key, int64_t g, bool lo_on,
                                          bool hi_on, float lo, float hi) {
   float y = 0.0f;
   for (uint32_t c = 1; c <= kMaxRetryCalls; ++c) {
     const U4 r = draw_words(key, g, c, kStreamRetry);
-    float mu0, sg0, r0, mu1, sg1, r1, mu2, sg2, r2, mu3, sg3, r3;
+    float mu0, sg0, r0, mu1, sg1, r1;
     comp_res(M, r.x, mu0, sg0, r0);
     comp_res(M, r.y, mu1, sg1, r1);
-    comp_res(M, r.z, mu2, sg2, r2);
-    comp_res(M, r.w, mu3, sg3, r3);
-    float z0, z1, z2, z3;
+    float z0, z1;
     bm_pair(r0, r1, z0, z1);
-    bm_pair(r2, r3, z2, z3);
     const float y0 = fmaf(sg0, z0, mu0), y1 = fmaf(sg1, z1, mu1);
-    const float y2 = fmaf(sg2, z2, mu2), y3 = fmaf(sg3, z3, mu3);
-    const bool a0 = accept32(y0, lo_on, hi_on, lo, hi), a1 = accept32(y1, lo_on, hi_on, lo, hi);
-    const bool a2 = accept32(y2, lo_on, hi_on, lo, hi);
-    y = a0 ? y0 : (a1 ? y1 : (a2 ? y2 : y3));
-    if (a0 || a1 || a2 || accept32(y3, lo_on, hi_on, lo, hi)) return y;
+    const bool a0 = accept32(y0, lo_on, hi_on, lo, hi);
+    y = a0 ? y0 : y1;
+    if (a0 || accept32(y1, lo_on, hi_on, lo, hi)) return y;
   }
   return clamp32(y, lo_on, hi_on, lo, hi);
 }

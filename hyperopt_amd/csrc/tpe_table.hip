@@ -82,7 +82,13 @@ constexpr int kTR = TPE_TR;          // candidates per thread and tile in the sc
 #endif
 constexpr int kTiles = TPE_TILES;    // tiles (kBS * kTR candidates) per scorer block
 constexpr int64_t kTile = (int64_t)kBS * kTR;
-constexpr int kBuildBlocks = 512;    // build blocks per job (grid-stride over cells)
+#ifndef TPE_BUILD_PAIR  // build: two items per lane per pass, summed in fp32 first
+#define TPE_BUILD_PAIR 0
+#endif
+#ifndef TPE_BUILD_BLOCKS
+#define TPE_BUILD_BLOCKS 512
+#endif
+constexpr int kBuildBlocks = TPE_BUILD_BLOCKS;  // build blocks per job (grid-stride over cells)
 constexpr int kCoopCells = 4096;     // labels with at most this many cells build a quad per block
 constexpr float kLn2T = 0.6931471805599453f;
 
@@ -552,10 +558,67 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
   // series and the per-component tests in fp32, the nine P_n sums in fp64 (a
   // sum of ~10^3 fp32 terms would carry ~10^3 roundings into the error bound,
   // mix_eps).  The next item's coefficients are loaded before this item's work.
-  double P[kP];
+  // P_0..P_3 are summed in fp64 (a sum of ~10^2 fp32 terms per lane would
+  // carry ~10^2 roundings into mix_eps), P_4..P_8 in fp32: at most 2 % of the
+  // terms' absolute sum lies there (tools/table_bounds.py), so their rounding
+  // costs mix_eps K 2^-24 0.0198
+  constexpr int kP64 = 4;
+  double P[kP64];
+  float Q[kP - kP64];
 #pragma unroll
-  for (int n = 0; n < kP; ++n) P[n] = 0.0;
+  for (int n = 0; n < kP64; ++n) P[n] = 0.0;
+#pragma unroll
+  for (int n = 0; n < kP - kP64; ++n) Q[n] = 0.0f;
+  auto acc = [&](int n, float t) __attribute__((always_inline)) {
+    if (n < kP64)
+      P[n] += (double)t;
+    else
+      Q[n - kP64] += t;
+  };
   bool bad = false;
+#if TPE_BUILD_PAIR
+  // Two items per lane per pass (it, it + stride): their nine terms are added
+  // in fp32 first (one rounding, u of their absolute sum: mix_eps's pair
+  // term), then once into the fp64 sums -- half the fp64 adds (half-rate on
+  // gfx950) and conversions.
+  auto term = [&](int it2, const double4& c, float& e, float& Af, float& B2) {
+    float tmax;
+    const bool inc = it2 < items && item_max(it2, c, tmax);  // (branch-free)
+    const double dy = y0 - c.x;
+    const float dyf = (float)dy, inv = (float)c.y;
+    const double zc = dy * c.y;
+    const double v = c.z - 0.5 * zc * zc;
+    const float hi2 = hf * inv * inv;
+    Af = inc ? -dyf * hi2 : 0.0f;  // A and 2B
+    B2 = inc ? -hf * hi2 : 0.0f;
+    bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > (float)(kRhoLim * (1.0 + 1e-5)));
+    // the exponent (v - ml) log2 e formed in fp64, rounded once to fp32
+    e = inc ? __builtin_amdgcn_exp2f((float)((v - ml) * kLog2e)) : 0.0f;
+  };
+  const double4 zero4 = make_double4(0.0, 0.0, 0.0, 0.0);
+  for (int it = wv * 16 + l; it < items; it += 2 * stride) {
+    const int it2 = it + stride;
+    const double4 c1 = ld4(coef64, off + comp(it));
+    const double4 c2 = it2 < items ? ld4(coef64, off + comp(it2)) : zero4;
+    float e1, A1, B1, e2, A2, B2;
+    term(it, c1, e1, A1, B1);
+    term(it2, c2, e2, A2, B2);
+    // the series in fp32 (a v_fma_f64 takes twice the cycles of a v_fma_f32
+    // on gfx950: an fp64 recurrence made this kernel 8 % slower)
+    float cm1 = 0.0f, cc1 = e1, cm2 = 0.0f, cc2 = e2;  // e * c_n
+    acc(0, e1 + e2);
+#pragma unroll
+    for (int n = 0; n + 1 < kP; ++n) {
+      const float x1 = fmaf(A1, cc1, B1 * cm1) * (1.0f / (float)(n + 1));
+      const float x2 = fmaf(A2, cc2, B2 * cm2) * (1.0f / (float)(n + 1));
+      acc(n + 1, x1 + x2);
+      cm1 = cc1;
+      cc1 = x1;
+      cm2 = cc2;
+      cc2 = x2;
+    }
+  }
+#else
   int it = wv * 16 + l;  // the block's four waves split the items, 16 lanes per cell each
   int k = it < items ? comp(it) : 0;
   double4 c = it < items ? ld4(coef64, off + k) : make_double4(0.0, 0.0, 0.0, 0.0);
@@ -575,19 +638,23 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     // the term: exponent (v - ml) log2 e formed in fp64, rounded once to fp32
     const float e = inc ? __builtin_amdgcn_exp2f((float)((v - ml) * kLog2e)) : 0.0f;
     float cm = 0.0f, cc = e;  // e * c_n
-    P[0] += (double)e;
+    acc(0, e);
 #pragma unroll
     for (int n = 0; n + 1 < kP; ++n) {
       const float cnx = fmaf(Af, cc, B2 * cm) * (1.0f / (float)(n + 1));
-      P[n + 1] += (double)cnx;
+      acc(n + 1, cnx);
       cm = cc;
       cc = cnx;
     }
     k = kn;
     c = cn;
   }
+#endif
   static_assert(kP == 9, "row_sum9_transposed folds nine terms");
-  const double v = row_sum9_transposed(P);  // lane p of the row: the row's total of P_rev4(p)
+  double Pall[kP];
+#pragma unroll
+  for (int n = 0; n < kP; ++n) Pall[n] = n < kP64 ? P[n] : (double)Q[n - kP64];
+  const double v = row_sum9_transposed(Pall);  // lane p of the row: the row's total of P_rev4(p)
   bad = ((__ballot(bad) >> (lane & ~15)) & 0xFFFFull) != 0;
   // the four waves' partial sums of each row (cell), all at the row's scale
   double tot = v;
@@ -683,6 +750,8 @@ __host__ __device__ inline double mix_eps(int items, bool coop, double ab) {
          + 5.5 * u * ab                 // A, B rounded to fp32
          + 4.0 * u * ab * E2            // the fp32 series recurrence (4 roundings per step)
          + u * E2                       // P_0..P_5 stored in fp32
+         + (TPE_BUILD_PAIR ? u * E2 : 0.0)  // two items' terms added in fp32 before the fp64 sum
+         + (K + 1) * u * 0.0198 * 1.0001  // P_4..P_8 summed in fp32 (tools/table_bounds.py)
          + 1.5e-7 + 0x1.0p-25 * 4.2 * E1  // P_6..P_8 in fp16 (+ subnormal spacing)
          + (K + 8) * 2.0 * ud * E2;     // fp64 sums, rescale and merge factors of the P_n
 }

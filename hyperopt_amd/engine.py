@@ -318,6 +318,67 @@ class DeviceHistory:
         self._ordered = key
 
 
+_LAUNCH_STATE = frozenset(('BS', 'JS', '_hmark', 'band_jobs', 'base', 'cat', 'cnt_off', 'cobs_off', 'csegs', 'd_best', 'd_c32', 'd_c32n', 'd_c64', 'd_ccdf', 'd_cdf', 'd_csegs', 'd_err', 'd_fs', 'd_logp', 'd_mu', 'd_pairs', 'd_pm', 'd_segs', 'd_sig', 'd_sm', 'd_stats', 'd_w', 'd_w32', 'exchange', 'fb_jobs', 'fit_ids', 'g_arr', 'groups', 'h_arr', 'hist_mode', 'histories', 'history', 'inj', 'jobs', 'lat_off', 'lat_ready', 'max_obs', 'n_comp', 'n_jobs', 'n_obs_total', 'n_rows', 'nfs', 'o_cand', 'o_cobs', 'o_fb', 'o_g', 'o_h', 'o_isb', 'o_jobs', 'o_lcnt', 'o_obs', 'o_p', 'o_rows', 'o_slot', 'o_xslot', 'out_off', 'outputs', 'p_pool', 'posteriors', 'precision', 'qfb_off', 'sample_only', 'segs', 'sort_off', 'sorted_fit', 'sp', 'stream', 'table_scores', 'torch', 'works', 'x_comm', 'x_labels', 'x_world'))
+
+
+class _LevelState:
+    """A prepared level's plan, workspace pointers and pack offsets (the locals
+    of Engine.run that its launches read; Engine._launch_level)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def __getattr__(self, name):  # (pointers of paths the level does not take)
+        if name in _LAUNCH_STATE:
+            return None
+        raise AttributeError(name)
+
+
+class _LaunchCtx:
+    """Timer events and cross-stream ordering of one level's launches, issued
+    eagerly or appended to the _OpList being recorded (``cap``)."""
+
+    def __init__(self, eng, stream, timers, timer_groups):
+        self.eng, self.stream, self.timers, self.timer_groups = eng, stream, timers, timer_groups
+        self.cap = None
+
+    def tick(self, name, on=None):
+        if self.timers is None or (self.timer_groups is not None and name not in self.timer_groups):
+            return None
+        if self.cap is not None:
+            return self.cap.record(self.eng._hip, self.stream if on is None else on)
+        e = self.eng.torch.cuda.Event(enable_timing=True)
+        e.record(self.stream if on is None else on)
+        return e
+
+    def tock(self, name, e0, on=None):
+        if e0 is None:
+            return
+        if self.cap is not None:
+            self.cap.timed.append((name, e0, self.tick(name, on)))
+        else:
+            self.timers.setdefault(name, []).append((e0, self.tick(name, on)))
+
+    def stream_order(self, name, src, dst):
+        if isinstance(self.cap, _OpList):
+            self.cap.order(self.eng._event(name), src, dst)
+        else:
+            self.eng._order(name, src, dst)
+
+    def stream_rec(self, name, src):  # event `name` marks `src`'s work so far
+        if isinstance(self.cap, _OpList):
+            self.cap.add(L.OP_EVENT_RECORD, self.eng._event(name), src)
+        else:
+            L.hip_check(self.eng._hip.hipEventRecord(self.eng._event(name), src), "hipEventRecord")
+
+    def stream_wait(self, name, dst):  # `dst` waits for event `name`
+        if isinstance(self.cap, _OpList):
+            self.cap.add(L.OP_STREAM_WAIT, dst, self.eng._event(name))
+        else:
+            L.hip_check(self.eng._hip.hipStreamWaitEvent(dst, self.eng._event(name), 0),
+                        "hipStreamWaitEvent")
+
+
 class Engine:
     """Owns the device workspace; one instance per device (kept by tpe.py)."""
 
@@ -1098,391 +1159,13 @@ class Engine:
                     self.cat_early, self.cat_issue,
                     "off" if timers is None else
                     ("all" if timer_groups is None else frozenset(timer_groups)))
-        cap = None  # _OpList being recorded (tick/tock follow it)
         band_jobs = []  # (first, end) job positions scored by tpe_score_table_fast
+        ctx = _LaunchCtx(self, stream, timers, timer_groups)
+        here = locals()  # (outside the comprehension: its own scope)
+        lv = _LevelState(**{k: v for k, v in here.items() if k in _LAUNCH_STATE})
 
-        def tick(name, on=None):
-            if timers is None or (timer_groups is not None and name not in timer_groups):
-                return None
-            if cap is not None:
-                return cap.record(self._hip, stream if on is None else on)
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(stream if on is None else on)
-            return e
-
-        def tock(name, e0, on=None):
-            if e0 is None:
-                return
-            if cap is not None:
-                cap.timed.append((name, e0, tick(name, on)))
-            else:
-                timers.setdefault(name, []).append((e0, tick(name, on)))
-
-        def stream_order(name, src, dst):
-            if isinstance(cap, _OpList):
-                cap.order(self._event(name), src, dst)
-            else:
-                self._order(name, src, dst)
-
-        def stream_rec(name, src):  # event `name` marks `src`'s work so far
-            if isinstance(cap, _OpList):
-                cap.add(L.OP_EVENT_RECORD, self._event(name), src)
-            else:
-                L.hip_check(self._hip.hipEventRecord(self._event(name), src), "hipEventRecord")
-
-        def stream_wait(name, dst):  # `dst` waits for event `name`
-            if isinstance(cap, _OpList):
-                cap.add(L.OP_STREAM_WAIT, dst, self._event(name))
-            else:
-                L.hip_check(self._hip.hipStreamWaitEvent(dst, self._event(name), 0),
-                            "hipStreamWaitEvent")
-
-        def launch_level(lib=lib):
-            side = None
-            if self.side_stream != "0" and not sample_only and not posteriors and any(
-                    ids for k, ids in groups if k in SIDE_KINDS):
-                if self._side is None:
-                    self._side = torch.cuda.Stream(self.device)
-                side = self._side
-            side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
-            # with the sorted fit the gather only lists the categorical labels'
-            # observations, which only their posterior (side stream) reads: it
-            # runs there, behind an event after the upload, and the main
-            # stream starts with the fit
-            gather_side = hist_mode and histories is None and sorted_fit and \
-                side is not None and bool(cat) and self.cat_early
-            if hist_mode:
-                d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
-                d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
-                gs, gsp = (side, side_p) if gather_side else (None, sp)
-                if gather_side:
-                    stream_order("uploaded", sp, side_p)
-                e0 = tick("gather", gs)
-                g0 = nfs if sorted_fit else 0  # (the sorted fit reads the history itself)
-                if histories is None:
-                    if len(g_arr) > g0:
-                        L.check(lib.tpe_gather_obs(history.vals.data_ptr(),
-                                                   history.active.data_ptr(), history.ld,
-                                                   base + o_rows if o_rows is not None else None,
-                                                   _V("n_rows", n_rows), base + o_isb,
-                                                   base + o_g + g0 * L.GATHER_DTYPE.itemsize,
-                                                   g_arr.ctypes.data + g0 * L.GATHER_DTYPE.itemsize,
-                                                   len(g_arr) - g0, d_obs, d_cobs, d_err, gsp),
-                                "tpe_gather_obs")
-                else:
-                    L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
-                                                     len(h_arr), base, base + o_g,
-                                                     g_arr.ctypes.data_as(ctypes.c_void_p),
-                                                     len(g_arr), d_obs, d_cobs, d_err, sp),
-                            "tpe_gather_obs_multi")
-                tock("gather", e0, gs)
-            else:
-                d_obs, d_cobs = base + o_obs, base + o_cobs
-
-            _hmark('upload+gather')
-            # side stream (TPE_SIDE_STREAM != "0"): quantized and categorical work
-            # overlaps the continuous pipeline; the categorical posterior starts on
-            # it as soon as the lists are gathered (it needs nothing else)
-            # main-stream issue order: gather, fit, table build, scorers; the
-            # side stream's launches are issued after the table build (host
-            # launches cost a few us each: at a one-eighth label share the main
-            # stream would otherwise idle behind them) and start
-            # from one event recorded on the main stream after the fit (the
-            # categorical posterior could start at the gather, but the side
-            # stream has the slack and the fork costs two more host calls)
-            d_cand = base + o_cand
-            d_bl = d_al = d_x = None
-            d_sc = d_eps = None
-            if outputs:
-                d_bl = self._buf("out_bl", 8 * max(out_off, 1))
-                d_al = self._buf("out_al", 8 * max(out_off, 1))
-                d_x = self._buf("out_x", 8 * max(out_off, 1))
-            elif table_scores:
-                d_sc = self._buf("out_sc", 8 * max(out_off, 1))
-                d_x = self._buf("out_x", 8 * max(out_off, 1))
-                d_eps = self._buf("out_eps", 8 * max(out_off, 1))
-            table_calls = []
-            band_jobs.clear()
-            jobs_ptr = jobs.__array_interface__["data"][0]
-            joined = side is None
-            side_started = side is None
-            cat_started = False
-
-            def cat_fit():  # on the side stream (after its fork)
-                e0 = tick("cat_fit", side)
-                d_p = base + o_p  # the posterior is formed in place in the staged pool
-                L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
-                                              int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
-                                              side_p), "tpe_cat_posterior")
-                tock("cat_fit", e0, side)
-
-            def launch_group(g, stage):
-                nonlocal joined, side_started, cat_started
-                kind, ids = groups[g]
-                if not ids:
-                    return
-                if cat_early and kind == "cat" and not cat_started:
-                    cat_started = True  # the categorical work needs only the gather
-                    if not gather_side:  # (else the gather ran on the side stream)
-                        stream_wait("gathered", side_p)
-                    cat_fit()
-                if not side_started and kind in SIDE_KINDS and not (cat_early and kind == "cat"):
-                    side_started = True  # the side stream's groups that need the fit
-                    stream_wait("fitted", side_p)
-                    if cat and not cat_early:
-                        cat_fit()
-                if sample_only:
-                    if kind in ("cont", "lat", "qfb"):
-                        a, b = _slice_of(groups, g)
-                        hj = jobs[a:b]
-                        L.check(lib.tpe_sample(base + o_jobs + a * L.JOB_DTYPE.itemsize,
-                                               hj.ctypes.data_as(ctypes.c_void_p), b - a, d_segs,
-                                               d_mu, d_sig, d_cdf, precision, d_x, sp), "tpe_sample")
-                    return
-                a, b = _slice_of(groups, g)
-                hj = jobs[a:b]
-                hjp = jobs_ptr + a * JS  # host copy of the slice (plain int: no ctypes object)
-                dj = base + o_jobs + a * JS
-                db = d_best + a * BS
-                nj = b - a
-                on_side = side is not None and kind in SIDE_KINDS
-                ks = side_p if on_side else sp
-                kst = side if on_side else None
-                pname = "partial_side" if on_side else "partial"
-                e0 = tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst) \
-                    if stage != "score" else None
-                if kind == "cont":
-                    npart = lib.tpe_score_partials(hjp, nj)
-                    d_part = self._buf("partial", 32 * max(npart, 1))
-                    L.check(lib.tpe_score_continuous(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
-                                                     d_c64, d_c32, d_cand, precision, d_bl, d_al, d_x,
-                                                     d_part, npart, db, sp), "tpe_score_continuous")
-                elif kind == "sorted":
-                    npart = lib.tpe_score_partials(hjp, nj) * 2
-                    d_part = self._buf("partial", 32 * max(npart, 1))
-                    d_cnt = self._buf("sort_cnt", 8 * max(cnt_off, 1))
-                    d_gen = self._buf("sort_gen", 4 * max(sort_off, 1))
-                    d_sx = self._buf("sort_x", 4 * max(sort_off, 1))
-                    d_si = self._buf("sort_i", 4 * max(sort_off, 1))
-                    L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
-                                                    d_gen, d_sx, d_si, sp), "tpe_sort_candidates")
-                    tock("sort", e0)
-                    e0 = tick("sorted")
-                    L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,
-                                                 d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
-                            "tpe_score_sorted")
-                elif kind == "table":
-                    # (stage "build" / "score": the two halves of an early-built group)
-                    npart = lib.tpe_table_partials(hjp, nj)
-                    d_part = self._buf("partial", 32 * max(npart, 1))
-                    d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
-                    d_cells = self._buf("cells", 128 * int(hj["tbl_off"].max() + TABLE_CAP
-                                                           - hj["tbl_off"].min()))
-                    d_cells -= 128 * int(hj["tbl_off"].min())
-                    d_rh = self._buf("reach_hi", 8 * n_comp)
-                    d_rl = self._buf("reach_lo", 8 * n_comp)
-                    d_wide = self._buf("wide_idx", 4 * n_comp)
-                    max_comp = _V("max_comp", max_obs + 1)
-                    d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
-                    if stage != "score":
-                        L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64,
-                                                    max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab,
-                                                    d_cells, d_stats, sp), "tpe_table_build")
-                        tock("table_build", e0)
-                    if stage == "build":
-                        return
-                    if not joined and self.side_stream == "2":
-                        stream_order("joined", side_p, sp)
-                        joined = True
-                    e0 = tick("table")
-                    if outputs or inj(ids[0]) or self.table_scorer == "poly":
-                        L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32,
-                                                    d_tab, d_cells, d_cand, d_bl, d_al, d_x, d_part,
-                                                    npart, db, d_stats, sp), "tpe_score_table")
-                    else:  # the suggest path: one score cubic per candidate, exact argmax
-                        ctl_b, work_b = ctypes.c_int64(0), ctypes.c_int64(0)
-                        nbb = lib.tpe_band_bytes(hjp, nj, ctypes.byref(ctl_b),
-                                                 ctypes.byref(work_b))
-                        d_band = self._buf("band", nbb)
-                        d_bctl = self._buf("band_ctl", ctl_b.value)
-                        d_bwork = self._zbuf("band_work", work_b.value)
-                        L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
-                                                         d_c32, d_tab, d_cells, d_band, d_bctl,
-                                                         d_sc, d_x, d_eps, d_part, npart,
-                                                         BAND_TILE_CAP, d_stats, sp),
-                                "tpe_score_table_fast")
-                        tock("table", e0)
-                        self._tables_slice = (a, b)  # (the test hook reads these tables back)
-                        e0 = tick("band")
-                        L.check(lib.tpe_band_rescore(dj, hjp, nj, d_segs, d_c64, d_tab, d_band,
-                                                     d_bctl, d_part, npart, db, d_bwork, sp),
-                                "tpe_band_rescore")
-                        tock("band", e0)
-                        e0 = None
-                        band_jobs.append((a, b))
-                    table_calls.append(nj)
-                elif kind == "pruned64":
-                    npart = lib.tpe_pruned64_partials(hjp, nj)
-                    d_part = self._buf("partial", 32 * max(npart, 1))
-                    d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
-                    d_rh = self._buf("reach_hi", 8 * n_comp)
-                    d_rl = self._buf("reach_lo", 8 * n_comp)
-                    d_wide = self._buf("wide_idx", 4 * n_comp)
-                    max_comp = _V("max_comp", max_obs + 1)
-                    d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
-                    L.check(lib.tpe_score_pruned64(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c64,
-                                                   max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab, d_cand,
-                                                   d_bl, d_al, d_x, d_part, npart, db, sp),
-                            "tpe_score_pruned64")
-                elif kind == "lat":
-                    d_vals = self._buf("lat_vals", 8 * lat_off)
-                    d_first = self._buf("lat_first", 8 * lat_off)
-                    if lat_ready:
-                        d_slot, d_cnt = base + o_slot, base + o_lcnt
-                    else:
-                        d_slot = self._buf("lat_slot", 8 * lat_off)
-                        d_cnt = self._buf("lat_cnt", 8 * nj)
-                    max_vals = int(hj["lat_n"].max())
-                    if self.lat_prefix and max_vals <= LAT_SUGGEST_MAX_SLOTS and \
-                            int(hj["n_cand"].max()) > self.lat_prefix:
-                        # prefix first: the rest of a stream only where an unseen
-                        # value could still win (tpe_lattice_suggest)
-                        npart = nj * max_vals
-                        d_part = self._buf(pname, 32 * npart)
-                        d_need = self._buf("lat_need", 4 * nj)
-                        L.check(lib.tpe_lattice_suggest(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
-                                                        d_slot, self.lat_prefix, d_part, npart,
-                                                        d_need, db, d_err, ks),
-                                "tpe_lattice_suggest")
-                    else:
-                        L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
-                                                       d_slot, d_err, ks), "tpe_lattice_sample")
-                        L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt,
-                                                        ks), "tpe_lattice_compact")
-                        npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                        d_part = self._buf(pname, 32 * max(npart, 1))
-                        L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig,
-                                                        d_vals, d_first, d_cnt, max_vals, None, None,
-                                                        d_part, npart, db, d_err, ks),
-                                "tpe_score_quantized")
-                elif kind in ("qfb", "qinj"):
-                    vals = d_cand
-                    if kind == "qfb":
-                        vals = self._buf("q_cand", 8 * max(qfb_off, 1))
-                        L.check(lib.tpe_sample(base + o_fb, fb_jobs.ctypes.data_as(ctypes.c_void_p),
-                                               nj, d_segs, d_mu, d_sig, d_cdf, 64, vals, ks),
-                                "tpe_sample")
-                    max_vals = int(hj["n_cand"].max())
-                    npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                    d_part = self._buf(pname, 32 * max(npart, 1))
-                    L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, vals, None,
-                                                    None, max_vals, d_bl, d_al, d_part, npart, db,
-                                                    d_err, ks), "tpe_score_quantized")
-                else:
-                    npart = lib.tpe_categorical_partials(hjp, nj)
-                    d_part = self._buf(pname, 32 * max(npart, 1))
-                    if self.lat_prefix and not inj(ids[0]) and d_bl is None and d_x is None and \
-                            int(hj["n_cand"].max()) > self.lat_prefix:
-                        # prefix first: the rest of a stream only where an unseen
-                        # better category could still be drawn (tpe_categorical_suggest)
-                        d_need = self._buf("cat_need", 4 * nj)
-                        L.check(lib.tpe_categorical_suggest(dj, hjp, nj, d_csegs, d_logp, d_ccdf,
-                                                            self.lat_prefix, d_part, npart, d_need,
-                                                            db, ks), "tpe_categorical_suggest")
-                    else:
-                        L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf,
-                                                          d_cand, d_bl, d_al, d_x, d_part, npart,
-                                                          db, ks), "tpe_score_categorical")
-                tock(kind, e0, kst)
-
-            # categorical labels need only the gathered lists: with cat_early
-            # the side stream starts their posterior and scoring from an event
-            # recorded after the gather, so they run beside the latency-bound
-            # fit kernels instead of the VALU-bound table build and scorer
-            # (issued on the host after the fit's launches: the fit is not
-            # delayed, and the table build still reaches the GPU before the
-            # fit ends)
-            cat_early = side is not None and bool(cat) and self.cat_early
-            if cat_early:
-                if not gather_side:
-                    stream_rec("gathered", sp)
-                if self.cat_issue == "pre":  # issued before the fit's launches
-                    for g, (k, ids) in enumerate(groups):
-                        if k == "cat" and ids:
-                            launch_group(g, "all")
-            # ---- posterior fit ------------------------------------------------------
-            if fit_ids and sorted_fit:
-                e0 = tick("fit")
-                d_fss = self._buf("fit_sorted_scratch",
-                                  lib.tpe_fit_sorted_scratch_bytes(len(segs), n_rows))
-                L.check(lib.tpe_fit_sorted(history.vals.data_ptr(), history.active.data_ptr(),
-                                           history.ld, history.order.data_ptr(),
-                                           _V("n_rows", n_rows),
-                                           base + o_isb, base + o_g, g_arr.ctypes.data, d_segs,
-                                           len(segs), d_fss, d_w, d_mu, d_sig, d_cdf, d_c64,
-                                           d_c32, d_err, sp), "tpe_fit_sorted")
-                tock("fit", e0)
-            elif fit_ids:
-                e0 = tick("fit")
-                L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), _V("max_obs", max_obs),
-                                           _V("n_obs_total", n_obs_total),
-                                           d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n, d_w32,
-                                           d_pm, d_sm, sp), "tpe_parzen_fit")
-                tock("fit", e0)
-
-            if cat and side is None:
-                cat_fit()
-
-            if posteriors:
-                return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
-                                             d_segs, stream, o_p), True
-
-            _hmark('jobs')
-
-            _hmark('fit')
-            # ---- scoring, one call per group ----------------------------------------
-            # quantized and categorical groups go to the side stream (after the job
-            # table has landed); continuous groups stay on `stream`
-            if side is not None:  # quantized groups need the continuous fit
-                stream_rec("fitted", sp)
-            # launch order: the first sampled table group's build (the main
-            # stream's next kernels after the fit), then the side groups, then
-            # the main-stream scorers -- the host issues launches at a few us
-            # each, and at a one-eighth label share the main stream would
-            # otherwise sit idle behind the side stream's launches
-            g_order = [(g, "all") for g in range(len(groups))]
-            early = None
-            tgroups = [g for g, (k, ids) in enumerate(groups) if k == "table" and ids]
-            if side is not None:
-                if len(tgroups) == 1 and not inj(groups[tgroups[0]][1][0]):
-                    early = tgroups[0]  # (one table group: the workspace tables are its own)
-                side_gs = [g for g in range(len(groups)) if groups[g][0] in SIDE_KINDS]
-                # categorical groups first, issued right after the fit's
-                # launches (they wait for the gather only, so they run beside
-                # the fit; the table build is still issued before the fit ends)
-                cat_gs = [g for g in side_gs if cat_early and groups[g][0] == "cat"]
-                pre = [(g, "all") for g in cat_gs] if self.cat_issue == "post" else []
-                late = [(g, "all") for g in cat_gs] if self.cat_issue == "late" else []
-                g_order = pre + ([(early, "build")] if early is not None else []) + late + \
-                    [(g, "all") for g in side_gs if g not in cat_gs] + \
-                    [(g, "score" if g == early else "all") for g in range(len(groups))
-                     if groups[g][0] not in SIDE_KINDS]
-            for g, stage in g_order:
-                launch_group(g, stage)
-
-            if not side_started:  # (no side group: only the categorical posterior)
-                if cat and not cat_early:
-                    cat_fit()
-            if not joined:  # join before the readback
-                stream_order("joined", side_p, sp)
-            if exchange is not None:  # label-sharded level: the cross-rank argmax
-                d_xl = self._buf("xchg_local", x_labels * BS)
-                d_xg = self._buf("xchg_gathered", x_world * x_labels * BS)
-                L.check(lib.tpe_best_scatter(d_best, base + o_xslot, n_jobs, d_xl, x_labels, sp),
-                        "tpe_best_scatter")
-                L.check(lib.tpe_maxloc_allreduce(d_xl, d_xg, d_best + n_jobs * BS, x_labels,
-                                                 x_comm, sp), "tpe_maxloc_allreduce")
-            return table_calls, False
+        def launch_level(lib=None):
+            return self._launch_level(lv, ctx, lib)
 
         nbytes = 64 + n_jobs * BS + xbytes  # the result block read back at the end
         ops = None
@@ -1495,12 +1178,12 @@ class Engine:
                 rec = _OpList(self.lib)
                 dst, src, nb = self._staged
                 rec.add(L.OP_MEMCPY, dst, src, _V("pack_size", nb), L.H2D, sp)
-                cap = rec
+                ctx.cap = rec
                 try:
                     rec.table_calls, _ = launch_level(rec)
                     rec.band_jobs = list(band_jobs)
                 finally:
-                    cap = None
+                    ctx.cap = None
                 pin = self._res_pinned(nbytes)
                 rec.add(L.OP_MEMCPY, pin.data_ptr(), d_res, nbytes, L.D2H, sp)
                 if batch is not None:
@@ -1594,6 +1277,375 @@ class Engine:
                                   xbytes, groups, table_calls, outputs, table_scores, out_off,
                                   works, order, cont, modes, _hmark, xinfo)
 
+
+    def _launch_level(self, lv, ctx, lib=None):
+        """The level's launches, in stream order: the body of run() for a prepared
+        level (``lv``: its plan, workspace pointers and pack offsets; ``ctx``: the
+        timer / stream-ordering helpers, which follow a recording _OpList).
+        ``lib`` is the library, or the _OpList the launches are recorded into.
+        Returns (table_calls, posteriors_done)."""
+        if lib is None:
+            lib = self.lib
+        BS, JS, _hmark, band_jobs, base, cat = lv.BS, lv.JS, lv._hmark, lv.band_jobs, lv.base, lv.cat
+        cnt_off, cobs_off, csegs, d_best, d_c32, d_c32n = lv.cnt_off, lv.cobs_off, lv.csegs, lv.d_best, lv.d_c32, lv.d_c32n
+        d_c64, d_ccdf, d_cdf, d_csegs, d_err, d_fs = lv.d_c64, lv.d_ccdf, lv.d_cdf, lv.d_csegs, lv.d_err, lv.d_fs
+        d_logp, d_mu, d_pairs, d_pm, d_segs, d_sig = lv.d_logp, lv.d_mu, lv.d_pairs, lv.d_pm, lv.d_segs, lv.d_sig
+        d_sm, d_stats, d_w, d_w32, exchange, fb_jobs = lv.d_sm, lv.d_stats, lv.d_w, lv.d_w32, lv.exchange, lv.fb_jobs
+        fit_ids, g_arr, groups, h_arr, hist_mode, histories = lv.fit_ids, lv.g_arr, lv.groups, lv.h_arr, lv.hist_mode, lv.histories
+        history, inj, jobs, lat_off, lat_ready, max_obs = lv.history, lv.inj, lv.jobs, lv.lat_off, lv.lat_ready, lv.max_obs
+        n_comp, n_jobs, n_obs_total, n_rows, nfs, o_cand = lv.n_comp, lv.n_jobs, lv.n_obs_total, lv.n_rows, lv.nfs, lv.o_cand
+        o_cobs, o_fb, o_g, o_h, o_isb, o_jobs = lv.o_cobs, lv.o_fb, lv.o_g, lv.o_h, lv.o_isb, lv.o_jobs
+        o_lcnt, o_obs, o_p, o_rows, o_slot, o_xslot = lv.o_lcnt, lv.o_obs, lv.o_p, lv.o_rows, lv.o_slot, lv.o_xslot
+        out_off, outputs, p_pool, posteriors, precision, qfb_off = lv.out_off, lv.outputs, lv.p_pool, lv.posteriors, lv.precision, lv.qfb_off
+        sample_only, segs, sort_off, sorted_fit, sp, stream = lv.sample_only, lv.segs, lv.sort_off, lv.sorted_fit, lv.sp, lv.stream
+        table_scores, torch, works, x_comm, x_labels, x_world = lv.table_scores, lv.torch, lv.works, lv.x_comm, lv.x_labels, lv.x_world
+        tick, tock, stream_order = ctx.tick, ctx.tock, ctx.stream_order
+        stream_rec, stream_wait = ctx.stream_rec, ctx.stream_wait
+        side = None
+        if self.side_stream != "0" and not sample_only and not posteriors and any(
+                ids for k, ids in groups if k in SIDE_KINDS):
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            side = self._side
+        side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
+        # with the sorted fit the gather only lists the categorical labels'
+        # observations, which only their posterior (side stream) reads: it
+        # runs there, behind an event after the upload, and the main
+        # stream starts with the fit
+        gather_side = hist_mode and histories is None and sorted_fit and \
+            side is not None and bool(cat) and self.cat_early
+        if hist_mode:
+            d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
+            d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
+            gs, gsp = (side, side_p) if gather_side else (None, sp)
+            if gather_side:
+                stream_order("uploaded", sp, side_p)
+            e0 = tick("gather", gs)
+            g0 = nfs if sorted_fit else 0  # (the sorted fit reads the history itself)
+            if histories is None:
+                if len(g_arr) > g0:
+                    L.check(lib.tpe_gather_obs(history.vals.data_ptr(),
+                                               history.active.data_ptr(), history.ld,
+                                               base + o_rows if o_rows is not None else None,
+                                               _V("n_rows", n_rows), base + o_isb,
+                                               base + o_g + g0 * L.GATHER_DTYPE.itemsize,
+                                               g_arr.ctypes.data + g0 * L.GATHER_DTYPE.itemsize,
+                                               len(g_arr) - g0, d_obs, d_cobs, d_err, gsp),
+                            "tpe_gather_obs")
+            else:
+                L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
+                                                 len(h_arr), base, base + o_g,
+                                                 g_arr.ctypes.data_as(ctypes.c_void_p),
+                                                 len(g_arr), d_obs, d_cobs, d_err, sp),
+                        "tpe_gather_obs_multi")
+            tock("gather", e0, gs)
+        else:
+            d_obs, d_cobs = base + o_obs, base + o_cobs
+
+        _hmark('upload+gather')
+        # side stream (TPE_SIDE_STREAM != "0"): quantized and categorical work
+        # overlaps the continuous pipeline; the categorical posterior starts on
+        # it as soon as the lists are gathered (it needs nothing else)
+        # main-stream issue order: gather, fit, table build, scorers; the
+        # side stream's launches are issued after the table build (host
+        # launches cost a few us each: at a one-eighth label share the main
+        # stream would otherwise idle behind them, DESIGN.md 6) and start
+        # from one event recorded on the main stream after the fit (the
+        # categorical posterior could start at the gather, but the side
+        # stream has the slack and the fork costs two more host calls)
+        d_cand = base + o_cand
+        d_bl = d_al = d_x = None
+        d_sc = d_eps = None
+        if outputs:
+            d_bl = self._buf("out_bl", 8 * max(out_off, 1))
+            d_al = self._buf("out_al", 8 * max(out_off, 1))
+            d_x = self._buf("out_x", 8 * max(out_off, 1))
+        elif table_scores:
+            d_sc = self._buf("out_sc", 8 * max(out_off, 1))
+            d_x = self._buf("out_x", 8 * max(out_off, 1))
+            d_eps = self._buf("out_eps", 8 * max(out_off, 1))
+        table_calls = []
+        band_jobs.clear()
+        jobs_ptr = jobs.__array_interface__["data"][0]
+        joined = side is None
+        side_started = side is None
+        cat_started = False
+
+        def cat_fit():  # on the side stream (after its fork)
+            e0 = tick("cat_fit", side)
+            d_p = base + o_p  # the posterior is formed in place in the staged pool
+            L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
+                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
+                                          side_p), "tpe_cat_posterior")
+            tock("cat_fit", e0, side)
+
+        def launch_group(g, stage):
+            nonlocal joined, side_started, cat_started
+            kind, ids = groups[g]
+            if not ids:
+                return
+            if cat_early and kind == "cat" and not cat_started:
+                cat_started = True  # the categorical work needs only the gather
+                if not gather_side:  # (else the gather ran on the side stream)
+                    stream_wait("gathered", side_p)
+                cat_fit()
+            if not side_started and kind in SIDE_KINDS and not (cat_early and kind == "cat"):
+                side_started = True  # the side stream's groups that need the fit
+                stream_wait("fitted", side_p)
+                if cat and not cat_early:
+                    cat_fit()
+            if sample_only:
+                if kind in ("cont", "lat", "qfb"):
+                    a, b = _slice_of(groups, g)
+                    hj = jobs[a:b]
+                    L.check(lib.tpe_sample(base + o_jobs + a * L.JOB_DTYPE.itemsize,
+                                           hj.ctypes.data_as(ctypes.c_void_p), b - a, d_segs,
+                                           d_mu, d_sig, d_cdf, precision, d_x, sp), "tpe_sample")
+                return
+            a, b = _slice_of(groups, g)
+            hj = jobs[a:b]
+            hjp = jobs_ptr + a * JS  # host copy of the slice (plain int: no ctypes object)
+            dj = base + o_jobs + a * JS
+            db = d_best + a * BS
+            nj = b - a
+            on_side = side is not None and kind in SIDE_KINDS
+            ks = side_p if on_side else sp
+            kst = side if on_side else None
+            pname = "partial_side" if on_side else "partial"
+            e0 = tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst) \
+                if stage != "score" else None
+            if kind == "cont":
+                npart = lib.tpe_score_partials(hjp, nj)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                L.check(lib.tpe_score_continuous(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
+                                                 d_c64, d_c32, d_cand, precision, d_bl, d_al, d_x,
+                                                 d_part, npart, db, sp), "tpe_score_continuous")
+            elif kind == "sorted":
+                npart = lib.tpe_score_partials(hjp, nj) * 2
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_cnt = self._buf("sort_cnt", 8 * max(cnt_off, 1))
+                d_gen = self._buf("sort_gen", 4 * max(sort_off, 1))
+                d_sx = self._buf("sort_x", 4 * max(sort_off, 1))
+                d_si = self._buf("sort_i", 4 * max(sort_off, 1))
+                L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
+                                                d_gen, d_sx, d_si, sp), "tpe_sort_candidates")
+                tock("sort", e0)
+                e0 = tick("sorted")
+                L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,
+                                             d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
+                        "tpe_score_sorted")
+            elif kind == "table":
+                # (stage "build" / "score": the two halves of an early-built group)
+                npart = lib.tpe_table_partials(hjp, nj)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
+                d_cells = self._buf("cells", 128 * int(hj["tbl_off"].max() + TABLE_CAP
+                                                       - hj["tbl_off"].min()))
+                d_cells -= 128 * int(hj["tbl_off"].min())
+                d_rh = self._buf("reach_hi", 8 * n_comp)
+                d_rl = self._buf("reach_lo", 8 * n_comp)
+                d_wide = self._buf("wide_idx", 4 * n_comp)
+                max_comp = _V("max_comp", max_obs + 1)
+                d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
+                if stage != "score":
+                    L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64,
+                                                max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab,
+                                                d_cells, d_stats, sp), "tpe_table_build")
+                    tock("table_build", e0)
+                if stage == "build":
+                    return
+                if not joined and self.side_stream == "2":
+                    stream_order("joined", side_p, sp)
+                    joined = True
+                e0 = tick("table")
+                if outputs or inj(ids[0]) or self.table_scorer == "poly":
+                    L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32,
+                                                d_tab, d_cells, d_cand, d_bl, d_al, d_x, d_part,
+                                                npart, db, d_stats, sp), "tpe_score_table")
+                else:  # the suggest path: one score cubic per candidate, exact argmax
+                    ctl_b, work_b = ctypes.c_int64(0), ctypes.c_int64(0)
+                    nbb = lib.tpe_band_bytes(hjp, nj, ctypes.byref(ctl_b),
+                                             ctypes.byref(work_b))
+                    d_band = self._buf("band", nbb)
+                    d_bctl = self._buf("band_ctl", ctl_b.value)
+                    d_bwork = self._zbuf("band_work", work_b.value)
+                    L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
+                                                     d_c32, d_tab, d_cells, d_band, d_bctl,
+                                                     d_sc, d_x, d_eps, d_part, npart,
+                                                     BAND_TILE_CAP, d_stats, sp),
+                            "tpe_score_table_fast")
+                    tock("table", e0)
+                    self._tables_slice = (a, b)  # (the test hook reads these tables back)
+                    e0 = tick("band")
+                    L.check(lib.tpe_band_rescore(dj, hjp, nj, d_segs, d_c64, d_tab, d_band,
+                                                 d_bctl, d_part, npart, db, d_bwork, sp),
+                            "tpe_band_rescore")
+                    tock("band", e0)
+                    e0 = None
+                    band_jobs.append((a, b))
+                table_calls.append(nj)
+            elif kind == "pruned64":
+                npart = lib.tpe_pruned64_partials(hjp, nj)
+                d_part = self._buf("partial", 32 * max(npart, 1))
+                d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
+                d_rh = self._buf("reach_hi", 8 * n_comp)
+                d_rl = self._buf("reach_lo", 8 * n_comp)
+                d_wide = self._buf("wide_idx", 4 * n_comp)
+                max_comp = _V("max_comp", max_obs + 1)
+                d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
+                L.check(lib.tpe_score_pruned64(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c64,
+                                               max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab, d_cand,
+                                               d_bl, d_al, d_x, d_part, npart, db, sp),
+                        "tpe_score_pruned64")
+            elif kind == "lat":
+                d_vals = self._buf("lat_vals", 8 * lat_off)
+                d_first = self._buf("lat_first", 8 * lat_off)
+                if lat_ready:
+                    d_slot, d_cnt = base + o_slot, base + o_lcnt
+                else:
+                    d_slot = self._buf("lat_slot", 8 * lat_off)
+                    d_cnt = self._buf("lat_cnt", 8 * nj)
+                max_vals = int(hj["lat_n"].max())
+                if self.lat_prefix and max_vals <= LAT_SUGGEST_MAX_SLOTS and \
+                        int(hj["n_cand"].max()) > self.lat_prefix:
+                    # prefix first: the rest of a stream only where an unseen
+                    # value could still win (tpe_lattice_suggest)
+                    npart = nj * max_vals
+                    d_part = self._buf(pname, 32 * npart)
+                    d_need = self._buf("lat_need", 4 * nj)
+                    L.check(lib.tpe_lattice_suggest(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
+                                                    d_slot, self.lat_prefix, d_part, npart,
+                                                    d_need, db, d_err, ks),
+                            "tpe_lattice_suggest")
+                else:
+                    L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
+                                                   d_slot, d_err, ks), "tpe_lattice_sample")
+                    L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt,
+                                                    ks), "tpe_lattice_compact")
+                    npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+                    d_part = self._buf(pname, 32 * max(npart, 1))
+                    L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig,
+                                                    d_vals, d_first, d_cnt, max_vals, None, None,
+                                                    d_part, npart, db, d_err, ks),
+                            "tpe_score_quantized")
+            elif kind in ("qfb", "qinj"):
+                vals = d_cand
+                if kind == "qfb":
+                    vals = self._buf("q_cand", 8 * max(qfb_off, 1))
+                    L.check(lib.tpe_sample(base + o_fb, fb_jobs.ctypes.data_as(ctypes.c_void_p),
+                                           nj, d_segs, d_mu, d_sig, d_cdf, 64, vals, ks),
+                            "tpe_sample")
+                max_vals = int(hj["n_cand"].max())
+                npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+                d_part = self._buf(pname, 32 * max(npart, 1))
+                L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, vals, None,
+                                                None, max_vals, d_bl, d_al, d_part, npart, db,
+                                                d_err, ks), "tpe_score_quantized")
+            else:
+                npart = lib.tpe_categorical_partials(hjp, nj)
+                d_part = self._buf(pname, 32 * max(npart, 1))
+                if self.lat_prefix and not inj(ids[0]) and d_bl is None and d_x is None and \
+                        int(hj["n_cand"].max()) > self.lat_prefix:
+                    # prefix first: the rest of a stream only where an unseen
+                    # better category could still be drawn (tpe_categorical_suggest)
+                    d_need = self._buf("cat_need", 4 * nj)
+                    L.check(lib.tpe_categorical_suggest(dj, hjp, nj, d_csegs, d_logp, d_ccdf,
+                                                        self.lat_prefix, d_part, npart, d_need,
+                                                        db, ks), "tpe_categorical_suggest")
+                else:
+                    L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf,
+                                                      d_cand, d_bl, d_al, d_x, d_part, npart,
+                                                      db, ks), "tpe_score_categorical")
+            tock(kind, e0, kst)
+
+        # categorical labels need only the gathered lists: with cat_early
+        # the side stream starts their posterior and scoring from an event
+        # recorded after the gather, so they run beside the latency-bound
+        # fit kernels instead of the VALU-bound table build and scorer
+        # (issued on the host after the fit's launches: the fit is not
+        # delayed, and the table build still reaches the GPU before the
+        # fit ends)
+        cat_early = side is not None and bool(cat) and self.cat_early
+        if cat_early:
+            if not gather_side:
+                stream_rec("gathered", sp)
+            if self.cat_issue == "pre":  # issued before the fit's launches
+                for g, (k, ids) in enumerate(groups):
+                    if k == "cat" and ids:
+                        launch_group(g, "all")
+        # ---- posterior fit ------------------------------------------------------
+        if fit_ids and sorted_fit:
+            e0 = tick("fit")
+            d_fss = self._buf("fit_sorted_scratch",
+                              lib.tpe_fit_sorted_scratch_bytes(len(segs), n_rows))
+            L.check(lib.tpe_fit_sorted(history.vals.data_ptr(), history.active.data_ptr(),
+                                       history.ld, history.order.data_ptr(),
+                                       _V("n_rows", n_rows),
+                                       base + o_isb, base + o_g, g_arr.ctypes.data, d_segs,
+                                       len(segs), d_fss, d_w, d_mu, d_sig, d_cdf, d_c64,
+                                       d_c32, d_err, sp), "tpe_fit_sorted")
+            tock("fit", e0)
+        elif fit_ids:
+            e0 = tick("fit")
+            L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), _V("max_obs", max_obs),
+                                       _V("n_obs_total", n_obs_total),
+                                       d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n, d_w32,
+                                       d_pm, d_sm, sp), "tpe_parzen_fit")
+            tock("fit", e0)
+
+        if cat and side is None:
+            cat_fit()
+
+        if posteriors:
+            return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
+                                         d_segs, stream, o_p), True
+
+        _hmark('jobs')
+
+        _hmark('fit')
+        # ---- scoring, one call per group ----------------------------------------
+        # quantized and categorical groups go to the side stream (after the job
+        # table has landed); continuous groups stay on `stream`
+        if side is not None:  # quantized groups need the continuous fit
+            stream_rec("fitted", sp)
+        # launch order: the first sampled table group's build (the main
+        # stream's next kernels after the fit), then the side groups, then
+        # the main-stream scorers -- the host issues launches at a few us
+        # each, and at a one-eighth label share the main stream would
+        # otherwise sit idle behind the side stream's launches
+        g_order = [(g, "all") for g in range(len(groups))]
+        early = None
+        tgroups = [g for g, (k, ids) in enumerate(groups) if k == "table" and ids]
+        if side is not None:
+            if len(tgroups) == 1 and not inj(groups[tgroups[0]][1][0]):
+                early = tgroups[0]  # (one table group: the workspace tables are its own)
+            side_gs = [g for g in range(len(groups)) if groups[g][0] in SIDE_KINDS]
+            # categorical groups first, issued right after the fit's
+            # launches (they wait for the gather only, so they run beside
+            # the fit; the table build is still issued before the fit ends)
+            cat_gs = [g for g in side_gs if cat_early and groups[g][0] == "cat"]
+            pre = [(g, "all") for g in cat_gs] if self.cat_issue == "post" else []
+            late = [(g, "all") for g in cat_gs] if self.cat_issue == "late" else []
+            g_order = pre + ([(early, "build")] if early is not None else []) + late + \
+                [(g, "all") for g in side_gs if g not in cat_gs] + \
+                [(g, "score" if g == early else "all") for g in range(len(groups))
+                 if groups[g][0] not in SIDE_KINDS]
+        for g, stage in g_order:
+            launch_group(g, stage)
+
+        if not side_started:  # (no side group: only the categorical posterior)
+            if cat and not cat_early:
+                cat_fit()
+        if not joined:  # join before the readback
+            stream_order("joined", side_p, sp)
+        if exchange is not None:  # label-sharded level: the cross-rank argmax
+            d_xl = self._buf("xchg_local", x_labels * BS)
+            d_xg = self._buf("xchg_gathered", x_world * x_labels * BS)
+            L.check(lib.tpe_best_scatter(d_best, base + o_xslot, n_jobs, d_xl, x_labels, sp),
+                    "tpe_best_scatter")
+            L.check(lib.tpe_maxloc_allreduce(d_xl, d_xg, d_best + n_jobs * BS, x_labels,
+                                             x_comm, sp), "tpe_maxloc_allreduce")
+        return table_calls, False
 
     def _read_results(self, stream, sp, sync, after, pin, nbytes, n_jobs, fix, jobs, xbytes,
                       groups, table_calls, outputs, table_scores, out_off, works, order, cont,
