@@ -82,9 +82,6 @@ constexpr int kTR = TPE_TR;          // candidates per thread and tile in the sc
 #endif
 constexpr int kTiles = TPE_TILES;    // tiles (kBS * kTR candidates) per scorer block
 constexpr int64_t kTile = (int64_t)kBS * kTR;
-#ifndef TPE_BUILD_PAIR  // build: two items per lane per pass, summed in fp32 first
-#define TPE_BUILD_PAIR 0
-#endif
 #ifndef TPE_BUILD_BLOCKS
 #define TPE_BUILD_BLOCKS 512
 #endif
@@ -497,10 +494,18 @@ __device__ __forceinline__ double row_sum9_transposed(const double (&P)[9]) {
 // a superset of each cell's own, whose components the exclusion test below
 // drops -- then the wide list; every row walks the same items.
 struct BuildLds {  // the block's four waves' partial expansions of one mixture
-  float m[kBS / kWave][4];       // per wave and row: its share's largest log term (the scale pass)
+  int m[kBS / kWave][4];         // per wave and row: its scale (a power of two's exponent)
   double p[kBS / kWave][kWave];  // per wave and lane: its row's sum of P_rev4(lane & 15)
   int bad[kBS / kWave][4];
 };
+__device__ __forceinline__ int row_max_i(int v) {  // max over the lane's 16-lane DPP row
+  v = max(v, __builtin_amdgcn_mov_dpp(v, kDppXor1, 0xF, 0xF, true));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, kDppXor2, 0xF, 0xF, true));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, kDppHalfMirror, 0xF, 0xF, true));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, kDppMirror, 0xF, 0xF, true));
+  return v;
+}
+constexpr int kNoScale = -100000;  // a lane that has summed nothing yet
 __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __restrict__ coef64,
                                           int k_lo, int k_hi,
                                           const int32_t* __restrict__ wide_idx, int n_wide,
@@ -522,46 +527,18 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     return it < nwin ? k_lo + it : wide_idx[off + (it - nwin)];
   };
   const float hf = (float)h, Tf = (float)T;
-  // an item's largest log term over the cell (fp32) and whether it is summed:
-  // window items that are wide come from the list instead; an item below the
-  // plan's floor on the whole cell is left out
-  auto item_max = [&](int it, const double4& c, float& tmax) -> bool {
-    const bool skip = it < nwin && is_wide(S, comp(it), c.y);
-    const float zn = fmaxf(fabsf((float)(y0 - c.x)) - hf, 0.0f) * (float)c.y;
-    tmax = (float)c.z - 0.5f * zn * zn;
-    return !skip && tmax >= Tf;
-  };
-  // Pass 1: the row's scale ml, the largest log term of a summed item over
-  // the cell (all of the cell's items, across the block's waves in coop), so
-  // every summed term e^(v - ml) at the cell centre is <= ~1 and no partial
-  // sum is ever rescaled.  Terms that can matter are >= T >= ml - ~60 (the
-  // plan's floor) and a centre value lies within ~11 of its cell maximum
-  // (admissible h): e^-71 at least, far inside fp32's normal range.
-  float mf = -INFINITY;
-  for (int it = wv * 16 + l; it < items; it += stride) {
-    const double4 c = ld4(coef64, off + comp(it));
-    float t;
-    if (item_max(it, c, t)) mf = fmaxf(mf, t);
-  }
-  mf = fmaxf(mf, dpp_f<kDppXor1>(mf));
-  mf = fmaxf(mf, dpp_f<kDppXor2>(mf));
-  mf = fmaxf(mf, dpp_f<kDppHalfMirror>(mf));
-  mf = fmaxf(mf, dpp_f<kDppMirror>(mf));  // the row's max in every lane of the row
-  if (coop) {
-    if (l == 0) X.m[wv][row] = mf;
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < kNW; ++w) mf = fmaxf(mf, X.m[w][row]);
-  }
-  const double ml = mf == -INFINITY ? 0.0 : (double)mf;
-  // Pass 2: every summed component.  The exponent is formed in fp64, the
-  // series and the per-component tests in fp32, the nine P_n sums in fp64 (a
-  // sum of ~10^3 fp32 terms would carry ~10^3 roundings into the error bound,
-  // mix_eps).  The next item's coefficients are loaded before this item's work.
-  // P_0..P_3 are summed in fp64 (a sum of ~10^2 fp32 terms per lane would
-  // carry ~10^2 roundings into mix_eps), P_4..P_8 in fp32: at most 2 % of the
-  // terms' absolute sum lies there (tools/table_bounds.py), so their rounding
-  // costs mix_eps K 2^-24 0.0198
+  // One pass over the items.  Each lane keeps its own scale 2^sl (sl an
+  // integer, raised when a term would exceed 2^8 of it) and rescales its
+  // partial sums by exact powers of two; the row's lanes (and the block's
+  // waves, coop) meet at the largest scale the same way, and the cell's sums
+  // are finally normalised by the power of two that puts P_0 in [1, 2) --
+  // every rescaling exact, P_0 >= 1 as the storage bound assumes.  The
+  // exponent is formed in fp64, the series and the per-component tests in
+  // fp32.  P_0..P_3 are summed in fp64 (a sum of ~10^2 fp32 terms per lane
+  // would carry ~10^2 roundings into mix_eps), P_4..P_8 in fp32: at most 2 %
+  // of the terms' absolute sum lies there (tools/table_bounds.py), so their
+  // rounding costs mix_eps K 2^-24 0.0198.  The next item's coefficients are
+  // loaded before this item's work.
   constexpr int kP64 = 4;
   double P[kP64];
   float Q[kP - kP64];
@@ -575,50 +552,14 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     else
       Q[n - kP64] += t;
   };
-  bool bad = false;
-#if TPE_BUILD_PAIR
-  // Two items per lane per pass (it, it + stride): their nine terms are added
-  // in fp32 first (one rounding, u of their absolute sum: mix_eps's pair
-  // term), then once into the fp64 sums -- half the fp64 adds (half-rate on
-  // gfx950) and conversions.
-  auto term = [&](int it2, const double4& c, float& e, float& Af, float& B2) {
-    float tmax;
-    const bool inc = it2 < items && item_max(it2, c, tmax);  // (branch-free)
-    const double dy = y0 - c.x;
-    const float dyf = (float)dy, inv = (float)c.y;
-    const double zc = dy * c.y;
-    const double v = c.z - 0.5 * zc * zc;
-    const float hi2 = hf * inv * inv;
-    Af = inc ? -dyf * hi2 : 0.0f;  // A and 2B
-    B2 = inc ? -hf * hi2 : 0.0f;
-    bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > (float)(kRhoLim * (1.0 + 1e-5)));
-    // the exponent (v - ml) log2 e formed in fp64, rounded once to fp32
-    e = inc ? __builtin_amdgcn_exp2f((float)((v - ml) * kLog2e)) : 0.0f;
-  };
-  const double4 zero4 = make_double4(0.0, 0.0, 0.0, 0.0);
-  for (int it = wv * 16 + l; it < items; it += 2 * stride) {
-    const int it2 = it + stride;
-    const double4 c1 = ld4(coef64, off + comp(it));
-    const double4 c2 = it2 < items ? ld4(coef64, off + comp(it2)) : zero4;
-    float e1, A1, B1, e2, A2, B2;
-    term(it, c1, e1, A1, B1);
-    term(it2, c2, e2, A2, B2);
-    // the series in fp32 (a v_fma_f64 takes twice the cycles of a v_fma_f32
-    // on gfx950: an fp64 recurrence made this kernel 8 % slower)
-    float cm1 = 0.0f, cc1 = e1, cm2 = 0.0f, cc2 = e2;  // e * c_n
-    acc(0, e1 + e2);
+  auto rescale = [&](int d) __attribute__((always_inline)) {  // multiply the sums by 2^d
 #pragma unroll
-    for (int n = 0; n + 1 < kP; ++n) {
-      const float x1 = fmaf(A1, cc1, B1 * cm1) * (1.0f / (float)(n + 1));
-      const float x2 = fmaf(A2, cc2, B2 * cm2) * (1.0f / (float)(n + 1));
-      acc(n + 1, x1 + x2);
-      cm1 = cc1;
-      cc1 = x1;
-      cm2 = cc2;
-      cc2 = x2;
-    }
-  }
-#else
+    for (int n = 0; n < kP64; ++n) P[n] = ldexp(P[n], d);
+#pragma unroll
+    for (int n = 0; n < kP - kP64; ++n) Q[n] = ldexpf(Q[n], d);
+  };
+  int sl = kNoScale;
+  bool bad = false;
   int it = wv * 16 + l;  // the block's four waves split the items, 16 lanes per cell each
   int k = it < items ? comp(it) : 0;
   double4 c = it < items ? ld4(coef64, off + k) : make_double4(0.0, 0.0, 0.0, 0.0);
@@ -626,17 +567,32 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     const int itn = it + stride;
     const int kn = itn < items ? comp(itn) : 0;
     const double4 cn = itn < items ? ld4(coef64, off + kn) : c;
-    float tmax;
-    const bool inc = item_max(it, c, tmax);  // (branch-free: an excluded item adds zero terms)
+    // window items that are wide come from the list instead; an item below
+    // the plan's floor on the whole cell is left out (branch-free: an
+    // excluded item adds zero terms)
+    const bool skip = it < nwin && is_wide(S, k, c.y);
     const double dy = y0 - c.x;
     const float dyf = (float)dy, inv = (float)c.y;
+    const float zn = fmaxf(fabsf(dyf) - hf, 0.0f) * inv;
+    const bool inc = !skip && ((float)c.z - 0.5f * zn * zn >= Tf);
     const double zc = dy * c.y;
-    const double v = c.z - 0.5 * zc * zc;
+    const double t2 = (c.z - 0.5 * zc * zc) * kLog2e;  // log2 of the term at the centre
+    const bool up = inc && t2 > (double)(sl + 8);
+    if (__any(up)) {
+      if (up) {
+        const int ns = (int)ceil(t2);
+        rescale(max(sl - ns, -1100));
+        sl = ns;
+      }
+    }
     const float hi2 = hf * inv * inv;
     const float Af = inc ? -dyf * hi2 : 0.0f, B2 = inc ? -hf * hi2 : 0.0f;  // A and 2B
     bad = bad || (9.0f * fabsf(Af) + 32.5f * fabsf(B2) > (float)(kRhoLim * (1.0 + 1e-5)));
-    // the term: exponent (v - ml) log2 e formed in fp64, rounded once to fp32
-    const float e = inc ? __builtin_amdgcn_exp2f((float)((v - ml) * kLog2e)) : 0.0f;
+    // the term 2^(t2 - sl) = 2^n 2^f, n = floor(t2 - sl) exact and f in [0, 1)
+    // rounded once to fp32: a relative error <= ln2 2^-24 (+ v_exp_f32's),
+    // whatever the term's size
+    const double xs = t2 - (double)sl, xn = floor(xs);
+    const float e = inc ? ldexpf(__builtin_amdgcn_exp2f((float)(xs - xn)), (int)xn) : 0.0f;
     float cm = 0.0f, cc = e;  // e * c_n
     acc(0, e);
 #pragma unroll
@@ -649,27 +605,43 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     k = kn;
     c = cn;
   }
-#endif
+  // the row's lanes at the row's largest scale (exact); then the block's
+  // waves at theirs (coop)
+  int sr = row_max_i(sl);
+  rescale(max(sl - sr, -1100));
   static_assert(kP == 9, "row_sum9_transposed folds nine terms");
   double Pall[kP];
 #pragma unroll
   for (int n = 0; n < kP; ++n) Pall[n] = n < kP64 ? P[n] : (double)Q[n - kP64];
-  const double v = row_sum9_transposed(Pall);  // lane p of the row: the row's total of P_rev4(p)
+  double tot = row_sum9_transposed(Pall);  // lane p of the row: the row's total of P_rev4(p)
   bad = ((__ballot(bad) >> (lane & ~15)) & 0xFFFFull) != 0;
-  // the four waves' partial sums of each row (cell), all at the row's scale
-  double tot = v;
   bool anybad = bad;
   if (coop) {
-    if (l == 0) X.bad[wv][row] = bad;
-    X.p[wv][lane] = v;
+    if (l == 0) {
+      X.bad[wv][row] = bad;
+      X.m[wv][row] = sr;
+    }
+    X.p[wv][lane] = tot;
     __syncthreads();
+    int sb = X.m[0][row];
+#pragma unroll
+    for (int w = 1; w < kNW; ++w) sb = max(sb, X.m[w][row]);
     tot = 0.0;
     anybad = false;
     for (int w = 0; w < kNW; ++w) {
-      tot += X.p[w][lane];
+      tot += ldexp(X.p[w][lane], max(X.m[w][row] - sb, -1100));
       anybad = anybad || X.bad[w][row];
     }
+    sr = sb;
     __syncthreads();  // (X is reused by the next call)
+  }
+  // normalise: P_0 (the row's lane 0) in [1, 2)
+  const double p0 = __shfl(tot, lane & ~15, kWave);
+  int e0 = 0;
+  if (p0 > 0.0) {
+    (void)frexp(p0, &e0);  // p0 = f 2^e0, f in [0.5, 1)
+    e0 -= 1;
+    tot = ldexp(tot, -e0);
   }
   const int n = rev4(l);
   if (store && wv == 0 && n < kP) {
@@ -678,7 +650,7 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
     else
       reinterpret_cast<_Float16*>(cell + 2 * kP32)[2 * (n - kP32) + mix] = (_Float16)(float)tot;
   }
-  m_out = mf == -INFINITY ? -INFINITY : ml;
+  m_out = (p0 > 0.0) ? (double)(sr + e0) * kLn2 : -INFINITY;
   return anybad;
 }
 
@@ -722,7 +694,10 @@ __device__ __forceinline__ bool build_mix(const tpe_seg& S, const double* __rest
 constexpr double kFitTol = 1.0e-6;   // cubic-vs-polynomial bound allowed (nats)
 constexpr int kScoreLanes = 8;       // lanes per cell: 4 nodes, 8 sub-intervals
 constexpr int kScoreCellsPerBlock = kBS / kScoreLanes;
-constexpr int kScoreBlocks = 256;    // per job (grid-stride over cells)
+#ifndef TPE_SCORE_BLOCKS
+#define TPE_SCORE_BLOCKS 256
+#endif
+constexpr int kScoreBlocks = TPE_SCORE_BLOCKS;  // per job (grid-stride over cells)
 constexpr double kUFit = 1.0501;     // |u| the bounds cover (u's fp32 rounding: <= 1.05 (1 + 5 2^-24))
 constexpr int kLogD = 7;             // log-series terms carried exactly
 constexpr int kLogM = 12;            // majorant terms summed (then Cauchy's tail)
@@ -745,12 +720,11 @@ __host__ __device__ inline double mix_eps(int items, bool coop, double ab) {
   const double E1 = exp(ab), E2 = E1 * E1;
   return 4.4e-7                         // series truncation (tools/table_bounds.py)
          + 1.0e-10                      // components below the exclusion floor
-         + (10.0 + 4.6e-4 * items) * u  // each term's exponent rounded to fp32
+         + 0.6932 * u + 1e-13           // each term's exponent: its fraction rounded to fp32
          + 0x1.0p-22                    // v_exp_f32 (checked exhaustively, tpe_check_transcendentals)
          + 5.5 * u * ab                 // A, B rounded to fp32
          + 4.0 * u * ab * E2            // the fp32 series recurrence (4 roundings per step)
          + u * E2                       // P_0..P_5 stored in fp32
-         + (TPE_BUILD_PAIR ? u * E2 : 0.0)  // two items' terms added in fp32 before the fp64 sum
          + (K + 1) * u * 0.0198 * 1.0001  // P_4..P_8 summed in fp32 (tools/table_bounds.py)
          + 1.5e-7 + 0x1.0p-25 * 4.2 * E1  // P_6..P_8 in fp16 (+ subnormal spacing)
          + (K + 8) * 2.0 * ud * E2;     // fp64 sums, rescale and merge factors of the P_n
@@ -1782,8 +1756,8 @@ struct BandWork {  // per job (tpe_band_bytes)
   int cells[kBandCells];                          // the listed cells (ascending)
   int ns, ncell, over, pad0;                      // survivors, cells, job overflowed
   long long tmark[8];                             // (TPE_BAND_TIMING diagnostic builds)
-  BestT win[kBandBlocks];                         // k_band_final: per block, its winner
-  unsigned int done;                              // k_band_final: blocks finished
+  BestT win[kBandBlocks];                         // (unused: k_band_final is one block per job)
+  unsigned int done;                              // (unused)
   unsigned int pad[3];
 };
 
@@ -2249,29 +2223,31 @@ __global__ __launch_bounds__(kBX) void k_band(
   TMARK(3)
 }
 
-// The band's decision (blocks (k, j), k < kBandBlocks; after k_band): the
-// survivors [k ns / B, (k + 1) ns / B) of job j, one per thread -- direct:
-// its chunks' partial sums combined in chunk order; cells: its cell's chunk
-// expansions merged in chunk order (into LDS, every listed cell) and
-// evaluated -- then np.argmax over the block's survivors into work[j].win[k];
-// the job's last block folds the blocks' winners into best[j] = {fp64
-// score, index, value, n_cand} and re-arms the counter.
-__global__ __launch_bounds__(kBX) void k_band_final(const tpe_job* __restrict__ jobs,
+// The band's decision (one block per job, after k_band): direct -- each
+// survivor's chunk partial sums combined in chunk order; cells -- each listed
+// cell's chunk expansions merged in chunk order (into LDS) and evaluated at
+// its survivors -- then np.argmax over all of the job's survivors into
+// best[j] = {fp64 score, index, value, n_cand}.  (Sixteen blocks per job with
+// a last-block hand-off spent 10-17 us of the job's ~30 in the hand-off;
+// one block scores a C3 band of ~4 000 survivors in ~4 us.)
+constexpr int kFX = 1024;  // k_band_final block: one per job, 16 waves (latency-bound fp64 chains)
+__global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ jobs,
                                                     const tpe_seg* __restrict__ segs,
                                                     const double* __restrict__ coef64,
                                                     const tpe_table* __restrict__ tables,
                                                     tpe_best* __restrict__ best,
                                                     BandWork* __restrict__ work) {
-  constexpr int kNW = kBX / kWave;
+  constexpr int kNW = kFX / kWave;
   __shared__ BestT red[kNW];
-  __shared__ double s_P[kBandCells][2][kBandD + 2];  // merged expansions: P_0..P_24, m
+  __shared__ double s_P[kBandCells][2][kBandD + 2];  // merged expansions: P_0..P_20, m
+  __shared__ double s_tmp[kBandCells][2][kBandD + 2];  // per (cell, chunk) unit: its P and m
   __shared__ int s_nd[kBandCells][2];
   __shared__ int s_ndu[kBandCells][2];             // per (cell, chunk) unit: slow components ...
   __shared__ int s_dir[kBandCells][2][kChunkDir];  // ... and their indices (units <= kBandCells)
   __shared__ int s_cells[kBandCells];
-  __shared__ bool s_last;
-  const int j = blockIdx.y, kb = blockIdx.x;
+  const int j = blockIdx.y;
   BandWork& W = work[j];
+  TMARK(4)
   if (W.over) return;  // (k_band gave the fp32 winner with n_scored = -1)
   const tpe_job J = jobs[j];
   const int ns = W.ns, ncell = W.ncell;
@@ -2279,10 +2255,10 @@ __global__ __launch_bounds__(kBX) void k_band_final(const tpe_job* __restrict__ 
   const bool lgmm = J.family == TPE_LGMM1;
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const tpe_table Tb = tables[j];
-  const int i0 = (int)((int64_t)kb * ns / kBandBlocks), i1 = (int)((int64_t)(kb + 1) * ns / kBandBlocks);
+  const int i0 = 0, i1 = ns;  // (one block per job: no cross-block hand-off)
   BestT bx{0.0, -1, 0.0};
   if (ns <= kBandSurv) {
-    for (int i = i0 + (int)threadIdx.x; i < i1; i += kBX) {
+    for (int i = i0 + (int)threadIdx.x; i < i1; i += kFX) {
       double l2[2];
       for (int mix = 0; mix < 2; ++mix) {
         double mm = W.part[0][i][2 * mix], ss = W.part[0][i][2 * mix + 1];
@@ -2293,33 +2269,41 @@ __global__ __launch_bounds__(kBX) void k_band_final(const tpe_job* __restrict__ 
       best_update(bx, l2[0] - l2[1], W.sidx[i], cand_value(W.sy[i], lgmm));
     }
   } else {
-    // merge: thread t takes (cell, mixture, term) items; every term summed
-    // over the chunks in order at the cell's largest scale
-    for (int t = threadIdx.x; t < ncell * 2 * (kBandD + 1); t += kBX) {
+    // merge: the chunks' expansions (P_0..P_20 and m per (cell, chunk,
+    // mixture)) staged in LDS with all their global reads in flight at once,
+    // then thread t takes (cell, mixture, term) items: every term summed over
+    // the chunks in order at the cell's largest scale
+    for (int t = threadIdx.x; t < ncell * nch * 2 * (kBandD + 2); t += kFX) {
+      const int n = t % (kBandD + 2), r = t / (kBandD + 2), u = r >> 1, mix = r & 1;
+      const BandMix& q = W.cpart[u / nch][u % nch][mix];
+      s_tmp[u][mix][n] = n <= kBandD ? q.P[n] : q.m;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < ncell * 2 * (kBandD + 1); t += kFX) {
       const int k = t / (2 * (kBandD + 1)), r = t % (2 * (kBandD + 1));
       const int mix = r / (kBandD + 1), n = r % (kBandD + 1);
       double mm = -INFINITY;
-      for (int c = 0; c < nch; ++c) mm = fmax(mm, W.cpart[k][c][mix].m);
+      for (int c = 0; c < nch; ++c) mm = fmax(mm, s_tmp[k * nch + c][mix][kBandD + 1]);
       double acc = 0.0;
       for (int c = 0; c < nch; ++c) {
-        const BandMix& q = W.cpart[k][c][mix];
-        acc += q.m == -INFINITY ? 0.0 : q.P[n] * exp(q.m - mm);
+        const double qm = s_tmp[k * nch + c][mix][kBandD + 1];
+        acc += qm == -INFINITY ? 0.0 : s_tmp[k * nch + c][mix][n] * exp(qm - mm);
       }
       s_P[k][mix][n] = acc;
       if (n == 0) s_P[k][mix][kBandD + 1] = mm;
     }
     // the slow-component lists (one thread per cell and mixture); -1: a
     // chunk's list overflowed (that cell's survivors take the direct sum)
-    for (int t = threadIdx.x; t < ncell * nch * 2; t += kBX) {
+    for (int t = threadIdx.x; t < ncell * nch * 2; t += kFX) {
       const int u = t >> 1, mix = t & 1;
       s_ndu[u][mix] = W.cpart[u / nch][u % nch][mix].n_dir;
     }
-    for (int t = threadIdx.x; t < ncell * nch * 2 * kChunkDir; t += kBX) {
+    for (int t = threadIdx.x; t < ncell * nch * 2 * kChunkDir; t += kFX) {
       const int d = t % kChunkDir, r = t / kChunkDir, u = r >> 1, mix = r & 1;
       s_dir[u][mix][d] = W.cpart[u / nch][u % nch][mix].dir[d];
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < ncell * 2; t += kBX) {
+    for (int t = threadIdx.x; t < ncell * 2; t += kFX) {
       const int k = t >> 1, mix = t & 1;
       int nd = 0;
       for (int c = 0; c < nch; ++c) {
@@ -2328,10 +2312,11 @@ __global__ __launch_bounds__(kBX) void k_band_final(const tpe_job* __restrict__ 
       }
       s_nd[k][mix] = nd;
     }
-    for (int t = threadIdx.x; t < ncell; t += kBX) s_cells[t] = W.cells[t];
+    for (int t = threadIdx.x; t < ncell; t += kFX) s_cells[t] = W.cells[t];
     __syncthreads();
+    TMARK(5)
     const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
-    for (int i = i0 + (int)threadIdx.x; i < i1; i += kBX) {
+    for (int i = i0 + (int)threadIdx.x; i < i1; i += kFX) {
       const float yf = W.sy[i];
       const int c = band_cell(Tb, yf);
       int lo = 0, hi = ncell;  // its listed position (k_band listed every survivor's cell)
@@ -2349,10 +2334,15 @@ __global__ __launch_bounds__(kBX) void k_band_final(const tpe_job* __restrict__ 
           continue;
         }
         const double u = (y - (double)cell_centre(g0, h32, c)) / Tb.h;
-        double p = s_P[k][mix][kBandD];
+        // the expansion's coefficients into registers first (their LDS reads
+        // issued together, not one per step of the Horner chain)
+        double cf[kBandD + 2];
 #pragma unroll
-        for (int n = kBandD - 1; n >= 0; --n) p = fma(p, u, s_P[k][mix][n]);
-        const double m = s_P[k][mix][kBandD + 1];
+        for (int n = 0; n <= kBandD + 1; ++n) cf[n] = s_P[k][mix][n];
+        double p = cf[kBandD];
+#pragma unroll
+        for (int n = kBandD - 1; n >= 0; --n) p = fma(p, u, cf[n]);
+        const double m = cf[kBandD + 1];
         for (int cc = 0; cc < nch; ++cc) {  // the slow components, term by term
           const int u = k * nch + cc, nd = s_ndu[u][mix];
           for (int d = 0; d < nd; ++d) {
@@ -2366,21 +2356,13 @@ __global__ __launch_bounds__(kBX) void k_band_final(const tpe_job* __restrict__ 
       best_update(bx, l2[0] - l2[1], W.sidx[i], cand_value(yf, lgmm));
     }
   }
-  bx = block_best<kBX>(bx, red);
+  TMARK(6)
+  bx = block_best<kFX>(bx, red);
   if (threadIdx.x == 0) {
-    W.win[kb] = bx;
-    __threadfence();  // this block's winner is visible before the count
-    s_last = atomicAdd(&W.done, 1u) == (unsigned)(kBandBlocks - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();  // (acquire: the other blocks' winners)
-  if (threadIdx.x == 0) {
-    BestT r = W.win[0];
-    for (int b = 1; b < kBandBlocks; ++b)
-      if (better(W.win[b].score, W.win[b].index, r.score, r.index)) r = W.win[b];
-    best[j] = tpe_best{r.score, r.index, r.value, J.n_cand};
-    W.done = 0u;
+    best[j] = tpe_best{bx.score, bx.index, bx.value, J.n_cand};
+#ifdef TPE_BAND_TIMING
+    W.tmark[7] = wall_clock64();
+#endif
   }
 }
 
@@ -2799,7 +2781,7 @@ extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, i
   hipLaunchKernelGGL(k_band, dim3(kBandBlocks, n_jobs), dim3(kBX), 0, (hipStream_t)stream, jobs,
                      segs, coef64, tables, band, band_ctl, partial, (int)gx, best,
                      static_cast<BandWork*>(work));
-  hipLaunchKernelGGL(k_band_final, dim3(kBandBlocks, n_jobs), dim3(kBX), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_band_final, dim3(1, n_jobs), dim3(kFX), 0, (hipStream_t)stream,
                      jobs, segs, coef64, tables, best, static_cast<BandWork*>(work));
   return check_launch("tpe_band_rescore");
 }

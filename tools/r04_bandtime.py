@@ -32,7 +32,9 @@ for j in range(30):
     tail = w[per - (16 + 16 * 24 + 64 + 16):]
     ns, ncell, over, _ = tail[:16].view(np.int32)
     tm = tail[16:80].view(np.int64)
-    print(j, "ns %5d ncell %3d over %d  phase us: %s" % (ns, ncell, over, np.round(np.diff(tm[:4]) / 100.0, 1)))
+    print(j, "ns %5d ncell %3d over %d  k_band phases us: %s  final: start->merged %s ->scored %s ->done %s  gap band->final %.1f" % (
+        ns, ncell, over, np.round(np.diff(tm[:4]) / 100.0, 1), round((tm[5] - tm[4]) / 100.0, 1),
+        round((tm[6] - tm[5]) / 100.0, 1), round((tm[7] - tm[6]) / 100.0, 1), (tm[4] - tm[3]) / 100.0))
 # tile headers: entries walked per job vs survivors
 ctl_b = ctypes.c_int64(0)
 lib.tpe_band_bytes(tj.ctypes.data, 30, ctypes.byref(ctl_b), None)
@@ -52,10 +54,10 @@ for j in range(30):
     if ns <= 128 or over:
         continue
     nch = max(1, 16 // max(ncell, 1))
-    nd = np.zeros(2, np.int64)
+    nd = [[], []]
     for k in range(ncell):
         for c in range(nch):
             for mix in range(2):
                 o = 65536 + ((k * 16 + c) * 2 + mix) * 248 + 176
-                nd[mix] += max(int(w[o:o + 4].view(np.int32)[0]), 0)
-    print(j, "ns %d ncell %d nch %d slow comps below %d above %d" % (ns, ncell, nch, nd[0], nd[1]))
+                nd[mix].append(int(w[o:o + 4].view(np.int32)[0]))
+    print(j, "ns %d ncell %d nch %d n_dir per chunk below %s above %s" % (ns, ncell, nch, nd[0], nd[1]))
