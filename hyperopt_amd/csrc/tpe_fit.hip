@@ -39,7 +39,10 @@ __device__ double np_pairwise_sum(const double* a, int64_t n) {
     int64_t s, n;
     double left;
     int st;
-  } stk[48];
+  };
+  // (one thread sums; its explicit stack lives in LDS, not in scratch: a
+  // private array here gave the calling kernel 1.5 KB of scratch per lane)
+  __shared__ Frame stk[48];
   int sp = 0;
   stk[0] = Frame{0, n, 0.0, 0};
   double ret = 0.0;

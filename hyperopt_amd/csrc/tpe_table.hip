@@ -1388,6 +1388,7 @@ constexpr int kHdrWords = 4;  // per tile: lo, hi_max (float bits), n, unused
 // take the two-polynomial cell, then the exact log-sum-exp, after the loop.
 // out_score / out_x / out_eps (nullable, tests): per-candidate fp32 score,
 // value and the bound eps the band used (+inf: always re-scored).
+template <bool HOOKS>  // HOOKS: the per-candidate test outputs (out_score / out_x / out_eps)
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_WPE))) void k_score_table_fast(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
@@ -1481,9 +1482,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
       by = take ? y : by;
       br = take ? r : br;
       stage[r * kWave + lane] = s;  // kept for the band
-      if (out_score) out_score[J.out_off + t0 + r] = (double)s;
+      if (HOOKS && out_score) out_score[J.out_off + t0 + r] = (double)s;
     }
-    if (out_x && valid) out_x[J.out_off + t0 + r] = cand_value(y, lgmm);
+    if (HOOKS && out_x && valid) out_x[J.out_off + t0 + r] = cand_value(y, lgmm);
   }
 #endif
   // the lane's best cubic-scored candidate (its bounds are monotone in s)
@@ -1511,7 +1512,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     const f4* cell4 = reinterpret_cast<const f4*>(region);
     auto fold = [&](int r, float s, float y, float keep) __attribute__((always_inline)) {
       stage[r * kWave + lane] = keep;
-      if (out_score) out_score[J.out_off + t0 + r] = (double)s;
+      if (HOOKS && out_score) out_score[J.out_off + t0 + r] = (double)s;
       const bool na = s != s, nbn = bs != bs;
       const bool take =
           (br < 0) || (na ? (!nbn || r < br) : (!nbn && (s > bs || (s == bs && r < br))));
@@ -1543,7 +1544,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
           fold(r, s, y, hi);
           lo_fb = fmaxf(lo_fb, dn(s - e2));
           hi_fb = fmaxf(hi_fb, hi);
-          if (out_eps) out_eps[J.out_off + t0 + r] = (double)hi - (double)s;
+          if (HOOKS && out_eps) out_eps[J.out_off + t0 + r] = (double)hi - (double)s;
           done = true;
         }
       }
@@ -1564,7 +1565,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
       if (lane == L) {
         fold(r, s, y, INFINITY);
         hi_fb = INFINITY;
-        if (out_eps) out_eps[J.out_off + t0 + r] = INFINITY;
+        if (HOOKS && out_eps) out_eps[J.out_off + t0 + r] = INFINITY;
         ex &= ex - 1;
       }
     }
@@ -1633,7 +1634,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     lo_blk = fmaxf(lo_blk, s_lo[w]);
     hi_blk = fmaxf(hi_blk, s_hi[w]);
   }
-  if (out_eps) {  // (test hook) the bound of every cubic-scored candidate
+  if (HOOKS && out_eps) {  // (test hook) the bound of every cubic-scored candidate
 #pragma unroll
     for (int r = 0; r < kTR; ++r)
       if (r < nvalid && !((fbm >> r) & 1u)) {
@@ -1728,7 +1729,10 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
 constexpr int kBandBlocks = 16;      // blocks per job
 constexpr int kBandSurv = 128;       // survivors scored directly (more: the cell expansions)
 constexpr int kSurvBatch = 4;        // survivors summed together per pass
-constexpr int kBX = 256;             // band block
+#ifndef TPE_BAND_BX
+#define TPE_BAND_BX 256
+#endif
+constexpr int kBX = TPE_BAND_BX;     // k_band block
 constexpr int kBandTiles = 4096;     // tiles of a job the kernel's LDS prefix holds (2^24 candidates;
                                      // a larger job takes the exact fallback)
 constexpr int kTilesPT = kBandTiles / kBX;  // tile headers per thread (prefix pass)
@@ -2749,10 +2753,16 @@ extern "C" int tpe_score_table_fast(const tpe_job* jobs, const tpe_job* host_job
     return TPE_E_UNSUPPORTED;
   }
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_score_table_fast, dim3((unsigned)(8 * per)), dim3(kBS), 0, st, jobs, segs,
-                     mu, sigma, wcdf, reinterpret_cast<const float4*>(coef32), tables, cells, band,
-                     band_ctl, out_score, out_x, out_eps, partial, (unsigned long long*)stats,
-                     (int)gx, n_jobs, tile_cap);
+  if (out_score || out_x || out_eps)
+    hipLaunchKernelGGL(k_score_table_fast<true>, dim3((unsigned)(8 * per)), dim3(kBS), 0, st, jobs,
+                       segs, mu, sigma, wcdf, reinterpret_cast<const float4*>(coef32), tables,
+                       cells, band, band_ctl, out_score, out_x, out_eps, partial,
+                       (unsigned long long*)stats, (int)gx, n_jobs, tile_cap);
+  else
+    hipLaunchKernelGGL(k_score_table_fast<false>, dim3((unsigned)(8 * per)), dim3(kBS), 0, st, jobs,
+                       segs, mu, sigma, wcdf, reinterpret_cast<const float4*>(coef32), tables,
+                       cells, band, band_ctl, out_score, out_x, out_eps, partial,
+                       (unsigned long long*)stats, (int)gx, n_jobs, tile_cap);
   return check_launch("tpe_score_table_fast");
 }
 
