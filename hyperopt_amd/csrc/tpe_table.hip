@@ -1375,7 +1375,9 @@ __device__ __forceinline__ float eps_2poly(const f4 q0, const f4 q1, const f4 q2
 // bound (+inf with a NaN or log-sum-exp candidate), entries = its candidates
 // with s + eps >= lo (a superset of the band's: G >= lo); a tile with more
 // than kTileSlots such candidates writes n = kTileFull and no entries.
-constexpr int kTileSlots = 64;
+constexpr int kTileSlots = 256;  // (a plateau of near-equal scores puts ~60 of a tile's 4096
+                                  // candidates in the band; 256 keeps such levels exact without
+                                  // the whole-stream fp64 fallback)
 constexpr uint32_t kTileFull = 0xFFFFFFFFu;
 constexpr int kHdrWords = 4;  // per tile: lo, hi_max (float bits), n, unused
 
@@ -1751,7 +1753,7 @@ struct BandMix {  // one mixture's expansion on one cell (or one chunk of its co
   int dir[kChunkDir];
 };
 constexpr int kEPT = 8;              // band entries per thread per window (k_band)
-constexpr int kBandSurvMax = 16384;  // survivors a job may have (more: the exact fallback)
+constexpr int kBandSurvMax = 65536;  // survivors a job may have (more: the exact fallback)
 struct BandWork {  // per job (tpe_band_bytes)
   double part[kBandBlocks][kBandSurv][4];         // direct: per chunk and survivor {m, s} b, a
   BandMix cpart[kBandCells][kBandBlocks][2];      // cells: per cell, chunk and mixture

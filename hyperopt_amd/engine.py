@@ -42,7 +42,7 @@ LATTICE_CAP = 1 << 22  # max lattice slots per quantized label before the dense 
 LAT_PACK_MAX = 1 << 16  # lattice slots of a level initialised through the upload (else memset)
 TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
-BAND_TILE_CAP = 64  # per scorer tile: band entries kept (tpe_score_table_fast's tile_cap, <= 64)
+BAND_TILE_CAP = 256  # per scorer tile: band entries kept (tpe_score_table_fast's tile_cap, <= 256)
 LAT_PREFIX = 1 << 16  # lattice argmax: candidates drawn before the early decision
 LAT_SUGGEST_MAX_SLOTS = 1 << 10  # ... for lattices of at most this many slots (all scored)
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
@@ -1716,7 +1716,8 @@ class Engine:
         a plateau of equal scores) are re-scored exactly: their fp32 candidate
         stream (TPE_F_DRAW32) through tpe_score_pruned64, every candidate in
         fp64.  Patches ``best_h`` (launch order) in place."""
-        pos = [p for a, b in band_jobs for p in range(a, b) if best_h["n_scored"][p] < 0]
+        ns = best_h["n_scored"]  # (one field view: per-element structured access is ~20 us each)
+        pos = [p for a, b in band_jobs for p in (a + np.flatnonzero(ns[a:b] < 0)).tolist()]
         if not pos:
             return
         torch, lib = self.torch, self.lib
@@ -1741,6 +1742,8 @@ class Engine:
         for k, p in enumerate(pos):
             best_h[p] = res[k]
         self.band_overflows = getattr(self, "band_overflows", 0) + len(pos)
+        self.last_band_overflow = [(int(p), int(jobs[p]["family"]), int(jobs[p]["n_cand"]))
+                                   for p in pos]  # (diagnostic: launch position, family, n)
 
     def _exchange_fix(self, best_h, xrec, xinfo):
         """The exchange of a label-sharded level carries n_scored = -1 for a

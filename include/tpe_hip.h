@@ -403,8 +403,8 @@ int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
  * 4096 candidates) writes, without atomics, a header {lo = its best
  * s32 - eps, hi_max = its largest s32 + eps, n} (4 uint32 per tile in
  * band_ctl) and its candidates with s32 + eps >= lo (a superset: G >= lo)
- * into its own 64 entries of `band` (n = 0xFFFFFFFF: more than tile_cap,
- * <= 64, did not fit; tests shrink tile_cap to force the overflow path).
+ * into its own 256 entries of `band` (n = 0xFFFFFFFF: more than tile_cap,
+ * <= 256, did not fit; tests shrink tile_cap to force the overflow path).
  * tpe_band_rescore (one launch, 4 blocks per job) takes G from the headers,
  * keeps the entries with s32 + eps >= G and re-scores them in fp64 -- per
  * table cell, a degree-20 expansion of both mixtures around the cell centre

@@ -17,3 +17,4 @@ for it in range(2):
     batch = bench.history_batch(space, mat, hist, rb, it, n, 0, units, n)
     r = eng.run(batch, precision=32, history=hist, is_below=isb)
     print("level", it, eng.last_table_stats, flush=True)
+print("band overflows (bench level):", getattr(eng, "band_overflows", 0), getattr(eng, "last_band_overflow", None))
