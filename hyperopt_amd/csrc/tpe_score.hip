@@ -778,19 +778,39 @@ __host__ __device__ __forceinline__ bool lattice_pow2(const tpe_job& j) {
          j.lat_n <= kLatLds;
 }
 
+__device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
+                                           const tpe_seg* __restrict__ segs,
+                                           const double* __restrict__ w,
+                                           const double* __restrict__ mu,
+                                           const double* __restrict__ sigma,
+                                           tpe_best* __restrict__ partial, int job, int64_t s,
+                                           int64_t nper, double* sh);
+
 // Candidates [start, min(n_cand, limit)) of every job (start a multiple of the
 // kBS * kLatR tile); need (nullable): only the jobs whose flag is set.
+// slot_n > 0 (tpe_lattice_suggest's first launch): the grid's first
+// slot_n * n_jobs blocks score the lattice slots instead (score_slot; the
+// slot scores do not depend on the draws, so they share the launch)
 template <bool POW2>
 __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
     int32_t* __restrict__ err, int n_tiles, int n_jobs, int64_t start, int64_t limit,
-    const int32_t* __restrict__ need) {
+    const int32_t* __restrict__ need, const double* __restrict__ w,
+    tpe_best* __restrict__ slot_part, int slot_n) {
   extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
   __shared__ float s_stage[kLatR * kBS];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
+  const int64_t slot_blocks = (int64_t)slot_n * n_jobs;
+  if ((int64_t)blockIdx.x < slot_blocks) {  // block-uniform
+    const int job = (int)(blockIdx.x / slot_n);
+    score_slot(jobs, segs, w, mu, sigma, slot_part, job, (int64_t)blockIdx.x - (int64_t)job * slot_n,
+               slot_n, reinterpret_cast<double*>(s_stage));
+    return;
+  }
+  const unsigned bid = (unsigned)((int64_t)blockIdx.x - slot_blocks);
   // one (job, tile) work item
   auto tile = [&](int job, int64_t base) __attribute__((always_inline)) {
     const tpe_job J = jobs[job];
@@ -900,7 +920,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     // eighth of the (job, tile) list, so a job's first-index atomics stay in
     // few XCDs' L2s
     const int64_t W = (int64_t)n_tiles * n_jobs, per = (W + 7) / 8;
-    const int64_t wi = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    const int64_t wi = (int64_t)(bid & 7) * per + (bid >> 3);
     if (wi >= W) return;
     const int job = (int)(wi / n_tiles);
     tile(job, (wi - (int64_t)job * n_tiles) * tb);
@@ -911,7 +931,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     // of ~10^4 such blocks cost ~80 us of dispatch)
     for (int job = 0; job < n_jobs; ++job) {
       if (!need[job]) continue;  // block-uniform
-      for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+      for (int64_t t = bid; t < n_tiles; t += (int64_t)gridDim.x - slot_blocks) {
         __syncthreads();  // the previous tile's LDS reads are done
         tile(job, t * tb);
       }
@@ -1030,29 +1050,29 @@ __global__ __launch_bounds__(kBS) void k_score_q(
 // (np.argmax: first index of the maximum).  So after the first `prefix`
 // candidates the winner is settled unless some value not yet seen scores
 // strictly higher (or is NaN while the best seen is not): a value first seen
-// later has a larger index and loses every tie.  k_score_slots scores every
+// later has a larger index and loses every tie.  score_slot scores every
 // slot of the lattice (seen or not), k_lattice_decide takes the argmax over
 // the seen ones and flags the jobs where an unseen slot could still win; only
 // those draw the rest of their stream (the sampler with `need`) and decide
-// again over everything seen.
-__global__ __launch_bounds__(kBS) void k_score_slots(
-    const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
-    const double* __restrict__ w, const double* __restrict__ mu,
-    const double* __restrict__ sigma, tpe_best* __restrict__ partial, int32_t* __restrict__ err) {
-  __shared__ double sh[kBS / kWave];
-  const tpe_job J = jobs[blockIdx.y];
-  const int64_t s = blockIdx.x;
+// again over everything seen.  (The slots are scored by extra blocks of the
+// prefix's sampling launch, k_lattice_sample.)
+__device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
+                                           const tpe_seg* __restrict__ segs,
+                                           const double* __restrict__ w,
+                                           const double* __restrict__ mu,
+                                           const double* __restrict__ sigma,
+                                           tpe_best* __restrict__ partial, int job, int64_t s,
+                                           int64_t nper, double* sh) {
+  const tpe_job J = jobs[job];
   if (s >= J.lat_n) return;  // block-uniform
   const double v = (double)(J.lat_kmin + s) * J.q;  // np.round(x/q) * q, as k_lattice_compact
   // every slot is scored, drawn or not: a slot below 0 (the bracket under a
   // qloguniform / qlognormal lattice, never drawn) must not raise the
   // reference's negative-argument error (tpe.py:196-197) -- a drawn value
   // x = round(exp(y)/q)*q >= 0 never has ub = x + q/2 < 0, so no err here
-  (void)err;
   const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, nullptr, sh);
   const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, nullptr, sh);
-  if (threadIdx.x == 0)
-    partial[(int64_t)blockIdx.y * gridDim.x + s] = tpe_best{bl - al, -1, v, 0};
+  if (threadIdx.x == 0) partial[(int64_t)job * nper + s] = tpe_best{bl - al, -1, v, 0};
 }
 
 // Can the sampler put a draw on slot s at all?  Only unseen slots that could
@@ -1542,14 +1562,16 @@ static bool launch_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
                                   const tpe_seg* segs, const double* mu, const double* sigma,
                                   const double* wcdf, uint64_t* slot_first, int32_t* err,
                                   int64_t start, int64_t limit, const int32_t* need,
-                                  hipStream_t st, const char* who) {
+                                  hipStream_t st, const char* who, const double* w = nullptr,
+                                  tpe_best* slot_part = nullptr, int64_t slot_n = 0) {
   int64_t gx = 1;
   for (int i = 0; i < n_jobs; ++i) {
     const int64_t n = std::min(host_jobs[i].n_cand, limit);
     gx = std::max(gx, (n + (int64_t)kBS * kLatR - 1) / ((int64_t)kBS * kLatR));
   }
   const int64_t per = (gx * n_jobs + 7) / 8;
-  if (gx > INT32_MAX || 8 * per > INT32_MAX) {
+  const int64_t sblocks = need ? 0 : slot_n * n_jobs;  // slot scoring rides on the prefix launch
+  if (gx > INT32_MAX || 8 * per + sblocks > INT32_MAX || slot_n > INT32_MAX) {
     set_error("%s: %lld work items", who, (long long)(gx * n_jobs));
     return false;
   }
@@ -1562,13 +1584,17 @@ static bool launch_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
   const size_t lds = (size_t)n_loc * sizeof(uint32_t);
   unsigned long long* sf = (unsigned long long*)slot_first;
   // with need: a grid-stride grid (k_lattice_sample): two blocks per CU
-  const unsigned grid = need ? (unsigned)std::min<int64_t>(8 * per, 512) : (unsigned)(8 * per);
+  const unsigned grid =
+      need ? (unsigned)std::min<int64_t>(8 * per, 512) : (unsigned)(8 * per + sblocks);
+  const int sn = need ? 0 : (int)slot_n;
   if (pow2)
     hipLaunchKernelGGL(k_lattice_sample<true>, dim3(grid), dim3(kBS), lds, st, jobs, segs, mu,
-                       sigma, wcdf, sf, err, (int)gx, n_jobs, start, limit, need);
+                       sigma, wcdf, sf, err, (int)gx, n_jobs, start, limit, need, w, slot_part,
+                       sn);
   else
     hipLaunchKernelGGL(k_lattice_sample<false>, dim3(grid), dim3(kBS), lds, st, jobs, segs, mu,
-                       sigma, wcdf, sf, err, (int)gx, n_jobs, start, limit, need);
+                       sigma, wcdf, sf, err, (int)gx, n_jobs, start, limit, need, w, slot_part,
+                       sn);
   return true;
 }
 
@@ -1642,10 +1668,8 @@ extern "C" int tpe_lattice_suggest(const tpe_job* jobs, const tpe_job* host_jobs
     return check_launch("tpe_lattice_suggest memset");
   unsigned long long* sf = (unsigned long long*)slot_first;
   if (!launch_lattice_sample(jobs, host_jobs, n_jobs, segs, mu, sigma, wcdf, slot_first, err, 0,
-                             prefix, nullptr, st, "tpe_lattice_suggest"))
+                             prefix, nullptr, st, "tpe_lattice_suggest", w, partial, max_n))
     return TPE_E_UNSUPPORTED;
-  hipLaunchKernelGGL(k_score_slots, dim3((unsigned)max_n, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
-                     segs, w, mu, sigma, partial, err);
   hipLaunchKernelGGL(k_lattice_decide, dim3(n_jobs), dim3(kBS), 0, st, jobs, segs, mu, sigma,
                      partial, max_n, sf, prefix, 0, need, best);
   bool more = false;

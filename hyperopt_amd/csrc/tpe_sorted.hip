@@ -7,7 +7,7 @@
 // its rows sorted by (transformed value, row) -- updated when trials are
 // appended (tpe_history_order: the new rows sorted in LDS, then merged into
 // the existing order, O(T) per append instead of O(T log T) per suggest) --
-// and a suggest's fit (tpe_fit_sorted) is a chunked compaction (three
+// and a suggest's fit (tpe_fit_sorted) is a chunked compaction (two
 // launches over (chunk, segment) blocks), then the fit's bandwidth /
 // coefficient launches:
 //
@@ -138,9 +138,11 @@ __global__ __launch_bounds__(256) void k_order_copy(const tpe_colspec* __restric
 // kChunk; every (chunk, segment) pair is a 256-thread block, so a segment's
 // random gathers through its column's order (the rows' flags, values and list
 // positions) are spread over many CUs instead of one CU's load pipeline.
-// Three launches: counts per chunk, then the tid-order emit (list positions),
-// then the sorted-order emit (means and ramp weights); each block re-reduces
-// the few counts of the chunks before it (fixed order).
+// Two launches: counts per chunk with every row's rank among its chunk's
+// members, then the sorted-order emit (means and ramp weights), which adds
+// the row's chunk base (an exclusive prefix of the chunk counts, formed in
+// LDS by every block) to the rank it gathers; each block re-reduces the few
+// counts of the chunks before it (fixed order).
 constexpr int kCB = 256;                 // block size of the compaction kernels
 constexpr int kCR = 4;                   // items per thread
 constexpr int kChunk = kCB * kCR;        // items per chunk (item u * kCB + t of a chunk)
@@ -193,13 +195,16 @@ __device__ __forceinline__ int chunk_ranks(const bool (&tk)[kCR], int (&rank)[kC
 }
 
 // K1: per (chunk, segment): members in the tid-order chunk, how many of them
-// lie below the prior mean, the first member row; members in the sorted chunk
+// lie below the prior mean, the first member row; members in the sorted
+// chunk; and every row's word: its rank among the chunk's members (-1 for a
+// non-member) -- the chunk's base is added where the word is read (K3)
 __global__ __launch_bounds__(kCB) void k_fit_count(
     const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
     const int32_t* __restrict__ order, int64_t n_rows, const uint8_t* __restrict__ is_below,
     const tpe_gather* __restrict__ gathers, const tpe_seg* __restrict__ segs,
-    int32_t* __restrict__ cnt) {
-  __shared__ int sh[4 * (kCB / kWave)];
+    int32_t* __restrict__ cnt, int32_t* __restrict__ gi_scr) {
+  __shared__ int sh[kCR * (kCB / kWave)];
+  static_assert(kCR >= 4, "four block reductions share sh");
   const int sg = blockIdx.y;
   const SegView Q = seg_view(vals, active, order, ld, gathers[sg], segs[sg]);
   const int64_t c0 = (int64_t)blockIdx.x * kChunk;
@@ -210,16 +215,26 @@ __global__ __launch_bounds__(kCB) void k_fit_count(
     rows[u] = e < n_rows ? Q.O[e] : -1;
   }
   int n1 = 0, nlt = 0, n2 = 0, first = INT32_MAX;
+  bool tk[kCR];
 #pragma unroll
   for (int u = 0; u < kCR; ++u) {
     const int64_t r = c0 + u * kCB + threadIdx.x;
-    if (r < n_rows && Q.A[r] && is_below[r] == Q.side) {
+    tk[u] = r < n_rows && Q.A[r] && is_below[r] == Q.side;
+    if (tk[u]) {
       ++n1;
       nlt += order_key(obs_transform(Q.V[r], Q.transform, Q.floor_)) < Q.kp ? 1 : 0;
       first = min(first, (int)r);
     }
     const int32_t row = rows[u];
     if (row >= 0 && Q.A[row] && is_below[row] == Q.side) ++n2;
+  }
+  int rk[kCR];
+  chunk_ranks(tk, rk, sh);
+  int32_t* GI = gi_scr + (int64_t)sg * n_rows;
+#pragma unroll
+  for (int u = 0; u < kCR; ++u) {
+    const int64_t r = c0 + u * kCB + threadIdx.x;
+    if (r < n_rows) GI[r] = tk[u] ? rk[u] : -1;
   }
   n1 = block_sum<kCB, int>(n1, sh);
   nlt = block_sum<kCB, int>(nlt, sh + kCB / kWave);
@@ -234,6 +249,35 @@ __global__ __launch_bounds__(kCB) void k_fit_count(
   }
 }
 
+// exclusive block scan of one int per thread (sh: >= kCB / kWave ints,
+// reusable after the call); total: the block's sum
+__device__ __forceinline__ int block_excl_sum(int v, int* sh, int& total) {
+  constexpr int kNW = kCB / kWave;
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int x = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += x;
+  }
+  __syncthreads();
+  if (lane == kWave - 1) sh[wid] = incl;
+  __syncthreads();
+  int pos = incl - v;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < kNW; ++w) {
+    pos += w < wid ? sh[w] : 0;
+    total += sh[w];
+  }
+  __syncthreads();
+  return pos;
+}
+
+// columns of up to kPreChunks chunks (4M rows) take the chunk bases from LDS
+// in K3; longer ones globalize the words first (K2)
+constexpr int kPreChunks = 4096;
+
 // sum of field f over chunks [0, c) (all threads; fixed order)
 __device__ __forceinline__ int64_t chunks_before(const int32_t* C, int c, int f, int64_t* sh) {
   int64_t v = 0;
@@ -241,35 +285,24 @@ __device__ __forceinline__ int64_t chunks_before(const int32_t* C, int c, int f,
   return block_sum<kCB, int64_t>(v, sh);
 }
 
-// K2: tid-order emit -- each member row's position in the segment's list
-__global__ __launch_bounds__(kCB) void k_fit_emit_tid(
-    const uint8_t* __restrict__ active, int64_t ld, int64_t n_rows,
-    const uint8_t* __restrict__ is_below, const tpe_gather* __restrict__ gathers,
-    const int32_t* __restrict__ cnt, int32_t* __restrict__ gi_scr) {
-  __shared__ int sh[kCR * (kCB / kWave)];
+// K2 (columns of more than kPreChunks chunks only): the chunk's base added
+// to its members' words in place, so K3 reads global list positions
+__global__ __launch_bounds__(kCB) void k_fit_globalize(int64_t n_rows,
+                                                       const int32_t* __restrict__ cnt,
+                                                       int32_t* __restrict__ gi_scr) {
   __shared__ int64_t sh64[kCB / kWave];
   const int sg = blockIdx.y;
-  const tpe_gather G = gathers[sg];
-  const uint8_t* A = active + (int64_t)G.col * ld;
-  const uint8_t side = G.below ? 1 : 0;
   const int32_t* C = cnt + (int64_t)sg * gridDim.x * kCnt;
   const int64_t base = chunks_before(C, blockIdx.x, 0, sh64);
   const int64_t c0 = (int64_t)blockIdx.x * kChunk;
-  bool tk[kCR];
-#pragma unroll
-  for (int u = 0; u < kCR; ++u) {
-    const int64_t r = c0 + u * kCB + threadIdx.x;
-    tk[u] = r < n_rows && A[r] && is_below[r] == side;
-  }
-  int rk[kCR];
-  chunk_ranks(tk, rk, sh);
   int32_t* GI = gi_scr + (int64_t)sg * n_rows;
-  // every row gets its word: the list position of a member, -1 otherwise
-  // (so the sorted-order emit gathers this word alone for membership)
 #pragma unroll
   for (int u = 0; u < kCR; ++u) {
     const int64_t r = c0 + u * kCB + threadIdx.x;
-    if (r < n_rows) GI[r] = tk[u] ? (int32_t)(base + rk[u]) : -1;
+    if (r < n_rows) {
+      const int32_t g = GI[r];
+      if (g >= 0) GI[r] = (int32_t)(base + g);
+    }
   }
 }
 
@@ -277,6 +310,7 @@ __global__ __launch_bounds__(kCB) void k_fit_emit_tid(
 // at its slot: searchsorted(obs, prior_mu, 'left') (tpe.py:427), or the
 // len == 1 rule (tpe.py:414-421).  A count other than gathers[sg].count sets
 // bit 4 of *err and writes nothing.
+template <bool LOCAL>  // LOCAL: the words are chunk-local ranks (K2 skipped)
 __global__ __launch_bounds__(kCB) void k_fit_emit_sorted(
     const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
     const int32_t* __restrict__ order, int64_t n_rows, const uint8_t* __restrict__ is_below,
@@ -285,6 +319,7 @@ __global__ __launch_bounds__(kCB) void k_fit_emit_sorted(
     double* __restrict__ w, double* __restrict__ mu, int32_t* __restrict__ err) {
   __shared__ int sh[kCR * (kCB / kWave)];
   __shared__ int64_t sh64[kCB / kWave];
+  __shared__ int32_t s_pre[LOCAL ? kPreChunks : 1];  // tid chunks' member bases
   const int sg = blockIdx.y;
   tpe_seg* S = segs + sg;
   const tpe_gather G = gathers[sg];
@@ -298,6 +333,18 @@ __global__ __launch_bounds__(kCB) void k_fit_emit_sorted(
   }
   const int64_t n_lt = chunks_before(C, nch, 1, sh64);
   const int64_t base = chunks_before(C, blockIdx.x, 3, sh64);
+  if constexpr (LOCAL) {  // exclusive prefix of the tid chunks' member counts
+    int carry = 0;
+    for (int q0 = 0; q0 < nch; q0 += kCB) {
+      const int q = q0 + (int)threadIdx.x;
+      const int c = q < nch ? C[q * kCnt] : 0;
+      int total;
+      const int ex = block_excl_sum(c, sh, total);
+      if (q < nch) s_pre[q] = carry + ex;
+      carry += total;
+    }
+    __syncthreads();
+  }
   int prior_pos = 0;
   if (n >= 2) {
     prior_pos = (int)n_lt;
@@ -324,6 +371,7 @@ __global__ __launch_bounds__(kCB) void k_fit_emit_sorted(
     v[u] = in ? Q.V[row] : 0.0;
     gi[u] = in ? gi_scr[(int64_t)sg * n_rows + row] : -1;  // -1: not a member
     tk[u] = gi[u] >= 0;
+    if (LOCAL && tk[u]) gi[u] += s_pre[row / kChunk];
   }
   int rk[kCR];
   chunk_ranks(tk, rk, sh);
@@ -437,11 +485,15 @@ extern "C" int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t
   double* part = reinterpret_cast<double*>(p + gi_bytes(n_seg, n_rows) + cnt_bytes(n_seg, n_rows));
   const dim3 grid((unsigned)n_chunks(n_rows), (unsigned)n_seg);
   hipLaunchKernelGGL(k_fit_count, grid, dim3(kCB), 0, st, vals, active, ld, order, n_rows,
-                     is_below, gathers, segs, cnt);
-  hipLaunchKernelGGL(k_fit_emit_tid, grid, dim3(kCB), 0, st, active, ld, n_rows, is_below,
-                     gathers, cnt, gi);
-  hipLaunchKernelGGL(k_fit_emit_sorted, grid, dim3(kCB), 0, st, vals, active, ld, order, n_rows,
-                     is_below, gathers, segs, cnt, gi, w, mu, err);
+                     is_below, gathers, segs, cnt, gi);
+  if (n_chunks(n_rows) <= kPreChunks) {
+    hipLaunchKernelGGL(k_fit_emit_sorted<true>, grid, dim3(kCB), 0, st, vals, active, ld, order,
+                       n_rows, is_below, gathers, segs, cnt, gi, w, mu, err);
+  } else {
+    hipLaunchKernelGGL(k_fit_globalize, grid, dim3(kCB), 0, st, n_rows, cnt, gi);
+    hipLaunchKernelGGL(k_fit_emit_sorted<false>, grid, dim3(kCB), 0, st, vals, active, ld, order,
+                       n_rows, is_below, gathers, segs, cnt, gi, w, mu, err);
+  }
   fit_tail(segs, n_seg, max_obs, part, w, mu, sigma, wcdf, coef64, coef32, st);
   return check_launch("tpe_fit_sorted");
 }
