@@ -27,6 +27,7 @@
 // identity row list, and ties keep tid order -- np.argsort(kind="stable") of
 // the reference's list (tie semantics).
 #include <algorithm>
+#include <cstdlib>
 
 #include "tpe_common.hpp"
 
@@ -486,7 +487,9 @@ extern "C" int tpe_fit_sorted(const double* vals, const uint8_t* active, int64_t
   const dim3 grid((unsigned)n_chunks(n_rows), (unsigned)n_seg);
   hipLaunchKernelGGL(k_fit_count, grid, dim3(kCB), 0, st, vals, active, ld, order, n_rows,
                      is_below, gathers, segs, cnt, gi);
-  if (n_chunks(n_rows) <= kPreChunks) {
+  // TPE_FIT_GLOBALIZE=1 (tests): the long-column path at any size
+  const char* gl = getenv("TPE_FIT_GLOBALIZE");
+  if (n_chunks(n_rows) <= kPreChunks && !(gl && gl[0] == '1')) {
     hipLaunchKernelGGL(k_fit_emit_sorted<true>, grid, dim3(kCB), 0, st, vals, active, ld, order,
                        n_rows, is_below, gathers, segs, cnt, gi, w, mu, err);
   } else {

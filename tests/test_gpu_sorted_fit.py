@@ -86,6 +86,32 @@ def test_sorted_fit_equals_sort_fit(T, inactive):
                [(r.index, r.value, r.score) for r in b]
 
 
+@pytest.mark.parametrize("T", [9, 5000, 12000])
+def test_long_column_path_gives_the_same_bits(T, monkeypatch):
+    """Columns of more than 4096 chunks globalise the chunk-local ranks in a
+    launch of their own (k_fit_globalize) instead of adding the chunk bases
+    from LDS; TPE_FIT_GLOBALIZE=1 takes that path at these sizes -- the same
+    posteriors and winners as the default path."""
+    from hyperopt_amd.engine import DeviceHistory, Engine
+    rng = np.random.RandomState(T + 1)
+    mat = _cols(T, rng)
+    active = rng.uniform(size=mat.shape) >= 0.1
+    losses = rng.normal(size=T)
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("TPE_FIT_GLOBALIZE", env)
+        eng = Engine()
+        eng.sorted_fit = True
+        h = DeviceHistory(eng, len(SPACE), cap=32)
+        h.append(mat, active)
+        works, isb = _level(h, mat, active, losses, T)
+        post = eng.run(works, posteriors=True, history=h, is_below=isb)
+        win = eng.run(works, precision=32, history=h, is_below=isb)
+        out.append((post, [(r.index, r.value, r.score) for r in win]))
+    _same_posteriors(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+
+
 def test_sorted_fit_through_appends():
     """The order merged in after every append -- 1, 7, 2048, 2049, 3000 rows
     (one and several tpe_history_order chunks) -- gives the sort fit's bits
