@@ -781,17 +781,21 @@ __device__ __forceinline__ bool log_taylor(const double (&p)[kP], double c, doub
   }
   w4 *= 1.001f;
   if (!(w4 <= 0.5f)) return false;
-  float tail = 0.0f, rk = 1.0f;
+  float tail = 0.0f, rk = 1.0f, jm[kLogM + 1];  // jm[j] = j m_j
   const float rf = (float)r;
 #pragma unroll
   for (int k = 1; k <= kLogM; ++k) {
-    float s = k < kP ? aa[k] : 0.0f;
+    // m_k = |a_k| + (1/k) sum_j j m_j |a_{k-j}| (fp32 rounding inside the
+    // 1e-3 inflation below)
+    float s = 0.0f;
 #pragma unroll
     for (int j = 1; j < k; ++j)
-      if (k - j < kP) s = fmaf((float)j * m[j] * (1.0f / (float)k), aa[k - j], s);
-    m[k] = s;
+      if (k - j < kP) s = fmaf(jm[j], aa[k - j], s);
+    const float mk = fmaf(s, 1.0f / (float)k, k < kP ? aa[k] : 0.0f);
+    m[k] = mk;
+    jm[k] = (float)k * mk;
     rk *= rf;
-    if (k > kLogD) tail = fmaf(s, rk, tail);
+    if (k > kLogD) tail = fmaf(mk, rk, tail);
   }
   // past kLogM: m_k (4r)^k <= ln 2, so sum_{k > kLogM} m_k r^k <= ln2 4^-(M+1) / (3/4)
   rem = (double)tail * 1.001 + 0.6931471805599453 * ldexp(1.0, -2 * (kLogM + 1)) / 0.75;
@@ -820,6 +824,8 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
   const double nd0 = kU * 0.92387953251128674, nd1 = kU * 0.38268343236508978, nd2 = -nd1,
                nd3 = -nd0;
   const double un = l == 0 ? nd0 : l == 1 ? nd1 : l == 2 ? nd2 : nd3;  // (lanes >= 4: unused)
+  const double i10 = 1.0 / (nd1 - nd0), i21 = 1.0 / (nd2 - nd1), i32 = 1.0 / (nd3 - nd2),
+               i20 = 1.0 / (nd2 - nd0), i31 = 1.0 / (nd3 - nd1), i30 = 1.0 / (nd3 - nd0);
   const float uf = (float)un;
   constexpr double r = kUFit / kScoreLanes;
   const double cI = -kUFit + (2 * l + 1) * r;  // this lane's sub-interval centre
@@ -849,11 +855,13 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
     const double f0 = __shfl(f, gbase + 0, kWave), f1 = __shfl(f, gbase + 1, kWave),
                  f2 = __shfl(f, gbase + 2, kWave), f3 = __shfl(f, gbase + 3, kWave);
     const bool nodes_ok = ((__ballot(!ok_pt) >> gbase) & 0xFull) == 0;
-    // Newton divided differences -> monomial coefficients of the cubic
-    const double d01 = (f1 - f0) / (nd1 - nd0), d12 = (f2 - f1) / (nd2 - nd1),
-                 d23 = (f3 - f2) / (nd3 - nd2);
-    const double d012 = (d12 - d01) / (nd2 - nd0), d123 = (d23 - d12) / (nd3 - nd1);
-    const double d0123 = (d123 - d012) / (nd3 - nd0);
+    // Newton divided differences -> monomial coefficients of the cubic (the
+    // node spacings' reciprocals are constants: multiplies, not fp64
+    // divisions -- q is an approximation whose own error the bound below
+    // measures, so its last bits are free)
+    const double d01 = (f1 - f0) * i10, d12 = (f2 - f1) * i21, d23 = (f3 - f2) * i32;
+    const double d012 = (d12 - d01) * i20, d123 = (d23 - d12) * i31;
+    const double d0123 = (d123 - d012) * i30;
     const double c3 = d0123;
     const double c2 = d012 - d0123 * (nd0 + nd1 + nd2);
     const double c1 = d01 - d012 * (nd0 + nd1) + d0123 * (nd0 * nd1 + nd0 * nd2 + nd1 * nd2);

@@ -8,6 +8,6 @@ for rep in 1 2; do
   for t in "$@"; do
     n=$( [ "$t" = "." ] && echo base || basename $t )
     ( cd $t && timeout -k 10 200 python3 -u bench.py --steps 20 --warmup 3 --no-extras --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/abb/${n}_${rep}.json 2>/dev/null ) || exit 1
-    echo "$n $rep $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/abb/${n}_${rep}.json) $(grep -o '"avg_launch_ms": [0-9.]*' gpurun_out/abb/${n}_${rep}.json)"
+    echo "$n $rep $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/abb/${n}_${rep}.json) $(grep -o '"avg_launch_ms": [0-9.]*' gpurun_out/abb/${n}_${rep}.json) $(grep -o '"table_build": [0-9.]*' gpurun_out/abb/${n}_${rep}.json)"
   done
 done
