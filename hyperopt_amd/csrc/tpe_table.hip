@@ -1736,7 +1736,10 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
 //  4. The last block of the job to finish takes np.argmax over the
 //     survivors (largest score, then smallest index, NaN first): best[j] =
 //     {fp64 score, index, value, n_cand}, and re-arms the counter.
-constexpr int kBandBlocks = 16;      // blocks per job
+#ifndef TPE_BAND_BLOCKS  // diagnostic builds: k_band blocks per job
+#define TPE_BAND_BLOCKS 16
+#endif
+constexpr int kBandBlocks = TPE_BAND_BLOCKS;  // blocks per job
 constexpr int kBandSurv = 128;       // survivors scored directly (more: the cell expansions)
 constexpr int kSurvBatch = 4;        // survivors summed together per pass
 #ifndef TPE_BAND_BX
