@@ -801,7 +801,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     tpe_best* __restrict__ slot_part, int slot_n) {
   extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
-  __shared__ float s_stage[kLatR * kBS];
+  __shared__ alignas(16) float s_stage[kLatR * kBS];  // (also the slot blocks' fp64 scratch)
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   const int64_t slot_blocks = (int64_t)slot_n * n_jobs;
   if ((int64_t)blockIdx.x < slot_blocks) {  // block-uniform

@@ -186,8 +186,8 @@ def collect_history(trials, labels):
         # finished documents' losses come from the cache (Columnar.losses)
         losses = col.losses()
         keep = ~np.isnan(losses)
-        if keep.all():
-            return History(col.key_tid[:n].copy(), losses, col.obs_tid[:n].copy(), col=col)
+        if keep.all():  # (views: the cache only appends past row n during the call)
+            return History(col.key_tid[:n], losses, col.obs_tid[:n], col=col)
         rows = np.flatnonzero(keep)
         return History(col.key_tid[rows], losses[rows], col.obs_tid[rows], col=col, rows=rows)
     best_loss, best_doc = {}, {}
@@ -304,14 +304,18 @@ class LevelInputs(object):
             return
         c = hist.col
         T = hist.tids.size
-        flags = np.full(T, 2, np.uint8)
-        flags[isa] = 0
-        flags[isb] = 1
         below_pos = np.flatnonzero(isb)
+        every_above = T - below_pos.size == int(np.count_nonzero(isa))
+        if every_above:  # every row below (1) or above (0): the mask's bytes are the flags
+            flags = np.ascontiguousarray(isb).view(np.uint8)
+        else:
+            flags = np.full(T, 2, np.uint8)
+            flags[isa] = 0
+            flags[isb] = 1
         crow = below_pos if hist.rows is None else hist.rows[below_pos]
         self.vb, self.ab = c.vals[crow], c.active[crow]
         self.nb = nb = self.ab.sum(0)
-        if T - below_pos.size == int(np.count_nonzero(isa)):  # every other row is above
+        if every_above:
             self.n_above = hist.label_counts() - nb
         else:
             self.n_above = hist.active[isa].sum(0)
