@@ -221,6 +221,7 @@ class DeviceHistory:
         self.order_rows = {}
         self.active_host = np.zeros((0, self.n_labels), bool)
         self.n_active = np.zeros(self.n_labels, np.int64)
+        self._stage = self._stage_ev = None  # pinned staging of appended rows, its upload event
         self._grow(max(int(cap), 16))
 
     @property
@@ -255,10 +256,32 @@ class DeviceHistory:
         if self.rows + k > self.cap:
             self._grow(max(2 * self.cap, self.rows + k))
         r0, t = self.rows, self.torch
-        src_v = t.from_numpy(np.ascontiguousarray(np.where(active, vals, 0.0).T))
-        src_a = t.from_numpy(np.ascontiguousarray(active.T.astype(np.uint8)))
-        self.vals[:, r0:r0 + k].copy_(src_v.to(self.device))
-        self.active[:, r0:r0 + k].copy_(src_a.to(self.device))
+        # the new rows, label-major, through a pinned staging buffer: one
+        # async upload on torch's current stream (the level's), then one
+        # strided device copy per array into columns r0..r0+k -- no host wait
+        nl = self.n_labels
+        nv = nl * k * 8
+        need = nv + nl * k
+        hip = L.hip()
+        if self._stage is None or self._stage.numel() < need:
+            self._stage = t.empty(max(need, 4096), dtype=t.uint8, pin_memory=True)
+            self._stage_ev = None
+        if self._stage_ev is not None:  # the previous append's upload has read the stage
+            L.hip_check(hip.hipEventSynchronize(self._stage_ev), "hipEventSynchronize")
+        st = self._stage.numpy()
+        np.copyto(st[:nv].view(np.float64).reshape(nl, k), np.where(active, vals, 0.0).T)
+        np.copyto(st[nv:need].reshape(nl, k), active.T)
+        dev = self._stage[:need].to(self.device, non_blocking=True)
+        self.vals[:, r0:r0 + k].copy_(dev[:nv].view(t.float64).view(nl, k))
+        self.active[:, r0:r0 + k].copy_(dev[nv:need].view(nl, k))
+        if self._stage_ev is None:
+            ev = ctypes.c_void_p()
+            L.hip_check(hip.hipEventCreateWithFlags(ctypes.byref(ev), L.EVENT_NO_TIMING),
+                        "hipEventCreateWithFlags")
+            self._stage_ev = ev
+        L.hip_check(hip.hipEventRecord(self._stage_ev,
+                                       t.cuda.current_stream(self.device).cuda_stream),
+                    "hipEventRecord")
         self.active_host[r0:r0 + k] = active
         self.n_active += active.sum(0)
         self.rows += k
