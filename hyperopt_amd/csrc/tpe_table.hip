@@ -730,6 +730,19 @@ __host__ __device__ inline double mix_eps(int items, bool coop, double ab) {
          + (K + 8) * 2.0 * ud * E2;     // fp64 sums, rescale and merge factors of the P_n
 }
 
+// The LGMM1 candidate drawn as y (fp32) is returned as x = exp(y) in fp64
+// (cand_value), and the reference scores log(x) (tpe.py:284-287 via
+// lognormal_lpdf, :208-217), which differs from y by the two roundings:
+// |log(exp(y)) - y| <= 2^-51 (1 + |y|).  In cell units (|y| <= max(|lo|, |hi|)
+// on the grid) that is a shift of u by at most this; the error bounds add it
+// times the slope (the cubic's, or |P'| of the two-polynomial cell), so the
+// band holds the winner of the scores at log(x).  0 for GMM1.
+__host__ __device__ inline float lgmm_du(const tpe_job& J, const tpe_table& T) {
+  if (J.family != TPE_LGMM1 || !(T.h > 0.0)) return 0.0f;
+  const double ym = fmax(fabs(T.lo), fabs(T.hi)) + 2.0 * T.h;
+  return (float)(0x1.0p-51 * (1.0 + ym) / T.h * 1.01);
+}
+
 __device__ __forceinline__ const float4* score_cells_of(const char* region, int64_t cap) {
   return reinterpret_cast<const float4*>(region + ((cap * (int64_t)(kCellF * 4 + 8) + 15) & ~15ll));
 }
@@ -827,6 +840,9 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
   const double i10 = 1.0 / (nd1 - nd0), i21 = 1.0 / (nd2 - nd1), i32 = 1.0 / (nd3 - nd2),
                i20 = 1.0 / (nd2 - nd0), i31 = 1.0 / (nd3 - nd1), i30 = 1.0 / (nd3 - nd0);
   const float uf = (float)un;
+  // LGMM1: the exact score is taken at log(exp(y)) of the returned value, not
+  // at y (cand_value) -- a shift of u by at most du_lg (lgmm_du)
+  const float du_lg = lgmm_du(J, Tb);
   constexpr double r = kUFit / kScoreLanes;
   const double cI = -kUFit + (2 * l + 1) * r;  // this lane's sub-interval centre
   float slope = 0.0f, epsc = 0.0f;  // over this thread's unflagged cells (lane 0 of a group)
@@ -912,7 +928,8 @@ __global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__
         slope = fmaxf(slope, sl);
         const float ev = 0x1.0p-21f * (1.0501f * fabsf(q.y) + 1.1028f * fabsf(q.z) +
                                         1.1581f * fabsf(q.w));
-        const float ec = bmax + ev + 4.5f * 0x1.0p-24f * sl + 0x1.0p-24f * 1.0001f * (float)fabs(off);
+        const float ec = bmax + ev + (4.5f * 0x1.0p-24f + du_lg) * sl +
+                         0x1.0p-24f * 1.0001f * (float)fabs(off);
         epsc = fmaxf(epsc, ec * 1.0001f);
       }
     }
@@ -1327,10 +1344,15 @@ __device__ __forceinline__ float ord_dec(uint32_t e) {
 }
 
 // the value of an unquantized candidate drawn as y in fp32: y (GMM1) or
-// exp(y) evaluated in fp64 (LGMM1) -- so log(value) is y up to fp64 rounding
-// and the value's exact score is the score at y
+// exp(y) evaluated in fp64 (LGMM1)
 __device__ __forceinline__ double cand_value(float y, bool lgmm) {
   return lgmm ? exp((double)y) : (double)y;
+}
+// the coordinate its exact fp64 score is taken at: the returned value (GMM1)
+// or log of it (LGMM1: the reference scores log(x) of the value it returns,
+// tpe.py:284-287 / lognormal_lpdf :208-217) -- within lgmm_du of y in cell units
+__device__ __forceinline__ double score_coord(float y, bool lgmm) {
+  return lgmm ? log(cand_value(y, true)) : (double)y;
 }
 
 // relative error bound of one mixture's two-polynomial value p (fp32 Horner
@@ -1338,7 +1360,7 @@ __device__ __forceinline__ double cand_value(float y, bool lgmm) {
 // exact u: gamma_6 times the absolute polynomial, the fp16 tail's rounding
 // (u to fp16, two fp16 FMAs, subnormal spacing), and u's fp32 rounding times
 // a bound of |P'|; +inf when it is not below p
-__device__ __forceinline__ float poly_rel_err(const float (&P)[kP], float u, float p) {
+__device__ __forceinline__ float poly_rel_err(const float (&P)[kP], float u, float p, float du) {
   const float au = fabsf(u);
   float pabs = 0.0f, pd = 0.0f;
 #pragma unroll
@@ -1347,7 +1369,7 @@ __device__ __forceinline__ float poly_rel_err(const float (&P)[kP], float u, flo
     if (n >= 1) pd = fmaf(pd, 1.0501f, (float)n * fabsf(P[n]));
   }
   const float dt = 0x1.0p-9f * 1.16f * (fabsf(P[6]) + fabsf(P[7]) + fabsf(P[8])) + 0x1.0p-23f;
-  const float dp = (6.1f * 0x1.0p-24f * pabs + 1.35f * dt + 4.5f * 0x1.0p-24f * pd) * 1.001f;
+  const float dp = (6.1f * 0x1.0p-24f * pabs + 1.35f * dt + du * pd) * 1.001f;
   return dp < p ? dp / (p - dp) : INFINITY;
 }
 
@@ -1355,7 +1377,7 @@ __device__ __forceinline__ float poly_rel_err(const float (&P)[kP], float u, flo
 // beyond the polynomials' own 2.0001 eps_mix
 __device__ __forceinline__ float eps_2poly(const f4 q0, const f4 q1, const f4 q2, const f4 q3,
                                            float u, float pb, float pa, float lb2, float la2,
-                                           float s) {
+                                           float s, float du) {
   float Pb[kP], Pa[kP];
   const float c[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
 #pragma unroll
@@ -1368,7 +1390,7 @@ __device__ __forceinline__ float eps_2poly(const f4 q0, const f4 q1, const f4 q2
   Pb[6] = (float)t6.x; Pa[6] = (float)t6.y;
   Pb[7] = (float)t7.x; Pa[7] = (float)t7.y;
   Pb[8] = (float)t8.x; Pa[8] = (float)t8.y;
-  const float rb = poly_rel_err(Pb, u, pb), ra = poly_rel_err(Pa, u, pa);
+  const float rb = poly_rel_err(Pb, u, pb, du), ra = poly_rel_err(Pa, u, pa, du);
   const float off = fabsf(q3.w);
   return (0x1.0p-24f * off + rb + ra +
           kLn2T * kEtaLog2 * (fmaxf(1.0f, fabsf(lb2)) + fmaxf(1.0f, fabsf(la2))) +
@@ -1548,7 +1570,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
           isfinite(pb) && isfinite(pa)) {
         const float lb2 = __builtin_amdgcn_logf(pb), la2 = __builtin_amdgcn_logf(pa);
         const float s = q3.w + (lb2 - la2) * kLn2T;
-        const float e2 = eps_2poly(q0, q1, q2, q3, u, pb, pa, lb2, la2, s) + 2.0001f * Tb.eps_mix;
+        const float e2 = eps_2poly(q0, q1, q2, q3, u, pb, pa, lb2, la2, s,
+                                   4.5f * 0x1.0p-24f + lgmm_du(J, Tb)) +
+                         2.0001f * Tb.eps_mix;
         if (s == s && e2 < INFINITY) {
           const float hi = up(s + e2);
           fold(r, s, y, hi);
@@ -2158,6 +2182,7 @@ __global__ __launch_bounds__(kBX) void k_band(
     return;
   }
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
+  const bool lgmm = J.family == TPE_LGMM1;
   if (ns <= kBandSurv) {
     // ---- 3a. direct: this block's component chunk, for every survivor ----
     for (int mix = 0; mix < 2; ++mix) {
@@ -2172,7 +2197,7 @@ __global__ __launch_bounds__(kBX) void k_band(
         for (int i = 0; i < kSurvBatch; ++i) {
           m[i] = -INFINITY;
           sm[i] = 0.0;
-          y[i] = (double)s_y[min(b0 + i, ns - 1)];
+          y[i] = score_coord(s_y[min(b0 + i, ns - 1)], lgmm);
         }
         for (int k = k0 + (int)threadIdx.x; k < k1; k += kBX) {
           const double4 c = C[k];
@@ -2342,7 +2367,7 @@ __global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ 
         if (s_cells[mid] < c) lo = mid + 1; else hi = mid;
       }
       const int k = lo;
-      const double y = (double)yf;
+      const double y = score_coord(yf, lgmm);
       double l2[2];
       for (int mix = 0; mix < 2; ++mix) {
         const tpe_seg& S = mix ? SA : SB;
@@ -2538,8 +2563,8 @@ __global__ __launch_bounds__(kBS) void k_score_pruned64(
         // the table path's fp32 stream (the exact re-score of an overflowed band)
         const float y32 = draw32(M, J.key, J.cand_base + li, lo_on, hi_on, (float)J.low,
                                  (float)J.high);
-        y = (double)y32;
         x = cand_value(y32, lgmm);
+        y = score_coord(y32, lgmm);  // (LGMM1: log of the returned value, as INJ)
       } else {
         x = draw64(M, J.key, J.cand_base + li, lo_on, hi_on, J.low, J.high);
         if (lgmm) x = exp(x);

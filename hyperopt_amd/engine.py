@@ -263,11 +263,12 @@ class DeviceHistory:
         nv = nl * k * 8
         need = nv + nl * k
         hip = L.hip()
-        if self._stage is None or self._stage.numel() < need:
-            self._stage = t.empty(max(need, 4096), dtype=t.uint8, pin_memory=True)
-            self._stage_ev = None
         if self._stage_ev is not None:  # the previous append's upload has read the stage
             L.hip_check(hip.hipEventSynchronize(self._stage_ev), "hipEventSynchronize")
+        if self._stage is None or self._stage.numel() < need:
+            # grown geometrically; the event is kept (it only orders the stage's reuse)
+            old = 0 if self._stage is None else self._stage.numel()
+            self._stage = t.empty(max(need, 2 * old, 4096), dtype=t.uint8, pin_memory=True)
         st = self._stage.numpy()
         np.copyto(st[:nv].view(np.float64).reshape(nl, k), np.where(active, vals, 0.0).T)
         np.copyto(st[nv:need].reshape(nl, k), active.T)
@@ -1871,15 +1872,19 @@ class _Pending(object):
             st = res_h[16:40].view(np.int64).tolist()
             eng.last_table_stats = {"exact_candidates": st[0], "failed_cells": st[1],
                                     "failed_score_cells": st[2]}
-        _raise_errors(err)
         n = self.order.size
         best_h = res_h[64:64 + n * L.BEST_DTYPE.itemsize].view(L.BEST_DTYPE)
+        # the same order as Engine._read_results: the band fix and the settle
+        # exchange first, the error bits after -- a rank whose level set an
+        # error bit still takes part in an owed second all-gather, so its
+        # peers are not left blocked in it
         if self.fix is not None:
             self.fix(best_h, self.jobs)
         eng.last_exchange = res_h[self.xoff:].view(L.BEST_DTYPE).copy() \
             if self.xoff is not None else None
         if self.xoff is not None:
             eng.last_exchange = eng._exchange_fix(best_h, eng.last_exchange, self.xinfo)
+        _raise_errors(err)
         by = np.empty(n, L.BEST_DTYPE)
         by[self.order] = best_h[:n]
         self._res = BatchResult(by["index"].copy(), by["value"].copy(), by["score"].copy(),

@@ -7,7 +7,8 @@ level (same space, history, split, Philox keys, candidate ranges; first run
 and its replay) is run once more and EVERY label's winner is re-derived
 exactly from the label's own materialised candidate stream:
   * continuous labels (table path): np.argmax over the fp64 scores of the
-    2^22 drawn values (the pruned exact fp64 scorer on the injected stream);
+    2^22 drawn values (the pruned exact fp64 scorer on the injected stream),
+    and the winner and runner-up re-scored by the ORACLE;
   * quantized labels (prefix-first lattice path): the ORACLE's fp64 score of
     each distinct drawn value, np.argmax over the stream (first index);
   * categorical labels (prefix-first categorical path): the ORACLE's
@@ -77,10 +78,25 @@ def test_every_label_is_the_exact_argmax_of_its_stream(level, kind):
         if kind in ("uniform", "loguniform", "normal"):
             cand = _stream(eng, w).cand
             x, = ex.run([LabelWork(lab, k, a, w.obs_below, w.obs_above, cand=cand)],
-                        precision=64)
+                        precision=64, outputs=True)
             assert index[j] == x.index, (lab, index[j], x.index)
             assert value[j] == cand[x.index]
             np.testing.assert_allclose(score[j], x.score, rtol=1e-12, atol=1e-12)
+            # pinned to the oracle directly: the winner and the runner-up of
+            # the stream re-scored by the numpy restatement (tpe.py:117-180,
+            # 265-307), same values, same order
+            s64 = x.below_llik - x.above_llik
+            best = int(index[j])
+            assert best == int(np.argmax(s64))
+            second = int(np.argmax(np.where(np.arange(n) == best, -np.inf, s64)))
+            pick = np.array([best, second])
+            with np.errstate(all="ignore"):
+                ref = O.continuous_label_scores(k, a, w.obs_below, w.obs_above, cand[pick])
+            rs = ref["below_llik"] - ref["above_llik"]
+            np.testing.assert_allclose(rs, s64[pick], rtol=1e-9, atol=1e-9)
+            gap = s64[best] - s64[second]
+            if gap > 1e-13 * max(1.0, abs(s64[best])):  # beyond fp64 rounding noise
+                assert rs[0] > rs[1], (lab, rs, gap)
         elif kind == "quniform":
             cand = _stream(eng, w).cand
             u, inv = np.unique(cand, return_inverse=True)

@@ -43,8 +43,7 @@ def test_precision32_small_levels_are_exact(engine, kind, args, gen, n_cand, n_h
     e, = engine.run([w64], precision=64, outputs=True)
     s = e.below_llik - e.above_llik
     best = int(np.argmax(s))
-    if r.index == best:
-        assert r.value == d.cand[best]
-    else:  # LGMM1: the value is exp(y) in fp64, its log is y up to one rounding
-        assert kind == "loguniform"
-        assert abs(s[r.index] - s[best]) <= 1e-12 * max(1.0, abs(s[best]))
+    # every kind index-exact (LGMM1: scored at log of the returned value, as
+    # the injected path and the reference score it)
+    assert r.index == best
+    assert r.value == d.cand[best]

@@ -361,3 +361,37 @@ def test_lpdf_matches_oracle(precision, lg, bounded, q):
     assert np.array_equal(fin, np.isfinite(got))
     err = np.abs(got - want)[fin]
     assert np.all(err <= tol[fin]), (np.max(err), np.argmax(err - tol[fin]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", PREC)
+@pytest.mark.parametrize("lg", [False, True])
+@pytest.mark.parametrize("q", [0.5, 1.0])
+def test_quantized_lpdf_outside_the_rounded_support(precision, lg, q):
+    """Quantized values the bounded label cannot take (beyond round(low/q)q or
+    round(high/q)q, and between the bound and that slot): the reference clips
+    the bin to [low, high] with max/min (tpe.py:154-158, 296-300), so a bin
+    past a bound has a negative or empty mass -- NaN or -inf, whichever its
+    log gives -- and a bin straddling a bound a partial one.  The HIP lpdf
+    gives the oracle's value, NaN and -inf included."""
+    _gpu()
+    from oracle import tpe_oracle as O
+    rng = np.random.RandomState(71 + 2 * lg + int(4 * q))
+    w, mu, s = _random_mixture(rng, 9, lg)
+    low, high = (-1.0, 2.0) if lg else (0.5, 5.5)
+    lo_v, hi_v = (np.exp(low), np.exp(high)) if lg else (low, high)
+    ks = np.arange(np.floor(lo_v / q) - 4, np.ceil(hi_v / q) + 5)
+    x = ks * q
+    if lg:
+        x = x[x > 0]
+    x = x[(x < np.round(lo_v / q) * q + 2 * q) | (x > np.round(hi_v / q) * q - 2 * q)]
+    f = M.LGMM1_lpdf if lg else M.GMM1_lpdf
+    o = O.lgmm1_lpdf if lg else O.gmm1_lpdf
+    with np.errstate(all="ignore"):
+        want = o(x, w, mu, s, low=low, high=high, q=q)
+    got = f(x, w, mu, s, low=low, high=high, q=q, precision=precision)
+    assert (~np.isfinite(want)).any()  # the case is exercised
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_array_equal(np.isneginf(got), np.isneginf(want))
+    fin = np.isfinite(want)
+    np.testing.assert_allclose(got[fin], want[fin], rtol=1e-8, atol=1e-8)

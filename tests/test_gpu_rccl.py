@@ -104,3 +104,74 @@ def test_level_exchange_one_rank(native):
             assert eng.graph_stats.get("native", 0) >= 2
     finally:
         rccl.ncclCommDestroy(comm)
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_level_exchange_settles_band_overflow(native, monkeypatch):
+    """A table-path label whose band overflows (BAND_TILE_CAP = 0: every
+    scorer tile is full) leaves the level with n_scored = -1; the in-level
+    exchange carries the -1 to every rank, and Engine._exchange_fix runs the
+    exchange once more on the rank's exact records (after _band_fix re-scored
+    the stream in fp64).  On a one-rank communicator: one fix per level, the
+    label record holds the full count and the exact argmax of the stream --
+    first run and the replayed (re-issued) run alike."""
+    import torch
+    import hyperopt_amd.engine as E
+    from oracle import tpe_oracle as O
+    monkeypatch.setattr(E, "BAND_TILE_CAP", 0)
+    torch.cuda.set_device(0)
+    rccl, comm = _comm()
+    try:
+        eng = E.Engine()
+        eng.native = native
+        rng = np.random.RandomState(5)
+        T, n = 3000, 1 << 17
+        mat = np.stack([rng.uniform(-5, 5, T), np.exp(rng.uniform(-5, 0, T))], 1)
+        hist = E.DeviceHistory(eng, 2, cap=4096)
+        hist.append(mat)
+        isb = np.zeros(T, np.uint8)
+        isb[np.argsort(rng.normal(size=T))[:T // 4]] = 1
+        space = [("u", "uniform", (-5.0, 5.0)), ("l", "loguniform", (-5.0, 0.0))]
+        slots = [1, 0]
+        ref = None
+        for step in range(3):
+            works = []
+            for col, (lab, kind, a) in enumerate(space):
+                works.append(E.LabelWork(lab, kind, a, mat[:, col][isb == 1], None, n_cand=n,
+                                         key=4242 + col, col=col,
+                                         n_above=int((isb == 0).sum()), n_total=n))
+            before = getattr(eng, "exchange_fixes", 0)
+            res = eng.run(works, precision=32, history=hist, is_below=isb,
+                          exchange=(comm.value, 2, 1, slots))
+            assert getattr(eng, "exchange_fixes", 0) == before + 1
+            got = eng.last_exchange
+            assert list(got["n_scored"]) == [n, n]
+            for col, (lab, kind, a) in enumerate(space):
+                r, x = res[col], got[slots[col]]
+                assert r.n_scored == n
+                assert (int(x["index"]), float(x["value"])) == (r.index, r.value)
+            if ref is None:
+                ref = [(r.index, r.value) for r in res]
+                # the exact argmax of each label's materialised fp32 stream
+                for col, (lab, kind, a) in enumerate(space):
+                    w = works[col]
+                    s, = E.Engine().run([E.LabelWork(lab, kind, a, w.obs_below,
+                                                     mat[:, col][isb == 0], n_cand=n,
+                                                     key=w.key)],
+                                        precision=32, sample_only=True)
+                    d, = E.Engine().run([E.LabelWork(lab, kind, a, w.obs_below,
+                                                     mat[:, col][isb == 0], cand=s.cand)],
+                                        precision=64, outputs=True)
+                    best = int(np.argmax(d.below_llik - d.above_llik))
+                    assert res[col].index == best and res[col].value == s.cand[best]
+                    with np.errstate(all="ignore"):
+                        o = O.continuous_label_scores(kind, a, w.obs_below,
+                                                      mat[:, col][isb == 0], s.cand[[best]])
+                    np.testing.assert_allclose(o["below_llik"] - o["above_llik"],
+                                               res[col].score, rtol=1e-9, atol=1e-9)
+            else:
+                assert [(r.index, r.value) for r in res] == ref
+        if native:
+            assert eng.graph_stats.get("native", 0) >= 1
+    finally:
+        rccl.ncclCommDestroy(comm)
