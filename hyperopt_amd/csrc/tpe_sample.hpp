@@ -371,5 +371,231 @@ __device__ __forceinline__ void draw32_pairs(const Mix& M, uint64_t key, int64_t
   }
 }
 
+// ---------------------------------------------------------------------------
+// Lean fp32 sampler (round 5): the same stream as attempt32_quad / draw32 /
+// draw32_pairs -- bit for bit -- with the component lookup cut to one guide
+// read, one compare and one select per word.  For below mixtures of at most
+// kStage components (tpe.suggest's are at most 26: n_below <= the LF cap 25,
+// tpe.py:633-636, plus the prior); the scorers keep the generic path for
+// larger ones.  The guide entry of bucket b = w >> 24 is
+//   {thr[g], byte offset of cw[g], byte offset of cw[g + step], multi}
+// (g, step, multi as in stage_mix), so a word's component record is
+// cw[w >= thr[g] ? g + step : g] -- no bit fields, no uniform flags in
+// VGPRs; a bucket holding a second threshold (multi) walks thr[] as comp_of
+// does, tested once per Philox call for its four words.
+// ---------------------------------------------------------------------------
+struct LeanMix {
+  uint4 gd[kGuide];
+  float4 cw[kStage];  // {mu, sigma, bits of thr[k], 1 / (thr[k] - thr[k-1])}, as MixLds::cw
+  uint32_t thr[kStage];
+};
+
+// stage a below mixture of n <= kStage components (call by all threads)
+__device__ __forceinline__ void stage_lean(const tpe_seg& S, const double* wcdf, const double* mu,
+                                           const double* sigma, LeanMix& L) {
+  const int n = S.n_obs + 1;
+  const double total = wcdf[S.comp_off + n - 1];
+  for (int k = threadIdx.x; k < n; k += kBS) {
+    const double t = ceil(wcdf[S.comp_off + k] / total * 4294967296.0);
+    L.thr[k] = (t >= 4294967295.0) ? 0xFFFFFFFFu : (t > 0.0 ? (uint32_t)t : 0u);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < n; k += kBS) {
+    const uint32_t lo = k ? L.thr[k - 1] : 0u, width = L.thr[k] - lo;
+    L.cw[k] = make_float4((float)mu[S.comp_off + k], (float)sigma[S.comp_off + k],
+                          __uint_as_float(L.thr[k]), width ? 1.0f / (float)width : 0.0f);
+  }
+  for (int b = threadIdx.x; b < kGuide; b += kBS) {
+    const uint32_t w = (uint32_t)b << 24;
+    int lo = 0, hi = n - 1;  // first k with thr[k] > w (n-1 if none)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (w < L.thr[mid]) hi = mid; else lo = mid + 1;
+    }
+    const uint32_t top = w | 0xFFFFFFu;
+    const int step = lo < n - 1 ? 1 : 0;
+    const uint32_t multi = (lo + 1 < n - 1 && L.thr[lo + 1] <= top) ? 1u : 0u;
+    L.gd[b] = make_uint4(L.thr[lo], (uint32_t)lo * 16u, (uint32_t)(lo + step) * 16u, multi);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ const float4& lean_cw(const LeanMix& L, uint32_t off) {
+  return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(L.cw) + off);
+}
+// the rare walk of a multi bucket (comp_of's), from the selected component
+__device__ __forceinline__ uint32_t lean_walk(const LeanMix& L, int n, uint32_t w,
+                                                        uint32_t off) {
+  int k = (int)(off >> 4);
+  while (k < n - 1 && w >= L.thr[k]) ++k;
+  return (uint32_t)k << 4;
+}
+__device__ __forceinline__ uint32_t lean_sel(const uint4& e, uint32_t w) {
+  return w >= e.x ? e.z : e.y;
+}
+// word -> (mu, sigma, upper residual), as comp_res
+__device__ __forceinline__ void lean_res(const LeanMix& L, uint32_t off, uint32_t w, float& mu,
+                                         float& sg, float& res) {
+  const float4 c = lean_cw(L, off);
+  mu = c.x;
+  sg = c.y;
+  res = (float)(__float_as_uint(c.z) - w) * c.w;
+}
+
+// attempt 0 of candidates 4m .. 4m+3 (attempt32_quad)
+__device__ __forceinline__ void lean_quad(const LeanMix& L, int n, uint32_t k0, uint32_t k1,
+                                          int64_t m, float& y0, float& y1, float& y2, float& y3) {
+  const U4 r = philox(U4{(uint32_t)m, (uint32_t)((uint64_t)m >> 32), 0u, kStreamSample}, k0, k1);
+  const uint4 e0 = L.gd[r.x >> 24], e1 = L.gd[r.y >> 24], e2 = L.gd[r.z >> 24],
+              e3 = L.gd[r.w >> 24];
+  uint32_t o0 = lean_sel(e0, r.x), o1 = lean_sel(e1, r.y), o2 = lean_sel(e2, r.z),
+           o3 = lean_sel(e3, r.w);
+  if (__builtin_expect((e0.w | e1.w | e2.w | e3.w) != 0u, 0)) {
+    if (e0.w) o0 = lean_walk(L, n, r.x, o0);
+    if (e1.w) o1 = lean_walk(L, n, r.y, o1);
+    if (e2.w) o2 = lean_walk(L, n, r.z, o2);
+    if (e3.w) o3 = lean_walk(L, n, r.w, o3);
+  }
+  float mu0, sg0, r0, mu1, sg1, r1, mu2, sg2, r2, mu3, sg3, r3;
+  lean_res(L, o0, r.x, mu0, sg0, r0);
+  lean_res(L, o1, r.y, mu1, sg1, r1);
+  lean_res(L, o2, r.z, mu2, sg2, r2);
+  lean_res(L, o3, r.w, mu3, sg3, r3);
+  float z0, z1, z2, z3;
+  bm_pair(r0, r1, z0, z1);
+  bm_pair(r2, r3, z2, z3);
+  y0 = fmaf(sg0, z0, mu0);
+  y1 = fmaf(sg1, z1, mu1);
+  y2 = fmaf(sg2, z2, mu2);
+  y3 = fmaf(sg3, z3, mu3);
+}
+
+__device__ __forceinline__ uint32_t lean_comp(const LeanMix& L, int n, uint32_t w) {
+  const uint4 e = L.gd[w >> 24];
+  const uint32_t o = lean_sel(e, w);
+  return e.w ? lean_walk(L, n, w, o) : o;
+}
+
+// attempt 0 of candidate g alone (attempt32_first)
+__device__ __forceinline__ float lean_first(const LeanMix& L, int n, uint64_t key, int64_t g) {
+  const U4 r = draw_words(key, g >> 2, 0u, kStreamSample);
+  const bool hi_pair = (g & 2) != 0, second = (g & 1) != 0;
+  const uint32_t wa = hi_pair ? r.z : r.x, wb = hi_pair ? r.w : r.y;
+  float mua, sga, ra, mub, sgb, rb;
+  lean_res(L, lean_comp(L, n, wa), wa, mua, sga, ra);
+  lean_res(L, lean_comp(L, n, wb), wb, mub, sgb, rb);
+  float z0, z1;
+  bm_pair(ra, rb, z0, z1);
+  return second ? fmaf(sgb, z1, mub) : fmaf(sga, z0, mua);
+}
+
+// retries of candidate g (retry32)
+__device__ __forceinline__ float lean_retry(const LeanMix& L, int n, uint64_t key,
+                                                      int64_t g, bool lo_on, bool hi_on, float lo,
+                                                      float hi) {
+  float y = 0.0f;
+  for (uint32_t c = 1; c <= kMaxRetryCalls; ++c) {
+    const U4 r = draw_words(key, g, c, kStreamRetry);
+    float mu0, sg0, r0, mu1, sg1, r1;
+    lean_res(L, lean_comp(L, n, r.x), r.x, mu0, sg0, r0);
+    lean_res(L, lean_comp(L, n, r.y), r.y, mu1, sg1, r1);
+    float z0, z1;
+    bm_pair(r0, r1, z0, z1);
+    const float y0 = fmaf(sg0, z0, mu0), y1 = fmaf(sg1, z1, mu1);
+    const bool a0 = accept32(y0, lo_on, hi_on, lo, hi);
+    y = a0 ? y0 : y1;
+    if (a0 || accept32(y1, lo_on, hi_on, lo, hi)) return y;
+  }
+  return clamp32(y, lo_on, hi_on, lo, hi);
+}
+
+// candidate g exactly as draw32 draws it
+__device__ __forceinline__ float lean_draw1(const LeanMix& L, int n, uint64_t key, int64_t g,
+                                            bool lo_on, bool hi_on, float lo, float hi) {
+  const float y = lean_first(L, n, key, g);
+  if (accept32(y, lo_on, hi_on, lo, hi)) return y;
+  return lean_retry(L, n, key, g, lo_on, hi_on, lo, hi);
+}
+
+// R consecutive candidates g0 .. per thread (draw32_pairs' stream, its retry
+// list) into the wave's stage: candidate r of lane l at wstage[r * 64 + l]
+// (the draws never sit in VGPRs: the scorer reads them back one at a time,
+// which keeps it under 80 VGPRs without spills).  BOUNDED = false: a label
+// without bounds (nothing is rejected).  Slots r >= n hold draws past the
+// job's end (not candidates; never retried).
+template <int R, bool BOUNDED>
+__device__ __forceinline__ void lean_draw(const LeanMix& L, int nmix, uint64_t key, int64_t g0,
+                                          int n, bool lo_on, bool hi_on, float lo, float hi,
+                                          float* wstage, uint16_t* wlist) {
+  static_assert(R % 4 == 0 && R <= 32, "quads, one mask bit per candidate");
+  const int lane = lane_id();
+  float* st = wstage + lane;
+  const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+  const float lo_e = lo_on ? lo : -INFINITY, hi_e = hi_on ? hi : INFINITY;
+  uint32_t rej = 0;
+  auto put = [&](int r, float y) __attribute__((always_inline)) {
+    st[r * kWave] = y;  // (slots r >= n are drawn too and never read as candidates)
+    if (BOUNDED) rej |= (lo_e <= y && y < hi_e) ? 0u : (1u << r);
+  };
+  if ((g0 & 3) == 0) {
+#pragma unroll
+    for (int q = 0; q < R / 4; ++q) {
+      float y0, y1, y2, y3;
+      lean_quad(L, nmix, k0, k1, (g0 >> 2) + q, y0, y1, y2, y3);
+      put(4 * q, y0);
+      put(4 * q + 1, y1);
+      put(4 * q + 2, y2);
+      put(4 * q + 3, y3);
+    }
+  } else {
+#pragma unroll 1
+    for (int r = 0; r < R; ++r) {
+      const float y = lean_first(L, nmix, key, g0 + r);
+      st[r * kWave] = y;
+      if (BOUNDED && !(lo_e <= y && y < hi_e)) rej |= 1u << r;
+    }
+  }
+  if (!BOUNDED) return;
+  rej &= n >= R ? ~0u : (n <= 0 ? 0u : (1u << n) - 1u);
+  if (__any(rej != 0)) {
+    // the wave's rejections listed and retried 64 at a time (draw32_pairs)
+    const int cnt = __popc(rej);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int o = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += o;
+    }
+    const int total = min(__shfl(incl, kWave - 1, kWave), kRetryList);
+    int pos = incl - cnt;
+    uint32_t left = 0;
+    for (uint32_t m = rej; m; m &= m - 1) {
+      const int r = __builtin_ctz(m);
+      if (pos < kRetryList)
+        wlist[pos] = (uint16_t)((lane << 5) | r);
+      else
+        left |= 1u << r;
+      ++pos;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int b = 0; b < total; b += kWave) {
+      const int e = b + lane;
+      const int ent = e < total ? (int)wlist[e] : 0;
+      const int owner = ent >> 5, r = ent & 31;
+      const int64_t go = __shfl(g0, owner, kWave);
+      if (e < total)
+        wstage[r * kWave + owner] = lean_retry(L, nmix, key, go + r, lo_on, hi_on, lo, hi);
+    }
+    while (left) {
+      const int r = __builtin_ctz(left);
+      left &= left - 1;
+      st[r * kWave] = lean_retry(L, nmix, key, g0 + r, lo_on, hi_on, lo, hi);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 }  // namespace
 }  // namespace tpe

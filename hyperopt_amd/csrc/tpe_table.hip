@@ -1430,7 +1430,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     double* __restrict__ out_score, double* __restrict__ out_x, double* __restrict__ out_eps,
     tpe_best* __restrict__ partial, unsigned long long* __restrict__ stats, int n_tiles,
     int n_jobs, int tile_cap) {
-  __shared__ MixLds s_mix;
+  __shared__ LeanMix s_lean;
   // retry staging, then each lane's scores (slot r of lane l at r * 64 + l)
   __shared__ float s_stage[(kBS / kWave) * kTR * kWave];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
@@ -1470,55 +1470,98 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   const float4* sc = score_cells_of(region, J.tbl_cap);
   const int lane = lane_id();
   float* stage = s_stage + (threadIdx.x / kWave) * (kTR * kWave);
-  const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
+  // the below mixture: staged for the lean sampler (tpe.suggest: always --
+  // at most 26 components) or read from global memory (draw32_pairs)
+  const int nmix = SB.n_obs + 1;
+  const bool lean = nmix <= kStage;  // block-uniform
+  const Mix M{wcdf + SB.comp_off, mu + SB.comp_off, sigma + SB.comp_off, nullptr, nullptr,
+              nullptr, nmix};
   const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
   const int nvalid = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
-  float x[kTR];  // candidates in the scoring coordinate y (log x for LGMM1)
-  draw32_pairs<kTR>(M, J.key, J.cand_base + t0, nvalid, lo_on, hi_on, (float)J.low,
-                    (float)J.high, false, stage, s_list + (threadIdx.x / kWave) * kRetryList, x);
-  auto cell_of = [&](float y) __attribute__((always_inline)) -> int {
-    const float t = (y - g0) * inv_w;
-    const int c = (t >= 0.0f) ? (int)t : 0;  // NaN -> 0
-    return min(c, nb - 1);
+  const float lo32 = (float)J.low, hi32 = (float)J.high;
+  uint16_t* wlist = s_list + (threadIdx.x / kWave) * kRetryList;
+  // the candidates, in the scoring coordinate y (log x for LGMM1), into the
+  // wave's stage (slot r of lane l at r * 64 + l)
+  if (lean) {
+    stage_lean(SB, wcdf, mu, sigma, s_lean);
+    if (lo_on || hi_on)
+      lean_draw<kTR, true>(s_lean, nmix, J.key, J.cand_base + t0, nvalid, lo_on, hi_on, lo32,
+                           hi32, stage, wlist);
+    else
+      lean_draw<kTR, false>(s_lean, nmix, J.key, J.cand_base + t0, nvalid, false, false, lo32,
+                            hi32, stage, wlist);
+  } else {
+    // a below mixture past the LDS staging (explicit observation lists, never
+    // tpe.suggest's): one candidate at a time, the same stream (draw32)
+#pragma unroll 1
+    for (int r = 0; r < kTR; ++r)
+      stage[r * kWave + lane] =
+          r < nvalid ? draw32(M, J.key, J.cand_base + t0 + r, lo_on, hi_on, lo32, hi32) : 1.0f;
+  }
+  // candidate g again, exactly as drawn above (the tile winner's and the band
+  // entries' values: x[] need not live through the tail)
+  auto redraw = [&](int64_t g) __attribute__((always_inline)) -> float {
+    return lean ? lean_draw1(s_lean, nmix, J.key, g, lo_on, hi_on, lo32, hi32)
+                : draw32(M, J.key, g, lo_on, hi_on, lo32, hi32);
   };
-  float bs = -INFINITY, by = 0.0f;
+  const float nbm1 = (float)(nb - 1);
+  // the cell of y: trunc of (y - origin) / 2h clamped to [0, nb - 1] (NaN -> 0)
+  auto cell_of = [&](float y) __attribute__((always_inline)) -> int {
+    return (int)__builtin_amdgcn_fmed3f((y - g0) * inv_w, 0.0f, nbm1);
+  };
+  auto cubic_at = [&](int c) __attribute__((always_inline)) -> float4 {
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc) +
+                                            ((uint32_t)c << 4));
+  };
+  float bs = -INFINITY;
   int br = -1;
   uint32_t fb = 0;  // candidates the score cells do not cover
+  // FULL: every slot of the thread valid (all but a job's last tile).  y is
+  // read back from the stage four candidates ahead of its score, together
+  // with its cell's cubic; the slot then takes the score (or, for a fallback
+  // candidate, keeps y).  Branch-free: slots past the job's end are scored
+  // like the rest and masked out of the argmax and the fallback mask.
+  auto score_all = [&](auto full_tag) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(full_tag)::value;
+    float yq[4];
+    float4 q[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      yq[r] = stage[r * kWave + lane];
+      q[r] = cubic_at(cell_of(yq[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < kTR; ++r) {
+      const float y = yq[r & 3];
+      const int c = cell_of(y);
+      const float4 k = q[r & 3];
+      if (r + 4 < kTR) {
+        yq[r & 3] = stage[(r + 4) * kWave + lane];
+        q[r & 3] = cubic_at(cell_of(yq[r & 3]));
+      }
+      const float u = (y - cell_centre(g0, h32, c)) * inv_h;
+      const float s = fmaf(fmaf(fmaf(k.w, u, k.z), u, k.y), u, k.x);
 #ifdef TPE_DIAG_SKIP_SCORE  // diagnostic builds only: the sampler alone
-#pragma unroll
-  for (int r = 0; r < kTR; ++r)
-    if (r < nvalid && x[r] > bs) {
-      bs = x[r];
-      by = x[r];
-      br = r;
-    }
+      const bool ok = true;
 #else
-  float4 q[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) q[r] = sc[cell_of(x[r])];
-#pragma unroll
-  for (int r = 0; r < kTR; ++r) {
-    const float y = x[r];
-    const int c = cell_of(y);
-    const float4 k = q[r & 3];
-    if (r + 4 < kTR) q[r & 3] = sc[cell_of(x[r + 4])];
-    const float u = (y - cell_centre(g0, h32, c)) * inv_h;
-    const float s = fmaf(fmaf(fmaf(k.w, u, k.z), u, k.y), u, k.x);
-    const bool ok = (s == s) && (fabsf(u) <= kULim);
-    const bool valid = r < nvalid;
-    fb |= (valid && !ok) ? (1u << r) : 0u;
-    if (valid && ok) {
-      // finite scores: strict > keeps the first of equal scores (np.argmax)
-      const bool take = s > bs;
-      bs = take ? s : bs;
-      by = take ? y : by;
-      br = take ? r : br;
-      stage[r * kWave + lane] = s;  // kept for the band
-      if (HOOKS && out_score) out_score[J.out_off + t0 + r] = (double)s;
-    }
-    if (HOOKS && out_x && valid) out_x[J.out_off + t0 + r] = cand_value(y, lgmm);
-  }
+      const bool ok = (s == s) && (fabsf(u) <= kULim);
 #endif
+      fb |= ok ? 0u : (1u << r);
+      // finite scores: strict > keeps the first of equal scores (np.argmax)
+      const float sv = (ok && (FULL || r < nvalid)) ? s : -INFINITY;
+      br = sv > bs ? r : br;
+      bs = fmaxf(bs, sv);
+      // kept for the band (a fallback candidate keeps its y for the fallback pass)
+      stage[r * kWave + lane] = ok ? s : y;
+      if (HOOKS && out_score && ok && r < nvalid) out_score[J.out_off + t0 + r] = (double)s;
+      if (HOOKS && out_x && r < nvalid) out_x[J.out_off + t0 + r] = cand_value(y, lgmm);
+    }
+    if (!FULL) fb &= nvalid <= 0 ? 0u : (1u << nvalid) - 1u;
+  };
+  if (nvalid == kTR)
+    score_all(std::true_type{});
+  else
+    score_all(std::false_type{});
   // the lane's best cubic-scored candidate (its bounds are monotone in s)
   const float bs_cubic = bs;
   const float ea = (Tb.eps_cubic + 2.0001f * Tb.eps_mix) * 1.000001f;  // (covers its rounding)
@@ -1536,10 +1579,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     // the lane's candidates wait in its own column of the wave's stage, and
     // their UPPER BOUNDS (two-polynomial) or scores (log-sum-exp) replace
     // them there
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int r = 0; r < kTR; ++r)
-      if (fb & (1u << r)) stage[r * kWave + lane] = x[r];
+    // (the fallback candidates' y were staged by their own lanes above; the
+    // log-sum-exp below reads other lanes' columns)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const f4* cell4 = reinterpret_cast<const f4*>(region);
     auto fold = [&](int r, float s, float y, float keep) __attribute__((always_inline)) {
@@ -1551,7 +1593,6 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
       if (take) {
         bs = s;
         br = r;
-        by = y;
       }
       ++n_fb;
     };
@@ -1628,7 +1669,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     const uint64_t own = __ballot(code == wc && wc != 0u);
     if (own != 0ull && lane == (int)__builtin_ctzll(own)) {
       s_key[wid] = ((uint64_t)wc << 32) | (uint64_t)(~(uint32_t)(threadIdx.x * kTR + br));
-      s_wy[wid] = by;
+      s_wy[wid] = redraw(J.cand_base + t0 + br);  // (one lane of the wave)
     } else if (own == 0ull && lane == 0) {
       s_key[wid] = 0ull;
     }
@@ -1711,8 +1752,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
       if ((em >> r) & 1u) {
         // (its value drawn again -- draw32 gives candidate g exactly what
         // draw32_pairs gave it -- so x[] need not live through the tail)
-        const float yv = draw32(M, J.key, J.cand_base + t0 + r, lo_on, hi_on, (float)J.low,
-                                (float)J.high);
+        const float yv = redraw(J.cand_base + t0 + r);
         const float v = stage[r * kWave + lane];
         const float hi = ((lsem >> r) & 1u) ? INFINITY : ((fbm >> r) & 1u) ? v : up(v + eps_of(v));
         B[pos] = tpe_band{J.cand_base + t0 + r, yv, hi};
