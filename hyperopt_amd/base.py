@@ -775,3 +775,69 @@ class Domain(object):
 
     def new_result(self):
         return {"status": STATUS_NEW}
+
+
+# ---------------------------------------------------------------------------
+# reference-shaped domains (the plug point hyperopt.fmin(algo=...) uses)
+# ---------------------------------------------------------------------------
+def convert_graph(expr):
+    """A pyll graph built by another pyll implementation -- the reference's
+    ``hyperopt.pyll`` (pyll/base.py:232-560): nodes with ``name``,
+    ``pos_args``, ``named_args``, ``o_len``, ``pure``, literals named
+    "literal" with ``obj`` -- rebuilt from this package's Apply / Literal
+    nodes, node for node (shared nodes stay shared; iterative, so deep
+    graphs do not hit the recursion limit)."""
+    memo = {}
+    stack = [expr]
+    while stack:
+        n = stack[-1]
+        if id(n) in memo:
+            stack.pop()
+            continue
+        if n.name == "literal":
+            memo[id(n)] = pyll.Literal(n.obj)
+            stack.pop()
+            continue
+        kids = list(n.pos_args) + [v for _, v in n.named_args]
+        pending = [k for k in kids if id(k) not in memo]
+        if pending:
+            stack.extend(pending)
+            continue
+        stack.pop()
+        memo[id(n)] = pyll.Apply(n.name, [memo[id(a)] for a in n.pos_args],
+                                 [(k, memo[id(v)]) for k, v in n.named_args],
+                                 o_len=n.o_len, pure=n.pure)
+    return memo[id(expr)]
+
+
+def as_domain(domain):
+    """The suggest engine's view of ``domain``.
+
+    This package's Domain (anything with ``specs`` and ``reachable``) is used
+    as is.  A reference-shaped Domain -- hyperopt's own (base.py:783-870),
+    which ``hyperopt.fmin`` hands to its ``algo`` callable (fmin.py:268-270)
+    -- is converted once: its ``expr`` graph rebuilt with this package's
+    nodes (``convert_graph``), the same labels, prior kinds and arguments,
+    and the same conditional structure; ``cmd`` / ``workdir`` /
+    ``new_result`` stay the original's.  The conversion is cached on the
+    original object."""
+    if hasattr(domain, "specs") and hasattr(domain, "reachable"):
+        return domain
+    d = getattr(domain, "__dict__", None)
+    conv = d.get("_hyperopt_amd_domain") if d is not None else None
+    if conv is None:
+        conv = Domain(getattr(domain, "fn", None), convert_graph(domain.expr),
+                      workdir=getattr(domain, "workdir", None),
+                      pass_expr_memo_ctrl=getattr(domain, "pass_expr_memo_ctrl", None),
+                      name=getattr(domain, "name", None),
+                      loss_target=getattr(domain, "loss_target", None))
+        if hasattr(domain, "cmd"):
+            conv.cmd = domain.cmd
+        if hasattr(domain, "new_result"):
+            conv.new_result = domain.new_result
+        if set(getattr(domain, "params", conv.params)) != set(conv.params):
+            raise ValueError("domain conversion lost labels: %s vs %s"
+                             % (sorted(domain.params), sorted(conv.params)))
+        if d is not None:
+            d["_hyperopt_amd_domain"] = conv
+    return conv

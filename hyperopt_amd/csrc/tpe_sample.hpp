@@ -557,6 +557,11 @@ __device__ __forceinline__ void lean_draw(const LeanMix& L, int nmix, uint64_t k
   }
   if (!BOUNDED) return;
   rej &= n >= R ? ~0u : (n <= 0 ? 0u : (1u << n) - 1u);
+#ifdef TPE_DIAG_NO_RETRY  // diagnostic builds only: rejected draws clamped, no retries
+  for (int r = 0; r < R; ++r)
+    if (rej & (1u << r)) st[r * kWave] = clamp32(st[r * kWave], lo_on, hi_on, lo, hi);
+  rej = 0;
+#endif
   if (__any(rej != 0)) {
     // the wave's rejections listed and retried 64 at a time (draw32_pairs)
     const int cnt = __popc(rej);

@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc) +
                                             ((uint32_t)c << 4));
   };
-  float bs = -INFINITY;
+  float bs = -INFINITY, by = 0.0f;
   int br = -1;
   uint32_t fb = 0;  // candidates the score cells do not cover
   // FULL: every slot of the thread valid (all but a job's last tile).  y is
@@ -1539,17 +1539,20 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
         yq[r & 3] = stage[(r + 4) * kWave + lane];
         q[r & 3] = cubic_at(cell_of(yq[r & 3]));
       }
-      const float u = (y - cell_centre(g0, h32, c)) * inv_h;
-      const float s = fmaf(fmaf(fmaf(k.w, u, k.z), u, k.y), u, k.x);
-#ifdef TPE_DIAG_SKIP_SCORE  // diagnostic builds only: the sampler alone
+#ifdef TPE_DIAG_SKIP_SCORE  // diagnostic builds only: the sampler alone (the draw is its score)
+      const float s = y + 0.0f * (float)c + 0.0f * k.x;
       const bool ok = true;
 #else
+      const float u = (y - cell_centre(g0, h32, c)) * inv_h;
+      const float s = fmaf(fmaf(fmaf(k.w, u, k.z), u, k.y), u, k.x);
       const bool ok = (s == s) && (fabsf(u) <= kULim);
 #endif
       fb |= ok ? 0u : (1u << r);
       // finite scores: strict > keeps the first of equal scores (np.argmax)
       const float sv = (ok && (FULL || r < nvalid)) ? s : -INFINITY;
-      br = sv > bs ? r : br;
+      const bool take = sv > bs;
+      br = take ? r : br;
+      by = take ? y : by;
       bs = fmaxf(bs, sv);
       // kept for the band (a fallback candidate keeps its y for the fallback pass)
       stage[r * kWave + lane] = ok ? s : y;
@@ -1593,6 +1596,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
       if (take) {
         bs = s;
         br = r;
+        by = y;
       }
       ++n_fb;
     };
@@ -1669,7 +1673,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     const uint64_t own = __ballot(code == wc && wc != 0u);
     if (own != 0ull && lane == (int)__builtin_ctzll(own)) {
       s_key[wid] = ((uint64_t)wc << 32) | (uint64_t)(~(uint32_t)(threadIdx.x * kTR + br));
-      s_wy[wid] = redraw(J.cand_base + t0 + br);  // (one lane of the wave)
+      s_wy[wid] = by;
     } else if (own == 0ull && lane == 0) {
       s_key[wid] = 0ull;
     }
@@ -1750,9 +1754,9 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
       if ((em >> r) & 1u) {
-        // (its value drawn again -- draw32 gives candidate g exactly what
-        // draw32_pairs gave it -- so x[] need not live through the tail)
-        const float yv = redraw(J.cand_base + t0 + r);
+        // (the lane's own best is almost always the entry; any other one is
+        // drawn again -- exactly as above -- so x[] need not live through the tail)
+        const float yv = r == br ? by : redraw(J.cand_base + t0 + r);
         const float v = stage[r * kWave + lane];
         const float hi = ((lsem >> r) & 1u) ? INFINITY : ((fbm >> r) & 1u) ? v : up(v + eps_of(v));
         B[pos] = tpe_band{J.cand_base + t0 + r, yv, hi};

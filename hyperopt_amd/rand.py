@@ -18,6 +18,8 @@ import ctypes
 
 import numpy as np
 
+from .base import as_domain
+
 
 def sample_config(domain, rng):
     """{label: value} for the labels live under the sampled choices."""
@@ -38,6 +40,7 @@ def _misc(domain, new_id, config):
 
 
 def suggest(new_ids, domain, trials, seed):
+    domain = as_domain(domain)
     rng = np.random.RandomState(seed)
     rval = []
     for new_id in new_ids:
@@ -48,6 +51,7 @@ def suggest(new_ids, domain, trials, seed):
 
 
 def suggest_batch(new_ids, domain, trials, seed):
+    domain = as_domain(domain)
     rng = np.random.RandomState(seed)
     idxs = {lab: [] for lab in domain.params}
     vals = {lab: [] for lab in domain.params}
@@ -138,6 +142,7 @@ def _configs(domain, labels, vals):
 
 def suggest_device(new_ids, domain, trials, seed):
     """rand.suggest with the prior draws made on the GPU (see module doc)."""
+    domain = as_domain(domain)
     labels, vals = draw_priors(domain, seed, len(new_ids))
     rval = []
     for new_id, config in zip(new_ids, _configs(domain, labels, vals)):

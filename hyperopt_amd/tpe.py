@@ -38,7 +38,7 @@ import numpy as np
 from . import _lib as _L
 from . import dist as hdist
 from . import rand
-from .base import doc_loss
+from .base import as_domain, doc_loss
 from .engine import (DEFAULT_LF, Engine, LabelResult, LabelWork, WorkBatch, _lattice_range,
                      _params)
 
@@ -338,6 +338,7 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
             precision=None):
     """TPE suggest: one new trial document for new_ids[0] (tpe.py:837-964)."""
     t0 = time.time()
+    domain = as_domain(domain)  # (hyperopt's own Domain too: fmin(algo=tpe.suggest))
     labels = list(domain.params)
     hist = collect_history(trials, labels)
     if verbose:
@@ -604,6 +605,7 @@ def _suggest_many(requests, shard_studies=False):
                   n_EI_candidates=_default_n_EI_candidates, gamma=_default_gamma,
                   linear_forgetting=_default_linear_forgetting, precision=None)
         kw.update({k: v for k, v in rq.kwargs.items() if k != "verbose"})
+        rq.domain = as_domain(rq.domain)
         labels = list(rq.domain.params)
         hist = collect_history(rq.trials, labels)
         if hist.tids.size < kw["n_startup_jobs"]:
