@@ -62,8 +62,8 @@ constexpr int kCellF = 16;           // floats per cell (64 B: four 16-B chunks)
 constexpr int kSlotB = 128;          // bytes per cell slot of a job's region (cells + m pairs)
 constexpr int kChunks = 4;           // 16-B chunks of a cell the scorer reads
 constexpr double kRhoLim = 5.8;      // admissible 9|A| + 65|B|
-#ifndef TPE_SCORE_WPE  // waves per SIMD the fast scorer is compiled for (its VGPR budget)
-#define TPE_SCORE_WPE 6
+#ifndef TPE_SCORE_WPE  // waves per SIMD the fast scorer is compiled for (its VGPR budget;
+#define TPE_SCORE_WPE 4  // its 32 KB draw stage per block allows four blocks per CU anyway)
 #endif
 #ifndef TPE_TAU_TABLE
 #define TPE_TAU_TABLE 17.0
@@ -82,6 +82,13 @@ constexpr int kTR = TPE_TR;          // candidates per thread and tile in the sc
 #endif
 constexpr int kTiles = TPE_TILES;    // tiles (kBS * kTR candidates) per scorer block
 constexpr int64_t kTile = (int64_t)kBS * kTR;
+#ifndef TPE_TRF
+#define TPE_TRF 32
+#endif
+constexpr int kTRF = TPE_TRF;        // candidates per thread in the fast scorer (tpe_score_table_fast;
+                                     // 32: its per-block setup and band tail over 8192 candidates --
+                                     // 0.288 -> 0.272 ms per C3 level against 16, one-box A/B)
+constexpr int64_t kTileF = (int64_t)kBS * kTRF;  // its tile: one band tile per scorer block
 #ifndef TPE_BUILD_BLOCKS
 #define TPE_BUILD_BLOCKS 512
 #endif
@@ -1432,7 +1439,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     int n_jobs, int tile_cap) {
   __shared__ LeanMix s_lean;
   // retry staging, then each lane's scores (slot r of lane l at r * 64 + l)
-  __shared__ float s_stage[(kBS / kWave) * kTR * kWave];
+  __shared__ float s_stage[(kBS / kWave) * kTRF * kWave];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   __shared__ uint64_t s_key[kBS / kWave];
   __shared__ float s_wy[kBS / kWave];
@@ -1450,7 +1457,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   const tpe_job J = jobs[job];
   tpe_best* P = partial + (int64_t)job * n_tiles + bx;
   uint32_t* hdr = band_ctl + ((int64_t)job * n_tiles + bx) * kHdrWords;
-  const int64_t base = (int64_t)bx * kTile;
+  const int64_t base = (int64_t)bx * kTileF;
   if (base >= J.n_cand) {
     if (threadIdx.x == 0) {
       *P = empty_best();
@@ -1469,15 +1476,15 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   const char* region = reinterpret_cast<const char*>(cells) + J.tbl_off * kSlotB;
   const float4* sc = score_cells_of(region, J.tbl_cap);
   const int lane = lane_id();
-  float* stage = s_stage + (threadIdx.x / kWave) * (kTR * kWave);
+  float* stage = s_stage + (threadIdx.x / kWave) * (kTRF * kWave);
   // the below mixture: staged for the lean sampler (tpe.suggest: always --
   // at most 26 components) or read from global memory (draw32_pairs)
   const int nmix = SB.n_obs + 1;
   const bool lean = nmix <= kStage;  // block-uniform
   const Mix M{wcdf + SB.comp_off, mu + SB.comp_off, sigma + SB.comp_off, nullptr, nullptr,
               nullptr, nmix};
-  const int64_t t0 = base + (int64_t)threadIdx.x * kTR;
-  const int nvalid = (int)max((int64_t)0, min((int64_t)kTR, J.n_cand - t0));
+  const int64_t t0 = base + (int64_t)threadIdx.x * kTRF;
+  const int nvalid = (int)max((int64_t)0, min((int64_t)kTRF, J.n_cand - t0));
   const float lo32 = (float)J.low, hi32 = (float)J.high;
   uint16_t* wlist = s_list + (threadIdx.x / kWave) * kRetryList;
   // the candidates, in the scoring coordinate y (log x for LGMM1), into the
@@ -1485,16 +1492,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   if (lean) {
     stage_lean(SB, wcdf, mu, sigma, s_lean);
     if (lo_on || hi_on)
-      lean_draw<kTR, true>(s_lean, nmix, J.key, J.cand_base + t0, nvalid, lo_on, hi_on, lo32,
+      lean_draw<kTRF, true>(s_lean, nmix, J.key, J.cand_base + t0, nvalid, lo_on, hi_on, lo32,
                            hi32, stage, wlist);
     else
-      lean_draw<kTR, false>(s_lean, nmix, J.key, J.cand_base + t0, nvalid, false, false, lo32,
+      lean_draw<kTRF, false>(s_lean, nmix, J.key, J.cand_base + t0, nvalid, false, false, lo32,
                             hi32, stage, wlist);
   } else {
     // a below mixture past the LDS staging (explicit observation lists, never
     // tpe.suggest's): one candidate at a time, the same stream (draw32)
 #pragma unroll 1
-    for (int r = 0; r < kTR; ++r)
+    for (int r = 0; r < kTRF; ++r)
       stage[r * kWave + lane] =
           r < nvalid ? draw32(M, J.key, J.cand_base + t0 + r, lo_on, hi_on, lo32, hi32) : 1.0f;
   }
@@ -1531,11 +1538,11 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
       q[r] = cubic_at(cell_of(yq[r]));
     }
 #pragma unroll
-    for (int r = 0; r < kTR; ++r) {
+    for (int r = 0; r < kTRF; ++r) {
       const float y = yq[r & 3];
       const int c = cell_of(y);
       const float4 k = q[r & 3];
-      if (r + 4 < kTR) {
+      if (r + 4 < kTRF) {
         yq[r & 3] = stage[(r + 4) * kWave + lane];
         q[r & 3] = cubic_at(cell_of(yq[r & 3]));
       }
@@ -1561,7 +1568,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     }
     if (!FULL) fb &= nvalid <= 0 ? 0u : (1u << nvalid) - 1u;
   };
-  if (nvalid == kTR)
+  if (nvalid == kTRF)
     score_all(std::true_type{});
   else
     score_all(std::false_type{});
@@ -1672,7 +1679,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
     for (int o = 32; o >= 1; o >>= 1) wc = max(wc, (uint32_t)__shfl_xor((int)wc, o, kWave));
     const uint64_t own = __ballot(code == wc && wc != 0u);
     if (own != 0ull && lane == (int)__builtin_ctzll(own)) {
-      s_key[wid] = ((uint64_t)wc << 32) | (uint64_t)(~(uint32_t)(threadIdx.x * kTR + br));
+      s_key[wid] = ((uint64_t)wc << 32) | (uint64_t)(~(uint32_t)(threadIdx.x * kTRF + br));
       s_wy[wid] = by;
     } else if (own == 0ull && lane == 0) {
       s_key[wid] = 0ull;
@@ -1715,7 +1722,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   }
   if (HOOKS && out_eps) {  // (test hook) the bound of every cubic-scored candidate
 #pragma unroll
-    for (int r = 0; r < kTR; ++r)
+    for (int r = 0; r < kTRF; ++r)
       if (r < nvalid && !((fbm >> r) & 1u)) {
         const float v = stage[r * kWave + lane];
         out_eps[J.out_off + t0 + r] = (double)up(v + eps_of(v)) - (double)v;
@@ -1736,7 +1743,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   uint32_t em = 0;
   if (!(hi_t < lo_blk)) {
 #pragma unroll
-    for (int r = 0; r < kTR; ++r) {
+    for (int r = 0; r < kTRF; ++r) {
       if (r < nvalid) {
         const float v = stage[r * kWave + lane];
         const bool in = ((fbm >> r) & 1u) ? (((lsem >> r) & 1u) || !(v < lo_blk)) : !(v < s_thr);
@@ -1751,17 +1758,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
   if (total <= tile_cap && em) {
     tpe_band* B = band + ((int64_t)job * n_tiles + bx) * kTileSlots;
     int pos = pos0;
-#pragma unroll
-    for (int r = 0; r < kTR; ++r) {
-      if ((em >> r) & 1u) {
-        // (the lane's own best is almost always the entry; any other one is
-        // drawn again -- exactly as above -- so x[] need not live through the tail)
-        const float yv = r == br ? by : redraw(J.cand_base + t0 + r);
-        const float v = stage[r * kWave + lane];
-        const float hi = ((lsem >> r) & 1u) ? INFINITY : ((fbm >> r) & 1u) ? v : up(v + eps_of(v));
-        B[pos] = tpe_band{J.cand_base + t0 + r, yv, hi};
-        ++pos;
-      }
+    // over the lane's entries only (usually one: its own best, whose value
+    // it holds; any other entry is drawn again -- exactly as above -- so the
+    // draws need not live through the tail)
+    for (uint32_t m = em; m; m &= m - 1) {
+      const int r = __builtin_ctz(m);
+      const float yv = r == br ? by : redraw(J.cand_base + t0 + r);
+      const float v = stage[r * kWave + lane];
+      const float hi = ((lsem >> r) & 1u) ? INFINITY : ((fbm >> r) & 1u) ? v : up(v + eps_of(v));
+      B[pos] = tpe_band{J.cand_base + t0 + r, yv, hi};
+      ++pos;
     }
   }
   if (threadIdx.x == 0) {
@@ -2668,7 +2674,7 @@ __global__ __launch_bounds__(kBS) void k_reduce_t(const tpe_job* __restrict__ jo
 // scorer blocks (tiles) per job of the fast path: the partial layout
 int64_t tpe_table_fast_tiles(const tpe_job* hj, int n) {
   int64_t gx = 1;
-  for (int i = 0; i < n; ++i) gx = std::max(gx, (hj[i].n_cand + kTile - 1) / kTile);
+  for (int i = 0; i < n; ++i) gx = std::max(gx, (hj[i].n_cand + kTileF - 1) / kTileF);
   return gx;
 }
 
