@@ -400,7 +400,7 @@ int tpe_score_table(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
  * 2^-22 |s32|; a two-polynomial candidate carries its own; a log-sum-exp
  * candidate is always re-scored), candidate i can be the exact winner only if
  * s32_i + eps_i >= G := max_k (s32_k - eps_k).  Each scorer block (tile of
- * 4096 candidates) writes, without atomics, a header {lo = its best
+ * 8192 candidates) writes, without atomics, a header {lo = its best
  * s32 - eps, hi_max = its largest s32 + eps, n} (4 uint32 per tile in
  * band_ctl) and its candidates with s32 + eps >= lo (a superset: G >= lo)
  * into its own 256 entries of `band` (n = 0xFFFFFFFF: more than tile_cap,

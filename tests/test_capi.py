@@ -132,9 +132,9 @@ def test_argument_errors_are_reported():
     assert fast(64, eight, n_partial=0) == -1 and b"partial workspace" in lib.tpe_last_error()
     assert rescore(eight, n_partial=0) == -1 and b"partial workspace" in lib.tpe_last_error()
     ctl, work = ctypes.c_int64(0), ctypes.c_int64(0)
-    jobs["n_cand"] = 1 << 22  # 1024 tiles of 4096 candidates
+    jobs["n_cand"] = 1 << 22  # 512 tiles of 8192 candidates (256 threads x 32)
     nb = lib.tpe_band_bytes(hp_, 1, ctypes.byref(ctl), ctypes.byref(work))
-    assert nb == 1024 * 256 * L.BAND_DTYPE.itemsize and ctl.value == 1024 * 16 and work.value > 0
+    assert nb == 512 * 256 * L.BAND_DTYPE.itemsize and ctl.value == 512 * 16 and work.value > 0
     assert lib.tpe_band_bytes(hp_, -1, None, None) == -1
     rc = lib.tpe_table_build(None, hp_, 1, None, None, None, None, 8, *([None] * 8))
     assert rc == -1 and b"null pointer" in lib.tpe_last_error()
