@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -119,11 +119,11 @@ _SIGNATURES = {
                                   _P, _I64, _P, _P]),
     "tpe_lattice_sample": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_lattice_suggest": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P,
-                                 _P]),
+                                 _P, _P, _P]),
     "tpe_lattice_compact": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
     "tpe_quantized_partials": (_I64, [_P, _I, _I64]),
     "tpe_score_quantized": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _I64,
-                                 _P, _P, _P]),
+                                 _P, _P, _P, _P, _P]),
     "tpe_categorical_partials": (_I64, [_P, _I]),
     "tpe_score_categorical": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P]),
     "tpe_sample": (_I, [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P]),

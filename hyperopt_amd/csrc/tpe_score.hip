@@ -784,7 +784,8 @@ __device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
                                            const double* __restrict__ mu,
                                            const double* __restrict__ sigma,
                                            tpe_best* __restrict__ partial, int job, int64_t s,
-                                           int64_t nper, double* sh);
+                                           int64_t nper, double* sh, const double* __restrict__ P,
+                                           const double* __restrict__ Sm);
 
 // Candidates [start, min(n_cand, limit)) of every job (start a multiple of the
 // kBS * kLatR tile); need (nullable): only the jobs whose flag is set.
@@ -798,7 +799,8 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
     const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
     int32_t* __restrict__ err, int n_tiles, int n_jobs, int64_t start, int64_t limit,
     const int32_t* __restrict__ need, const double* __restrict__ w,
-    tpe_best* __restrict__ slot_part, int slot_n) {
+    tpe_best* __restrict__ slot_part, int slot_n, const double* __restrict__ qP,
+    const double* __restrict__ qS) {
   extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
   __shared__ alignas(16) float s_stage[kLatR * kBS];  // (also the slot blocks' fp64 scratch)
@@ -807,7 +809,7 @@ __global__ __launch_bounds__(kBS) void k_lattice_sample(
   if ((int64_t)blockIdx.x < slot_blocks) {  // block-uniform
     const int job = (int)(blockIdx.x / slot_n);
     score_slot(jobs, segs, w, mu, sigma, slot_part, job, (int64_t)blockIdx.x - (int64_t)job * slot_n,
-               slot_n, reinterpret_cast<double*>(s_stage));
+               slot_n, reinterpret_cast<double*>(s_stage), qP, qS);
     return;
   }
   const unsigned bid = (unsigned)((int64_t)blockIdx.x - slot_blocks);
@@ -953,14 +955,151 @@ __global__ __launch_bounds__(kBS) void k_lattice_compact(
   firsts[J.lat_off + pos] = (int64_t)f;
 }
 
+// Component windows of the quantized log-mass (round 5).  A component whose
+// two erf arguments are both beyond +-6.5 contributes exactly 0 (qlpdf skips
+// it), i.e. unless mu - b < ub and mu + b > lb, b = 6.5 max(sqrt2 sigma, EPS).
+// The means are sorted, so with P[k] = max_{j<=k} (mu_j + b_j) and
+// S[k] = min_{j>=k} (mu_j - b_j) (both non-decreasing; k_qreach) every
+// component that can contribute lies in [first k with P[k] > lb, last k with
+// S[k] < ub] -- found by a block-wide search -- and qlpdf loops over that
+// window only.  Each thread still visits its own components in the same
+// order and skips the same ones, so the sums are bit-identical to the full
+// loop's.  A NaN mean or sigma gives P = +inf / S = -inf from there on, which
+// keeps NaN components (sorted last) inside every window.
+constexpr int kQB = 256;  // k_qreach block: one per segment (small: it runs beside the table build)
+constexpr int kQPer = 8;   // components per thread per pass (all its loads issued together)
+__device__ __forceinline__ double qreach_b(double s) { return 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps); }
+
+// inclusive block scans over the threads' values in thread order: max from
+// the front (prefix) or min from the back (suffix); wave DPP / shuffles, then
+// the waves' totals through LDS
+__device__ __forceinline__ double block_prefix_max(double v, double* sw) {
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const double u = __shfl_up(v, o, kWave);
+    if (lane >= o) v = fmax(v, u);
+  }
+  __syncthreads();
+  if (lane == kWave - 1) sw[wid] = v;
+  __syncthreads();
+  for (int w = 0; w < wid; ++w) v = fmax(v, sw[w]);
+  return v;
+}
+__device__ __forceinline__ double block_suffix_min(double v, double* sw) {
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const double u = __shfl_down(v, o, kWave);
+    if (lane + o < kWave) v = fmin(v, u);
+  }
+  __syncthreads();
+  if (lane == 0) sw[wid] = v;
+  __syncthreads();
+  for (int w = wid + 1; w < kQB / kWave; ++w) v = fmin(v, sw[w]);
+  return v;
+}
+
+__global__ __launch_bounds__(kQB) void k_qreach(const tpe_job* __restrict__ jobs,
+                                               const tpe_seg* __restrict__ segs,
+                                               const double* __restrict__ mu,
+                                               const double* __restrict__ sigma,
+                                               double* __restrict__ P, double* __restrict__ Sm) {
+  __shared__ double sw[kQB / kWave];
+  const tpe_job J = jobs[blockIdx.x >> 1];
+  const tpe_seg S = segs[(blockIdx.x & 1) ? J.above : J.below];
+  const int nc = S.n_obs + 1;
+  const double* m = mu + S.comp_off;
+  const double* g = sigma + S.comp_off;
+  constexpr int kPass = kQB * kQPer;
+  const int npass = (nc + kPass - 1) / kPass;
+  // one pass: thread t holds components base + t * kQPer + i; its values
+  // (hi = mu + b, lo = mu - b; NaN -> +inf / -inf) in registers
+  auto load = [&](int base, double (&hv)[kQPer], double (&lv)[kQPer]) __attribute__((always_inline)) {
+    const int a = base + (int)threadIdx.x * kQPer;
+#pragma unroll
+    for (int i = 0; i < kQPer; ++i) {
+      const int k = a + i;
+      const double mk = k < nc ? m[k] : 0.0, gk = k < nc ? g[k] : 0.0;
+      const double r = qreach_b(gk);
+      const bool ok = mk == mk && r == r;
+      hv[i] = k >= nc ? -INFINITY : (ok ? mk + r : INFINITY);
+      lv[i] = k >= nc ? INFINITY : (ok ? mk - r : -INFINITY);
+    }
+  };
+  double carry = -INFINITY;  // prefix max of the earlier passes
+  for (int ps = 0; ps < npass; ++ps) {  // block-uniform
+    const int base = ps * kPass;
+    double hv[kQPer], lv[kQPer];
+    load(base, hv, lv);
+#pragma unroll
+    for (int i = 1; i < kQPer; ++i) hv[i] = fmax(hv[i], hv[i - 1]);
+    const double incl = block_prefix_max(hv[kQPer - 1], sw);
+    double before = __shfl_up(incl, 1, kWave);  // max over the threads before this one
+    if (lane_id() == 0) {
+      before = -INFINITY;
+      for (int w = 0; w < (int)threadIdx.x / kWave; ++w) before = fmax(before, sw[w]);
+    }
+    before = fmax(before, carry);
+    const int a = base + (int)threadIdx.x * kQPer;
+#pragma unroll
+    for (int i = 0; i < kQPer; ++i)
+      if (a + i < nc) P[S.comp_off + a + i] = fmax(before, hv[i]);
+    for (int w = 0; w < kQB / kWave; ++w) carry = fmax(carry, sw[w]);  // (the pass's total)
+    __syncthreads();
+  }
+  double carry_lo = INFINITY;  // suffix min of the later passes
+  for (int ps = npass - 1; ps >= 0; --ps) {
+    const int base = ps * kPass;
+    double hv[kQPer], lv[kQPer];
+    load(base, hv, lv);
+#pragma unroll
+    for (int i = kQPer - 2; i >= 0; --i) lv[i] = fmin(lv[i], lv[i + 1]);
+    const double incl = block_suffix_min(lv[0], sw);
+    double after = __shfl_down(incl, 1, kWave);  // min over the threads after this one
+    if (lane_id() == kWave - 1) {
+      after = INFINITY;
+      for (int w = (int)threadIdx.x / kWave + 1; w < kQB / kWave; ++w) after = fmin(after, sw[w]);
+    }
+    after = fmin(after, carry_lo);
+    const int a = base + (int)threadIdx.x * kQPer;
+#pragma unroll
+    for (int i = 0; i < kQPer; ++i)
+      if (a + i < nc) Sm[S.comp_off + a + i] = fmin(after, lv[i]);
+    for (int w = 0; w < kQB / kWave; ++w) carry_lo = fmin(carry_lo, sw[w]);  // (the pass's total)
+    __syncthreads();
+  }
+}
+
+// how many leading k in [0, n) satisfy pred (pred holds on a prefix): a
+// block-wide search, kBS probes per round (three rounds for n <= 2^24)
+template <typename F>
+__device__ __forceinline__ int prefix_count(int n, F pred) {
+  int lo = 0, len = n;
+  while (len > 0) {  // block-uniform
+    const int stride = (len + kBS - 1) / kBS;
+    const int nprobe = (len + stride - 1) / stride;
+    const int t = threadIdx.x;
+    const int p = lo + min((t + 1) * stride, len) - 1;
+    const int c = __syncthreads_count(t < nprobe && pred(p));
+    if (c == nprobe) return lo + len;
+    lo += c * stride;
+    len = min(stride, len - c * stride) - 1;  // (probe c failed: the boundary is before it)
+  }
+  return lo;
+}
+
 // quantized mixture log-mass of one value, one block, threads stride components.
 // tpe.py:159-174 (GMM1) and :288-305 (LGMM1): sum_k w_k*cdf(ub) - w_k*cdf(lb),
-// then log(prob) - log(p_accept).
+// then log(prob) - log(p_accept).  P / Sm (nullable): k_qreach's arrays --
+// the loop then covers the value's component window only (same sums).
 __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
                                         const double* __restrict__ w,
                                         const double* __restrict__ mu,
                                         const double* __restrict__ sigma, double x,
-                                        int32_t* err, double* sh) {
+                                        int32_t* err, double* sh,
+                                        const double* __restrict__ P = nullptr,
+                                        const double* __restrict__ Sm = nullptr) {
   const bool lg = J.family == TPE_LGMM1;
   const double hq = J.q / 2.0;
   double ub = x + hq, lb = x - hq;
@@ -980,13 +1119,22 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
   // skip test is cheap; a serial load -> test chain per component is what
   // bounded this loop)
   constexpr int kQU = 4;
-  for (int k0 = threadIdx.x; k0 < nc; k0 += kQU * kBS) {
+  int kbeg = 0, kend = nc;
+  const double dl = 1e-9 * (1.0 + fabs(xl) + fabs(xu));  // (covers the fp64 rounding of mu +- b)
+  const double wa = xl - dl, wb = xu + dl;
+  if (P && wa == wa && wb == wb) {  // block-uniform
+    kbeg = prefix_count(nc, [&](int k) { return P[S.comp_off + k] <= wa; });
+    kend = max(kbeg, prefix_count(nc, [&](int k) { return Sm[S.comp_off + k] < wb; }));
+  }
+  // the full loop's thread-to-component map, entered at the window's first pass
+  for (int k0 = kbeg / (kQU * kBS) * (kQU * kBS) + threadIdx.x; k0 < kend; k0 += kQU * kBS) {
     double mq[kQU], sq[kQU];
 #pragma unroll
     for (int u = 0; u < kQU; ++u) {
       const int k = k0 + u * kBS;
-      mq[u] = k < nc ? mu[S.comp_off + k] : INFINITY;
-      sq[u] = k < nc ? sigma[S.comp_off + k] : 1.0;
+      const bool in = k >= kbeg && k < kend;
+      mq[u] = in ? mu[S.comp_off + k] : INFINITY;
+      sq[u] = in ? sigma[S.comp_off + k] : 1.0;
     }
 #pragma unroll
     for (int u = 0; u < kQU; ++u) {
@@ -1022,7 +1170,7 @@ __global__ __launch_bounds__(kBS) void k_score_q(
     const double* __restrict__ sigma, const double* __restrict__ vals,
     const int64_t* __restrict__ firsts, const unsigned long long* __restrict__ counts,
     double* __restrict__ out_bl, double* __restrict__ out_al, tpe_best* __restrict__ partial,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, const double* __restrict__ qP, const double* __restrict__ qS) {
   __shared__ double sh[kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
   const int64_t cnt = counts ? (int64_t)counts[blockIdx.y] : J.n_cand;
@@ -1034,8 +1182,8 @@ __global__ __launch_bounds__(kBS) void k_score_q(
   }
   const int64_t voff = counts ? J.lat_off : J.cand_off;
   const double v = vals[voff + pos];
-  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err, sh);
-  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err, sh);
+  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err, sh, qP, qS);
+  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err, sh, qP, qS);
   if (threadIdx.x == 0) {
     const int64_t idx = firsts ? firsts[J.lat_off + pos] : J.cand_base + pos;
     if (out_bl) out_bl[J.out_off + pos] = bl;
@@ -1062,7 +1210,8 @@ __device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
                                            const double* __restrict__ mu,
                                            const double* __restrict__ sigma,
                                            tpe_best* __restrict__ partial, int job, int64_t s,
-                                           int64_t nper, double* sh) {
+                                           int64_t nper, double* sh, const double* __restrict__ P,
+                                           const double* __restrict__ Sm) {
   const tpe_job J = jobs[job];
   if (s >= J.lat_n) return;  // block-uniform
   const double v = (double)(J.lat_kmin + s) * J.q;  // np.round(x/q) * q, as k_lattice_compact
@@ -1070,8 +1219,8 @@ __device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
   // qloguniform / qlognormal lattice, never drawn) must not raise the
   // reference's negative-argument error (tpe.py:196-197) -- a drawn value
   // x = round(exp(y)/q)*q >= 0 never has ub = x + q/2 < 0, so no err here
-  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, nullptr, sh);
-  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, nullptr, sh);
+  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, nullptr, sh, P, Sm);
+  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, nullptr, sh, P, Sm);
   if (threadIdx.x == 0) partial[(int64_t)job * nper + s] = tpe_best{bl - al, -1, v, 0};
 }
 
@@ -1563,7 +1712,8 @@ static bool launch_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
                                   const double* wcdf, uint64_t* slot_first, int32_t* err,
                                   int64_t start, int64_t limit, const int32_t* need,
                                   hipStream_t st, const char* who, const double* w = nullptr,
-                                  tpe_best* slot_part = nullptr, int64_t slot_n = 0) {
+                                  tpe_best* slot_part = nullptr, int64_t slot_n = 0,
+                                  const double* qP = nullptr, const double* qS = nullptr) {
   int64_t gx = 1;
   for (int i = 0; i < n_jobs; ++i) {
     const int64_t n = std::min(host_jobs[i].n_cand, limit);
@@ -1590,11 +1740,11 @@ static bool launch_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
   if (pow2)
     hipLaunchKernelGGL(k_lattice_sample<true>, dim3(grid), dim3(kBS), lds, st, jobs, segs, mu,
                        sigma, wcdf, sf, err, (int)gx, n_jobs, start, limit, need, w, slot_part,
-                       sn);
+                       sn, qP, qS);
   else
     hipLaunchKernelGGL(k_lattice_sample<false>, dim3(grid), dim3(kBS), lds, st, jobs, segs, mu,
                        sigma, wcdf, sf, err, (int)gx, n_jobs, start, limit, need, w, slot_part,
-                       sn);
+                       sn, qP, qS);
   return true;
 }
 
@@ -1632,7 +1782,8 @@ extern "C" int tpe_lattice_suggest(const tpe_job* jobs, const tpe_job* host_jobs
                                    const tpe_seg* segs, const double* w, const double* mu,
                                    const double* sigma, const double* wcdf, uint64_t* slot_first,
                                    int64_t prefix, tpe_best* partial, int64_t n_partial,
-                                   int32_t* need, tpe_best* best, int32_t* err, void* stream) {
+                                   int32_t* need, tpe_best* best, int32_t* err, double* reach_hi,
+                                   double* reach_lo, void* stream) {
   if (!check_jobs("tpe_lattice_suggest", host_jobs, n_jobs)) return TPE_E_ARG;
   if (n_jobs == 0) return TPE_OK;
   if (!jobs || !segs || !w || !mu || !sigma || !wcdf || !slot_first || !partial || !need ||
@@ -1667,8 +1818,13 @@ extern "C" int tpe_lattice_suggest(const tpe_job* jobs, const tpe_job* host_jobs
   if (!ready && hipMemsetAsync(slot_first, 0xFF, (size_t)end * sizeof(uint64_t), st) != hipSuccess)
     return check_launch("tpe_lattice_suggest memset");
   unsigned long long* sf = (unsigned long long*)slot_first;
+  const bool win = reach_hi && reach_lo;  // the slots' component windows (k_qreach)
+  if (win)
+    hipLaunchKernelGGL(k_qreach, dim3(2 * n_jobs), dim3(kQB), 0, st, jobs, segs, mu, sigma,
+                       reach_hi, reach_lo);
   if (!launch_lattice_sample(jobs, host_jobs, n_jobs, segs, mu, sigma, wcdf, slot_first, err, 0,
-                             prefix, nullptr, st, "tpe_lattice_suggest", w, partial, max_n))
+                             prefix, nullptr, st, "tpe_lattice_suggest", w, partial, max_n,
+                             win ? reach_hi : nullptr, win ? reach_lo : nullptr))
     return TPE_E_UNSUPPORTED;
   hipLaunchKernelGGL(k_lattice_decide, dim3(n_jobs), dim3(kBS), 0, st, jobs, segs, mu, sigma,
                      partial, max_n, sf, prefix, 0, need, best);
@@ -1719,7 +1875,7 @@ extern "C" int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs
                                    const int64_t* firsts, const int64_t* counts, int64_t max_vals,
                                    double* out_bl, double* out_al, tpe_best* partial,
                                    int64_t n_partial, tpe_best* best, int32_t* err,
-                                   void* stream) {
+                                   double* reach_hi, double* reach_lo, void* stream) {
   if (!check_jobs("tpe_score_quantized", host_jobs, n_jobs)) return TPE_E_ARG;
   if (n_jobs == 0) return TPE_OK;
   if (!jobs || !segs || !w || !mu || !sigma || !vals || !partial || !best || !err ||
@@ -1739,9 +1895,13 @@ extern "C" int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs
     return TPE_E_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
+  const bool win = reach_hi && reach_lo;  // the values' component windows (k_qreach)
+  if (win)
+    hipLaunchKernelGGL(k_qreach, dim3(2 * n_jobs), dim3(kQB), 0, st, jobs, segs, mu, sigma,
+                       reach_hi, reach_lo);
   hipLaunchKernelGGL(k_score_q, dim3((unsigned)gx, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
                      segs, w, mu, sigma, vals, firsts, (const unsigned long long*)counts, out_bl,
-                     out_al, partial, err);
+                     out_al, partial, err, win ? reach_hi : nullptr, win ? reach_lo : nullptr);
   hipLaunchKernelGGL(k_reduce, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
   return check_launch("tpe_score_quantized");
 }

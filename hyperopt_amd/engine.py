@@ -1522,6 +1522,10 @@ class Engine:
                                                d_bl, d_al, d_x, d_part, npart, db, sp),
                         "tpe_score_pruned64")
             elif kind == "lat":
+                # the lattice values' component windows (k_qreach, on the
+                # quantized jobs' own components of the reach arrays)
+                d_rh = self._buf("reach_hi", 8 * n_comp)
+                d_rl = self._buf("reach_lo", 8 * n_comp)
                 d_vals = self._buf("lat_vals", 8 * lat_off)
                 d_first = self._buf("lat_first", 8 * lat_off)
                 if lat_ready:
@@ -1539,7 +1543,7 @@ class Engine:
                     d_need = self._buf("lat_need", 4 * nj)
                     L.check(lib.tpe_lattice_suggest(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
                                                     d_slot, self.lat_prefix, d_part, npart,
-                                                    d_need, db, d_err, ks),
+                                                    d_need, db, d_err, d_rh, d_rl, ks),
                             "tpe_lattice_suggest")
                 else:
                     L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
@@ -1550,9 +1554,11 @@ class Engine:
                     d_part = self._buf(pname, 32 * max(npart, 1))
                     L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig,
                                                     d_vals, d_first, d_cnt, max_vals, None, None,
-                                                    d_part, npart, db, d_err, ks),
+                                                    d_part, npart, db, d_err, d_rh, d_rl, ks),
                             "tpe_score_quantized")
             elif kind in ("qfb", "qinj"):
+                d_rh = self._buf("reach_hi", 8 * n_comp)
+                d_rl = self._buf("reach_lo", 8 * n_comp)
                 vals = d_cand
                 if kind == "qfb":
                     vals = self._buf("q_cand", 8 * max(qfb_off, 1))
@@ -1564,7 +1570,7 @@ class Engine:
                 d_part = self._buf(pname, 32 * max(npart, 1))
                 L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, vals, None,
                                                 None, max_vals, d_bl, d_al, d_part, npart, db,
-                                                d_err, ks), "tpe_score_quantized")
+                                                d_err, d_rh, d_rl, ks), "tpe_score_quantized")
             else:
                 npart = lib.tpe_categorical_partials(hjp, nj)
                 d_part = self._buf(pname, 32 * max(npart, 1))

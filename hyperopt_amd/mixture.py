@@ -119,9 +119,11 @@ class _Mixture:
                 "tpe_sample")
         return out[:n].cpu().numpy()
 
-    def lpdf(self, x, flags, low, high, q, precision):
+    def lpdf(self, x, flags, low, high, q, precision, windows=True):
         """Per-value log-density (unquantized) or log-mass (quantized) of the
-        normalised-weight mixture, truncation-normalised as the kernels do."""
+        normalised-weight mixture, truncation-normalised as the kernels do.
+        windows (quantized): each value sums only its window of unsaturated
+        components (tpe_score_quantized's reach arrays; the same bits)."""
         torch, lib = self.torch, self.lib
         n = x.size
         job = self.job(n, flags | L.F_INJECTED, low, high, q)
@@ -136,10 +138,14 @@ class _Mixture:
             partial = torch.empty(max(npart, 1) * L.BEST_DTYPE.itemsize, dtype=torch.uint8,
                                   device=self.dev)
             err = torch.zeros(1, dtype=torch.int32, device=self.dev)
+            reach = torch.empty(2 * self.K if windows else 1, dtype=torch.float64, device=self.dev)
+            rh = _P(reach.data_ptr()) if windows else None
+            rl = _P(reach.data_ptr() + 8 * self.K) if windows else None
             L.check(lib.tpe_score_quantized(
                 _P(d_job.data_ptr()), hj, 1, _P(self.d_seg.data_ptr()), w, mu, s,
                 _P(d_x.data_ptr()), None, None, n, _P(out_bl.data_ptr()), None,
-                _P(partial.data_ptr()), npart, _P(best.data_ptr()), _P(err.data_ptr()), sp),
+                _P(partial.data_ptr()), npart, _P(best.data_ptr()), _P(err.data_ptr()), rh,
+                rl, sp),
                 "tpe_score_quantized")
             if int(err.item()):
                 raise ValueError("negative arg to lognormal_cdf", x)  # tpe.py:196-197

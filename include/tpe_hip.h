@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 17
+#define TPE_ABI_VERSION 18
 
 enum {
   TPE_OK = 0,
@@ -482,12 +482,19 @@ int tpe_lattice_compact(const tpe_job* jobs, const tpe_job* host_jobs, int n_job
  * err: int32 flag set to 1 on a negative lognormal_cdf argument
  * (tpe.py:196-197). */
 int64_t tpe_quantized_partials(const tpe_job* host_jobs, int n_jobs, int64_t max_vals);
+/* reach_hi / reach_lo (nullable, both or neither): scratch of one double per
+ * component of the pools (indexed by comp_off like the table path's): the
+ * prefix max of mu + b / suffix min of mu - b, b = 6.5 max(sqrt2 sigma, EPS),
+ * of every job's two mixtures (written here, k_qreach), so each value sums
+ * only the window of components whose erf pair is not saturated -- the same
+ * sums bit for bit as the full loop (NULL). */
 int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
                         const tpe_seg* segs, const double* w, const double* mu,
                         const double* sigma, const double* vals, const int64_t* firsts,
                         const int64_t* counts, int64_t max_vals, double* out_bl,
                         double* out_al, tpe_best* partial, int64_t n_partial,
-                        tpe_best* best, int32_t* err, void* stream);
+                        tpe_best* best, int32_t* err, double* reach_hi, double* reach_lo,
+                        void* stream);
 /* The suggest path's lattice argmax, prefix first (replaces sample + compact
  * + score + reduce for sampled jobs without per-candidate outputs; the
  * result is the same tpe_best).  Draws the first `prefix` candidates of every
@@ -501,7 +508,8 @@ int tpe_lattice_suggest(const tpe_job* jobs, const tpe_job* host_jobs, int n_job
                         const tpe_seg* segs, const double* w, const double* mu,
                         const double* sigma, const double* wcdf, uint64_t* slot_first,
                         int64_t prefix, tpe_best* partial, int64_t n_partial, int32_t* need,
-                        tpe_best* best, int32_t* err, void* stream);
+                        tpe_best* best, int32_t* err, double* reach_hi, double* reach_lo,
+                        void* stream);  /* reach_hi / reach_lo: as tpe_score_quantized */
 
 /* ---- categorical labels: sample (or read) + score + argmax ---------------- */
 int64_t tpe_categorical_partials(const tpe_job* host_jobs, int n_jobs);

@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 17
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 18
     sizes = (ctypes.c_int32 * 11)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 11) == 11
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -197,7 +197,7 @@ def test_lattice_suggest_argument_errors():
 
     def call(prefix, n_partial, need=one, n_jobs=1):
         return lib.tpe_lattice_suggest(one, hp_, n_jobs, *ptrs, prefix, one, n_partial, need, one,
-                                       one, None)
+                                       one, None, None, None)
     assert call(1 << 16, 1 << 10, n_jobs=0) == 0  # nothing to do
     assert call(1 << 16, 1 << 10) == -1
     assert b"not a sampled quantized job" in lib.tpe_last_error()
