@@ -168,6 +168,7 @@ class Columnar(object):
         self.obs_tid = np.zeros(0, np.int64)
         self.n_active = np.zeros(len(self.labels), np.int64)
         self.keys_increasing = True  # key_tid strictly increasing: one document per tid
+        self.n_alias = 0  # rows whose observations are filed under another tid (from_tid)
         self.loss = np.zeros(0)
         self.n_final = 0  # rows [0, n_final) are DONE and their losses cached
         self._device = {}
@@ -203,6 +204,8 @@ class Columnar(object):
             key = misc.get("from_tid", doc["tid"])
             self.key_tid[r] = key
             self.obs_tid[r] = misc["tid"]
+            if key != misc["tid"]:
+                self.n_alias += 1
             if inc and last is not None and not key > last:
                 inc = False
             last = key

@@ -105,13 +105,16 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
   auto fold = [&]() {
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
+      // kFoldB weights read together (one LDS latency per batch, not per add),
+      // then added in list order: the fp64 add chain is the only serial part
+      constexpr int kFoldB = 32;
       int j = 0;
-      for (; j + 4 <= filled; j += 4) {
-        const double a = list[j], b = list[j + 1], c = list[j + 2], d = list[j + 3];
-        cnt = __dadd_rn(cnt, a);
-        cnt = __dadd_rn(cnt, b);
-        cnt = __dadd_rn(cnt, c);
-        cnt = __dadd_rn(cnt, d);
+      for (; j + kFoldB <= filled; j += kFoldB) {
+        double v[kFoldB];
+#pragma unroll
+        for (int i = 0; i < kFoldB; ++i) v[i] = list[j + i];
+#pragma unroll
+        for (int i = 0; i < kFoldB; ++i) cnt = __dadd_rn(cnt, v[i]);
       }
       for (; j < filled; ++j) cnt = __dadd_rn(cnt, list[j]);
     }

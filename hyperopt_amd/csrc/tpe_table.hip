@@ -1815,7 +1815,12 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
 #endif
 constexpr int kBandBlocks = TPE_BAND_BLOCKS;  // blocks per job
 constexpr int kBandSurv = 128;       // survivors scored directly (more: the cell expansions)
-constexpr int kSurvBatch = 4;        // survivors summed together per pass
+#ifndef TPE_SURV_BATCH
+#define TPE_SURV_BATCH 8
+#endif
+constexpr int kSurvBatch = TPE_SURV_BATCH;  // survivors summed together per pass
+constexpr int kDirStage = 1024;      // a block's component chunk staged in LDS when it fits
+                                     // (a multiple of kBX: the per-thread order is unchanged)
 #ifndef TPE_BAND_BX
 #define TPE_BAND_BX 256
 #endif
@@ -1837,7 +1842,14 @@ struct BandMix {  // one mixture's expansion on one cell (or one chunk of its co
   int pad;
   int dir[kChunkDir];
 };
-constexpr int kEPT = 8;              // band entries per thread per window (k_band)
+#ifndef TPE_BAND_EPT
+#define TPE_BAND_EPT 8
+#endif
+#ifndef TPE_BAND_U
+#define TPE_BAND_U 2
+#endif
+constexpr int kEPT = TPE_BAND_EPT;   // band entries per thread per window (k_band)
+constexpr int kExpU = TPE_BAND_U;    // band_expand: component loads in flight per thread
 constexpr int kBandSurvMax = 65536;  // survivors a job may have (more: the exact fallback)
 struct BandWork {  // per job (tpe_band_bytes)
   double part[kBandBlocks][kBandSurv][4];         // direct: per chunk and survivor {m, s} b, a
@@ -1846,11 +1858,27 @@ struct BandWork {  // per job (tpe_band_bytes)
   int64_t sidx[kBandSurvMax];                     // ... and candidate index
   int cells[kBandCells];                          // the listed cells (ascending)
   int ns, ncell, over, pad0;                      // survivors, cells, job overflowed
-  long long tmark[8];                             // (TPE_BAND_TIMING diagnostic builds)
-  BestT win[kBandBlocks];                         // (unused: k_band_final is one block per job)
+  long long tmark[16];                            // (TPE_BAND_TIMING diagnostic builds)
+  BestT win[kBandBlocks];                         // k_band_final's per-block winners (k_band_pick)
   unsigned int done;                              // (unused)
   unsigned int pad[3];
 };
+
+// One step of the online log-sum-exp (s >= 1 at scale m) that needs no exp
+// and changes nothing in the result's bits: a term below e^-37 of the
+// scale adds < 2^-53 <= ulp(s)/2 to s (s is left as it is, as the rounded
+// add would); a term above e^60 of it makes s * e^(m - v) < 2^-53 for any
+// s < 1e10 (s = 1 + that rounds to 1).  NaN differences fall through.
+__device__ __forceinline__ bool lse_skip(double& m, double& s, double v) {
+  const double d = v - m;
+  if (d < -37.0) return true;
+  if (d > 60.0) {
+    s = 1.0;
+    m = v;
+    return true;
+  }
+  return false;
+}
 
 // (m, s): e^m s; combined in a fixed order
 __device__ __forceinline__ void lse_merge(double& m, double& s, double m2, double s2) {
@@ -1932,12 +1960,14 @@ __device__ void band_expand(const tpe_seg& S, const double* __restrict__ coef64,
     for (int n = 0; n <= kBandD; ++n) P[n] *= r;
   }
   // block sums of the kBandD + 1 terms (fixed order: deterministic)
+  // (every term's butterfly stepped together: their LDS exchanges overlap)
 #pragma unroll
-  for (int n = 0; n <= kBandD; ++n) {
-    double v = P[n];
+  for (int o = 32; o >= 1; o >>= 1) {
+    double t[kBandD + 1];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
-    P[n] = v;
+    for (int n = 0; n <= kBandD; ++n) t[n] = __shfl_xor(P[n], o, kWave);
+#pragma unroll
+    for (int n = 0; n <= kBandD; ++n) P[n] += t[n];
   }
   __syncthreads();  // (E.n_dir complete; dred free)
   const int wid = threadIdx.x / kWave;
@@ -1982,6 +2012,7 @@ __device__ __forceinline__ double band_direct(const tpe_seg& S, const double* __
     const double4 c = ld4(coef64, S.comp_off + k);
     const double t = (y - c.x) * c.y;
     const double v = -0.5 * (t * t) + c.z;
+    if (lse_skip(mo, so, v)) continue;
     const bool up = v > mo;
     const double e = exp(up ? mo - v : v - mo);
     so = up ? so * e + 1.0 : so + e;
@@ -2022,6 +2053,7 @@ __global__ __launch_bounds__(kBX) void k_band(
   __shared__ int s_over, s_off;
   __shared__ int s_tile[kEPT * kBX];
   __shared__ int s_wm[kNW];
+  __shared__ double4 s_cst[kDirStage];  // direct path: the block's chunk of one mixture
   const int j = blockIdx.y, kb = blockIdx.x;
   const int lane = lane_id(), wid = threadIdx.x / kWave;
   const tpe_job J = jobs[j];
@@ -2098,7 +2130,7 @@ __global__ __launch_bounds__(kBX) void k_band(
       b32 = block_best<kBX>(b32, red);
       if (threadIdx.x == 0) {
         best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
-        work[j].over = 1;  // (k_band_final leaves the job alone)
+        work[j].over = 1;  // (k_band_final / k_band_pick leave the job alone)
       }
     }
     return;
@@ -2241,6 +2273,14 @@ __global__ __launch_bounds__(kBX) void k_band(
       const int per = (nc + kBandBlocks - 1) / kBandBlocks;
       const int k0 = kb * per, k1 = min(nc, k0 + per);
       const double4* C = reinterpret_cast<const double4*>(coef64) + S.comp_off;
+      // the chunk in LDS once (every batch of survivors re-reads it; each
+      // thread's components and their order are the global loop's)
+      const bool staged = k1 - k0 <= kDirStage;
+      if (staged) {
+        for (int k = k0 + (int)threadIdx.x; k < k1; k += kBX) s_cst[k - k0] = C[k];
+        __syncthreads();
+      }
+      TMARK(8 + 3 * mix)
       for (int b0 = 0; b0 < ns; b0 += kSurvBatch) {
         double m[kSurvBatch], sm[kSurvBatch], y[kSurvBatch];
 #pragma unroll
@@ -2249,29 +2289,56 @@ __global__ __launch_bounds__(kBX) void k_band(
           sm[i] = 0.0;
           y[i] = score_coord(s_y[min(b0 + i, ns - 1)], lgmm);
         }
-        for (int k = k0 + (int)threadIdx.x; k < k1; k += kBX) {
-          const double4 c = C[k];
+        auto acc = [&](const double4 c) {
 #pragma unroll
           for (int i = 0; i < kSurvBatch; ++i) {
             const double t = (y[i] - c.x) * c.y;
             const double v = -0.5 * (t * t) + c.z;  // (log coefficient c.z: GMM1_lpdf's terms)
+            if (lse_skip(m[i], sm[i], v)) continue;
             const bool upv = v > m[i];
             const double e = exp(upv ? m[i] - v : v - m[i]);
             sm[i] = upv ? sm[i] * e + 1.0 : sm[i] + e;
             m[i] = upv ? v : m[i];
           }
+        };
+        if (staged) {
+          for (int k = k0 + (int)threadIdx.x; k < k1; k += kBX) acc(s_cst[k - k0]);
+        } else {
+          for (int k = k0 + (int)threadIdx.x; k < k1; k += kBX) acc(C[k]);
         }
+        if (b0 == 0) { TMARK(9 + 3 * mix) }
         // fixed reduction tree: the wave's largest scale (DPP max), each lane's
         // sum brought to it once, a plain wave sum; then the block's waves in
         // order (lse_merge)
+        // (wave_max_d / wave_sum_d's butterflies, the batch's survivors
+        // stepped together so their LDS exchanges overlap: same bits)
+        double mw[kSurvBatch], v[kSurvBatch];
 #pragma unroll
-        for (int i = 0; i < kSurvBatch; ++i) {
-          const double mw = wave_max_d(m[i]);
-          double v = (m[i] == -INFINITY) ? 0.0 : sm[i] * exp(m[i] - mw);
-          v = wave_sum_d(v);
-          if (lane == 0) {
-            s_red[wid][i][0] = mw;
-            s_red[wid][i][1] = v;
+        for (int i = 0; i < kSurvBatch; ++i) mw[i] = m[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          double t[kSurvBatch];
+#pragma unroll
+          for (int i = 0; i < kSurvBatch; ++i) t[i] = __shfl_xor(mw[i], off, kWave);
+#pragma unroll
+          for (int i = 0; i < kSurvBatch; ++i) mw[i] = fmax(mw[i], t[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < kSurvBatch; ++i)
+          v[i] = (m[i] == -INFINITY) ? 0.0 : sm[i] * exp(m[i] - mw[i]);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          double t[kSurvBatch];
+#pragma unroll
+          for (int i = 0; i < kSurvBatch; ++i) t[i] = __shfl_xor(v[i], off, kWave);
+#pragma unroll
+          for (int i = 0; i < kSurvBatch; ++i) v[i] += t[i];
+        }
+        if (lane == 0) {
+#pragma unroll
+          for (int i = 0; i < kSurvBatch; ++i) {
+            s_red[wid][i][0] = mw[i];
+            s_red[wid][i][1] = v[i];
           }
         }
         __syncthreads();
@@ -2282,7 +2349,8 @@ __global__ __launch_bounds__(kBX) void k_band(
           W.part[kb][b0 + i][2 * mix] = mm;
           W.part[kb][b0 + i][2 * mix + 1] = ss;
         }
-        __syncthreads();  // (s_red reused)
+        __syncthreads();  // (s_red reused; s_cst free after the last batch)
+        if (b0 == 0) { TMARK(10 + 3 * mix) }
       }
     }
   } else {
@@ -2300,7 +2368,7 @@ __global__ __launch_bounds__(kBX) void k_band(
         const int nc = S.n_obs + 1;
         const int per = (nc + nch - 1) / nch;
         const int k0 = min(nc, ch * per), k1 = min(nc, k0 + per);
-        band_expand<kBX, 2>(S, coef64, y0, Tb.h, s_eb, dred, k0, k1);
+        band_expand<kBX, kExpU>(S, coef64, y0, Tb.h, s_eb, dred, k0, k1);
         BandMix& Q = W.cpart[k][ch][mix];
         if (threadIdx.x <= kBandD) Q.P[threadIdx.x] = s_eb.P[threadIdx.x];
         if (threadIdx.x == 0) {
@@ -2315,19 +2383,30 @@ __global__ __launch_bounds__(kBX) void k_band(
   TMARK(3)
 }
 
-// The band's decision (one block per job, after k_band): direct -- each
-// survivor's chunk partial sums combined in chunk order; cells -- each listed
-// cell's chunk expansions merged in chunk order (into LDS) and evaluated at
-// its survivors -- then np.argmax over all of the job's survivors into
-// best[j] = {fp64 score, index, value, n_cand}.  (Sixteen blocks per job with
-// a last-block hand-off spent 10-17 us of the job's ~30 in the hand-off;
-// one block scores a C3 band of ~4 000 survivors in ~4 us.)
-constexpr int kFX = 1024;  // k_band_final block: one per job, 16 waves (latency-bound fp64 chains)
+// The band's decision (after k_band), kFinBlocks blocks per job, each
+// scoring a share of the job's survivors: direct -- a survivor's kBandBlocks
+// chunk partial sums merged on 16 lanes (the largest scale by a max
+// butterfly, the chunks' sums brought to it and added by a fixed butterfly);
+// cells -- each listed cell's chunk expansions merged in chunk order (into
+// LDS; every block the same) and evaluated at the block's survivors.  Each
+// block leaves its np.argmax in W.win[kb]; k_band_pick folds them into
+// best[j] = {fp64 score, index, value, n_cand}.  (One block per job scored a
+// C3 band of ~4 000 survivors in ~16 us on one CU: fp64-rate bound; a
+// last-block hand-off inside the kernel cost 10-17 us in round 3.)
+#ifndef TPE_BAND_FX
+#define TPE_BAND_FX 512
+#endif
+#ifndef TPE_BAND_FINB
+#define TPE_BAND_FINB 8
+#endif
+constexpr int kFX = TPE_BAND_FX;         // k_band_final block
+constexpr int kFinBlocks = TPE_BAND_FINB;  // k_band_final blocks per job (<= kBandBlocks: W.win)
+constexpr int kFStage = 4096;  // survivors staged in LDS per round (k_band_final, cells)
+static_assert(kFinBlocks <= kBandBlocks && kFinBlocks <= kWave, "W.win holds the blocks' winners");
 __global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ jobs,
                                                     const tpe_seg* __restrict__ segs,
                                                     const double* __restrict__ coef64,
                                                     const tpe_table* __restrict__ tables,
-                                                    tpe_best* __restrict__ best,
                                                     BandWork* __restrict__ work) {
   constexpr int kNW = kFX / kWave;
   __shared__ BestT red[kNW];
@@ -2337,9 +2416,11 @@ __global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ 
   __shared__ int s_ndu[kBandCells][2];             // per (cell, chunk) unit: slow components ...
   __shared__ int s_dir[kBandCells][2][kChunkDir];  // ... and their indices (units <= kBandCells)
   __shared__ int s_cells[kBandCells];
-  const int j = blockIdx.y;
+  __shared__ float s_sy[kFStage];
+  __shared__ int64_t s_si[kFStage];
+  const int j = blockIdx.y, kb = blockIdx.x;
   BandWork& W = work[j];
-  TMARK(4)
+  if (kb == 0) { TMARK(4) }
   if (W.over) return;  // (k_band gave the fp32 winner with n_scored = -1)
   const tpe_job J = jobs[j];
   const int ns = W.ns, ncell = W.ncell;
@@ -2347,18 +2428,31 @@ __global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ 
   const bool lgmm = J.family == TPE_LGMM1;
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const tpe_table Tb = tables[j];
-  const int i0 = 0, i1 = ns;  // (one block per job: no cross-block hand-off)
   BestT bx{0.0, -1, 0.0};
   if (ns <= kBandSurv) {
-    for (int i = i0 + (int)threadIdx.x; i < i1; i += kFX) {
-      double l2[2];
-      for (int mix = 0; mix < 2; ++mix) {
-        double mm = W.part[0][i][2 * mix], ss = W.part[0][i][2 * mix + 1];
-        for (int c = 1; c < kBandBlocks; ++c)
-          lse_merge(mm, ss, W.part[c][i][2 * mix], W.part[c][i][2 * mix + 1]);
-        l2[mix] = log(ss) + mm;
+    // one survivor per 16 lanes, lane c holding chunk c's partials
+    constexpr int kSPB = kFX / kBandBlocks;  // survivors per block pass
+    static_assert(kBandBlocks == 16, "16-lane groups");
+    const int c = threadIdx.x % kBandBlocks;
+    for (int i = kb * kSPB + (int)threadIdx.x / kBandBlocks; i < ns; i += kFinBlocks * kSPB) {
+      const double4 q = *reinterpret_cast<const double4*>(W.part[c][i]);
+      double mb = q.x, ma = q.z;
+#pragma unroll
+      for (int o = kBandBlocks / 2; o >= 1; o >>= 1) {
+        const double tb = __shfl_xor(mb, o, kWave), ta = __shfl_xor(ma, o, kWave);
+        mb = fmax(mb, tb);
+        ma = fmax(ma, ta);
       }
-      best_update(bx, l2[0] - l2[1], W.sidx[i], cand_value(W.sy[i], lgmm));
+      double sb = q.x == -INFINITY ? 0.0 : q.y * exp(q.x - mb);
+      double sa = q.z == -INFINITY ? 0.0 : q.w * exp(q.z - ma);
+#pragma unroll
+      for (int o = kBandBlocks / 2; o >= 1; o >>= 1) {
+        const double tb = __shfl_xor(sb, o, kWave), ta = __shfl_xor(sa, o, kWave);
+        sb += tb;
+        sa += ta;
+      }
+      if (c == 0) best_update(bx, (log(sb) + mb) - (log(sa) + ma), W.sidx[i],
+                              cand_value(W.sy[i], lgmm));
     }
   } else {
     // merge: the chunks' expansions (P_0..P_20 and m per (cell, chunk,
@@ -2406,52 +2500,79 @@ __global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ 
     }
     for (int t = threadIdx.x; t < ncell; t += kFX) s_cells[t] = W.cells[t];
     __syncthreads();
-    TMARK(5)
+    if (kb == 0) { TMARK(5) }
     const float g0 = (float)Tb.origin, h32 = (float)Tb.h;
-    for (int i = i0 + (int)threadIdx.x; i < i1; i += kFX) {
-      const float yf = W.sy[i];
-      const int c = band_cell(Tb, yf);
-      int lo = 0, hi = ncell;  // its listed position (k_band listed every survivor's cell)
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (s_cells[mid] < c) lo = mid + 1; else hi = mid;
+    // this block's survivors, in rounds of kFStage staged in LDS by
+    // coalesced loads all in flight at once
+    const int per = (ns + kFinBlocks - 1) / kFinBlocks;
+    const int i0 = min(ns, kb * per), i1 = min(ns, i0 + per);
+    for (int r0 = i0; r0 < i1; r0 += kFStage) {
+      const int rn = min(kFStage, i1 - r0);
+      __syncthreads();  // (the previous round's reads of s_sy / s_si done)
+      for (int t = threadIdx.x; t < rn; t += kFX) {
+        s_sy[t] = W.sy[r0 + t];
+        s_si[t] = W.sidx[r0 + t];
       }
-      const int k = lo;
-      const double y = score_coord(yf, lgmm);
-      double l2[2];
-      for (int mix = 0; mix < 2; ++mix) {
-        const tpe_seg& S = mix ? SA : SB;
-        if (s_nd[k][mix] < 0) {
-          l2[mix] = band_direct(S, coef64, y);
-          continue;
+      __syncthreads();
+      for (int t = threadIdx.x; t < rn; t += kFX) {
+        const float yf = s_sy[t];
+        const int c = band_cell(Tb, yf);
+        int lo = 0, hi = ncell;  // its listed position (k_band listed every survivor's cell)
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (s_cells[mid] < c) lo = mid + 1; else hi = mid;
         }
+        const int k = lo;
+        const double y = score_coord(yf, lgmm);
         const double u = (y - (double)cell_centre(g0, h32, c)) / Tb.h;
-        // the expansion's coefficients into registers first (their LDS reads
-        // issued together, not one per step of the Horner chain)
-        double cf[kBandD + 2];
+        auto horner = [&](int mix) {
+          double p = s_P[k][mix][kBandD];
 #pragma unroll
-        for (int n = 0; n <= kBandD + 1; ++n) cf[n] = s_P[k][mix][n];
-        double p = cf[kBandD];
-#pragma unroll
-        for (int n = kBandD - 1; n >= 0; --n) p = fma(p, u, cf[n]);
-        const double m = cf[kBandD + 1];
-        for (int cc = 0; cc < nch; ++cc) {  // the slow components, term by term
-          const int u = k * nch + cc, nd = s_ndu[u][mix];
-          for (int d = 0; d < nd; ++d) {
-            const double4 cf = ld4(coef64, S.comp_off + s_dir[u][mix][d]);
-            const double t = (y - cf.x) * cf.y;
-            p += exp(cf.z - 0.5 * t * t - m);
+          for (int n = kBandD - 1; n >= 0; --n) p = fma(p, u, s_P[k][mix][n]);
+          return p;
+        };
+        // log of the mixture from its expansion value p, plus its slow
+        // components term by term; the direct sum when a chunk's list overflowed
+        auto finish = [&](int mix, const tpe_seg& S, double p) -> double {
+          const int ndt = s_nd[k][mix];
+          if (ndt < 0) return band_direct(S, coef64, y);
+          const double m = s_P[k][mix][kBandD + 1];
+          if (ndt > 0) {
+            for (int cc = 0; cc < nch; ++cc) {
+              const int un = k * nch + cc, nd = s_ndu[un][mix];
+              for (int d = 0; d < nd; ++d) {
+                const double4 cf = ld4(coef64, S.comp_off + s_dir[un][mix][d]);
+                const double t = (y - cf.x) * cf.y;
+                p += exp(cf.z - 0.5 * t * t - m);
+              }
+            }
           }
-        }
-        l2[mix] = log(p) + m;
+          return log(p) + m;
+        };
+        const double pb = horner(0), pa = horner(1);
+        const double lb = finish(0, SB, pb);
+        const double la = finish(1, SA, pa);
+        best_update(bx, lb - la, s_si[t], cand_value(yf, lgmm));
       }
-      best_update(bx, l2[0] - l2[1], W.sidx[i], cand_value(yf, lgmm));
     }
   }
-  TMARK(6)
+  if (kb == 0) { TMARK(6) }
   bx = block_best<kFX>(bx, red);
-  if (threadIdx.x == 0) {
-    best[j] = tpe_best{bx.score, bx.index, bx.value, J.n_cand};
+  if (threadIdx.x == 0) W.win[kb] = bx;
+}
+
+// The job's winner from its k_band_final blocks' (one wave per job).
+__global__ __launch_bounds__(kWave) void k_band_pick(const tpe_job* __restrict__ jobs,
+                                                     tpe_best* __restrict__ best,
+                                                     BandWork* __restrict__ work) {
+  const int j = blockIdx.x, lane = threadIdx.x;
+  BandWork& W = work[j];
+  if (W.over) return;
+  BestT b{0.0, -1, 0.0};
+  if (lane < kFinBlocks) b = W.win[lane];
+  b = wave_best(b);
+  if (lane == 0) {
+    best[j] = tpe_best{b.score, b.index, b.value, jobs[j].n_cand};
 #ifdef TPE_BAND_TIMING
     W.tmark[7] = wall_clock64();
 #endif
@@ -2879,8 +3000,10 @@ extern "C" int tpe_band_rescore(const tpe_job* jobs, const tpe_job* host_jobs, i
   hipLaunchKernelGGL(k_band, dim3(kBandBlocks, n_jobs), dim3(kBX), 0, (hipStream_t)stream, jobs,
                      segs, coef64, tables, band, band_ctl, partial, (int)gx, best,
                      static_cast<BandWork*>(work));
-  hipLaunchKernelGGL(k_band_final, dim3(1, n_jobs), dim3(kFX), 0, (hipStream_t)stream,
-                     jobs, segs, coef64, tables, best, static_cast<BandWork*>(work));
+  hipLaunchKernelGGL(k_band_final, dim3(kFinBlocks, n_jobs), dim3(kFX), 0, (hipStream_t)stream,
+                     jobs, segs, coef64, tables, static_cast<BandWork*>(work));
+  hipLaunchKernelGGL(k_band_pick, dim3(n_jobs), dim3(kWave), 0, (hipStream_t)stream, jobs, best,
+                     static_cast<BandWork*>(work));
   return check_launch("tpe_band_rescore");
 }
 

@@ -82,24 +82,7 @@ extern "C" int64_t tpe_smallest_rows(const double* losses, int64_t n, int64_t k,
   std::vector<double> kv((size_t)k);
   std::vector<int64_t> ki((size_t)k);
   int64_t m = 0;  // kept pairs, ascending
-  constexpr int64_t kChunk = 64;
-  for (int64_t i = 0; i < n; ++i) {
-    const double v = losses[i];
-    if (m == k) {
-      const double worst = kv[(size_t)(k - 1)];
-      if (worst == worst && (i % kChunk) == 0 && i + kChunk <= n) {
-        // a chunk without a loss below the kept worst changes nothing (equal
-        // losses come later than the kept one, NaN never beats a number):
-        // one vectorisable test per chunk
-        bool any = false;
-        for (int64_t j = i; j < i + kChunk; ++j) any |= losses[j] < worst;
-        if (!any) {
-          i += kChunk - 1;
-          continue;
-        }
-      }
-      if (!loss_before(v, i, worst, ki[(size_t)(k - 1)])) continue;
-    }
+  auto insert = [&](double v, int64_t i) {  // (v, i) beats the kept worst, or the set is not full
     int64_t p = m < k ? m++ : k - 1;  // slot freed at the end, then shifted into place
     while (p > 0 && loss_before(v, i, kv[(size_t)(p - 1)], ki[(size_t)(p - 1)])) {
       kv[(size_t)p] = kv[(size_t)(p - 1)];
@@ -108,6 +91,33 @@ extern "C" int64_t tpe_smallest_rows(const double* losses, int64_t n, int64_t k,
     }
     kv[(size_t)p] = v;
     ki[(size_t)p] = i;
+  };
+  constexpr int64_t kChunk = 64;
+  int64_t i = 0;
+  while (i < n) {
+    const double worst = m == k ? kv[(size_t)(k - 1)] : NAN;
+    if (!(worst == worst)) {  // filling, or NaN kept: the general rule, one loss
+      const double v = losses[i];
+      if (m < k || loss_before(v, i, worst, ki[(size_t)(k - 1)])) insert(v, i);
+      ++i;
+      continue;
+    }
+    // the kept worst is a number and every kept row precedes this chunk: a
+    // loss beats it iff it is smaller (equal ones come later, NaN never
+    // does) -- one vectorisable test per chunk, then only its hits
+    const int64_t end = std::min(n, i + kChunk);
+    bool any = false;
+    for (int64_t j = i; j < end; ++j) any |= losses[j] < worst;
+    if (any) {
+      double w = worst;
+      for (int64_t j = i; j < end; ++j) {
+        if (losses[j] < w) {
+          insert(losses[j], j);
+          w = kv[(size_t)(k - 1)];
+        }
+      }
+    }
+    i = end;
   }
   std::sort(ki.begin(), ki.end());
   std::copy(ki.begin(), ki.end(), out);

@@ -259,6 +259,8 @@ class DeviceHistory:
         # the new rows, label-major, through a pinned staging buffer: one
         # async upload on torch's current stream (the level's), then one
         # strided device copy per array into columns r0..r0+k -- no host wait
+        # (hipMemcpy2DAsync straight into the columns: ~0.3 ms more per
+        # suggest on the GPU, measured)
         nl = self.n_labels
         nv = nl * k * 8
         need = nv + nl * k
@@ -272,6 +274,7 @@ class DeviceHistory:
         st = self._stage.numpy()
         np.copyto(st[:nv].view(np.float64).reshape(nl, k), np.where(active, vals, 0.0).T)
         np.copyto(st[nv:need].reshape(nl, k), active.T)
+        sp = t.cuda.current_stream(self.device).cuda_stream
         dev = self._stage[:need].to(self.device, non_blocking=True)
         self.vals[:, r0:r0 + k].copy_(dev[:nv].view(t.float64).view(nl, k))
         self.active[:, r0:r0 + k].copy_(dev[nv:need].view(nl, k))
@@ -280,9 +283,7 @@ class DeviceHistory:
             L.hip_check(hip.hipEventCreateWithFlags(ctypes.byref(ev), L.EVENT_NO_TIMING),
                         "hipEventCreateWithFlags")
             self._stage_ev = ev
-        L.hip_check(hip.hipEventRecord(self._stage_ev,
-                                       t.cuda.current_stream(self.device).cuda_stream),
-                    "hipEventRecord")
+        L.hip_check(hip.hipEventRecord(self._stage_ev, sp), "hipEventRecord")
         self.active_host[r0:r0 + k] = active
         self.n_active += active.sum(0)
         self.rows += k

@@ -227,7 +227,10 @@ def split_masks(hist, gamma, gamma_cap=DEFAULT_LF):
     T = hist.losses.size
     n_below = min(int(np.ceil(gamma * np.sqrt(T))), gamma_cap)
     below_rows = _smallest_rows(hist.losses, n_below)
-    if hist.obs_tids.size == T and np.array_equal(hist.obs_tids, hist.tids):
+    # (a columnar history over cached rows without from_tid rows needs no compare)
+    same = hist.col is not None and hist.col.n_alias == 0 and hist.tids.size == T and \
+        hist.obs_tids.size == T
+    if same or (hist.obs_tids.size == T and np.array_equal(hist.obs_tids, hist.tids)):
         isb = np.zeros(T, bool)  # no from_tid aliasing: rows are the tids
         isb[below_rows] = True
         return isb, ~isb
@@ -361,7 +364,12 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
     live = []
     if n_ei > 0:
         eng = engine()
+        hm = eng.host_marks  # (diagnostic phase marks, Engine.host_marks)
+        if hm is not None:
+            hm.append(("suggest:split", time.perf_counter()))
         obs = LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY)
+        if hm is not None:
+            hm.append(("suggest:inputs", time.perf_counter()))
         while True:
             live = domain.reachable(walk)
             level = [lab for lab in live if lab not in walk]
@@ -390,6 +398,8 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
                 values = [r.value for r in res]
             for lab, v in zip(level, values):
                 walk[lab], stored[lab] = _decode(domain.specs[lab], v)
+            if hm is not None:
+                hm.append(("suggest:decoded", time.perf_counter()))
     live = set(live)
     misc = {"tid": first_new_id, "cmd": domain.cmd, "workdir": domain.workdir,
             "idxs": {lab: ([first_new_id] if lab in live else []) for lab in labels},
