@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -73,6 +73,7 @@ OP_CODES["tpe_band_rescore"] = OP_STREAM_SYNC + 4
 OP_CODES["tpe_fit_sorted"] = OP_STREAM_SYNC + 5
 OP_CODES["tpe_history_order"] = OP_STREAM_SYNC + 6
 OP_CODES["tpe_categorical_suggest"] = OP_STREAM_SYNC + 7
+OP_CODES["tpe_cat_posterior_hist"] = OP_STREAM_SYNC + 8
 PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
     PRIOR_CATEGORICAL = range(6)
 
@@ -94,6 +95,8 @@ _SIGNATURES = {
     "tpe_score_sorted": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
                               _P]),
     "tpe_cat_posterior": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
+    "tpe_cat_posterior_hist": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _I, _P, _P, _P, _P,
+                                    _P]),
     "tpe_gather_obs": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _P, _P, _P, _P]),
     "tpe_gather_obs_multi": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P]),
     "tpe_table_partials": (_I64, [_P, _I]),

@@ -77,13 +77,165 @@ constexpr int kCatWaves = kCatBS / kWave;
 
 // Weighted counts, one wave per (segment, category): np.bincount's sum
 // (pyll/base.py:1053-1060) adds the LF weights of a category's observations
-// sequentially in observation order, so the fp64 chain itself cannot be
-// split.  The wave scans 64 observations per step, ballots the matches, and
-// every matching lane writes its weight (computed in parallel) into the
-// wave's LDS list at its rank; when the list fills, lane 0 folds it into the
-// running count in list order -- the only serial work left is one fp64 add
-// per match.
-constexpr int kCatList = 512;  // weights buffered per wave before a fold
+// sequentially in observation order, fl(..fl(fl(c + w0) + w1)..), and the
+// result must be that chain's bits.  The wave scans 64 observations per
+// step, ballots the matches, and every matching lane writes its weight
+// (computed in parallel) into the wave's LDS list at its rank; a full list
+// is folded into the running count by seq_fold below -- the same bits as the
+// serial chain, in a few wave-wide passes instead of one fp64 add latency
+// per match (a 60 000-match category: ~0.45 ms serially).
+constexpr int kCatList = 1024;  // weights buffered per wave before a fold
+constexpr int kSE = 8;  // list entries per lane in seq_fold (64 * kSE per call)
+constexpr int kFoldN = kSE * kWave;
+
+// The sequential fp64 sum S_{k+1} = fl(S_k + w_k) over list[0, n), wave-
+// parallel and bit-exact (every lane returns it).  While S stays in one
+// binade [2^e, 2^(e+1)) its values are A * u (u = 2^(e-52), A < 2^53 an
+// integer) and each step adds d_k * u with d_k = w_k / u rounded to an
+// integer -- nearest, ties to the even A_{k+1} (IEEE round-to-nearest-even
+// on the binade's grid).  d_k is a shift of w_k's mantissa except at a tie
+// (remainder exactly u/2), where it depends on the parity of A_k; parities
+// compose as maps P -> a P ^ c (a tie: P -> 0, else P -> P ^ (d_k & 1)), so
+// one wave scan of those maps and one of the d_k give every A_k.  The first
+// step whose A would reach 2^53 (the next binade, where the grid is 2u), or
+// whose w_k is at least 2^(e+1), is taken by the hardware add from its exact
+// predecessor, and the pass repeats from the step after it.  Passes: one
+// per list plus one per binade crossed.  (Checked against the serial chain
+// on LF ramps, dyadic tie-heavy weights and 24-decade ranges:
+// tests/test_seq_fold.py restates it on the host; the GPU tests compare the
+// counts with np.bincount's.)
+// wave scans by DPP (row shifts, then the row broadcasts of 15 and 31):
+// lanes whose source is outside the wave keep `old`, the scan's identity
+template <int CTRL, int ROWM>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWM, 0xF, false);
+}
+template <int CTRL, int ROWM>
+__device__ __forceinline__ void scan_step_u64(uint64_t& v) {
+  const uint32_t lo = dpp_u32<CTRL, ROWM>(0u, (uint32_t)v);
+  const uint32_t hi = dpp_u32<CTRL, ROWM>(0u, (uint32_t)(v >> 32));
+  v += ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_incl_sum_u64(uint64_t v) {
+  scan_step_u64<0x111, 0xF>(v);  // row_shr:1
+  scan_step_u64<0x112, 0xF>(v);  // row_shr:2
+  scan_step_u64<0x114, 0xF>(v);  // row_shr:4
+  scan_step_u64<0x118, 0xF>(v);  // row_shr:8
+  scan_step_u64<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  scan_step_u64<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+// parity maps P -> a P ^ c packed as a | c << 1; y (earlier) then x
+__device__ __forceinline__ uint32_t map_then(uint32_t y, uint32_t x) {
+  const uint32_t a2 = x & 1u, c2 = (x >> 1) & 1u;
+  return (a2 & y & 1u) | ((((a2 & (y >> 1)) ^ c2) & 1u) << 1);
+}
+template <int CTRL, int ROWM>
+__device__ __forceinline__ void scan_step_map(uint32_t& x) {
+  x = map_then(dpp_u32<CTRL, ROWM>(1u, x), x);  // (1: the identity map)
+}
+
+__device__ double seq_fold(double S, const double* list, int n, int lane) {
+  double v[kSE];
+#pragma unroll
+  for (int j = 0; j < kSE; ++j) {
+    const int i = lane * kSE + j;
+    v[j] = i < n ? list[i] : 0.0;
+  }
+  constexpr uint64_t kFrac = (1ull << 52) - 1, kTop = 1ull << 53;
+  int r0 = 0;
+  while (r0 < n) {  // (wave-uniform)
+    const uint64_t sb = (uint64_t)__double_as_longlong(S);
+    const int es = (int)((sb >> 52) & 0x7ff);
+    if (S == 0.0 || es == 0) {  // 0 + w = w; a subnormal sum (never on the LF ramp): one add
+      S = __dadd_rn(S, list[r0]);
+      ++r0;
+      continue;
+    }
+    const uint64_t A = (sb & kFrac) | (1ull << 52);
+    uint64_t d[kSE];
+    uint32_t tie = 0, huge = 0;
+#pragma unroll
+    for (int j = 0; j < kSE; ++j) {
+      d[j] = 0;
+      const int i = lane * kSE + j;
+      if (i < r0 || i >= n) continue;
+      const uint64_t wb = (uint64_t)__double_as_longlong(v[j]);
+      const int ew = (int)((wb >> 52) & 0x7ff);
+      const uint64_t M = (wb & kFrac) | (ew ? (1ull << 52) : 0ull);
+      const int sh = es - max(ew, 1);
+      if (sh < 0) {
+        huge |= 1u << j;
+      } else if (sh == 0) {
+        d[j] = M;
+      } else if (sh < 64) {
+        const uint64_t rem = M & ((1ull << sh) - 1), half = 1ull << (sh - 1);
+        d[j] = (M >> sh) + (rem > half ? 1ull : 0ull);
+        if (rem == half) tie |= 1u << j;
+      }
+    }
+    // parity maps (bit 0: a, bit 1: c), composed over the lane, then an
+    // inclusive wave scan (later o earlier: a = a2 a1, c = a2 c1 ^ c2)
+    uint32_t a = 1, c = 0;
+#pragma unroll
+    for (int j = 0; j < kSE; ++j) {
+      if ((tie >> j) & 1u) {
+        a = 0;
+        c = 0;
+      } else {
+        c ^= (uint32_t)(d[j] & 1ull);
+      }
+    }
+    uint32_t x = a | (c << 1);
+    scan_step_map<0x111, 0xF>(x);
+    scan_step_map<0x112, 0xF>(x);
+    scan_step_map<0x114, 0xF>(x);
+    scan_step_map<0x118, 0xF>(x);
+    scan_step_map<0x142, 0xA>(x);
+    scan_step_map<0x143, 0xC>(x);
+    const uint32_t ex = dpp_u32<0x138, 0xF>(1u, x);  // wave_shr:1 (lane 0: the identity)
+    uint32_t P = ((ex & 1u) & (uint32_t)(A & 1ull)) ^ (ex >> 1);
+    uint64_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < kSE; ++j) {
+      if ((tie >> j) & 1u) {
+        d[j] += (P + d[j]) & 1ull;  // ties to the even A_{k+1}
+        P = 0;
+      } else {
+        P ^= (uint32_t)(d[j] & 1ull);
+      }
+      tot += d[j];
+    }
+    const uint64_t incl = wave_incl_sum_u64(tot);
+    // the first step leaving the binade
+    uint64_t cum = incl - tot;
+    int jc = -1;
+#pragma unroll
+    for (int j = 0; j < kSE; ++j) {
+      if (jc < 0) {
+        if (((huge >> j) & 1u) || A + cum + d[j] >= kTop) jc = j;
+        else cum += d[j];
+      }
+    }
+    const uint64_t bal = __ballot(jc >= 0);
+    auto lane_u64 = [](uint64_t v, int l) {
+      return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    };
+    if (bal == 0) {
+      const uint64_t Dt = lane_u64(incl, kWave - 1);
+      S = ldexp((double)(A + Dt), es - 1075);
+      r0 = n;
+    } else {
+      const int L = __ffsll((unsigned long long)bal) - 1;
+      const int g = L * kSE + __builtin_amdgcn_readlane(jc, L);
+      const uint64_t Dx = lane_u64(cum, L);
+      S = __dadd_rn(ldexp((double)(A + Dx), es - 1075), list[g]);
+      r0 = g + 1;
+    }
+  }
+  return S;
+}
 
 __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict__ obs,
                                                        const tpe_cat_seg* __restrict__ segs,
@@ -104,37 +256,36 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
   int filled = 0;
   auto fold = [&]() {
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-      // kFoldB weights read together (one LDS latency per batch, not per add),
-      // then added in list order: the fp64 add chain is the only serial part
-      constexpr int kFoldB = 32;
-      int j = 0;
-      for (; j + kFoldB <= filled; j += kFoldB) {
-        double v[kFoldB];
-#pragma unroll
-        for (int i = 0; i < kFoldB; ++i) v[i] = list[j + i];
-#pragma unroll
-        for (int i = 0; i < kFoldB; ++i) cnt = __dadd_rn(cnt, v[i]);
-      }
-      for (; j < filled; ++j) cnt = __dadd_rn(cnt, list[j]);
-    }
+    for (int f = 0; f < filled; f += kFoldN) cnt = seq_fold(cnt, list + f, min(kFoldN, filled - f), lane);
     filled = 0;
     __builtin_amdgcn_wave_barrier();
   };
-  constexpr int kDepth = 32;  // tiles of 64 observations in flight per step (latency-bound scan)
+  // kDepth tiles of 64 observations per step, the next step's loads issued
+  // before this step's matches are listed (a latency-bound scan); the list
+  // holds a whole step, so it is folded only between steps
+  constexpr int kDepth = 16;
+  static_assert(kDepth * kWave <= kCatList, "a step's matches fit the list");
+  const int64_t* O = obs + S.obs_off;
+  int64_t nxt[kDepth];
+#pragma unroll
+  for (int b = 0; b < kDepth; ++b) {
+    const int i = b * kWave + lane;
+    nxt[b] = i < n ? O[i] : -1;
+  }
   for (int t0 = 0; t0 < n; t0 += kDepth * kWave) {
     int64_t cur[kDepth];
 #pragma unroll
     for (int b = 0; b < kDepth; ++b) {
-      const int i = t0 + b * kWave + lane;
-      cur[b] = i < n ? obs[S.obs_off + i] : -1;
+      cur[b] = nxt[b];
+      const int i = t0 + (kDepth + b) * kWave + lane;
+      nxt[b] = i < n ? O[i] : -1;
     }
+    if (filled + kDepth * kWave > kCatList) fold();
 #pragma unroll
     for (int b = 0; b < kDepth; ++b) {
       const bool hit = cur[b] == (int64_t)k;
       const uint64_t m = __ballot(hit);
       if (m == 0) continue;  // wave-uniform
-      if (filled + kWave > kCatList) fold();
       if (hit) {
         const int64_t i = t0 + b * kWave + lane;
         double wt = 1.0;
@@ -150,6 +301,122 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
   }
   fold();
   if (lane == 0) {
+    double pseudo;
+    if (S.mode == 0) {
+      pseudo = cnt + S.prior_weight;  // tpe.py:589
+    } else {
+      const double pk = p[S.prior_p_off + k];
+      pseudo = cnt + (double)S.n_cat * (S.prior_weight * pk);  // tpe.py:603
+    }
+    p[S.p_off + k] = pseudo;
+  }
+}
+
+// The same counts read straight from the HBM history (the gathered lists'
+// work folded in): one 1024-thread block per (segment, category) walks the
+// rows in windows of kCHW (row order = tid order, as tpe_gather_obs lists
+// them), a row being an observation of the segment when the label is active
+// there and the row is on the segment's side of the split.  One block scan
+// of the packed (observations << 16 | matches) counts per (tile, wave) gives
+// every observation its position in the segment -- its LF weight -- and
+// every match its rank in the window; the window's match weights go to LDS in
+// order and wave 0 folds them (seq_fold).  A segment whose observation count
+// differs from S.n_obs sets bit 4 of *err (tpe_gather_obs' rule).
+constexpr int kCHB = 1024;             // block
+constexpr int kCHT = 8;                // rows per thread per window
+constexpr int kCHW = kCHB * kCHT;      // rows per window
+constexpr int kCHWaves = kCHB / kWave;
+constexpr int kCHSlots = kCHT * kCHWaves;  // (tile, wave) counts per window
+static_assert(kCHSlots == 2 * kWave, "the slot scan: two slots per lane of wave 0");
+static_assert(kCHW < (1 << 16), "packed 16-bit counts");
+
+__global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
+    const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
+    const int32_t* __restrict__ rows, int64_t n_rows, const uint8_t* __restrict__ is_below,
+    const tpe_gather* __restrict__ gathers, const tpe_cat_seg* __restrict__ segs,
+    double* __restrict__ p, int32_t* __restrict__ err) {
+  __shared__ double s_w[kCHW];
+  __shared__ uint32_t s_slot[kCHSlots];
+  __shared__ uint32_t s_tot;
+  const tpe_cat_seg S = segs[blockIdx.y];
+  const int k = blockIdx.x;
+  if (k >= S.n_cat) return;  // (block-uniform)
+  const tpe_gather G = gathers[blockIdx.y];
+  const double* __restrict__ V = vals + (int64_t)G.col * ld;
+  const uint8_t* __restrict__ Ac = active + (int64_t)G.col * ld;
+  const uint8_t side = G.below ? 1 : 0;
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int n = S.n_obs;
+  const bool ramp = S.lf > 0 && S.lf < n;
+  const int64_t num = n - S.lf;
+  const double start = 1.0 / (double)n;
+  const double step = (ramp && num > 1) ? (1.0 - start) / (double)(num - 1) : 0.0;
+  double cnt = 0.0;   // (wave 0)
+  int64_t carry = 0;  // observations before the window
+  for (int64_t p0 = 0; p0 < n_rows; p0 += kCHW) {
+    bool mem[kCHT], hit[kCHT];
+#pragma unroll
+    for (int t = 0; t < kCHT; ++t) {
+      const int64_t i = p0 + (int64_t)t * kCHB + threadIdx.x;
+      mem[t] = hit[t] = false;
+      if (i < n_rows) {
+        const int64_t r = rows ? (int64_t)rows[i] : i;
+        const bool a = Ac[r] != 0;
+        const double v = V[r];  // (read unconditionally: one latency, not two)
+        mem[t] = a && is_below[i] == side;
+        hit[t] = mem[t] && (int64_t)v - G.offset == (int64_t)k;
+      }
+    }
+    uint32_t pre[kCHT];  // this lane's packed (observations, matches) before it in its tile-wave
+#pragma unroll
+    for (int t = 0; t < kCHT; ++t) {
+      const uint64_t bm = __ballot(mem[t]), bh = __ballot(hit[t]);
+      pre[t] = ((uint32_t)__popcll(bm & lt) << 16) | (uint32_t)__popcll(bh & lt);
+      if (lane == 0) s_slot[t * kCHWaves + wid] = ((uint32_t)__popcll(bm) << 16) |
+                                                  (uint32_t)__popcll(bh);
+    }
+    __syncthreads();
+    // exclusive scan of the slots (tile-major, then wave: row order) on
+    // wave 0, two slots per lane
+    if (wid == 0) {
+      const uint32_t c0 = s_slot[2 * lane], c1 = s_slot[2 * lane + 1];
+      uint32_t incl = c0 + c1;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o, kWave);
+        if (lane >= o) incl += y;
+      }
+      const uint32_t ex = incl - (c0 + c1);
+      s_slot[2 * lane] = ex;
+      s_slot[2 * lane + 1] = ex + c0;
+      if (lane == kWave - 1) s_tot = incl;
+    }
+    __syncthreads();
+    const uint32_t tot = s_tot;
+#pragma unroll
+    for (int t = 0; t < kCHT; ++t) {
+      if (hit[t]) {
+        const uint32_t ex = s_slot[t * kCHWaves + wid] + pre[t];
+        const int64_t pos = carry + (int64_t)(ex >> 16);
+        double wt = 1.0;
+        if (ramp && pos < num) {
+          if (num == 1) wt = start;
+          else if (pos == num - 1) wt = 1.0;
+          else wt = __dadd_rn(__dmul_rn((double)pos, step), start);
+        }
+        s_w[ex & 0xffffu] = wt;
+      }
+    }
+    __syncthreads();
+    const int nh = (int)(tot & 0xffffu);
+    if (wid == 0)
+      for (int f = 0; f < nh; f += kFoldN) cnt = seq_fold(cnt, s_w + f, min(kFoldN, nh - f), lane);
+    carry += (int64_t)(tot >> 16);
+    __syncthreads();  // (s_w, s_slot reused)
+  }
+  if (threadIdx.x == 0) {
+    if (carry != (int64_t)n && err) atomicOr(err, 4);
     double pseudo;
     if (S.mode == 0) {
       pseudo = cnt + S.prior_weight;  // tpe.py:589
@@ -225,4 +492,29 @@ extern "C" int tpe_cat_posterior(const int64_t* obs, const tpe_cat_seg* segs, in
   hipLaunchKernelGGL(k_cat_finalize, dim3(n_seg), dim3(kCatBS), 0, st, segs, p_pool, logp_pool,
                      cdf_pool);
   return check_launch("tpe_cat_posterior");
+}
+
+extern "C" int tpe_cat_posterior_hist(const double* vals, const uint8_t* active, int64_t ld,
+                                      const int32_t* rows, int64_t n_rows,
+                                      const uint8_t* is_below, const tpe_gather* gathers,
+                                      const tpe_cat_seg* segs, int n_seg, int max_cat,
+                                      double* p_pool, double* logp_pool, double* cdf_pool,
+                                      int32_t* err, void* stream) {
+  if (n_seg < 0 || n_rows < 0 ||
+      (n_seg > 0 && (!vals || !active || !is_below || !gathers || !segs || !p_pool ||
+                     !logp_pool || !cdf_pool))) {
+    set_error("tpe_cat_posterior_hist: bad arguments");
+    return TPE_E_ARG;
+  }
+  if (n_seg == 0) return TPE_OK;
+  if (n_seg > 65535 || max_cat < 0) {
+    set_error("tpe_cat_posterior_hist: n_seg=%d max_cat=%d", n_seg, max_cat);
+    return TPE_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_cat_counts_hist, dim3(std::max(max_cat, 1), n_seg), dim3(kCHB), 0, st,
+                     vals, active, ld, rows, n_rows, is_below, gathers, segs, p_pool, err);
+  hipLaunchKernelGGL(k_cat_finalize, dim3(n_seg), dim3(kCatBS), 0, st, segs, p_pool, logp_pool,
+                     cdf_pool);
+  return check_launch("tpe_cat_posterior_hist");
 }

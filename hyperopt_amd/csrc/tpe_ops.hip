@@ -89,6 +89,7 @@ int run_one(const tpe_op& op) {
     TPE_CALL(TPE_OP_FIT_SORTED, tpe_fit_sorted);
     TPE_CALL(TPE_OP_HISTORY_ORDER, tpe_history_order);
     TPE_CALL(TPE_OP_CATEGORICAL_SUGGEST, tpe_categorical_suggest);
+    TPE_CALL(TPE_OP_CAT_POSTERIOR_HIST, tpe_cat_posterior_hist);
 #undef TPE_CALL
     case TPE_OP_EVENT_RECORD:
       return runtime(hipEventRecord((hipEvent_t)ptr(op.a[0]),

@@ -442,6 +442,10 @@ class Engine:
         # categorical posterior + scoring on the side stream before the fit
         # (TPE_CAT_EARLY=1) or after it with the quantized labels (0)
         self.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
+        # categorical posteriors of a single-history level counted straight
+        # from the HBM history (tpe_cat_posterior_hist) instead of a gather
+        # of their lists plus tpe_cat_posterior (TPE_CAT_HIST=0)
+        self.cat_hist = os.environ.get("TPE_CAT_HIST", "1") == "1"
         # where the host issues that categorical work: "pre" (before the fit's
         # launches), "post" (after them), "late" (after the table build)
         self.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
@@ -1181,7 +1185,7 @@ class Engine:
                     None if exchange is None else
                     (int(x_comm), int(x_labels), int(x_world), x_slots.tobytes()),
                     self.side_stream, self.table_scorer, self.exact64, self.lat_prefix,
-                    self.cat_early, self.cat_issue,
+                    self.cat_early, self.cat_issue, self.cat_hist,
                     "off" if timers is None else
                     ("all" if timer_groups is None else frozenset(timer_groups)))
         band_jobs = []  # (first, end) job positions scored by tpe_score_table_fast
@@ -1339,6 +1343,13 @@ class Engine:
         # stream starts with the fit
         gather_side = hist_mode and histories is None and sorted_fit and \
             side is not None and bool(cat) and self.cat_early
+        # the categorical posteriors can count their labels in the history
+        # itself (no gathered lists): the gather then lists only the fit's
+        # sets, and none with the sorted fit (it reads the history itself)
+        cat_hist = hist_mode and histories is None and bool(cat) and self.cat_hist
+        g0 = nfs if sorted_fit else 0
+        g1 = nfs if cat_hist else (len(g_arr) if g_arr is not None else 0)
+        # (the categorical descriptors follow the fit's)
         if hist_mode:
             d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
             d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
@@ -1346,16 +1357,15 @@ class Engine:
             if gather_side:
                 stream_order("uploaded", sp, side_p)
             e0 = tick("gather", gs)
-            g0 = nfs if sorted_fit else 0  # (the sorted fit reads the history itself)
             if histories is None:
-                if len(g_arr) > g0:
+                if g1 > g0:
                     L.check(lib.tpe_gather_obs(history.vals.data_ptr(),
                                                history.active.data_ptr(), history.ld,
                                                base + o_rows if o_rows is not None else None,
                                                _V("n_rows", n_rows), base + o_isb,
                                                base + o_g + g0 * L.GATHER_DTYPE.itemsize,
                                                g_arr.ctypes.data + g0 * L.GATHER_DTYPE.itemsize,
-                                               len(g_arr) - g0, d_obs, d_cobs, d_err, gsp),
+                                               g1 - g0, d_obs, d_cobs, d_err, gsp),
                             "tpe_gather_obs")
             else:
                 L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
@@ -1399,9 +1409,17 @@ class Engine:
         def cat_fit():  # on the side stream (after its fork)
             e0 = tick("cat_fit", side)
             d_p = base + o_p  # the posterior is formed in place in the staged pool
-            L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
-                                          int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
-                                          side_p), "tpe_cat_posterior")
+            if cat_hist:  # (the categorical gather descriptors follow the fit's nfs)
+                L.check(lib.tpe_cat_posterior_hist(
+                    history.vals.data_ptr(), history.active.data_ptr(), history.ld,
+                    base + o_rows if o_rows is not None else None, _V("n_rows", n_rows),
+                    base + o_isb, base + o_g + nfs * L.GATHER_DTYPE.itemsize, d_csegs,
+                    len(csegs), int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, d_err, side_p),
+                    "tpe_cat_posterior_hist")
+            else:
+                L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
+                                              int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
+                                              side_p), "tpe_cat_posterior")
             tock("cat_fit", e0, side)
 
         def launch_group(g, stage):
@@ -1947,8 +1965,8 @@ class _Replay(object):
         return (stream, works.key, float(prior_weight), int(lf), int(precision), scorer, pruned,
                 history.vals.data_ptr(), history.active.data_ptr(), history.ld,
                 exchange, eng.side_stream, eng.table_scorer, eng.exact64, eng.lat_prefix,
-                eng.cat_early, eng.cat_issue, eng.device_events, eng.sorted_fit,
-                "off" if timers is None else
+                eng.cat_early, eng.cat_issue, eng.cat_hist, eng.device_events,
+                eng.sorted_fit, "off" if timers is None else
                 ("all" if timer_groups is None else frozenset(timer_groups)))
 
     def _put(self, name, arr):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 18
+#define TPE_ABI_VERSION 19
 
 enum {
   TPE_OK = 0,
@@ -264,6 +264,21 @@ int tpe_mixture_prepare(tpe_seg* segs, int n_seg, int max_comp, void* scratch, d
  * max_cat: the largest n_cat over segs (host value, sizes the grid). */
 int tpe_cat_posterior(const int64_t* obs, const tpe_cat_seg* segs, int n_seg, int max_cat,
                       double* p_pool, double* logp_pool, double* cdf_pool, void* stream);
+
+/* The same posteriors read straight from an HBM-resident history (the
+ * arguments of tpe_gather_obs below): segment i's observations are the rows
+ * of column gathers[i].col active there and on side gathers[i].below of the
+ * split (is_below; rows: optional row list), in row order, their category
+ * (int64)value - gathers[i].offset -- the lists tpe_gather_obs would write,
+ * counted without writing them.  gathers: device array aligned with segs
+ * (obs_off unused).  An observation count other than segs[i].n_obs sets bit
+ * 4 of *err.  Replaces tpe_gather_obs + tpe_cat_posterior for the
+ * categorical labels of a level (tpe.py:578-615, pyll/base.py:1053-1060). */
+int tpe_cat_posterior_hist(const double* vals, const uint8_t* active, int64_t ld,
+                           const int32_t* rows, int64_t n_rows, const uint8_t* is_below,
+                           const struct tpe_gather* gathers, const tpe_cat_seg* segs, int n_seg,
+                           int max_cat, double* p_pool, double* logp_pool, double* cdf_pool,
+                           int32_t* err, void* stream);
 
 /* ---- continuous candidates: sample (or read) + score + argmax ------------
  * Replaces GMM1/LGMM1 sampling (tpe.py:79-106, 229-257), GMM1_lpdf /
@@ -620,6 +635,7 @@ enum {
   TPE_OP_FIT_SORTED,           /* tpe_fit_sorted                             */
   TPE_OP_HISTORY_ORDER,        /* tpe_history_order                          */
   TPE_OP_CATEGORICAL_SUGGEST,  /* tpe_categorical_suggest                    */
+  TPE_OP_CAT_POSTERIOR_HIST,   /* tpe_cat_posterior_hist                     */
   TPE_OP_COUNT
 };
 #define TPE_OP_ARGS 23

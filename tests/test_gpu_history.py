@@ -96,16 +96,54 @@ def test_history_posterior_matches_oracle(engine):
             np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
 
 
-def test_history_count_mismatch_raises(engine):
+@pytest.mark.parametrize("j", [0, 4])
+def test_history_count_mismatch_raises(engine, j):
+    """A continuous (sorted fit) or categorical (tpe_cat_posterior_hist)
+    label whose host count disagrees with the rows the device finds."""
     from hyperopt_amd import _lib as L
     from hyperopt_amd.engine import DeviceHistory
     mat, active, losses = _history(500, 9)
     hist = DeviceHistory(engine, len(SPACE))
     hist.append(mat, active)
     hw, isb = _works(mat, active, losses, np.arange(500), hist=hist)
-    hw[0].n_above -= 3  # the host claims fewer rows than the gather finds
+    hw[j].n_above -= 3  # the host claims fewer rows than the device finds
     with pytest.raises(L.TpeHipError, match="counts"):
         engine.run(hw, history=hist, is_below=isb)
+
+
+@pytest.mark.parametrize("T,K", [(60000, 3), (120000, 40)])
+def test_history_categorical_counts_long(engine, T, K):
+    """Categorical posteriors counted in the HBM history (no gathered lists)
+    over long LF-ramped histories: bit-exact against np.bincount's
+    sequential sums (the oracle) and the upload path."""
+    from hyperopt_amd.engine import DeviceHistory, LabelWork
+    rng = np.random.RandomState(T + K)
+    p = rng.dirichlet(np.full(K, 0.5))
+    mat = np.stack([rng.choice(K, size=T, p=p).astype(float),
+                    (rng.choice(K, size=T, p=p) + 2).astype(float)], axis=1)
+    active = rng.uniform(size=mat.shape) >= 0.1
+    losses = rng.normal(size=T)
+    hist = DeviceHistory(engine, 2)
+    hist.append(mat, active)
+    n_below = min(int(np.ceil(0.25 * np.sqrt(T))), 25)
+    isb = np.zeros(T, np.uint8)
+    isb[np.argsort(losses, kind="stable")[:n_below]] = 1
+    specs = [("c", "categorical", (tuple(p.tolist()),)), ("r", "randint", (2, 2 + K))]
+    works = []
+    for j, (lab, kind, a) in enumerate(specs):
+        v = mat[active[:, j], j]
+        b = isb[active[:, j]] == 1
+        w = LabelWork(lab, kind, a, v[b], None, col=j, n_above=int((~b).sum()))
+        works.append(w)
+    res = engine.run(works, posteriors=True, history=hist, is_below=isb)
+    for j, (lab, kind, a) in enumerate(specs):
+        v = mat[active[:, j], j].astype(np.int64)
+        b = isb[active[:, j]] == 1
+        if kind == "categorical":
+            want = O.categorical_posterior(v[~b], 1.0, p)
+        else:
+            want = O.randint_posterior(v[~b], 1.0, 2, 2 + K)
+        np.testing.assert_array_equal(res[j].extra["p_above"], want, err_msg=lab)
 
 
 def _suggest_both(monkeypatch, trials, domain, n_ei, seed=7):

@@ -101,3 +101,22 @@ def test_p_accept_bounded(engine):
         ww, mm, ss = r.extra[half]
         ref = np.sum(ww * (O.normal_cdf(5.0, mm, ss) - O.normal_cdf(-5.0, mm, ss)))
         np.testing.assert_allclose(r.extra["p_accept"][k], ref, rtol=1e-12)
+
+
+@pytest.mark.parametrize("n,k", [(3000, 3), (60000, 3), (150000, 7), (40000, 40)])
+def test_categorical_counts_long_histories(engine, n, k):
+    """Categorical / randint pseudocounts over long LF-ramped histories (the
+    wave-parallel exact fold, tpe_fit.hip seq_fold, crossing many binades):
+    bit-exact against np.bincount's sequential sums."""
+    from hyperopt_amd.engine import LabelWork
+    rng = np.random.RandomState(n + k)
+    p = rng.dirichlet(np.full(k, 0.5))
+    below = rng.choice(k, size=25, p=p).astype(np.int64)
+    above = rng.choice(k, size=n, p=p).astype(np.int64)
+    works = [LabelWork("c", "categorical", (tuple(p.tolist()),), below, above),
+             LabelWork("r", "randint", (3, 3 + k), below + 3, above + 3)]
+    rc, rr = engine.run(works, prior_weight=1.0, posteriors=True)
+    np.testing.assert_array_equal(rc.extra["p_above"], O.categorical_posterior(above, 1.0, p))
+    np.testing.assert_array_equal(rc.extra["p_below"], O.categorical_posterior(below, 1.0, p))
+    np.testing.assert_array_equal(rr.extra["p_above"], O.randint_posterior(above + 3, 1.0, 3,
+                                                                           3 + k))
