@@ -682,7 +682,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
-        "suggest_p50_ms": float(np.median(step_times)) * 1e3,
+        "engine_step_p50_ms": float(np.median(step_times)) * 1e3,
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,

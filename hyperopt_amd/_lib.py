@@ -95,6 +95,7 @@ _SIGNATURES = {
     "tpe_score_sorted": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
                               _P]),
     "tpe_cat_posterior": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
+    "tpe_history_append": (_I, [_P, _I, _I64, _P, _P, _I64, _I64, _P]),
     "tpe_cat_posterior_hist": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _I, _P, _P, _P, _P,
                                     _P]),
     "tpe_gather_obs": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _P, _P, _P, _P]),

@@ -410,7 +410,12 @@ __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
     }
     __syncthreads();
     const int nh = (int)(tot & 0xffffu);
+#ifdef TPE_DIAG_CAT_NOFOLD  // (diagnostic builds: the scan alone)
+    if (wid == 0 && nh > 0) cnt += s_w[nh - 1];
+    if (false)
+#else
     if (wid == 0)
+#endif
       for (int f = 0; f < nh; f += kFoldN) cnt = seq_fold(cnt, s_w + f, min(kFoldN, nh - f), lane);
     carry += (int64_t)(tot >> 16);
     __syncthreads();  // (s_w, s_slot reused)

@@ -132,10 +132,40 @@ __global__ __launch_bounds__(kGBS) void k_gather_obs_multi(const tpe_history* __
   gather_one(H.vals + (int64_t)G.col * H.ld, H.active + (int64_t)G.col * H.ld, rows, H.n_rows,
              aux + H.isb_off, G, out_f, out_i, err, wsum, carry_s);
 }
+// appended rows: stage = vals (n_labels x k fp64, label-major) then the
+// active flags (n_labels x k bytes), scattered into columns r0..r0+k-1
+__global__ __launch_bounds__(256) void k_history_append(const uint8_t* __restrict__ stage,
+                                                        int n_labels, int64_t k,
+                                                        double* __restrict__ vals,
+                                                        uint8_t* __restrict__ active, int64_t ld,
+                                                        int64_t r0) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)n_labels * k) return;
+  const int64_t l = t / k, j = t % k;
+  const double* sv = reinterpret_cast<const double*>(stage);
+  const uint8_t* sa = stage + (int64_t)n_labels * k * 8;
+  vals[l * ld + r0 + j] = sv[t];
+  active[l * ld + r0 + j] = sa[t];
+}
 }  // namespace
 }  // namespace tpe
 
 using namespace tpe;
+
+extern "C" int tpe_history_append(const void* stage, int n_labels, int64_t k, double* vals,
+                                  uint8_t* active, int64_t ld, int64_t r0, void* stream) {
+  if (n_labels < 0 || k < 0 || r0 < 0 || ld < r0 + k ||
+      ((int64_t)n_labels * k > 0 && (!stage || !vals || !active))) {
+    set_error("tpe_history_append: bad arguments");
+    return TPE_E_ARG;
+  }
+  const int64_t n = (int64_t)n_labels * k;
+  if (n == 0) return TPE_OK;
+  hipLaunchKernelGGL(k_history_append, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, static_cast<const uint8_t*>(stage), n_labels, k, vals,
+                     active, ld, r0);
+  return check_launch("tpe_history_append");
+}
 
 extern "C" int tpe_gather_obs(const double* vals, const uint8_t* active, int64_t ld,
                               const int32_t* rows, int64_t n_rows, const uint8_t* is_below,

@@ -209,6 +209,7 @@ class DeviceHistory:
     def __init__(self, engine, n_labels, cap=1024):
         self.torch = engine.torch
         self.device = engine.device
+        self.lib = engine.lib
         self.n_labels = int(n_labels)
         self.rows = 0
         self.cap = 0
@@ -222,6 +223,7 @@ class DeviceHistory:
         self.active_host = np.zeros((0, self.n_labels), bool)
         self.n_active = np.zeros(self.n_labels, np.int64)
         self._stage = self._stage_ev = None  # pinned staging of appended rows, its upload event
+        self._dstage = None  # its device copy (tpe_history_append's input)
         self._grow(max(int(cap), 16))
 
     @property
@@ -257,10 +259,11 @@ class DeviceHistory:
             self._grow(max(2 * self.cap, self.rows + k))
         r0, t = self.rows, self.torch
         # the new rows, label-major, through a pinned staging buffer: one
-        # async upload on torch's current stream (the level's), then one
-        # strided device copy per array into columns r0..r0+k -- no host wait
-        # (hipMemcpy2DAsync straight into the columns: ~0.3 ms more per
-        # suggest on the GPU, measured)
+        # async upload on torch's current stream (the level's) into a device
+        # stage, then one scatter into columns r0..r0+k (tpe_history_append)
+        # -- no host wait, two runtime calls (torch's copies cost ~40 us of
+        # host time per suggest; hipMemcpy2DAsync straight into the columns
+        # ~0.3 ms more on the GPU, measured)
         nl = self.n_labels
         nv = nl * k * 8
         need = nv + nl * k
@@ -275,9 +278,13 @@ class DeviceHistory:
         np.copyto(st[:nv].view(np.float64).reshape(nl, k), np.where(active, vals, 0.0).T)
         np.copyto(st[nv:need].reshape(nl, k), active.T)
         sp = t.cuda.current_stream(self.device).cuda_stream
-        dev = self._stage[:need].to(self.device, non_blocking=True)
-        self.vals[:, r0:r0 + k].copy_(dev[:nv].view(t.float64).view(nl, k))
-        self.active[:, r0:r0 + k].copy_(dev[nv:need].view(nl, k))
+        if self._dstage is None or self._dstage.numel() < need:
+            self._dstage = t.empty(self._stage.numel(), dtype=t.uint8, device=self.device)
+        L.hip_check(hip.hipMemcpyAsync(self._dstage.data_ptr(), self._stage.data_ptr(), need, 1,
+                                       sp), "hipMemcpyAsync")
+        L.check(self.lib.tpe_history_append(self._dstage.data_ptr(), nl, k, self.vals.data_ptr(),
+                                             self.active.data_ptr(), self.ld, r0, sp),
+                "tpe_history_append")
         if self._stage_ev is None:
             ev = ctypes.c_void_p()
             L.hip_check(hip.hipEventCreateWithFlags(ctypes.byref(ev), L.EVENT_NO_TIMING),
@@ -1996,7 +2003,11 @@ class _Replay(object):
             return None
         (_, _, _, fit_ids, _, nf, segs, _, n_obs_total, n_comp, max_obs, csegs, _, _, _,
          cobs_off, _, _, _, _, _, g_arr) = eng._plan_fast(P, batch.n_below, batch.n_above)
+        if hm is not None:
+            hm.append(("replay:plan_fast", time.perf_counter()))
         jobs, _, fb_jobs = eng._jobs_fast(P, batch.keys, batch.cand_base)[:3]
+        if hm is not None:
+            hm.append(("replay:jobs", time.perf_counter()))
         pack_size = self.offs["isb"] + max(n_rows, 1)
         gen0 = eng._gen
         if pack_size > self.pinned.numel():
@@ -2006,11 +2017,15 @@ class _Replay(object):
                      n_rows if self.history is not None else 0)
         if eng._gen != gen0:
             return None
+        if hm is not None:
+            hm.append(("replay:presize", time.perf_counter()))
         if self.history is not None:  # rows appended since: merged into the sorted orders
             nfs = 2 * nf
             self.history.ensure_order(eng, eng.torch.cuda.current_stream(eng.device),
                                       g_arr["col"][:nfs:2], segs["transform"][::2],
                                       segs["floor"][::2])
+        if hm is not None:
+            hm.append(("replay:order", time.perf_counter()))
         for name, arr in (("segs", segs), ("csegs", csegs), ("g", g_arr), ("jobs", jobs),
                           ("fb", fb_jobs), ("isb", isb)):
             self._put(name, arr)

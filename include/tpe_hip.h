@@ -180,6 +180,12 @@ typedef struct tpe_gather {
   int32_t to_int;       /* 1: int64 output, 0: fp64 output                   */
   int32_t hist;         /* tpe_gather_obs_multi: index of the history (else 0) */
 } tpe_gather;
+/* Rows appended to an HBM-resident history: `stage` (device) holds the new
+ * rows' values, label-major (n_labels x k fp64), then their active flags
+ * (n_labels x k bytes); they are written to rows r0..r0+k-1 of vals / active
+ * (label-major, leading dimension ld). */
+int tpe_history_append(const void* stage, int n_labels, int64_t k, double* vals, uint8_t* active,
+                       int64_t ld, int64_t r0, void* stream);
 int tpe_gather_obs(const double* vals, const uint8_t* active, int64_t ld, const int32_t* rows,
                    int64_t n_rows, const uint8_t* is_below, const tpe_gather* gathers,
                    const tpe_gather* host_gathers, int n_gathers, double* obs_f64,

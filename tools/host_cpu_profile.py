@@ -79,7 +79,7 @@ class _Lib(object):
         self._lib = lib
 
     def __getattr__(self, name):
-        if name in L.OP_CODES or name == "tpe_run_ops":
+        if name in L.OP_CODES or name in ("tpe_run_ops", "tpe_history_append"):
             return lambda *a: 0
         return getattr(self._lib, name)
 
@@ -101,6 +101,7 @@ def make_engine():
     eng.exact64 = "auto"
     eng.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
     eng.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
+    eng.cat_hist = os.environ.get("TPE_CAT_HIST", "1") == "1"
     eng.lat_prefix = int(os.environ.get("TPE_LAT_PREFIX", str(E.LAT_PREFIX)))
     eng.device_events = True
     eng.sorted_fit = os.environ.get("TPE_SORTED_FIT", "1") == "1"
@@ -109,6 +110,7 @@ def make_engine():
     eng.native = os.environ.get("TPE_NATIVE_LAUNCH", "1") != "0"
     eng._oplists, eng._oplist_once, eng._replays, eng._staged_sig = {}, None, {}, None
     E.torch_shim = shim
+    L.hip = lambda: eng._hip  # (DeviceHistory.append's event calls)
     return eng
 
 
