@@ -85,8 +85,6 @@ constexpr int kCatWaves = kCatBS / kWave;
 // serial chain, in a few wave-wide passes instead of one fp64 add latency
 // per match (a 60 000-match category: ~0.45 ms serially).
 constexpr int kCatList = 1024;  // weights buffered per wave before a fold
-constexpr int kSE = 8;  // list entries per lane in seq_fold (64 * kSE per call)
-constexpr int kFoldN = kSE * kWave;
 
 // The sequential fp64 sum S_{k+1} = fl(S_k + w_k) over list[0, n), wave-
 // parallel and bit-exact (every lane returns it).  While S stays in one
@@ -135,6 +133,53 @@ __device__ __forceinline__ void scan_step_map(uint32_t& x) {
   x = map_then(dpp_u32<CTRL, ROWM>(1u, x), x);  // (1: the identity map)
 }
 
+// The same sum by lane 0 alone (list reads batched; every lane returns it):
+// one dependent fp64 add per entry, cheaper than seq_fold's passes while the
+// sum is small and crosses a binade every few entries (the first ~4k of a
+// chain: a pass per crossing)
+constexpr int kSerialHits = 4096;
+__device__ double serial_fold(double S, const double* list, int n, int lane) {
+  if (lane == 0) {
+    constexpr int kB = 8;
+    int j = 0;
+    for (; j + kB <= n; j += kB) {
+      double v[kB];
+#pragma unroll
+      for (int i = 0; i < kB; ++i) v[i] = list[j + i];
+#pragma unroll
+      for (int i = 0; i < kB; ++i) S = __dadd_rn(S, v[i]);
+    }
+    for (; j < n; ++j) S = __dadd_rn(S, list[j]);
+  }
+  return __shfl(S, 0, kWave);
+}
+// list[0, n) into S, the first entries of a chain (done < kSerialHits)
+// serially, the rest by seq_fold
+template <int kSE>
+__device__ double fold_list(double S, const double* list, int n, int64_t& done, int lane);
+
+// one entry's d (w / u rounded on the binade of biased exponent es, ties
+// left for the parity scan: bit j of tie), or bit j of huge (w >= 2^(e+1))
+__device__ __forceinline__ uint64_t fold_step(double w, int es, bool on, uint32_t& tie,
+                                              uint32_t& huge, int j) {
+  if (!on) return 0;
+  constexpr uint64_t kFrac = (1ull << 52) - 1;
+  const uint64_t wb = (uint64_t)__double_as_longlong(w);
+  const int ew = (int)((wb >> 52) & 0x7ff);
+  const uint64_t M = (wb & kFrac) | (ew ? (1ull << 52) : 0ull);
+  const int sh = es - max(ew, 1);
+  if (sh < 0) {
+    huge |= 1u << j;
+    return 0;
+  }
+  if (sh == 0) return M;
+  if (sh >= 64) return 0;
+  const uint64_t rem = M & ((1ull << sh) - 1), half = 1ull << (sh - 1);
+  if (rem == half) tie |= 1u << j;
+  return (M >> sh) + (rem > half ? 1ull : 0ull);
+}
+
+template <int kSE>
 __device__ double seq_fold(double S, const double* list, int n, int lane) {
   double v[kSE];
 #pragma unroll
@@ -157,22 +202,8 @@ __device__ double seq_fold(double S, const double* list, int n, int lane) {
     uint32_t tie = 0, huge = 0;
 #pragma unroll
     for (int j = 0; j < kSE; ++j) {
-      d[j] = 0;
       const int i = lane * kSE + j;
-      if (i < r0 || i >= n) continue;
-      const uint64_t wb = (uint64_t)__double_as_longlong(v[j]);
-      const int ew = (int)((wb >> 52) & 0x7ff);
-      const uint64_t M = (wb & kFrac) | (ew ? (1ull << 52) : 0ull);
-      const int sh = es - max(ew, 1);
-      if (sh < 0) {
-        huge |= 1u << j;
-      } else if (sh == 0) {
-        d[j] = M;
-      } else if (sh < 64) {
-        const uint64_t rem = M & ((1ull << sh) - 1), half = 1ull << (sh - 1);
-        d[j] = (M >> sh) + (rem > half ? 1ull : 0ull);
-        if (rem == half) tie |= 1u << j;
-      }
+      d[j] = fold_step(v[j], es, i >= r0 && i < n, tie, huge, j);
     }
     // parity maps (bit 0: a, bit 1: c), composed over the lane, then an
     // inclusive wave scan (later o earlier: a = a2 a1, c = a2 c1 ^ c2)
@@ -237,6 +268,19 @@ __device__ double seq_fold(double S, const double* list, int n, int lane) {
   return S;
 }
 
+template <int kSE>
+__device__ double fold_list(double S, const double* list, int n, int64_t& done, int lane) {
+  int f = 0;
+  if (done < kSerialHits) {
+    f = (int)std::min<int64_t>(n, kSerialHits - done);
+    S = serial_fold(S, list, f, lane);
+  }
+  constexpr int kN = kSE * kWave;
+  for (; f < n; f += kN) S = seq_fold<kSE>(S, list + f, min(kN, n - f), lane);
+  done += n;
+  return S;
+}
+
 __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict__ obs,
                                                        const tpe_cat_seg* __restrict__ segs,
                                                        double* __restrict__ p) {
@@ -254,9 +298,10 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
   const uint64_t lt = (1ull << lane) - 1ull;
   double cnt = 0.0;
   int filled = 0;
+  int64_t folded = 0;
   auto fold = [&]() {
     __builtin_amdgcn_wave_barrier();
-    for (int f = 0; f < filled; f += kFoldN) cnt = seq_fold(cnt, list + f, min(kFoldN, filled - f), lane);
+    cnt = fold_list<8>(cnt, list, filled, folded, lane);
     filled = 0;
     __builtin_amdgcn_wave_barrier();
   };
@@ -327,6 +372,8 @@ constexpr int kCHT = 8;                // rows per thread per window
 constexpr int kCHW = kCHB * kCHT;      // rows per window
 constexpr int kCHWaves = kCHB / kWave;
 constexpr int kCHSlots = kCHT * kCHWaves;  // (tile, wave) counts per window
+constexpr int kCHSE = 8;               // seq_fold entries per lane (512 per pass; wider
+                                       // passes measured slower: 16 +25 %, 32 +65 %)
 static_assert(kCHSlots == 2 * kWave, "the slot scan: two slots per lane of wave 0");
 static_assert(kCHW < (1 << 16), "packed 16-bit counts");
 
@@ -352,7 +399,8 @@ __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
   const int64_t num = n - S.lf;
   const double start = 1.0 / (double)n;
   const double step = (ramp && num > 1) ? (1.0 - start) / (double)(num - 1) : 0.0;
-  double cnt = 0.0;   // (wave 0)
+  double cnt = 0.0;     // (wave 0)
+  int64_t folded = 0;  // (wave 0) matches folded so far
   int64_t carry = 0;  // observations before the window
   for (int64_t p0 = 0; p0 < n_rows; p0 += kCHW) {
     bool mem[kCHT], hit[kCHT];
@@ -412,11 +460,9 @@ __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
     const int nh = (int)(tot & 0xffffu);
 #ifdef TPE_DIAG_CAT_NOFOLD  // (diagnostic builds: the scan alone)
     if (wid == 0 && nh > 0) cnt += s_w[nh - 1];
-    if (false)
 #else
-    if (wid == 0)
+    if (wid == 0) cnt = fold_list<kCHSE>(cnt, s_w, nh, folded, lane);
 #endif
-      for (int f = 0; f < nh; f += kFoldN) cnt = seq_fold(cnt, s_w + f, min(kFoldN, nh - f), lane);
     carry += (int64_t)(tot >> 16);
     __syncthreads();  // (s_w, s_slot reused)
   }
