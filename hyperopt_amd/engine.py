@@ -295,6 +295,7 @@ class DeviceHistory:
         self.n_active += active.sum(0)
         self.rows += k
 
+
     ORDER_CHUNK = 2048  # new rows merged per tpe_history_order call
 
     def ensure_order(self, eng, stream, cols, transforms, floors):
@@ -306,19 +307,32 @@ class DeviceHistory:
         t = self.torch
         if self.order is None:
             self.order = t.zeros((self.n_labels, self.cap), dtype=t.int32, device=self.device)
-        key = (self.rows, np.asarray(cols).tobytes(), np.asarray(transforms).tobytes(),
+        sig = (np.asarray(cols).tobytes(), np.asarray(transforms).tobytes(),
                np.asarray(floors, np.float64).tobytes())
+        key = (self.rows,) + sig
         if self.__dict__.get("_ordered") == key:
             return  # (the same columns and transforms, nothing appended since)
-        todo = {}
-        for c, tr, fl in zip(np.asarray(cols).tolist(), np.asarray(transforms).tolist(),
-                             np.asarray(floors).tolist()):
-            spec = (int(tr), float(fl))
-            if self.order_spec.get(c) != spec:
-                self.order_spec[c] = spec
-                self.order_rows[c] = 0
-            if self.order_rows[c] < self.rows:
-                todo.setdefault(self.order_rows[c], []).append((c,) + spec)
+        # (merging right after each append instead, on the GPU while the host
+        # plans the level: same-box A/B 1.050 vs 1.036 ms per drop-in suggest)
+        last = self.__dict__.get("_ordered")
+        if last is not None and last[1:] == sig and all(
+                self.order_rows.get(c) == last[0] for c in self.__dict__["_order_cols"]):
+            # (the same columns and specs as last time, every one at its rows)
+            todo = {last[0]: self._order_specs}
+        else:
+            todo = {}
+            specs_all = []
+            for c, tr, fl in zip(np.asarray(cols).tolist(), np.asarray(transforms).tolist(),
+                                 np.asarray(floors).tolist()):
+                spec = (int(tr), float(fl))
+                specs_all.append((c,) + spec)
+                if self.order_spec.get(c) != spec:
+                    self.order_spec[c] = spec
+                    self.order_rows[c] = 0
+                if self.order_rows[c] < self.rows:
+                    todo.setdefault(self.order_rows[c], []).append((c,) + spec)
+            self._order_specs = specs_all
+            self._order_cols = [x[0] for x in specs_all]
         if not todo:
             return
         lib = eng.lib
