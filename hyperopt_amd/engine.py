@@ -196,6 +196,15 @@ class _Pack:
         return off
 
 
+def _knob(name, default):
+    """A level-launcher switch kept for A/B runs: the product
+    path takes ``default``; an environment override is read only when
+    TPE_DIAG=1 (diagnostic runs)."""
+    if os.environ.get("TPE_DIAG") == "1":
+        return os.environ.get(name, default)
+    return default
+
+
 class DeviceHistory:
     """A trials x labels history resident in HBM, appended in place.
 
@@ -450,40 +459,40 @@ class Engine:
         # -11% at an 8-way label share (tools/rank_share.py).
         # "1": join at the end of the level; "2": the table scorer waits for
         # the side stream; "0": everything on the caller's stream
-        self.side_stream = os.environ.get("TPE_SIDE_STREAM", "1")
+        self.side_stream = _knob("TPE_SIDE_STREAM", "1")
         self._side = None
         # sampled table jobs without per-candidate outputs: "cubic" scores
         # each candidate by its cell's score cubic (tpe_score_table_fast);
         # "poly" evaluates both cell polynomials (tpe_score_table)
-        self.table_scorer = os.environ.get("TPE_TABLE_SCORER", "cubic")
+        self.table_scorer = _knob("TPE_TABLE_SCORER", "cubic")
         # fp64 continuous labels: "auto" prunes components (tpe_score_pruned64)
         # once the above mixture has PRUNED64_MIN_COMP components, "dense"
         # always sums every component (tpe_score_continuous), "pruned" always prunes
-        self.exact64 = os.environ.get("TPE_EXACT64", "auto")
+        self.exact64 = _knob("TPE_EXACT64", "auto")
         # categorical posterior + scoring on the side stream before the fit
         # (TPE_CAT_EARLY=1) or after it with the quantized labels (0)
-        self.cat_early = os.environ.get("TPE_CAT_EARLY", "1") == "1"
+        self.cat_early = _knob("TPE_CAT_EARLY", "1") == "1"
         # categorical posteriors of a single-history level counted straight
         # from the HBM history (tpe_cat_posterior_hist) instead of a gather
         # of their lists plus tpe_cat_posterior (TPE_CAT_HIST=0)
-        self.cat_hist = os.environ.get("TPE_CAT_HIST", "1") == "1"
+        self.cat_hist = _knob("TPE_CAT_HIST", "1") == "1"
         # where the host issues that categorical work: "pre" (before the fit's
         # launches), "post" (after them), "late" (after the table build)
-        self.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
+        self.cat_issue = _knob("TPE_CAT_ISSUE", "post")
         # quantized labels of a suggest level: decide the argmax after the first
         # lat_prefix candidates where no unseen lattice value can still win
         # (tpe_lattice_suggest); 0 (TPE_LAT_PREFIX=0): every stream drawn in full
-        self.lat_prefix = _lat_prefix(os.environ.get("TPE_LAT_PREFIX", str(LAT_PREFIX)))
+        self.lat_prefix = _lat_prefix(_knob("TPE_LAT_PREFIX", str(LAT_PREFIX)))
         # stream-ordering events (one stream of this device waits for another)
         # without the system-scope fence: a device-scope release is all a
         # consumer on the same GPU needs, and the system-scope one writes back
         # the L2s (~14 us of idle GPU per event on C3 levels).  The host-read
         # "result" event keeps it.  TPE_DEVICE_EVENTS=0: every event system-scope.
-        self.device_events = os.environ.get("TPE_DEVICE_EVENTS", "1") == "1"
+        self.device_events = _knob("TPE_DEVICE_EVENTS", "1") == "1"
         # the fit from the history's sorted orders (tpe_fit_sorted) where the
         # level reads one history with its identity row list; "0": the
         # gather + sort + merge fit (tpe_parzen_fit) everywhere
-        self.sorted_fit = os.environ.get("TPE_SORTED_FIT", "1") == "1"
+        self.sorted_fit = _knob("TPE_SORTED_FIT", "1") == "1"
         self._last_gkey = None  # launch key of the previous eager level
         self._gen = 0           # bumped whenever a workspace buffer is (re)allocated
         self.graph_stats = {"eager": 0}  # levels issued eagerly / re-issued ("native", "replay")
@@ -492,7 +501,7 @@ class Engine:
         # call's is recorded once as tpe_run_ops records -- upload, every
         # launch, stream fork/join, readback and the final synchronise -- and
         # re-issued with one C call per level (hyperopt_amd/csrc/tpe_ops.hip)
-        self.native = os.environ.get("TPE_NATIVE_LAUNCH", "1") != "0"
+        self.native = _knob("TPE_NATIVE_LAUNCH", "1") != "0"
         self._oplists = {}      # launch key -> _OpList
         self._oplist_once = None
         self._replays = {}      # signature -> _Replay of a recorded WorkBatch level

@@ -2,7 +2,7 @@
 listed cells the select kernel leaves (library built with
 TPE_DIAG_BAND_KEEP, tools/diag_variants.sh), and the scorer's raw entries.
 
-    TPE_NATIVE_LAUNCH=0 HYPEROPT_AMD_LIB=tools/_variants/lib_BAND_KEEP.so python tools/band_probe.py
+    TPE_DIAG=1 TPE_NATIVE_LAUNCH=0 HYPEROPT_AMD_LIB=tools/_variants/lib_BAND_KEEP.so python tools/band_probe.py
 """
 import ctypes
 import os
