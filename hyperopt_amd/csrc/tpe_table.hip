@@ -1814,7 +1814,12 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
 #define TPE_BAND_BLOCKS 16
 #endif
 constexpr int kBandBlocks = TPE_BAND_BLOCKS;  // blocks per job
-constexpr int kBandSurv = 128;       // survivors scored directly (more: the cell expansions)
+constexpr int kBandSurv = 128;       // survivors a job may score directly
+#ifndef TPE_BAND_DIRECT
+#define TPE_BAND_DIRECT 16
+#endif
+constexpr int kBandDirect = TPE_BAND_DIRECT;  // ... and always does; more take the cell
+                                              // expansions where the cells can hold them
 #ifndef TPE_SURV_BATCH
 #define TPE_SURV_BATCH 8
 #endif
@@ -1857,7 +1862,7 @@ struct BandWork {  // per job (tpe_band_bytes)
   float sy[kBandSurvMax];                         // the survivors (flat entry order): y ...
   int64_t sidx[kBandSurvMax];                     // ... and candidate index
   int cells[kBandCells];                          // the listed cells (ascending)
-  int ns, ncell, over, pad0;                      // survivors, cells, job overflowed
+  int ns, ncell, over, direct;                    // survivors, cells, job overflowed, path
   long long tmark[16];                            // (TPE_BAND_TIMING diagnostic builds)
   BestT win[kBandBlocks];                         // k_band_final's per-block winners (k_band_pick)
   unsigned int done;                              // (unused)
@@ -2244,11 +2249,19 @@ __global__ __launch_bounds__(kBX) void k_band(
   }
   __syncthreads();
   TMARK(2)
-  const bool over = ns > kBandSurv && (ncell > kBandCells || s_off || ns > kBandSurvMax);
+  // the path: a few survivors are summed directly; more take the cell
+  // expansions (their cost does not grow with the survivors: ~12 us against
+  // ~5 us per 8 direct survivors), up to kBandSurv directly when the cells
+  // cannot hold them (too many, or survivors off the grid); else the exact
+  // fallback
+  const bool cells_ok = ncell <= kBandCells && !s_off && ns <= kBandSurvMax;
+  const bool direct = ns <= kBandDirect || (ns <= kBandSurv && !cells_ok);
+  const bool over = !direct && !cells_ok;
   if (kb == 0 && threadIdx.x == 0) {
     W.ns = ns;
     W.ncell = min(ncell, kBandCells);
     W.over = over;
+    W.direct = direct;
   }
   if (over) {
     // many survivors, off the grid or over too many cells: the exact fallback
@@ -2265,7 +2278,7 @@ __global__ __launch_bounds__(kBX) void k_band(
   }
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const bool lgmm = J.family == TPE_LGMM1;
-  if (ns <= kBandSurv) {
+  if (direct) {
     // ---- 3a. direct: this block's component chunk, for every survivor ----
     for (int mix = 0; mix < 2; ++mix) {
       const tpe_seg& S = mix ? SA : SB;
@@ -2429,7 +2442,7 @@ __global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ 
   const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const tpe_table Tb = tables[j];
   BestT bx{0.0, -1, 0.0};
-  if (ns <= kBandSurv) {
+  if (W.direct) {
     // one survivor per 16 lanes, lane c holding chunk c's partials
     constexpr int kSPB = kFX / kBandBlocks;  // survivors per block pass
     static_assert(kBandBlocks == 16, "16-lane groups");
