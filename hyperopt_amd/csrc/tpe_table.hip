@@ -822,7 +822,10 @@ __device__ __forceinline__ bool log_taylor(const double (&p)[kP], double c, doub
   return true;
 }
 
-__global__ __launch_bounds__(kBS) void k_table_score(const tpe_job* __restrict__ jobs,
+#ifndef TPE_TSCORE_WPE  // diagnostic builds: waves-per-EU target of the cubics kernel
+#define TPE_TSCORE_WPE 4
+#endif
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_TSCORE_WPE))) void k_table_score(const tpe_job* __restrict__ jobs,
                                                      tpe_table* __restrict__ tables,
                                                      float* __restrict__ cells,
                                                      unsigned long long* __restrict__ stats) {
