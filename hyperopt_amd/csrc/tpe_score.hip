@@ -793,7 +793,10 @@ __device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
 // slot_n * n_jobs blocks score the lattice slots instead (score_slot; the
 // slot scores do not depend on the draws, so they share the launch)
 template <bool POW2>
-__global__ __launch_bounds__(kBS) void k_lattice_sample(
+#ifndef TPE_LAT_WPE  // diagnostic builds: waves-per-EU target of the lattice sampler
+#define TPE_LAT_WPE 4     // (power-of-two candidate counts: 128 VGPRs, no spill)
+#endif
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_LAT_WPE : 1))) void k_lattice_sample(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
