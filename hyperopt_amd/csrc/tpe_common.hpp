@@ -120,6 +120,28 @@ __device__ __forceinline__ BestT wave_best(BestT b) {
   return b;
 }
 
+// this thread's np.argmax over P[tid], P[tid + BS], ... (< nper), eight loads
+// in flight at a time (a job's partials are thousands of 32-B records: one
+// load per dependent step left the reduce latency-bound)
+template <int BS>
+__device__ __forceinline__ BestT thread_best(const tpe_best* __restrict__ P, int64_t nper) {
+  BestT b{0.0, -1, 0.0};
+  int64_t i = threadIdx.x;
+  constexpr int kU = 8;
+  for (; i + (kU - 1) * BS < nper; i += kU * BS) {
+    tpe_best p[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) p[u] = P[i + u * BS];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) best_update(b, p[u].score, p[u].index, p[u].value);
+  }
+  for (; i < nper; i += BS) {
+    const tpe_best p = P[i];
+    best_update(b, p.score, p.index, p.value);
+  }
+  return b;
+}
+
 // block-wide argmax; result valid in every thread. `sh` holds >= nwaves BestT.
 template <int BS>
 __device__ __forceinline__ BestT block_best(BestT b, BestT* sh) {

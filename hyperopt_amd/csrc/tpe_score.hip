@@ -403,12 +403,7 @@ __global__ __launch_bounds__(kBS) void k_reduce(const tpe_job* __restrict__ jobs
                                                 const tpe_best* __restrict__ partial, int64_t nper,
                                                 tpe_best* __restrict__ best) {
   __shared__ BestT red[kBS / kWave];
-  BestT b{0.0, -1, 0.0};
-  const tpe_best* P = partial + (int64_t)blockIdx.x * nper;
-  for (int64_t i = threadIdx.x; i < nper; i += kBS) {
-    const tpe_best p = P[i];
-    best_update(b, p.score, p.index, p.value);
-  }
+  BestT b = thread_best<kBS>(partial + (int64_t)blockIdx.x * nper, nper);
   b = block_best<kBS>(b, red);
   if (threadIdx.x == 0) best[blockIdx.x] = tpe_best{b.score, b.index, b.value, jobs[blockIdx.x].n_cand};
 }

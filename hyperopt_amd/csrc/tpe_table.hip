@@ -2130,11 +2130,7 @@ __global__ __launch_bounds__(kBX) void k_band(
   __syncthreads();
   if (s_over) {  // the fp32 winner; the caller re-scores the job exactly
     if (kb == 0) {
-      BestT b32{0.0, -1, 0.0};
-      for (int i = threadIdx.x; i < n_tiles; i += kBX) {
-        const tpe_best p = partial[(int64_t)j * n_tiles + i];
-        best_update(b32, p.score, p.index, p.value);
-      }
+      BestT b32 = thread_best<kBX>(partial + (int64_t)j * n_tiles, n_tiles);
       b32 = block_best<kBX>(b32, red);
       if (threadIdx.x == 0) {
         best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
@@ -2269,11 +2265,7 @@ __global__ __launch_bounds__(kBX) void k_band(
   if (over) {
     // many survivors, off the grid or over too many cells: the exact fallback
     if (kb == 0) {
-      BestT b32{0.0, -1, 0.0};
-      for (int i = threadIdx.x; i < n_tiles; i += kBX) {
-        const tpe_best p = partial[(int64_t)j * n_tiles + i];
-        best_update(b32, p.score, p.index, p.value);
-      }
+      BestT b32 = thread_best<kBX>(partial + (int64_t)j * n_tiles, n_tiles);
       b32 = block_best<kBX>(b32, red);
       if (threadIdx.x == 0) best[j] = tpe_best{b32.score, b32.index, b32.value, -1};
     }
@@ -2797,12 +2789,7 @@ __global__ __launch_bounds__(kBS) void k_reduce_t(const tpe_job* __restrict__ jo
                                                   const tpe_best* __restrict__ partial,
                                                   int64_t nper, tpe_best* __restrict__ best) {
   __shared__ BestT red[kBS / kWave];
-  BestT b{0.0, -1, 0.0};
-  const tpe_best* P = partial + (int64_t)blockIdx.x * nper;
-  for (int64_t i = threadIdx.x; i < nper; i += kBS) {
-    const tpe_best p = P[i];
-    best_update(b, p.score, p.index, p.value);
-  }
+  BestT b = thread_best<kBS>(partial + (int64_t)blockIdx.x * nper, nper);
   b = block_best<kBS>(b, red);
   if (threadIdx.x == 0)
     best[blockIdx.x] = tpe_best{b.score, b.index, b.value, jobs[blockIdx.x].n_cand};
