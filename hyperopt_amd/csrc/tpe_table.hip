@@ -1842,7 +1842,12 @@ constexpr double kBandRho = 1.5;     // admissible 1.05 |A| + 1.1025 |B|
 constexpr int kBandCells = 64;       // cells expanded per job (sorted; the rest: direct)
 constexpr int kBandBits = 32768;     // cell bitmap (LDS)
 
-constexpr int kChunkDir = 16;        // slow components listed per (cell, chunk, mixture)
+#ifndef TPE_BAND_DIR
+#define TPE_BAND_DIR 16
+#endif
+constexpr int kChunkDir = TPE_BAND_DIR;  // slow components listed per (cell, chunk, mixture)
+                                          // (a full list sends the cell's survivors to the
+                                          // direct sum over every component)
 struct BandMix {  // one mixture's expansion on one cell (or one chunk of its components)
   double P[kBandD + 1];
   double m;
@@ -2495,6 +2500,22 @@ __global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ 
     for (int t = threadIdx.x; t < ncell * nch * 2 * kChunkDir; t += kFX) {
       const int d = t % kChunkDir, r = t / kChunkDir, u = r >> 1, mix = r & 1;
       s_dir[u][mix][d] = W.cpart[u / nch][u % nch][mix].dir[d];
+    }
+    __syncthreads();
+    // each list in component order (k_band lists them in atomic order): the
+    // slow components are then summed in a fixed order, run to run
+    for (int t = threadIdx.x; t < ncell * nch * 2; t += kFX) {
+      const int u = t >> 1, mix = t & 1, nd = s_ndu[u][mix];
+      int* L = s_dir[u][mix];
+      for (int a = 1; a < nd; ++a) {
+        const int v = L[a];
+        int b = a - 1;
+        while (b >= 0 && L[b] > v) {
+          L[b + 1] = L[b];
+          --b;
+        }
+        L[b + 1] = v;
+      }
     }
     __syncthreads();
     for (int t = threadIdx.x; t < ncell * 2; t += kFX) {
