@@ -2295,6 +2295,7 @@ __global__ __launch_bounds__(kBX) void k_band(
       }
       TMARK(8 + 3 * mix)
       for (int b0 = 0; b0 < ns; b0 += kSurvBatch) {
+        const int nbat = min(kSurvBatch, ns - b0);  // (block-uniform: the batch's real survivors)
         double m[kSurvBatch], sm[kSurvBatch], y[kSurvBatch];
 #pragma unroll
         for (int i = 0; i < kSurvBatch; ++i) {
@@ -2305,6 +2306,7 @@ __global__ __launch_bounds__(kBX) void k_band(
         auto acc = [&](const double4 c) {
 #pragma unroll
           for (int i = 0; i < kSurvBatch; ++i) {
+            if (i >= nbat) continue;  // (a short batch: no work for its empty slots)
             const double t = (y[i] - c.x) * c.y;
             const double v = -0.5 * (t * t) + c.z;  // (log coefficient c.z: GMM1_lpdf's terms)
             if (lse_skip(m[i], sm[i], v)) continue;
