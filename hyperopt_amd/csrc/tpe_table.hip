@@ -1827,8 +1827,9 @@ constexpr int kBandDirect = TPE_BAND_DIRECT;  // ... and always does; more take 
 #define TPE_SURV_BATCH 8
 #endif
 constexpr int kSurvBatch = TPE_SURV_BATCH;  // survivors summed together per pass
-constexpr int kDirStage = 1024;      // a block's component chunk staged in LDS when it fits
-                                     // (a multiple of kBX: the per-thread order is unchanged)
+constexpr int kDirStage = 256;       // a block's component chunk staged in LDS when it fits
+                                     // (a multiple of kBX: the per-thread order is unchanged;
+                                     // small: k_band shares CUs with the side stream's launches)
 #ifndef TPE_BAND_BX
 #define TPE_BAND_BX 256
 #endif
@@ -2416,7 +2417,8 @@ __global__ __launch_bounds__(kBX) void k_band(
 #endif
 constexpr int kFX = TPE_BAND_FX;         // k_band_final block
 constexpr int kFinBlocks = TPE_BAND_FINB;  // k_band_final blocks per job (<= kBandBlocks: W.win)
-constexpr int kFStage = 4096;  // survivors staged in LDS per round (k_band_final, cells)
+constexpr int kFStage = 512;   // survivors staged in LDS per round (k_band_final, cells; small:
+                               // the kernel shares CUs with the side stream's big launches)
 static_assert(kFinBlocks <= kBandBlocks && kFinBlocks <= kWave, "W.win holds the blocks' winners");
 __global__ __launch_bounds__(kFX) void k_band_final(const tpe_job* __restrict__ jobs,
                                                     const tpe_seg* __restrict__ segs,
