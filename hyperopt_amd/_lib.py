@@ -140,6 +140,7 @@ _SIGNATURES = {
     "tpe_mixture_scratch_bytes": (_I64, [_I, _I]),
     "tpe_mixture_prepare": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tpe_smallest_rows": (_I64, [_P, _I64, _I64, _P]),
+    "tpe_split_inputs": (_I64, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "tpe_last_error": (ctypes.c_char_p, []),
     "tpe_abi_version": (_I, []),
     "tpe_struct_sizes": (_I, [_P, _I]),

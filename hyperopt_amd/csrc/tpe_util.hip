@@ -1,6 +1,7 @@
 // tpe_util.hip -- error reporting shared by every C-ABI entry point.
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include <algorithm>
 #include <vector>
@@ -121,6 +122,33 @@ extern "C" int64_t tpe_smallest_rows(const double* losses, int64_t n, int64_t k,
   }
   std::sort(ki.begin(), ki.end());
   std::copy(ki.begin(), ki.end(), out);
+  return k;
+}
+
+// ---- host: the split and the level inputs of one history in one pass -----
+// The below rows (tpe_smallest_rows), a 0/1 flag per row, and per label the
+// below set's size nb[j] (active below rows) and the above set's size
+// na[j] = n_active[j] - nb[j] (every row is below or above: no from_tid
+// aliasing) -- what tpe.suggest's split_masks + LevelInputs compute with a
+// dozen numpy calls.  active: T x L bytes, row-major.  Returns the number of
+// below rows, or -1 on bad arguments.
+extern "C" int64_t tpe_split_inputs(const double* losses, int64_t T, int64_t n_below,
+                                    const uint8_t* active, int64_t L, const int64_t* n_active,
+                                    uint8_t* isb, int64_t* below_rows, int64_t* nb, int64_t* na) {
+  if (T < 0 || L < 0 || n_below < 0 || (T > 0 && (!losses || !isb)) ||
+      (L > 0 && (!nb || !na || !n_active || (T > 0 && !active))) || (n_below > 0 && !below_rows))
+    return -1;
+  const int64_t k = tpe_smallest_rows(losses, T, n_below, below_rows);
+  if (k < 0) return -1;
+  memset(isb, 0, (size_t)T);
+  for (int64_t j = 0; j < L; ++j) nb[j] = 0;
+  for (int64_t i = 0; i < k; ++i) {
+    const int64_t r = below_rows[i];
+    isb[r] = 1;
+    const uint8_t* a = active + r * L;
+    for (int64_t j = 0; j < L; ++j) nb[j] += a[j] != 0;
+  }
+  for (int64_t j = 0; j < L; ++j) na[j] = n_active[j] - nb[j];
   return k;
 }
 

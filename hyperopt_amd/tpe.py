@@ -325,6 +325,40 @@ class LevelInputs(object):
         rows = None if hist.rows is None else hist.rows.astype(np.int32)
         self.run_kwargs = dict(history=c.device_history(eng), rows=rows, is_below=flags)
 
+    @classmethod
+    def fast(cls, hist, gamma, eng, gamma_cap=DEFAULT_LF):
+        """split_masks + LevelInputs in one C pass (tpe_split_inputs) for the
+        common case -- a columnar history over every cached row, no from_tid
+        aliasing, device mode -- or None (the caller takes the general path).
+        Same split, flags and counts (tests/test_host_api.py)."""
+        c = hist.col
+        if c is None or hist.rows is not None or c.n_alias or eng is None:
+            return None
+        T = hist.tids.size
+        if T != c.rows or hist.obs_tids.size != T:
+            return None
+        L = len(c.labels)
+        n_below = min(int(np.ceil(gamma * np.sqrt(T))), gamma_cap)
+        losses = np.ascontiguousarray(hist.losses, dtype=np.float64)
+        act = c.active  # (cap, L) bool, row-major; rows [0, T) are the history
+        isb = np.empty(T, np.uint8)
+        rows_b = np.empty(max(n_below, 1), np.int64)
+        nb = np.empty(L, np.int64)
+        na = np.empty(L, np.int64)
+        got = _L.load().tpe_split_inputs(losses.ctypes.data, T, n_below, act.ctypes.data, L,
+                                         c.n_active.ctypes.data, isb.ctypes.data,
+                                         rows_b.ctypes.data, nb.ctypes.data, na.ctypes.data)
+        if got != min(n_below, T):
+            raise _L.TpeHipError("tpe_split_inputs returned %d" % got)
+        self = cls.__new__(cls)
+        self.hist, self.isb, self.isa = hist, isb.view(bool), None
+        self.device = True
+        rows_b = rows_b[:got]
+        self.vb, self.ab = c.vals[rows_b], c.active[rows_b]
+        self.nb, self.n_above = nb, na
+        self.run_kwargs = dict(history=c.device_history(eng), rows=None, is_below=isb)
+        return self
+
     def work(self, label, spec, j, **kw):
         if self.device:
             return LabelWork(label=label, kind=spec.kind, args=spec.args,
@@ -354,7 +388,6 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
         return rand.suggest_device(new_ids, domain, trials, seed)
 
     first_new_id = new_ids[0]
-    isb, isa = split_masks(hist, gamma)
     prec = _precision(precision, n_EI_candidates, hist.tids.size)
     rank, ws = hdist.world()
     n_ei = max(int(n_EI_candidates), 0)
@@ -367,7 +400,10 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
         hm = eng.host_marks  # (diagnostic phase marks, Engine.host_marks)
         if hm is not None:
             hm.append(("suggest:split", time.perf_counter()))
-        obs = LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY)
+        obs = LevelInputs.fast(hist, gamma, eng) if USE_DEVICE_HISTORY else None
+        if obs is None:
+            isb, isa = split_masks(hist, gamma)
+            obs = LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY)
         if hm is not None:
             hm.append(("suggest:inputs", time.perf_counter()))
         while True:
@@ -621,12 +657,14 @@ def _suggest_many(requests, shard_studies=False):
         if hist.tids.size < kw["n_startup_jobs"]:
             out[qi] = rand.suggest_device(rq.new_ids, rq.domain, rq.trials, rq.seed)
             return None
-        isb, isa = split_masks(hist, kw["gamma"])
         n_ei = max(int(kw["n_EI_candidates"]), 0)
         start, count = (0, n_ei) if (shard_studies or ws == 1) else hdist.shard(n_ei, rank, ws)
-        return dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist,
-                    obs=LevelInputs(hist, isb, isa, engine() if n_ei > 0 else None,
-                                    device=USE_DEVICE_HISTORY),
+        eng = engine() if n_ei > 0 else None
+        obs = LevelInputs.fast(hist, kw["gamma"], eng) if USE_DEVICE_HISTORY else None
+        if obs is None:
+            isb, isa = split_masks(hist, kw["gamma"])
+            obs = LevelInputs(hist, isb, isa, eng, device=USE_DEVICE_HISTORY)
+        return dict(qi=qi, rq=rq, kw=kw, labels=labels, hist=hist, obs=obs,
                     col={lab: j for j, lab in enumerate(labels)}, walk={}, stored={},
                     live=[], start=start, count=count, n_ei=n_ei, done=n_ei == 0,
                     prec=_precision(kw["precision"], n_ei, hist.tids.size))

@@ -657,6 +657,15 @@ int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op);
  * ap_split_trials (tpe.py:623-646) -- written to out (host) in ascending row
  * order; returns min(k, n), -1 on bad arguments. */
 int64_t tpe_smallest_rows(const double* losses, int64_t n, int64_t k, int64_t* out);
+/* host: tpe_smallest_rows plus the level inputs of the split in one pass:
+ * isb[r] = 1 for the below rows (else 0), nb[j] = active below rows of label
+ * j, na[j] = n_active[j] - nb[j] (a history without from_tid aliasing: every
+ * row is below or above).  active: T x L bytes, row-major.  Returns the
+ * number of below rows written to below_rows (ascending), -1 on bad
+ * arguments (ap_split_trials, tpe.py:623-646). */
+int64_t tpe_split_inputs(const double* losses, int64_t T, int64_t n_below, const uint8_t* active,
+                         int64_t L, const int64_t* n_active, uint8_t* isb, int64_t* below_rows,
+                         int64_t* nb, int64_t* na);
 
 const char* tpe_last_error(void);
 int tpe_abi_version(void);

@@ -345,3 +345,48 @@ def test_lat_prefix_setting_is_validated():
     for bad in ("1000", "-4096", "abc"):
         with pytest.raises(ValueError):
             _lat_prefix(bad)
+
+
+def test_split_inputs_fast_path_matches_split_masks():
+    """LevelInputs.fast (tpe_split_inputs: the split and the level inputs in
+    one C pass) gives the flags, below rows' values and the per-label counts
+    of split_masks + LevelInputs, on ties, inactive labels and +inf losses."""
+    from hyperopt_amd import _lib as L
+    from hyperopt_amd.tpe import History, LevelInputs, split_masks
+
+    class _Col:  # the columnar cache's fields the split reads
+        pass
+
+    rng = np.random.RandomState(2)
+    lib = L.load()
+    for T, Lb in ((1, 3), (40, 5), (997, 7), (5000, 4)):
+        col = _Col()
+        col.labels = tuple("l%d" % j for j in range(Lb))
+        col.rows = T
+        col.n_alias = 0
+        col.vals = rng.normal(size=(T + 3, Lb))
+        col.active = np.ascontiguousarray(rng.uniform(size=(T + 3, Lb)) < 0.7)
+        col.active[T:] = True  # (rows past the history must not count)
+        col.n_active = col.active[:T].sum(0).astype(np.int64)
+        losses = np.round(rng.normal(size=T) * 2) / 2
+        losses[rng.uniform(size=T) < 0.1] = np.inf
+        tids = np.arange(T, dtype=np.int64)
+        hist = History(tids, losses, tids, col=col)
+        for gamma in (0.25, 0.5):
+            isb, isa = split_masks(hist, gamma)
+            nb_ref = col.active[:T][isb].sum(0)
+            na_ref = col.active[:T][isa].sum(0)
+            n_below = min(int(np.ceil(gamma * np.sqrt(T))), 25)
+            flags = np.empty(T, np.uint8)
+            rows = np.empty(max(n_below, 1), np.int64)
+            nb = np.empty(Lb, np.int64)
+            na = np.empty(Lb, np.int64)
+            act = np.ascontiguousarray(col.active)
+            got = lib.tpe_split_inputs(losses.ctypes.data, T, n_below, act.ctypes.data, Lb,
+                                       col.n_active.ctypes.data, flags.ctypes.data,
+                                       rows.ctypes.data, nb.ctypes.data, na.ctypes.data)
+            assert got == min(n_below, T)
+            np.testing.assert_array_equal(flags.view(bool), isb)
+            np.testing.assert_array_equal(np.sort(rows[:got]), np.flatnonzero(isb))
+            np.testing.assert_array_equal(nb, nb_ref)
+            np.testing.assert_array_equal(na, na_ref)
