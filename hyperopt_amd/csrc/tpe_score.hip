@@ -998,73 +998,82 @@ __device__ __forceinline__ double block_suffix_min(double v, double* sw) {
   return v;
 }
 
+// One block per (job, mixture, direction): blockIdx.x = 4 job + 2 dir + mix,
+// dir 0 the prefix max P from the front, dir 1 the suffix min S from the
+// back; the next pass's loads are issued before this pass's scan (the block
+// walks ~50 passes of 2 048 components at C5's 10^5: each otherwise waited
+// one load round trip)
 __global__ __launch_bounds__(kQB) void k_qreach(const tpe_job* __restrict__ jobs,
                                                const tpe_seg* __restrict__ segs,
                                                const double* __restrict__ mu,
                                                const double* __restrict__ sigma,
                                                double* __restrict__ P, double* __restrict__ Sm) {
   __shared__ double sw[kQB / kWave];
-  const tpe_job J = jobs[blockIdx.x >> 1];
+  const tpe_job J = jobs[blockIdx.x >> 2];
+  const bool suffix = (blockIdx.x >> 1) & 1;
   const tpe_seg S = segs[(blockIdx.x & 1) ? J.above : J.below];
   const int nc = S.n_obs + 1;
   const double* m = mu + S.comp_off;
   const double* g = sigma + S.comp_off;
   constexpr int kPass = kQB * kQPer;
   const int npass = (nc + kPass - 1) / kPass;
-  // one pass: thread t holds components base + t * kQPer + i; its values
-  // (hi = mu + b, lo = mu - b; NaN -> +inf / -inf) in registers
-  auto load = [&](int base, double (&hv)[kQPer], double (&lv)[kQPer]) __attribute__((always_inline)) {
+  // thread t's raw loads of components base + t * kQPer + i
+  auto load = [&](int base, double (&mk)[kQPer], double (&gk)[kQPer]) __attribute__((always_inline)) {
     const int a = base + (int)threadIdx.x * kQPer;
 #pragma unroll
     for (int i = 0; i < kQPer; ++i) {
       const int k = a + i;
-      const double mk = k < nc ? m[k] : 0.0, gk = k < nc ? g[k] : 0.0;
-      const double r = qreach_b(gk);
-      const bool ok = mk == mk && r == r;
-      hv[i] = k >= nc ? -INFINITY : (ok ? mk + r : INFINITY);
-      lv[i] = k >= nc ? INFINITY : (ok ? mk - r : -INFINITY);
+      mk[i] = k < nc ? m[k] : 0.0;
+      gk[i] = k < nc ? g[k] : 0.0;
     }
   };
-  double carry = -INFINITY;  // prefix max of the earlier passes
-  for (int ps = 0; ps < npass; ++ps) {  // block-uniform
+  // (hi = mu + b for the prefix, lo = mu - b for the suffix; NaN -> +inf / -inf)
+  auto value = [&](int k, double mk, double gk) -> double {
+    const double r = qreach_b(gk);
+    const bool ok = mk == mk && r == r;
+    if (!suffix) return k >= nc ? -INFINITY : (ok ? mk + r : INFINITY);
+    return k >= nc ? INFINITY : (ok ? mk - r : -INFINITY);
+  };
+  double nm[kQPer], ng[kQPer];
+  load(suffix ? (npass - 1) * kPass : 0, nm, ng);
+  double carry = suffix ? INFINITY : -INFINITY;  // the earlier passes' max / later passes' min
+  for (int q = 0; q < npass; ++q) {  // block-uniform
+    const int ps = suffix ? npass - 1 - q : q;
     const int base = ps * kPass;
-    double hv[kQPer], lv[kQPer];
-    load(base, hv, lv);
-#pragma unroll
-    for (int i = 1; i < kQPer; ++i) hv[i] = fmax(hv[i], hv[i - 1]);
-    const double incl = block_prefix_max(hv[kQPer - 1], sw);
-    double before = __shfl_up(incl, 1, kWave);  // max over the threads before this one
-    if (lane_id() == 0) {
-      before = -INFINITY;
-      for (int w = 0; w < (int)threadIdx.x / kWave; ++w) before = fmax(before, sw[w]);
-    }
-    before = fmax(before, carry);
     const int a = base + (int)threadIdx.x * kQPer;
+    double v[kQPer];
 #pragma unroll
-    for (int i = 0; i < kQPer; ++i)
-      if (a + i < nc) P[S.comp_off + a + i] = fmax(before, hv[i]);
-    for (int w = 0; w < kQB / kWave; ++w) carry = fmax(carry, sw[w]);  // (the pass's total)
-    __syncthreads();
-  }
-  double carry_lo = INFINITY;  // suffix min of the later passes
-  for (int ps = npass - 1; ps >= 0; --ps) {
-    const int base = ps * kPass;
-    double hv[kQPer], lv[kQPer];
-    load(base, hv, lv);
+    for (int i = 0; i < kQPer; ++i) v[i] = value(a + i, nm[i], ng[i]);
+    if (q + 1 < npass) load((suffix ? ps - 1 : ps + 1) * kPass, nm, ng);  // (in flight)
+    if (!suffix) {
 #pragma unroll
-    for (int i = kQPer - 2; i >= 0; --i) lv[i] = fmin(lv[i], lv[i + 1]);
-    const double incl = block_suffix_min(lv[0], sw);
-    double after = __shfl_down(incl, 1, kWave);  // min over the threads after this one
-    if (lane_id() == kWave - 1) {
-      after = INFINITY;
-      for (int w = (int)threadIdx.x / kWave + 1; w < kQB / kWave; ++w) after = fmin(after, sw[w]);
+      for (int i = 1; i < kQPer; ++i) v[i] = fmax(v[i], v[i - 1]);
+      const double incl = block_prefix_max(v[kQPer - 1], sw);
+      double before = __shfl_up(incl, 1, kWave);  // max over the threads before this one
+      if (lane_id() == 0) {
+        before = -INFINITY;
+        for (int w = 0; w < (int)threadIdx.x / kWave; ++w) before = fmax(before, sw[w]);
+      }
+      before = fmax(before, carry);
+#pragma unroll
+      for (int i = 0; i < kQPer; ++i)
+        if (a + i < nc) P[S.comp_off + a + i] = fmax(before, v[i]);
+      for (int w = 0; w < kQB / kWave; ++w) carry = fmax(carry, sw[w]);  // (the pass's total)
+    } else {
+#pragma unroll
+      for (int i = kQPer - 2; i >= 0; --i) v[i] = fmin(v[i], v[i + 1]);
+      const double incl = block_suffix_min(v[0], sw);
+      double after = __shfl_down(incl, 1, kWave);  // min over the threads after this one
+      if (lane_id() == kWave - 1) {
+        after = INFINITY;
+        for (int w = (int)threadIdx.x / kWave + 1; w < kQB / kWave; ++w) after = fmin(after, sw[w]);
+      }
+      after = fmin(after, carry);
+#pragma unroll
+      for (int i = 0; i < kQPer; ++i)
+        if (a + i < nc) Sm[S.comp_off + a + i] = fmin(after, v[i]);
+      for (int w = 0; w < kQB / kWave; ++w) carry = fmin(carry, sw[w]);  // (the pass's total)
     }
-    after = fmin(after, carry_lo);
-    const int a = base + (int)threadIdx.x * kQPer;
-#pragma unroll
-    for (int i = 0; i < kQPer; ++i)
-      if (a + i < nc) Sm[S.comp_off + a + i] = fmin(after, lv[i]);
-    for (int w = 0; w < kQB / kWave; ++w) carry_lo = fmin(carry_lo, sw[w]);  // (the pass's total)
     __syncthreads();
   }
 }
@@ -1818,7 +1827,7 @@ extern "C" int tpe_lattice_suggest(const tpe_job* jobs, const tpe_job* host_jobs
   unsigned long long* sf = (unsigned long long*)slot_first;
   const bool win = reach_hi && reach_lo;  // the slots' component windows (k_qreach)
   if (win)
-    hipLaunchKernelGGL(k_qreach, dim3(2 * n_jobs), dim3(kQB), 0, st, jobs, segs, mu, sigma,
+    hipLaunchKernelGGL(k_qreach, dim3(4 * n_jobs), dim3(kQB), 0, st, jobs, segs, mu, sigma,
                        reach_hi, reach_lo);
   if (!launch_lattice_sample(jobs, host_jobs, n_jobs, segs, mu, sigma, wcdf, slot_first, err, 0,
                              prefix, nullptr, st, "tpe_lattice_suggest", w, partial, max_n,
@@ -1895,7 +1904,7 @@ extern "C" int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs
   hipStream_t st = (hipStream_t)stream;
   const bool win = reach_hi && reach_lo;  // the values' component windows (k_qreach)
   if (win)
-    hipLaunchKernelGGL(k_qreach, dim3(2 * n_jobs), dim3(kQB), 0, st, jobs, segs, mu, sigma,
+    hipLaunchKernelGGL(k_qreach, dim3(4 * n_jobs), dim3(kQB), 0, st, jobs, segs, mu, sigma,
                        reach_hi, reach_lo);
   hipLaunchKernelGGL(k_score_q, dim3((unsigned)gx, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
                      segs, w, mu, sigma, vals, firsts, (const unsigned long long*)counts, out_bl,
