@@ -361,20 +361,23 @@ __global__ __launch_bounds__(kCatBS) void k_cat_counts(const int64_t* __restrict
 // work folded in): one 1024-thread block per (segment, category) walks the
 // rows in windows of kCHW (row order = tid order, as tpe_gather_obs lists
 // them), a row being an observation of the segment when the label is active
-// there and the row is on the segment's side of the split.  One block scan
-// of the packed (observations << 16 | matches) counts per (tile, wave) gives
-// every observation its position in the segment -- its LF weight -- and
-// every match its rank in the window; the window's match weights go to LDS in
-// order and wave 0 folds them (seq_fold).  A segment whose observation count
-// differs from S.n_obs sets bit 4 of *err (tpe_gather_obs' rule).
+// there and the row is on the segment's side of the split.  Waves 1-15 scan:
+// one scan of the packed (observations << 16 | matches) counts per (tile,
+// wave) gives every observation its position in the segment -- its LF
+// weight -- and every match its rank in the window, the window's match
+// weights going to LDS in order; wave 0 folds (seq_fold) the previous
+// window's weights meanwhile, from the other of two LDS buffers (the fold of
+// a long chain is a serial-latency walk; the scan is load latency: they
+// overlap).  A segment whose observation count differs from S.n_obs sets
+// bit 4 of *err (tpe_gather_obs' rule).
 constexpr int kCHB = 1024;             // block
-constexpr int kCHT = 8;                // rows per thread per window
-constexpr int kCHW = kCHB * kCHT;      // rows per window
-constexpr int kCHWaves = kCHB / kWave;
-constexpr int kCHSlots = kCHT * kCHWaves;  // (tile, wave) counts per window
+constexpr int kCHScan = kCHB / kWave - 1;  // scanning waves (wave 0 folds)
+constexpr int kCHT = 8;                // rows per scanning thread per window
+constexpr int kCHW = kCHScan * kWave * kCHT;  // rows per window (7 680)
+constexpr int kCHSlots = kCHT * kCHScan;      // (tile, wave) counts per window
 constexpr int kCHSE = 8;               // seq_fold entries per lane (512 per pass; wider
                                        // passes measured slower: 16 +25 %, 32 +65 %)
-static_assert(kCHSlots == 2 * kWave, "the slot scan: two slots per lane of wave 0");
+static_assert(kCHSlots <= 2 * kWave, "the slot scan: two slots per lane of one wave");
 static_assert(kCHW < (1 << 16), "packed 16-bit counts");
 
 __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
@@ -382,9 +385,9 @@ __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
     const int32_t* __restrict__ rows, int64_t n_rows, const uint8_t* __restrict__ is_below,
     const tpe_gather* __restrict__ gathers, const tpe_cat_seg* __restrict__ segs,
     double* __restrict__ p, int32_t* __restrict__ err) {
-  __shared__ double s_w[kCHW];
-  __shared__ uint32_t s_slot[kCHSlots];
-  __shared__ uint32_t s_tot;
+  __shared__ double s_w[2][kCHW];
+  __shared__ uint32_t s_slot[2 * kWave];
+  __shared__ uint32_t s_tot[2];  // per buffer: the window's packed totals
   const tpe_cat_seg S = segs[blockIdx.y];
   const int k = blockIdx.x;
   if (k >= S.n_cat) return;  // (block-uniform)
@@ -393,6 +396,8 @@ __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
   const uint8_t* __restrict__ Ac = active + (int64_t)G.col * ld;
   const uint8_t side = G.below ? 1 : 0;
   const int lane = lane_id(), wid = threadIdx.x / kWave;
+  const int sw = wid - 1;                   // scanning wave index (waves 1..)
+  const int st = threadIdx.x - kWave;       // scanning thread index
   const uint64_t lt = (1ull << lane) - 1ull;
   const int n = S.n_obs;
   const bool ramp = S.lf > 0 && S.lf < n;
@@ -401,34 +406,51 @@ __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
   const double step = (ramp && num > 1) ? (1.0 - start) / (double)(num - 1) : 0.0;
   double cnt = 0.0;     // (wave 0)
   int64_t folded = 0;  // (wave 0) matches folded so far
-  int64_t carry = 0;  // observations before the window
-  for (int64_t p0 = 0; p0 < n_rows; p0 += kCHW) {
+  int64_t carry = 0;   // (scanners) observations before the window
+  const int64_t n_win = (n_rows + kCHW - 1) / kCHW;
+  for (int64_t it = 0; it <= n_win; ++it) {  // (block-uniform; the last round only folds)
+    const int buf = (int)(it & 1);
+    const bool scan = it < n_win;
     bool mem[kCHT], hit[kCHT];
+    uint32_t pre[kCHT];
+    // ---- phase 0: scanners load and ballot window `it`; wave 0 folds window it - 1
+    if (wid > 0 && scan) {
+      const int64_t p0 = it * kCHW;
 #pragma unroll
-    for (int t = 0; t < kCHT; ++t) {
-      const int64_t i = p0 + (int64_t)t * kCHB + threadIdx.x;
-      mem[t] = hit[t] = false;
-      if (i < n_rows) {
-        const int64_t r = rows ? (int64_t)rows[i] : i;
-        const bool a = Ac[r] != 0;
-        const double v = V[r];  // (read unconditionally: one latency, not two)
-        mem[t] = a && is_below[i] == side;
-        hit[t] = mem[t] && (int64_t)v - G.offset == (int64_t)k;
+      for (int t = 0; t < kCHT; ++t) {
+        const int64_t i = p0 + (int64_t)t * (kCHScan * kWave) + st;
+        mem[t] = hit[t] = false;
+        if (i < n_rows) {
+          const int64_t r = rows ? (int64_t)rows[i] : i;
+          const bool a = Ac[r] != 0;
+          const double v = V[r];  // (read unconditionally: one latency, not two)
+          mem[t] = a && is_below[i] == side;
+          hit[t] = mem[t] && (int64_t)v - G.offset == (int64_t)k;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < kCHT; ++t) {
+        const uint64_t bm = __ballot(mem[t]), bh = __ballot(hit[t]);
+        pre[t] = ((uint32_t)__popcll(bm & lt) << 16) | (uint32_t)__popcll(bh & lt);
+        if (lane == 0) s_slot[t * kCHScan + sw] = ((uint32_t)__popcll(bm) << 16) |
+                                                  (uint32_t)__popcll(bh);
       }
     }
-    uint32_t pre[kCHT];  // this lane's packed (observations, matches) before it in its tile-wave
-#pragma unroll
-    for (int t = 0; t < kCHT; ++t) {
-      const uint64_t bm = __ballot(mem[t]), bh = __ballot(hit[t]);
-      pre[t] = ((uint32_t)__popcll(bm & lt) << 16) | (uint32_t)__popcll(bh & lt);
-      if (lane == 0) s_slot[t * kCHWaves + wid] = ((uint32_t)__popcll(bm) << 16) |
-                                                  (uint32_t)__popcll(bh);
+    if (wid == 0 && it > 0) {
+      const int nh = (int)(s_tot[buf ^ 1] & 0xffffu);
+#ifdef TPE_DIAG_CAT_NOFOLD  // (diagnostic builds: the scan alone)
+      if (nh > 0) cnt += s_w[buf ^ 1][nh - 1];
+#else
+      cnt = fold_list<kCHSE>(cnt, s_w[buf ^ 1], nh, folded, lane);
+#endif
     }
     __syncthreads();
-    // exclusive scan of the slots (tile-major, then wave: row order) on
-    // wave 0, two slots per lane
-    if (wid == 0) {
-      const uint32_t c0 = s_slot[2 * lane], c1 = s_slot[2 * lane + 1];
+    if (!scan) break;
+    // ---- phase 1: exclusive scan of the slots (tile-major, then wave: row
+    // order) on wave 1, two slots per lane
+    if (wid == 1) {
+      const uint32_t c0 = 2 * lane < kCHSlots ? s_slot[2 * lane] : 0u;
+      const uint32_t c1 = 2 * lane + 1 < kCHSlots ? s_slot[2 * lane + 1] : 0u;
       uint32_t incl = c0 + c1;
 #pragma unroll
       for (int o = 1; o < kWave; o <<= 1) {
@@ -436,38 +458,35 @@ __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
         if (lane >= o) incl += y;
       }
       const uint32_t ex = incl - (c0 + c1);
-      s_slot[2 * lane] = ex;
-      s_slot[2 * lane + 1] = ex + c0;
-      if (lane == kWave - 1) s_tot = incl;
+      if (2 * lane < kCHSlots) s_slot[2 * lane] = ex;
+      if (2 * lane + 1 < kCHSlots) s_slot[2 * lane + 1] = ex + c0;
+      if (lane == kWave - 1) s_tot[buf] = incl;
     }
     __syncthreads();
-    const uint32_t tot = s_tot;
+    // ---- phase 2: the window's match weights into s_w[buf], in order
+    if (wid > 0) {
 #pragma unroll
-    for (int t = 0; t < kCHT; ++t) {
-      if (hit[t]) {
-        const uint32_t ex = s_slot[t * kCHWaves + wid] + pre[t];
-        const int64_t pos = carry + (int64_t)(ex >> 16);
-        double wt = 1.0;
-        if (ramp && pos < num) {
-          if (num == 1) wt = start;
-          else if (pos == num - 1) wt = 1.0;
-          else wt = __dadd_rn(__dmul_rn((double)pos, step), start);
+      for (int t = 0; t < kCHT; ++t) {
+        if (hit[t]) {
+          const uint32_t ex = s_slot[t * kCHScan + sw] + pre[t];
+          const int64_t pos = carry + (int64_t)(ex >> 16);
+          double wt = 1.0;
+          if (ramp && pos < num) {
+            if (num == 1) wt = start;
+            else if (pos == num - 1) wt = 1.0;
+            else wt = __dadd_rn(__dmul_rn((double)pos, step), start);
+          }
+          s_w[buf][ex & 0xffffu] = wt;
         }
-        s_w[ex & 0xffffu] = wt;
       }
+      carry += (int64_t)(s_tot[buf] >> 16);
     }
-    __syncthreads();
-    const int nh = (int)(tot & 0xffffu);
-#ifdef TPE_DIAG_CAT_NOFOLD  // (diagnostic builds: the scan alone)
-    if (wid == 0 && nh > 0) cnt += s_w[nh - 1];
-#else
-    if (wid == 0) cnt = fold_list<kCHSE>(cnt, s_w, nh, folded, lane);
-#endif
-    carry += (int64_t)(tot >> 16);
-    __syncthreads();  // (s_w, s_slot reused)
+    __syncthreads();  // (s_slot reused; s_w[buf] complete for the fold)
+  }
+  if (threadIdx.x == kWave) {  // (a scanner holds the observation count)
+    if (carry != (int64_t)n && err) atomicOr(err, 4);
   }
   if (threadIdx.x == 0) {
-    if (carry != (int64_t)n && err) atomicOr(err, 4);
     double pseudo;
     if (S.mode == 0) {
       pseudo = cnt + S.prior_weight;  // tpe.py:589
