@@ -1819,10 +1819,14 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(TPE_SCORE_W
 constexpr int kBandBlocks = TPE_BAND_BLOCKS;  // blocks per job
 constexpr int kBandSurv = 128;       // survivors a job may score directly
 #ifndef TPE_BAND_DIRECT
-#define TPE_BAND_DIRECT 16
+#define TPE_BAND_DIRECT 128
 #endif
 constexpr int kBandDirect = TPE_BAND_DIRECT;  // ... and always does; more take the cell
-                                              // expansions where the cells can hold them
+                                              // expansions where the cells can hold them.
+// (16 made drop-in bands of 30-130 survivors cheaper, but a rank's share of
+// a label can then take the other path than the whole label and score the
+// same candidate with other fp64 bits: the winners must not depend on the
+// rank count -- test_gpu_shard.py -- so a job's path keeps to 128.)
 #ifndef TPE_SURV_BATCH
 #define TPE_SURV_BATCH 8
 #endif
