@@ -389,6 +389,15 @@ class _LevelState:
         raise AttributeError(name)
 
 
+class _LaunchState:
+    """Launch-time state of one level shared by its stages (Engine._launch_level:
+    the library or recording _OpList, the streams, the output buffers, the side
+    stream's fork / join flags), and of one group's launch (its job slice)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
 class _LaunchCtx:
     """Timer events and cross-stream ordering of one level's launches, issued
     eagerly or appended to the _OpList being recorded (``cap``)."""
@@ -1223,69 +1232,13 @@ class Engine:
         here = locals()  # (outside the comprehension: its own scope)
         lv = _LevelState(**{k: v for k, v in here.items() if k in _LAUNCH_STATE})
 
-        def launch_level(lib=None):
-            return self._launch_level(lv, ctx, lib)
-
         nbytes = 64 + n_jobs * BS + xbytes  # the result block read back at the end
-        ops = None
-        if native_ok:
-            ops = self._oplists.get(gkey)
-            if ops is None and gkey == self._last_gkey:
-                # the second call in a row with this launch key: record the
-                # level's stream work once, re-issue it from C on later calls
-                gen0 = self._gen
-                rec = _OpList(self.lib)
-                dst, src, nb = self._staged
-                rec.add(L.OP_MEMCPY, dst, src, _V("pack_size", nb), L.H2D, sp)
-                ctx.cap = rec
-                try:
-                    rec.table_calls, _ = launch_level(rec)
-                    rec.band_jobs = list(band_jobs)
-                finally:
-                    ctx.cap = None
-                pin = self._res_pinned(nbytes)
-                rec.add(L.OP_MEMCPY, pin.data_ptr(), d_res, nbytes, L.D2H, sp)
-                if batch is not None:
-                    rec.add(L.OP_EVENT_RECORD, self._event("result"), sp)
-                else:
-                    rec.add(L.OP_STREAM_SYNC, sp)
-                rec.finish((jobs, fb_jobs, g_arr if hist_mode else None,
-                            h_arr if histories is not None else None))
-                if self._gen == gen0:  # every recorded pointer is still the live one
-                    if len(self._oplists) >= 16 or any(
-                            k[1] != gen0 for k in self._oplists):
-                        self._drop_oplists()
-                    self._oplists[gkey] = rec
-                else:
-                    if self._oplist_once is not None:
-                        self._oplist_once.destroy(self._hip)
-                    self._oplist_once = rec  # this call's only (its events freed later)
-                ops = rec
-            if ops is None:  # eager: the deferred upload first
-                dst, src, nb = self._staged
-                L.hip_check(self._hip.hipMemcpyAsync(dst, src, nb, L.H2D, sp), "hipMemcpyAsync")
-        if ops is not None:
-            ops.set_sizes(dict(n_rows=n_rows, max_obs=max_obs, n_obs_total=n_obs_total,
-                               max_comp=max_obs + 1, pack_size=pack.size))
-            keep = ops.keep  # the host copies the entry points validate: this call's
-            keep[0][...] = jobs
-            keep[1][...] = fb_jobs
-            if keep[2] is not None:
-                keep[2][...] = g_arr
-            failed = ctypes.c_int(-1)
-            rc = self.lib.tpe_run_ops(ops.ptr, ops.n, ctypes.byref(failed))
-            if rc != 0:
-                raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
-                    rc, failed.value, self.lib.tpe_last_error().decode(errors="replace")))
-            self.graph_stats["native"] = self.graph_stats.get("native", 0) + 1
-            table_calls = ops.table_calls
-            band_jobs = ops.band_jobs
-        else:
-            table_calls, post = launch_level()
-            if post:
-                return table_calls
-            self._last_gkey = gkey
-            self.graph_stats["eager"] += 1
+        ops, table_calls, band_jobs, post = self._issue_level(
+            lv, ctx, gkey, nbytes, d_res, batch is not None,
+            dict(n_rows=n_rows, max_obs=max_obs, n_obs_total=n_obs_total, max_comp=max_obs + 1,
+                 pack_size=pack.size))
+        if post:
+            return table_calls
         _hmark('score launches')
         # the exact re-score of a band that overflowed (a plateau of equal fp32
         # scores; tpe_score_table_fast leaves n_scored = -1): after the readback
@@ -1337,77 +1290,116 @@ class Engine:
                                   works, order, cont, modes, _hmark, xinfo)
 
 
+    def _issue_level(self, lv, ctx, gkey, nbytes, d_res, queued, sizes):
+        """Issue a prepared level's stream work: re-issue its recorded records
+        from C (tpe_run_ops); record them first on the second call in a row
+        with launch key ``gkey`` (None: the level is not recordable); or launch
+        eagerly, the deferred upload first.  ``queued``: the recorded readback
+        ends with an event (a WorkBatch, _Pending) instead of a stream sync.
+        ``sizes``: this call's size words of the records.
+        Returns (ops or None, table_calls, band_jobs, posteriors_done)."""
+        sp = lv.sp
+        ops = None
+        if gkey is not None:
+            ops = self._oplists.get(gkey)
+            if ops is None and gkey == self._last_gkey:
+                # the second call in a row with this launch key: record the
+                # level's stream work once, re-issue it from C on later calls
+                gen0 = self._gen
+                rec = _OpList(self.lib)
+                dst, src, nb = self._staged
+                rec.add(L.OP_MEMCPY, dst, src, _V("pack_size", nb), L.H2D, sp)
+                ctx.cap = rec
+                try:
+                    rec.table_calls, _ = self._launch_level(lv, ctx, rec)
+                    rec.band_jobs = list(lv.band_jobs)
+                finally:
+                    ctx.cap = None
+                pin = self._res_pinned(nbytes)
+                rec.add(L.OP_MEMCPY, pin.data_ptr(), d_res, nbytes, L.D2H, sp)
+                if queued:
+                    rec.add(L.OP_EVENT_RECORD, self._event("result"), sp)
+                else:
+                    rec.add(L.OP_STREAM_SYNC, sp)
+                rec.finish((lv.jobs, lv.fb_jobs, lv.g_arr if lv.hist_mode else None,
+                            lv.h_arr if lv.histories is not None else None))
+                if self._gen == gen0:  # every recorded pointer is still the live one
+                    if len(self._oplists) >= 16 or any(
+                            k[1] != gen0 for k in self._oplists):
+                        self._drop_oplists()
+                    self._oplists[gkey] = rec
+                else:
+                    if self._oplist_once is not None:
+                        self._oplist_once.destroy(self._hip)
+                    self._oplist_once = rec  # this call's only (its events freed later)
+                ops = rec
+            if ops is None:  # eager: the deferred upload first
+                dst, src, nb = self._staged
+                L.hip_check(self._hip.hipMemcpyAsync(dst, src, nb, L.H2D, sp), "hipMemcpyAsync")
+        if ops is None:
+            table_calls, post = self._launch_level(lv, ctx)
+            if not post:
+                self._last_gkey = gkey
+                self.graph_stats["eager"] += 1
+            return None, table_calls, lv.band_jobs, post
+        ops.set_sizes(sizes)
+        keep = ops.keep  # the host copies the entry points validate: this call's
+        keep[0][...] = lv.jobs
+        keep[1][...] = lv.fb_jobs
+        if keep[2] is not None:
+            keep[2][...] = lv.g_arr
+        failed = ctypes.c_int(-1)
+        rc = self.lib.tpe_run_ops(ops.ptr, ops.n, ctypes.byref(failed))
+        if rc != 0:
+            raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
+                rc, failed.value, self.lib.tpe_last_error().decode(errors="replace")))
+        self.graph_stats["native"] = self.graph_stats.get("native", 0) + 1
+        return ops, ops.table_calls, ops.band_jobs, False
+
     def _launch_level(self, lv, ctx, lib=None):
         """The level's launches, in stream order: the body of run() for a prepared
         level (``lv``: its plan, workspace pointers and pack offsets; ``ctx``: the
         timer / stream-ordering helpers, which follow a recording _OpList).
         ``lib`` is the library, or the _OpList the launches are recorded into.
+        Stages: the gather (_launch_gather), the posterior fit (_launch_fit),
+        the scorers, one call per group (_launch_group), then the join of the
+        side stream and the cross-rank exchange.
         Returns (table_calls, posteriors_done)."""
         if lib is None:
             lib = self.lib
-        BS, JS, _hmark, band_jobs, base, cat = lv.BS, lv.JS, lv._hmark, lv.band_jobs, lv.base, lv.cat
-        cnt_off, cobs_off, csegs, d_best, d_c32, d_c32n = lv.cnt_off, lv.cobs_off, lv.csegs, lv.d_best, lv.d_c32, lv.d_c32n
-        d_c64, d_ccdf, d_cdf, d_csegs, d_err, d_fs = lv.d_c64, lv.d_ccdf, lv.d_cdf, lv.d_csegs, lv.d_err, lv.d_fs
-        d_logp, d_mu, d_pairs, d_pm, d_segs, d_sig = lv.d_logp, lv.d_mu, lv.d_pairs, lv.d_pm, lv.d_segs, lv.d_sig
-        d_sm, d_stats, d_w, d_w32, exchange, fb_jobs = lv.d_sm, lv.d_stats, lv.d_w, lv.d_w32, lv.exchange, lv.fb_jobs
-        fit_ids, g_arr, groups, h_arr, hist_mode, histories = lv.fit_ids, lv.g_arr, lv.groups, lv.h_arr, lv.hist_mode, lv.histories
-        history, inj, jobs, lat_off, lat_ready, max_obs = lv.history, lv.inj, lv.jobs, lv.lat_off, lv.lat_ready, lv.max_obs
-        n_comp, n_jobs, n_obs_total, n_rows, nfs, o_cand = lv.n_comp, lv.n_jobs, lv.n_obs_total, lv.n_rows, lv.nfs, lv.o_cand
-        o_cobs, o_fb, o_g, o_h, o_isb, o_jobs = lv.o_cobs, lv.o_fb, lv.o_g, lv.o_h, lv.o_isb, lv.o_jobs
-        o_lcnt, o_obs, o_p, o_rows, o_slot, o_xslot = lv.o_lcnt, lv.o_obs, lv.o_p, lv.o_rows, lv.o_slot, lv.o_xslot
-        out_off, outputs, p_pool, posteriors, precision, qfb_off = lv.out_off, lv.outputs, lv.p_pool, lv.posteriors, lv.precision, lv.qfb_off
-        sample_only, segs, sort_off, sorted_fit, sp, stream = lv.sample_only, lv.segs, lv.sort_off, lv.sorted_fit, lv.sp, lv.stream
-        table_scores, torch, works, x_comm, x_labels, x_world = lv.table_scores, lv.torch, lv.works, lv.x_comm, lv.x_labels, lv.x_world
-        tick, tock, stream_order = ctx.tick, ctx.tock, ctx.stream_order
-        stream_rec, stream_wait = ctx.stream_rec, ctx.stream_wait
+        sp, cat, groups, hist_mode = lv.sp, lv.cat, lv.groups, lv.hist_mode
         side = None
-        if self.side_stream != "0" and not sample_only and not posteriors and any(
+        if self.side_stream != "0" and not lv.sample_only and not lv.posteriors and any(
                 ids for k, ids in groups if k in SIDE_KINDS):
             if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
+                self._side = lv.torch.cuda.Stream(self.device)
             side = self._side
         side_p = ctypes.c_void_p(side.cuda_stream) if side is not None else sp
-        # with the sorted fit the gather only lists the categorical labels'
-        # observations, which only their posterior (side stream) reads: it
-        # runs there, behind an event after the upload, and the main
-        # stream starts with the fit
-        gather_side = hist_mode and histories is None and sorted_fit and \
-            side is not None and bool(cat) and self.cat_early
-        # the categorical posteriors can count their labels in the history
-        # itself (no gathered lists): the gather then lists only the fit's
-        # sets, and none with the sorted fit (it reads the history itself)
-        cat_hist = hist_mode and histories is None and bool(cat) and self.cat_hist
-        g0 = nfs if sorted_fit else 0
-        g1 = nfs if cat_hist else (len(g_arr) if g_arr is not None else 0)
-        # (the categorical descriptors follow the fit's)
-        if hist_mode:
-            d_obs = self._buf("obs_dev", 8 * max(n_obs_total, 1))
-            d_cobs = self._buf("cobs_dev", 8 * max(cobs_off, 1))
-            gs, gsp = (side, side_p) if gather_side else (None, sp)
-            if gather_side:
-                stream_order("uploaded", sp, side_p)
-            e0 = tick("gather", gs)
-            if histories is None:
-                if g1 > g0:
-                    L.check(lib.tpe_gather_obs(history.vals.data_ptr(),
-                                               history.active.data_ptr(), history.ld,
-                                               base + o_rows if o_rows is not None else None,
-                                               _V("n_rows", n_rows), base + o_isb,
-                                               base + o_g + g0 * L.GATHER_DTYPE.itemsize,
-                                               g_arr.ctypes.data + g0 * L.GATHER_DTYPE.itemsize,
-                                               g1 - g0, d_obs, d_cobs, d_err, gsp),
-                            "tpe_gather_obs")
-            else:
-                L.check(lib.tpe_gather_obs_multi(base + o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
-                                                 len(h_arr), base, base + o_g,
-                                                 g_arr.ctypes.data_as(ctypes.c_void_p),
-                                                 len(g_arr), d_obs, d_cobs, d_err, sp),
-                        "tpe_gather_obs_multi")
-            tock("gather", e0, gs)
-        else:
-            d_obs, d_cobs = base + o_obs, base + o_cobs
-
-        _hmark('upload+gather')
+        st = _LaunchState(
+            lib=lib, ctx=ctx, side=side, side_p=side_p,
+            # with the sorted fit the gather only lists the categorical labels'
+            # observations, which only their posterior (side stream) reads: it
+            # runs there, behind an event after the upload, and the main
+            # stream starts with the fit
+            gather_side=hist_mode and lv.histories is None and lv.sorted_fit and
+            side is not None and bool(cat) and self.cat_early,
+            # the categorical posteriors can count their labels in the history
+            # itself (no gathered lists): the gather then lists only the fit's
+            # sets, and none with the sorted fit (it reads the history itself)
+            cat_hist=hist_mode and lv.histories is None and bool(cat) and self.cat_hist,
+            # categorical labels need only the gathered lists: with cat_early
+            # the side stream starts their posterior and scoring from an event
+            # recorded after the gather, so they run beside the latency-bound
+            # fit kernels instead of the VALU-bound table build and scorer
+            # (issued on the host after the fit's launches: the fit is not
+            # delayed, and the table build still reaches the GPU before the
+            # fit ends)
+            cat_early=side is not None and bool(cat) and self.cat_early,
+            joined=side is None, side_started=side is None, cat_started=False,
+            table_calls=[], jobs_ptr=lv.jobs.__array_interface__["data"][0],
+            d_obs=None, d_cobs=None)
+        self._launch_gather(lv, st)
+        lv._hmark('upload+gather')
         # side stream (TPE_SIDE_STREAM != "0"): quantized and categorical work
         # overlaps the continuous pipeline; the categorical posterior starts on
         # it as soon as the lists are gathered (it needs nothing else)
@@ -1418,313 +1410,390 @@ class Engine:
         # from one event recorded on the main stream after the fit (the
         # categorical posterior could start at the gather, but the side
         # stream has the slack and the fork costs two more host calls)
-        d_cand = base + o_cand
-        d_bl = d_al = d_x = None
-        d_sc = d_eps = None
-        if outputs:
-            d_bl = self._buf("out_bl", 8 * max(out_off, 1))
-            d_al = self._buf("out_al", 8 * max(out_off, 1))
-            d_x = self._buf("out_x", 8 * max(out_off, 1))
-        elif table_scores:
-            d_sc = self._buf("out_sc", 8 * max(out_off, 1))
-            d_x = self._buf("out_x", 8 * max(out_off, 1))
-            d_eps = self._buf("out_eps", 8 * max(out_off, 1))
-        table_calls = []
-        band_jobs.clear()
-        jobs_ptr = jobs.__array_interface__["data"][0]
-        joined = side is None
-        side_started = side is None
-        cat_started = False
-
-        def cat_fit():  # on the side stream (after its fork)
-            e0 = tick("cat_fit", side)
-            d_p = base + o_p  # the posterior is formed in place in the staged pool
-            if cat_hist:  # (the categorical gather descriptors follow the fit's nfs)
-                L.check(lib.tpe_cat_posterior_hist(
-                    history.vals.data_ptr(), history.active.data_ptr(), history.ld,
-                    base + o_rows if o_rows is not None else None, _V("n_rows", n_rows),
-                    base + o_isb, base + o_g + nfs * L.GATHER_DTYPE.itemsize, d_csegs,
-                    len(csegs), int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf, d_err, side_p),
-                    "tpe_cat_posterior_hist")
-            else:
-                L.check(lib.tpe_cat_posterior(d_cobs, d_csegs, len(csegs),
-                                              int(csegs["n_cat"].max()), d_p, d_logp, d_ccdf,
-                                              side_p), "tpe_cat_posterior")
-            tock("cat_fit", e0, side)
-
-        def launch_group(g, stage):
-            nonlocal joined, side_started, cat_started
-            kind, ids = groups[g]
-            if not ids:
-                return
-            if cat_early and kind == "cat" and not cat_started:
-                cat_started = True  # the categorical work needs only the gather
-                if not gather_side:  # (else the gather ran on the side stream)
-                    stream_wait("gathered", side_p)
-                cat_fit()
-            if not side_started and kind in SIDE_KINDS and not (cat_early and kind == "cat"):
-                side_started = True  # the side stream's groups that need the fit
-                stream_wait("fitted", side_p)
-                if cat and not cat_early:
-                    cat_fit()
-            if sample_only:
-                if kind in ("cont", "lat", "qfb"):
-                    a, b = _slice_of(groups, g)
-                    hj = jobs[a:b]
-                    L.check(lib.tpe_sample(base + o_jobs + a * L.JOB_DTYPE.itemsize,
-                                           hj.ctypes.data_as(ctypes.c_void_p), b - a, d_segs,
-                                           d_mu, d_sig, d_cdf, precision, d_x, sp), "tpe_sample")
-                return
-            a, b = _slice_of(groups, g)
-            hj = jobs[a:b]
-            hjp = jobs_ptr + a * JS  # host copy of the slice (plain int: no ctypes object)
-            dj = base + o_jobs + a * JS
-            db = d_best + a * BS
-            nj = b - a
-            on_side = side is not None and kind in SIDE_KINDS
-            ks = side_p if on_side else sp
-            kst = side if on_side else None
-            pname = "partial_side" if on_side else "partial"
-            e0 = tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst) \
-                if stage != "score" else None
-            if kind == "cont":
-                npart = lib.tpe_score_partials(hjp, nj)
-                d_part = self._buf("partial", 32 * max(npart, 1))
-                L.check(lib.tpe_score_continuous(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
-                                                 d_c64, d_c32, d_cand, precision, d_bl, d_al, d_x,
-                                                 d_part, npart, db, sp), "tpe_score_continuous")
-            elif kind == "sorted":
-                npart = lib.tpe_score_partials(hjp, nj) * 2
-                d_part = self._buf("partial", 32 * max(npart, 1))
-                d_cnt = self._buf("sort_cnt", 8 * max(cnt_off, 1))
-                d_gen = self._buf("sort_gen", 4 * max(sort_off, 1))
-                d_sx = self._buf("sort_x", 4 * max(sort_off, 1))
-                d_si = self._buf("sort_i", 4 * max(sort_off, 1))
-                L.check(lib.tpe_sort_candidates(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_cnt,
-                                                d_gen, d_sx, d_si, sp), "tpe_sort_candidates")
-                tock("sort", e0)
-                e0 = tick("sorted")
-                L.check(lib.tpe_score_sorted(dj, hjp, nj, d_segs, d_c32, d_c32n, d_w32, d_pm,
-                                             d_sm, d_sx, d_si, d_part, npart, db, d_pairs, sp),
-                        "tpe_score_sorted")
-            elif kind == "table":
-                # (stage "build" / "score": the two halves of an early-built group)
-                npart = lib.tpe_table_partials(hjp, nj)
-                d_part = self._buf("partial", 32 * max(npart, 1))
-                d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
-                d_cells = self._buf("cells", 128 * int(hj["tbl_off"].max() + TABLE_CAP
-                                                       - hj["tbl_off"].min()))
-                d_cells -= 128 * int(hj["tbl_off"].min())
-                d_rh = self._buf("reach_hi", 8 * n_comp)
-                d_rl = self._buf("reach_lo", 8 * n_comp)
-                d_wide = self._buf("wide_idx", 4 * n_comp)
-                max_comp = _V("max_comp", max_obs + 1)
-                d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
-                if stage != "score":
-                    L.check(lib.tpe_table_build(dj, hjp, nj, d_segs, d_mu, d_sig, d_c64,
-                                                max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab,
-                                                d_cells, d_stats, sp), "tpe_table_build")
-                    tock("table_build", e0)
-                if stage == "build":
-                    return
-                if not joined and self.side_stream == "2":
-                    stream_order("joined", side_p, sp)
-                    joined = True
-                e0 = tick("table")
-                if outputs or inj(ids[0]) or self.table_scorer == "poly":
-                    L.check(lib.tpe_score_table(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c32,
-                                                d_tab, d_cells, d_cand, d_bl, d_al, d_x, d_part,
-                                                npart, db, d_stats, sp), "tpe_score_table")
-                else:  # the suggest path: one score cubic per candidate, exact argmax
-                    ctl_b, work_b = ctypes.c_int64(0), ctypes.c_int64(0)
-                    nbb = lib.tpe_band_bytes(hjp, nj, ctypes.byref(ctl_b),
-                                             ctypes.byref(work_b))
-                    d_band = self._buf("band", nbb)
-                    d_bctl = self._buf("band_ctl", ctl_b.value)
-                    d_bwork = self._zbuf("band_work", work_b.value)
-                    L.check(lib.tpe_score_table_fast(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
-                                                     d_c32, d_tab, d_cells, d_band, d_bctl,
-                                                     d_sc, d_x, d_eps, d_part, npart,
-                                                     BAND_TILE_CAP, d_stats, sp),
-                            "tpe_score_table_fast")
-                    tock("table", e0)
-                    self._tables_slice = (a, b)  # (the test hook reads these tables back)
-                    e0 = tick("band")
-                    L.check(lib.tpe_band_rescore(dj, hjp, nj, d_segs, d_c64, d_tab, d_band,
-                                                 d_bctl, d_part, npart, db, d_bwork, sp),
-                            "tpe_band_rescore")
-                    tock("band", e0)
-                    e0 = None
-                    band_jobs.append((a, b))
-                table_calls.append(nj)
-            elif kind == "pruned64":
-                npart = lib.tpe_pruned64_partials(hjp, nj)
-                d_part = self._buf("partial", 32 * max(npart, 1))
-                d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
-                d_rh = self._buf("reach_hi", 8 * n_comp)
-                d_rl = self._buf("reach_lo", 8 * n_comp)
-                d_wide = self._buf("wide_idx", 4 * n_comp)
-                max_comp = _V("max_comp", max_obs + 1)
-                d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
-                L.check(lib.tpe_score_pruned64(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf, d_c64,
-                                               max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab, d_cand,
-                                               d_bl, d_al, d_x, d_part, npart, db, sp),
-                        "tpe_score_pruned64")
-            elif kind == "lat":
-                # the lattice values' component windows (k_qreach, on the
-                # quantized jobs' own components of the reach arrays)
-                d_rh = self._buf("reach_hi", 8 * n_comp)
-                d_rl = self._buf("reach_lo", 8 * n_comp)
-                d_vals = self._buf("lat_vals", 8 * lat_off)
-                d_first = self._buf("lat_first", 8 * lat_off)
-                if lat_ready:
-                    d_slot, d_cnt = base + o_slot, base + o_lcnt
-                else:
-                    d_slot = self._buf("lat_slot", 8 * lat_off)
-                    d_cnt = self._buf("lat_cnt", 8 * nj)
-                max_vals = int(hj["lat_n"].max())
-                if self.lat_prefix and max_vals <= LAT_SUGGEST_MAX_SLOTS and \
-                        int(hj["n_cand"].max()) > self.lat_prefix:
-                    # prefix first: the rest of a stream only where an unseen
-                    # value could still win (tpe_lattice_suggest)
-                    npart = nj * max_vals
-                    d_part = self._buf(pname, 32 * npart)
-                    d_need = self._buf("lat_need", 4 * nj)
-                    L.check(lib.tpe_lattice_suggest(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, d_cdf,
-                                                    d_slot, self.lat_prefix, d_part, npart,
-                                                    d_need, db, d_err, d_rh, d_rl, ks),
-                            "tpe_lattice_suggest")
-                else:
-                    L.check(lib.tpe_lattice_sample(dj, hjp, nj, d_segs, d_mu, d_sig, d_cdf,
-                                                   d_slot, d_err, ks), "tpe_lattice_sample")
-                    L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt,
-                                                    ks), "tpe_lattice_compact")
-                    npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                    d_part = self._buf(pname, 32 * max(npart, 1))
-                    L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig,
-                                                    d_vals, d_first, d_cnt, max_vals, None, None,
-                                                    d_part, npart, db, d_err, d_rh, d_rl, ks),
-                            "tpe_score_quantized")
-            elif kind in ("qfb", "qinj"):
-                d_rh = self._buf("reach_hi", 8 * n_comp)
-                d_rl = self._buf("reach_lo", 8 * n_comp)
-                vals = d_cand
-                if kind == "qfb":
-                    vals = self._buf("q_cand", 8 * max(qfb_off, 1))
-                    L.check(lib.tpe_sample(base + o_fb, fb_jobs.ctypes.data_as(ctypes.c_void_p),
-                                           nj, d_segs, d_mu, d_sig, d_cdf, 64, vals, ks),
-                            "tpe_sample")
-                max_vals = int(hj["n_cand"].max())
-                npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
-                d_part = self._buf(pname, 32 * max(npart, 1))
-                L.check(lib.tpe_score_quantized(dj, hjp, nj, d_segs, d_w, d_mu, d_sig, vals, None,
-                                                None, max_vals, d_bl, d_al, d_part, npart, db,
-                                                d_err, d_rh, d_rl, ks), "tpe_score_quantized")
-            else:
-                npart = lib.tpe_categorical_partials(hjp, nj)
-                d_part = self._buf(pname, 32 * max(npart, 1))
-                if self.lat_prefix and not inj(ids[0]) and d_bl is None and d_x is None and \
-                        int(hj["n_cand"].max()) > self.lat_prefix:
-                    # prefix first: the rest of a stream only where an unseen
-                    # better category could still be drawn (tpe_categorical_suggest)
-                    d_need = self._buf("cat_need", 4 * nj)
-                    L.check(lib.tpe_categorical_suggest(dj, hjp, nj, d_csegs, d_logp, d_ccdf,
-                                                        self.lat_prefix, d_part, npart, d_need,
-                                                        db, ks), "tpe_categorical_suggest")
-                else:
-                    L.check(lib.tpe_score_categorical(dj, hjp, nj, d_csegs, d_logp, d_ccdf,
-                                                      d_cand, d_bl, d_al, d_x, d_part, npart,
-                                                      db, ks), "tpe_score_categorical")
-            tock(kind, e0, kst)
-
-        # categorical labels need only the gathered lists: with cat_early
-        # the side stream starts their posterior and scoring from an event
-        # recorded after the gather, so they run beside the latency-bound
-        # fit kernels instead of the VALU-bound table build and scorer
-        # (issued on the host after the fit's launches: the fit is not
-        # delayed, and the table build still reaches the GPU before the
-        # fit ends)
-        cat_early = side is not None and bool(cat) and self.cat_early
-        if cat_early:
-            if not gather_side:
-                stream_rec("gathered", sp)
+        st.d_cand = lv.base + lv.o_cand
+        st.d_bl = st.d_al = st.d_x = st.d_sc = st.d_eps = None
+        if lv.outputs:
+            st.d_bl = self._buf("out_bl", 8 * max(lv.out_off, 1))
+            st.d_al = self._buf("out_al", 8 * max(lv.out_off, 1))
+            st.d_x = self._buf("out_x", 8 * max(lv.out_off, 1))
+        elif lv.table_scores:
+            st.d_sc = self._buf("out_sc", 8 * max(lv.out_off, 1))
+            st.d_x = self._buf("out_x", 8 * max(lv.out_off, 1))
+            st.d_eps = self._buf("out_eps", 8 * max(lv.out_off, 1))
+        lv.band_jobs.clear()
+        if st.cat_early:
+            if not st.gather_side:
+                ctx.stream_rec("gathered", sp)
             if self.cat_issue == "pre":  # issued before the fit's launches
                 for g, (k, ids) in enumerate(groups):
                     if k == "cat" and ids:
-                        launch_group(g, "all")
-        # ---- posterior fit ------------------------------------------------------
-        if fit_ids and sorted_fit:
-            e0 = tick("fit")
-            d_fss = self._buf("fit_sorted_scratch",
-                              lib.tpe_fit_sorted_scratch_bytes(len(segs), n_rows))
-            L.check(lib.tpe_fit_sorted(history.vals.data_ptr(), history.active.data_ptr(),
-                                       history.ld, history.order.data_ptr(),
-                                       _V("n_rows", n_rows),
-                                       base + o_isb, base + o_g, g_arr.ctypes.data, d_segs,
-                                       len(segs), d_fss, d_w, d_mu, d_sig, d_cdf, d_c64,
-                                       d_c32, d_err, sp), "tpe_fit_sorted")
-            tock("fit", e0)
-        elif fit_ids:
-            e0 = tick("fit")
-            L.check(lib.tpe_parzen_fit(d_obs, d_fs, d_segs, len(segs), _V("max_obs", max_obs),
-                                       _V("n_obs_total", n_obs_total),
-                                       d_w, d_mu, d_sig, d_cdf, d_c64, d_c32, d_c32n, d_w32,
-                                       d_pm, d_sm, sp), "tpe_parzen_fit")
-            tock("fit", e0)
-
+                        self._launch_group(lv, st, g, "all")
+        self._launch_fit(lv, st)
         if cat and side is None:
-            cat_fit()
-
-        if posteriors:
-            return self._read_posteriors(works, fit_ids, cat, segs, csegs, n_comp, p_pool.size,
-                                         d_segs, stream, o_p), True
-
-        _hmark('jobs')
-
-        _hmark('fit')
+            self._cat_fit(lv, st)
+        if lv.posteriors:
+            return self._read_posteriors(lv.works, lv.fit_ids, cat, lv.segs, lv.csegs,
+                                         lv.n_comp, lv.p_pool.size, lv.d_segs, lv.stream,
+                                         lv.o_p), True
+        lv._hmark('jobs')
+        lv._hmark('fit')
         # ---- scoring, one call per group ----------------------------------------
         # quantized and categorical groups go to the side stream (after the job
         # table has landed); continuous groups stay on `stream`
         if side is not None:  # quantized groups need the continuous fit
-            stream_rec("fitted", sp)
-        # launch order: the first sampled table group's build (the main
-        # stream's next kernels after the fit), then the side groups, then
-        # the main-stream scorers -- the host issues launches at a few us
-        # each, and at a one-eighth label share the main stream would
-        # otherwise sit idle behind the side stream's launches
-        g_order = [(g, "all") for g in range(len(groups))]
+            ctx.stream_rec("fitted", sp)
+        for g, stage in self._group_order(lv, st):
+            self._launch_group(lv, st, g, stage)
+        if not st.side_started:  # (no side group: only the categorical posterior)
+            if cat and not st.cat_early:
+                self._cat_fit(lv, st)
+        if not st.joined:  # join before the readback
+            ctx.stream_order("joined", side_p, sp)
+        if lv.exchange is not None:  # label-sharded level: the cross-rank argmax
+            BS = lv.BS
+            d_xl = self._buf("xchg_local", lv.x_labels * BS)
+            d_xg = self._buf("xchg_gathered", lv.x_world * lv.x_labels * BS)
+            L.check(lib.tpe_best_scatter(lv.d_best, lv.base + lv.o_xslot, lv.n_jobs, d_xl,
+                                         lv.x_labels, sp), "tpe_best_scatter")
+            L.check(lib.tpe_maxloc_allreduce(d_xl, d_xg, lv.d_best + lv.n_jobs * BS,
+                                             lv.x_labels, lv.x_comm, sp),
+                    "tpe_maxloc_allreduce")
+        return st.table_calls, False
+
+    def _group_order(self, lv, st):
+        """(group, stage) in host issue order.  Without a side stream: group
+        order.  With one: the first sampled table group's build (the main
+        stream's next kernels after the fit), then the side groups, then the
+        main-stream scorers -- the host issues launches at a few us each, and
+        at a one-eighth label share the main stream would otherwise sit idle
+        behind the side stream's launches."""
+        groups, inj = lv.groups, lv.inj
+        if st.side is None:
+            return [(g, "all") for g in range(len(groups))]
         early = None
         tgroups = [g for g, (k, ids) in enumerate(groups) if k == "table" and ids]
-        if side is not None:
-            if len(tgroups) == 1 and not inj(groups[tgroups[0]][1][0]):
-                early = tgroups[0]  # (one table group: the workspace tables are its own)
-            side_gs = [g for g in range(len(groups)) if groups[g][0] in SIDE_KINDS]
-            # categorical groups first, issued right after the fit's
-            # launches (they wait for the gather only, so they run beside
-            # the fit; the table build is still issued before the fit ends)
-            cat_gs = [g for g in side_gs if cat_early and groups[g][0] == "cat"]
-            pre = [(g, "all") for g in cat_gs] if self.cat_issue == "post" else []
-            late = [(g, "all") for g in cat_gs] if self.cat_issue == "late" else []
-            g_order = pre + ([(early, "build")] if early is not None else []) + late + \
-                [(g, "all") for g in side_gs if g not in cat_gs] + \
-                [(g, "score" if g == early else "all") for g in range(len(groups))
-                 if groups[g][0] not in SIDE_KINDS]
-        for g, stage in g_order:
-            launch_group(g, stage)
+        if len(tgroups) == 1 and not inj(groups[tgroups[0]][1][0]):
+            early = tgroups[0]  # (one table group: the workspace tables are its own)
+        side_gs = [g for g in range(len(groups)) if groups[g][0] in SIDE_KINDS]
+        # categorical groups first, issued right after the fit's launches
+        # (they wait for the gather only, so they run beside the fit; the
+        # table build is still issued before the fit ends)
+        cat_gs = [g for g in side_gs if st.cat_early and groups[g][0] == "cat"]
+        pre = [(g, "all") for g in cat_gs] if self.cat_issue == "post" else []
+        late = [(g, "all") for g in cat_gs] if self.cat_issue == "late" else []
+        return pre + ([(early, "build")] if early is not None else []) + late + \
+            [(g, "all") for g in side_gs if g not in cat_gs] + \
+            [(g, "score" if g == early else "all") for g in range(len(groups))
+             if groups[g][0] not in SIDE_KINDS]
 
-        if not side_started:  # (no side group: only the categorical posterior)
-            if cat and not cat_early:
-                cat_fit()
-        if not joined:  # join before the readback
-            stream_order("joined", side_p, sp)
-        if exchange is not None:  # label-sharded level: the cross-rank argmax
-            d_xl = self._buf("xchg_local", x_labels * BS)
-            d_xg = self._buf("xchg_gathered", x_world * x_labels * BS)
-            L.check(lib.tpe_best_scatter(d_best, base + o_xslot, n_jobs, d_xl, x_labels, sp),
-                    "tpe_best_scatter")
-            L.check(lib.tpe_maxloc_allreduce(d_xl, d_xg, d_best + n_jobs * BS, x_labels,
-                                             x_comm, sp), "tpe_maxloc_allreduce")
-        return table_calls, False
+    def _launch_gather(self, lv, st):
+        """The observation lists of the level's fit and categorical sets
+        (tpe_gather_obs / tpe_gather_obs_multi), or the uploaded lists."""
+        lib, ctx, sp = st.lib, st.ctx, lv.sp
+        if not lv.hist_mode:
+            st.d_obs, st.d_cobs = lv.base + lv.o_obs, lv.base + lv.o_cobs
+            return
+        nfs, g_arr, base, history = lv.nfs, lv.g_arr, lv.base, lv.history
+        g0 = nfs if lv.sorted_fit else 0
+        g1 = nfs if st.cat_hist else (len(g_arr) if g_arr is not None else 0)
+        # (the categorical descriptors follow the fit's)
+        st.d_obs = d_obs = self._buf("obs_dev", 8 * max(lv.n_obs_total, 1))
+        st.d_cobs = d_cobs = self._buf("cobs_dev", 8 * max(lv.cobs_off, 1))
+        gs, gsp = (st.side, st.side_p) if st.gather_side else (None, sp)
+        if st.gather_side:
+            ctx.stream_order("uploaded", sp, st.side_p)
+        e0 = ctx.tick("gather", gs)
+        if lv.histories is None:
+            if g1 > g0:
+                GI = L.GATHER_DTYPE.itemsize
+                L.check(lib.tpe_gather_obs(history.vals.data_ptr(), history.active.data_ptr(),
+                                           history.ld,
+                                           base + lv.o_rows if lv.o_rows is not None else None,
+                                           _V("n_rows", lv.n_rows), base + lv.o_isb,
+                                           base + lv.o_g + g0 * GI, g_arr.ctypes.data + g0 * GI,
+                                           g1 - g0, d_obs, d_cobs, lv.d_err, gsp),
+                        "tpe_gather_obs")
+        else:
+            h_arr = lv.h_arr
+            L.check(lib.tpe_gather_obs_multi(base + lv.o_h, h_arr.ctypes.data_as(ctypes.c_void_p),
+                                             len(h_arr), base, base + lv.o_g,
+                                             g_arr.ctypes.data_as(ctypes.c_void_p),
+                                             len(g_arr), d_obs, d_cobs, lv.d_err, sp),
+                    "tpe_gather_obs_multi")
+        ctx.tock("gather", e0, gs)
+
+    def _launch_fit(self, lv, st):
+        """The continuous labels' posterior fit: tpe_fit_sorted (reads the
+        history in its value order) or tpe_parzen_fit (the gathered lists)."""
+        if not lv.fit_ids:
+            return
+        lib, ctx, sp = st.lib, st.ctx, lv.sp
+        e0 = ctx.tick("fit")
+        if lv.sorted_fit:
+            history = lv.history
+            d_fss = self._buf("fit_sorted_scratch",
+                              lib.tpe_fit_sorted_scratch_bytes(len(lv.segs), lv.n_rows))
+            L.check(lib.tpe_fit_sorted(history.vals.data_ptr(), history.active.data_ptr(),
+                                       history.ld, history.order.data_ptr(),
+                                       _V("n_rows", lv.n_rows),
+                                       lv.base + lv.o_isb, lv.base + lv.o_g, lv.g_arr.ctypes.data,
+                                       lv.d_segs, len(lv.segs), d_fss, lv.d_w, lv.d_mu, lv.d_sig,
+                                       lv.d_cdf, lv.d_c64, lv.d_c32, lv.d_err, sp),
+                    "tpe_fit_sorted")
+        else:
+            L.check(lib.tpe_parzen_fit(st.d_obs, lv.d_fs, lv.d_segs, len(lv.segs),
+                                       _V("max_obs", lv.max_obs),
+                                       _V("n_obs_total", lv.n_obs_total),
+                                       lv.d_w, lv.d_mu, lv.d_sig, lv.d_cdf, lv.d_c64, lv.d_c32,
+                                       lv.d_c32n, lv.d_w32, lv.d_pm, lv.d_sm, sp),
+                    "tpe_parzen_fit")
+        ctx.tock("fit", e0)
+
+    def _cat_fit(self, lv, st):
+        """The categorical posteriors (on the side stream, after its fork):
+        counted in the history itself (tpe_cat_posterior_hist) or from the
+        gathered lists (tpe_cat_posterior)."""
+        lib, ctx, side, side_p, csegs = st.lib, st.ctx, st.side, st.side_p, lv.csegs
+        e0 = ctx.tick("cat_fit", side)
+        d_p = lv.base + lv.o_p  # the posterior is formed in place in the staged pool
+        if st.cat_hist:  # (the categorical gather descriptors follow the fit's nfs)
+            history = lv.history
+            L.check(lib.tpe_cat_posterior_hist(
+                history.vals.data_ptr(), history.active.data_ptr(), history.ld,
+                lv.base + lv.o_rows if lv.o_rows is not None else None, _V("n_rows", lv.n_rows),
+                lv.base + lv.o_isb, lv.base + lv.o_g + lv.nfs * L.GATHER_DTYPE.itemsize,
+                lv.d_csegs, len(csegs), int(csegs["n_cat"].max()), d_p, lv.d_logp, lv.d_ccdf,
+                lv.d_err, side_p), "tpe_cat_posterior_hist")
+        else:
+            L.check(lib.tpe_cat_posterior(st.d_cobs, lv.d_csegs, len(csegs),
+                                          int(csegs["n_cat"].max()), d_p, lv.d_logp, lv.d_ccdf,
+                                          side_p), "tpe_cat_posterior")
+        ctx.tock("cat_fit", e0, side)
+
+    def _launch_group(self, lv, st, g, stage):
+        """One group's scorer launches (``stage``: "all", or "build" / "score"
+        -- the two halves of an early-built table group), after the side
+        stream's fork where the group is the first to need it."""
+        kind, ids = lv.groups[g]
+        if not ids:
+            return
+        ctx = st.ctx
+        if st.cat_early and kind == "cat" and not st.cat_started:
+            st.cat_started = True  # the categorical work needs only the gather
+            if not st.gather_side:  # (else the gather ran on the side stream)
+                ctx.stream_wait("gathered", st.side_p)
+            self._cat_fit(lv, st)
+        if not st.side_started and kind in SIDE_KINDS and not (st.cat_early and kind == "cat"):
+            st.side_started = True  # the side stream's groups that need the fit
+            ctx.stream_wait("fitted", st.side_p)
+            if lv.cat and not st.cat_early:
+                self._cat_fit(lv, st)
+        a, b = _slice_of(lv.groups, g)
+        if lv.sample_only:
+            if kind in ("cont", "lat", "qfb"):
+                L.check(st.lib.tpe_sample(lv.base + lv.o_jobs + a * L.JOB_DTYPE.itemsize,
+                                          lv.jobs[a:b].ctypes.data_as(ctypes.c_void_p), b - a,
+                                          lv.d_segs, lv.d_mu, lv.d_sig, lv.d_cdf, lv.precision,
+                                          st.d_x, lv.sp), "tpe_sample")
+            return
+        on_side = st.side is not None and kind in SIDE_KINDS
+        kst = st.side if on_side else None
+        sl = _LaunchState(
+            kind=kind, ids=ids, a=a, b=b, nj=b - a, hj=lv.jobs[a:b],
+            hjp=st.jobs_ptr + a * lv.JS,  # host copy of the slice (plain int: no ctypes object)
+            dj=lv.base + lv.o_jobs + a * lv.JS, db=lv.d_best + a * lv.BS,
+            ks=st.side_p if on_side else lv.sp,
+            pname="partial_side" if on_side else "partial", stage=stage,
+            e0=ctx.tick({"sorted": "sort", "table": "table_build"}.get(kind, kind), kst)
+            if stage != "score" else None)
+        e0 = _GROUP_LAUNCH[kind](self, lv, st, sl)
+        ctx.tock(kind, e0, kst)
+
+    def _score_cont(self, lv, st, sl):
+        """Dense scoring of continuous labels (k_score64 / k_score32)."""
+        npart = st.lib.tpe_score_partials(sl.hjp, sl.nj)
+        d_part = self._buf("partial", 32 * max(npart, 1))
+        L.check(st.lib.tpe_score_continuous(sl.dj, sl.hjp, sl.nj, lv.d_segs, lv.d_w, lv.d_mu,
+                                            lv.d_sig, lv.d_cdf, lv.d_c64, lv.d_c32, st.d_cand,
+                                            lv.precision, st.d_bl, st.d_al, st.d_x, d_part,
+                                            npart, sl.db, lv.sp), "tpe_score_continuous")
+        return sl.e0
+
+    def _score_sorted(self, lv, st, sl):
+        """Bucketed candidates with component pruning (tpe_sort_candidates +
+        tpe_score_sorted)."""
+        lib, ctx, sp = st.lib, st.ctx, lv.sp
+        npart = lib.tpe_score_partials(sl.hjp, sl.nj) * 2
+        d_part = self._buf("partial", 32 * max(npart, 1))
+        d_cnt = self._buf("sort_cnt", 8 * max(lv.cnt_off, 1))
+        d_gen = self._buf("sort_gen", 4 * max(lv.sort_off, 1))
+        d_sx = self._buf("sort_x", 4 * max(lv.sort_off, 1))
+        d_si = self._buf("sort_i", 4 * max(lv.sort_off, 1))
+        L.check(lib.tpe_sort_candidates(sl.dj, sl.hjp, sl.nj, lv.d_segs, lv.d_mu, lv.d_sig,
+                                        lv.d_cdf, d_cnt, d_gen, d_sx, d_si, sp),
+                "tpe_sort_candidates")
+        ctx.tock("sort", sl.e0)
+        e0 = ctx.tick("sorted")
+        L.check(lib.tpe_score_sorted(sl.dj, sl.hjp, sl.nj, lv.d_segs, lv.d_c32, lv.d_c32n,
+                                     lv.d_w32, lv.d_pm, lv.d_sm, d_sx, d_si, d_part, npart,
+                                     sl.db, lv.d_pairs, sp), "tpe_score_sorted")
+        return e0
+
+    def _score_table(self, lv, st, sl):
+        """The cell-table path: tpe_table_build, then tpe_score_table (per-
+        candidate outputs, injected candidates) or the suggest path's fp32
+        cubic scorer + exact fp64 band re-score (tpe_score_table_fast +
+        tpe_band_rescore).  Stage "build" / "score": the two halves of an
+        early-built group."""
+        lib, ctx, sp = st.lib, st.ctx, lv.sp
+        hj, hjp, dj, nj, stage, n_comp = sl.hj, sl.hjp, sl.dj, sl.nj, sl.stage, lv.n_comp
+        npart = lib.tpe_table_partials(hjp, nj)
+        d_part = self._buf("partial", 32 * max(npart, 1))
+        d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * nj)
+        d_cells = self._buf("cells", 128 * int(hj["tbl_off"].max() + TABLE_CAP
+                                               - hj["tbl_off"].min()))
+        d_cells -= 128 * int(hj["tbl_off"].min())
+        d_rh = self._buf("reach_hi", 8 * n_comp)
+        d_rl = self._buf("reach_lo", 8 * n_comp)
+        d_wide = self._buf("wide_idx", 4 * n_comp)
+        max_comp = _V("max_comp", lv.max_obs + 1)
+        d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(nj, max_comp))
+        if stage != "score":
+            L.check(lib.tpe_table_build(dj, hjp, nj, lv.d_segs, lv.d_mu, lv.d_sig, lv.d_c64,
+                                        max_comp, d_rh, d_rl, d_wide, d_tsc, d_tab, d_cells,
+                                        lv.d_stats, sp), "tpe_table_build")
+            ctx.tock("table_build", sl.e0)
+        if stage == "build":
+            return None
+        if not st.joined and self.side_stream == "2":
+            ctx.stream_order("joined", st.side_p, sp)
+            st.joined = True
+        e0 = ctx.tick("table")
+        if lv.outputs or lv.inj(sl.ids[0]) or self.table_scorer == "poly":
+            L.check(lib.tpe_score_table(dj, hjp, nj, lv.d_segs, lv.d_mu, lv.d_sig, lv.d_cdf,
+                                        lv.d_c32, d_tab, d_cells, st.d_cand, st.d_bl, st.d_al,
+                                        st.d_x, d_part, npart, sl.db, lv.d_stats, sp),
+                    "tpe_score_table")
+        else:  # the suggest path: one score cubic per candidate, exact argmax
+            ctl_b, work_b = ctypes.c_int64(0), ctypes.c_int64(0)
+            nbb = lib.tpe_band_bytes(hjp, nj, ctypes.byref(ctl_b), ctypes.byref(work_b))
+            d_band = self._buf("band", nbb)
+            d_bctl = self._buf("band_ctl", ctl_b.value)
+            d_bwork = self._zbuf("band_work", work_b.value)
+            L.check(lib.tpe_score_table_fast(dj, hjp, nj, lv.d_segs, lv.d_mu, lv.d_sig,
+                                             lv.d_cdf, lv.d_c32, d_tab, d_cells, d_band, d_bctl,
+                                             st.d_sc, st.d_x, st.d_eps, d_part, npart,
+                                             BAND_TILE_CAP, lv.d_stats, sp),
+                    "tpe_score_table_fast")
+            ctx.tock("table", e0)
+            self._tables_slice = (sl.a, sl.b)  # (the test hook reads these tables back)
+            e0 = ctx.tick("band")
+            L.check(lib.tpe_band_rescore(dj, hjp, nj, lv.d_segs, lv.d_c64, d_tab, d_band, d_bctl,
+                                         d_part, npart, sl.db, d_bwork, sp), "tpe_band_rescore")
+            ctx.tock("band", e0)
+            e0 = None
+            lv.band_jobs.append((sl.a, sl.b))
+        st.table_calls.append(nj)
+        return e0
+
+    def _score_pruned64(self, lv, st, sl):
+        """The fp32 candidate stream scored exactly in fp64 with component
+        pruning (tpe_score_pruned64; sampled labels below TABLE_MIN_CAND)."""
+        lib, n_comp = st.lib, lv.n_comp
+        npart = lib.tpe_pruned64_partials(sl.hjp, sl.nj)
+        d_part = self._buf("partial", 32 * max(npart, 1))
+        d_tab = self._buf("tables", L.TABLE_DTYPE.itemsize * sl.nj)
+        d_rh = self._buf("reach_hi", 8 * n_comp)
+        d_rl = self._buf("reach_lo", 8 * n_comp)
+        d_wide = self._buf("wide_idx", 4 * n_comp)
+        max_comp = _V("max_comp", lv.max_obs + 1)
+        d_tsc = self._buf("table_scratch", lib.tpe_table_scratch_bytes(sl.nj, max_comp))
+        L.check(lib.tpe_score_pruned64(sl.dj, sl.hjp, sl.nj, lv.d_segs, lv.d_mu, lv.d_sig,
+                                       lv.d_cdf, lv.d_c64, max_comp, d_rh, d_rl, d_wide, d_tsc,
+                                       d_tab, st.d_cand, st.d_bl, st.d_al, st.d_x, d_part, npart,
+                                       sl.db, lv.sp), "tpe_score_pruned64")
+        return sl.e0
+
+    def _score_lat(self, lv, st, sl):
+        """Quantized labels scored on their value lattice: the prefix-first
+        tpe_lattice_suggest, or sample + compact + tpe_score_quantized.  The
+        lattice values' component windows come from k_qreach, on the quantized
+        jobs' own components of the reach arrays."""
+        lib, hj, hjp, dj, nj, ks = st.lib, sl.hj, sl.hjp, sl.dj, sl.nj, sl.ks
+        d_rh = self._buf("reach_hi", 8 * lv.n_comp)
+        d_rl = self._buf("reach_lo", 8 * lv.n_comp)
+        d_vals = self._buf("lat_vals", 8 * lv.lat_off)
+        d_first = self._buf("lat_first", 8 * lv.lat_off)
+        if lv.lat_ready:
+            d_slot, d_cnt = lv.base + lv.o_slot, lv.base + lv.o_lcnt
+        else:
+            d_slot = self._buf("lat_slot", 8 * lv.lat_off)
+            d_cnt = self._buf("lat_cnt", 8 * nj)
+        max_vals = int(hj["lat_n"].max())
+        if self.lat_prefix and max_vals <= LAT_SUGGEST_MAX_SLOTS and \
+                int(hj["n_cand"].max()) > self.lat_prefix:
+            # prefix first: the rest of a stream only where an unseen value
+            # could still win (tpe_lattice_suggest)
+            npart = nj * max_vals
+            d_part = self._buf(sl.pname, 32 * npart)
+            d_need = self._buf("lat_need", 4 * nj)
+            L.check(lib.tpe_lattice_suggest(dj, hjp, nj, lv.d_segs, lv.d_w, lv.d_mu, lv.d_sig,
+                                            lv.d_cdf, d_slot, self.lat_prefix, d_part, npart,
+                                            d_need, sl.db, lv.d_err, d_rh, d_rl, ks),
+                    "tpe_lattice_suggest")
+        else:
+            L.check(lib.tpe_lattice_sample(dj, hjp, nj, lv.d_segs, lv.d_mu, lv.d_sig, lv.d_cdf,
+                                           d_slot, lv.d_err, ks), "tpe_lattice_sample")
+            L.check(lib.tpe_lattice_compact(dj, hjp, nj, d_slot, d_vals, d_first, d_cnt, ks),
+                    "tpe_lattice_compact")
+            npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+            d_part = self._buf(sl.pname, 32 * max(npart, 1))
+            L.check(lib.tpe_score_quantized(dj, hjp, nj, lv.d_segs, lv.d_w, lv.d_mu, lv.d_sig,
+                                            d_vals, d_first, d_cnt, max_vals, None, None, d_part,
+                                            npart, sl.db, lv.d_err, d_rh, d_rl, ks),
+                    "tpe_score_quantized")
+        return sl.e0
+
+    def _score_quantized(self, lv, st, sl):
+        """Quantized labels scored on their candidates: fallback draws
+        ("qfb", tpe_sample first) or injected candidates ("qinj")."""
+        lib, hjp, nj, ks = st.lib, sl.hjp, sl.nj, sl.ks
+        d_rh = self._buf("reach_hi", 8 * lv.n_comp)
+        d_rl = self._buf("reach_lo", 8 * lv.n_comp)
+        vals = st.d_cand
+        if sl.kind == "qfb":
+            vals = self._buf("q_cand", 8 * max(lv.qfb_off, 1))
+            L.check(lib.tpe_sample(lv.base + lv.o_fb,
+                                   lv.fb_jobs.ctypes.data_as(ctypes.c_void_p), nj, lv.d_segs,
+                                   lv.d_mu, lv.d_sig, lv.d_cdf, 64, vals, ks), "tpe_sample")
+        max_vals = int(sl.hj["n_cand"].max())
+        npart = lib.tpe_quantized_partials(hjp, nj, max_vals)
+        d_part = self._buf(sl.pname, 32 * max(npart, 1))
+        L.check(lib.tpe_score_quantized(sl.dj, hjp, nj, lv.d_segs, lv.d_w, lv.d_mu, lv.d_sig,
+                                        vals, None, None, max_vals, st.d_bl, st.d_al, d_part,
+                                        npart, sl.db, lv.d_err, d_rh, d_rl, ks),
+                "tpe_score_quantized")
+        return sl.e0
+
+    def _score_cat(self, lv, st, sl):
+        """Categorical labels: the prefix-first tpe_categorical_suggest, or
+        tpe_score_categorical (per-candidate outputs, injected candidates)."""
+        lib, hj, hjp, nj, ks = st.lib, sl.hj, sl.hjp, sl.nj, sl.ks
+        npart = lib.tpe_categorical_partials(hjp, nj)
+        d_part = self._buf(sl.pname, 32 * max(npart, 1))
+        if self.lat_prefix and not lv.inj(sl.ids[0]) and st.d_bl is None and st.d_x is None \
+                and int(hj["n_cand"].max()) > self.lat_prefix:
+            # prefix first: the rest of a stream only where an unseen better
+            # category could still be drawn (tpe_categorical_suggest)
+            d_need = self._buf("cat_need", 4 * nj)
+            L.check(lib.tpe_categorical_suggest(sl.dj, hjp, nj, lv.d_csegs, lv.d_logp, lv.d_ccdf,
+                                                self.lat_prefix, d_part, npart, d_need, sl.db,
+                                                ks), "tpe_categorical_suggest")
+        else:
+            L.check(lib.tpe_score_categorical(sl.dj, hjp, nj, lv.d_csegs, lv.d_logp, lv.d_ccdf,
+                                              st.d_cand, st.d_bl, st.d_al, st.d_x, d_part, npart,
+                                              sl.db, ks), "tpe_score_categorical")
+        return sl.e0
 
     def _read_results(self, stream, sp, sync, after, pin, nbytes, n_jobs, fix, jobs, xbytes,
                       groups, table_calls, outputs, table_scores, out_off, works, order, cont,
@@ -2223,6 +2292,12 @@ def _raise_errors(err):
     if err & 4:
         raise L.TpeHipError("history gather: observation counts do not match the "
                             "segment sizes given by the host")
+
+
+_GROUP_LAUNCH = {"cont": Engine._score_cont, "sorted": Engine._score_sorted,
+                 "table": Engine._score_table, "pruned64": Engine._score_pruned64,
+                 "lat": Engine._score_lat, "qfb": Engine._score_quantized,
+                 "qinj": Engine._score_quantized, "cat": Engine._score_cat}
 
 
 def _slice_of(groups, g):
