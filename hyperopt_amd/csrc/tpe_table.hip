@@ -90,9 +90,14 @@ constexpr int kTRF = TPE_TRF;        // candidates per thread in the fast scorer
                                      // 0.288 -> 0.272 ms per C3 level against 16, one-box A/B)
 constexpr int64_t kTileF = (int64_t)kBS * kTRF;  // its tile: one band tile per scorer block
 #ifndef TPE_BUILD_BLOCKS
-#define TPE_BUILD_BLOCKS 512
+#define TPE_BUILD_BLOCKS 384
 #endif
-constexpr int kBuildBlocks = TPE_BUILD_BLOCKS;  // build blocks per job (grid-stride over cells)
+// build blocks per job (grid-stride over cells).  384, not 512: a C3 uniform
+// label has ~180 quads (one per block) and a normal label ~625 block rounds,
+// so 512 launched ~330 idle blocks per uniform job and left the normal jobs'
+// second round uneven; table-build group 0.229 -> 0.214 ms per C3 level,
+// C5 unchanged (1.74 -> 1.68-1.73 ms), two-round A/B on one box (late round 5)
+constexpr int kBuildBlocks = TPE_BUILD_BLOCKS;
 constexpr int kCoopCells = 4096;     // labels with at most this many cells build a quad per block
 constexpr float kLn2T = 0.6931471805599453f;
 
