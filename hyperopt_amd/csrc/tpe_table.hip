@@ -707,9 +707,13 @@ constexpr double kFitTol = 1.0e-6;   // cubic-vs-polynomial bound allowed (nats)
 constexpr int kScoreLanes = 8;       // lanes per cell: 4 nodes, 8 sub-intervals
 constexpr int kScoreCellsPerBlock = kBS / kScoreLanes;
 #ifndef TPE_SCORE_BLOCKS
-#define TPE_SCORE_BLOCKS 256
+#define TPE_SCORE_BLOCKS 160
 #endif
-constexpr int kScoreBlocks = TPE_SCORE_BLOCKS;  // per job (grid-stride over cells)
+// per job (grid-stride over cells).  160, not 256: a C3 normal label's ~10 000
+// cells are ~313 block rounds (two even rounds instead of 1.2), a uniform
+// label's 710 cells need 23 blocks; build group -5 us per C3 level, C5
+// unchanged (three one-box A/Bs, late round 5)
+constexpr int kScoreBlocks = TPE_SCORE_BLOCKS;
 constexpr double kUFit = 1.0501;     // |u| the bounds cover (u's fp32 rounding: <= 1.05 (1 + 5 2^-24))
 constexpr int kLogD = 7;             // log-series terms carried exactly
 constexpr int kLogM = 12;            // majorant terms summed (then Cauchy's tail)
