@@ -309,15 +309,49 @@ def readme_suggest_p50():
             "calls": int(t.size), "config": "README space, max_evals=100, n_EI=24"}
 
 
-def c3_trials(space, vals, losses):
+class ForeignTrials(object):
+    """A trials object shaped like the reference's ``hyperopt.Trials``
+    (base.py:252-698: ``_dynamic_trials``, ``refresh`` filtering to the valid
+    states, ``trials``, ``new_trial_docs``) without this package's
+    ``columnar()`` -- what ``hyperopt.fmin(..., algo=hyperopt_amd.tpe.suggest)``
+    hands the suggest (the reference itself is not on the GPU box)."""
+
+    def __init__(self):
+        self._dynamic_trials = []
+        self.refresh()
+
+    def refresh(self):
+        from hyperopt_amd.base import JOB_VALID_STATES
+        self._trials = [t for t in self._dynamic_trials if t["state"] in JOB_VALID_STATES]
+
+    @property
+    def trials(self):
+        return self._trials
+
+    def __len__(self):
+        return len(self._trials)
+
+    def insert_trial_docs(self, docs):
+        self._dynamic_trials.extend(docs)
+        return [d["tid"] for d in docs]
+
+    def new_trial_docs(self, tids, specs, results, miscs):
+        return [{"state": 0, "tid": tid, "spec": spec, "result": result, "misc": misc,
+                 "exp_key": None, "owner": None, "version": 0, "book_time": None,
+                 "refresh_time": None}
+                for tid, spec, result, misc in zip(tids, specs, results, miscs)]
+
+
+def c3_trials(space, vals, losses, foreign=False):
     """The C3 history as a drop-in ``Trials`` of T finished documents (and its
-    Domain), in the reference's document format (base.py:459-482)."""
+    Domain), in the reference's document format (base.py:459-482);
+    ``foreign``: in a ForeignTrials instead."""
     from hyperopt_amd import Trials, hp
     from hyperopt_amd.base import JOB_STATE_DONE, Domain
     hps = {lab: (hp.randint(lab, a[0]) if kind == "randint" else getattr(hp, kind)(lab, *a))
            for lab, kind, a in space}
     domain = Domain(lambda p: 0.0, hps)
-    trials = Trials()
+    trials = ForeignTrials() if foreign else Trials()
     T = losses.size
     ints = {lab for lab, kind, _ in space if kind == "randint"}
     cols = {lab: (vals[lab].astype(np.int64).tolist() if lab in ints else vals[lab].tolist())
@@ -334,15 +368,17 @@ def c3_trials(space, vals, losses):
     return domain, trials
 
 
-def dropin_suggest_p50(space, vals, losses, n_cand, calls=20, warmup=3):
+def dropin_suggest_p50(space, vals, losses, n_cand, calls=20, warmup=3, foreign=False):
     """suggest p50 through the drop-in API on C3: ``tpe.suggest(new_ids,
     domain, trials, seed, n_EI_candidates=n_cand)`` on the 10k-document Trials
     (per-tid history, split, HBM mirror of the columnar cache appended with the
     previous call's document, every level's kernels, the returned document).
-    Each call's document is completed with a loss and inserted, as fmin does."""
+    Each call's document is completed with a loss and inserted, as fmin does.
+    ``foreign``: the same on a reference-shaped ForeignTrials (no columnar(),
+    the cache kept beside it: base.foreign_columnar)."""
     from hyperopt_amd import tpe
     from hyperopt_amd.base import JOB_STATE_DONE
-    domain, trials = c3_trials(space, vals, losses)
+    domain, trials = c3_trials(space, vals, losses, foreign=foreign)
     rng = np.random.RandomState(9)
     times = []
     for k in range(warmup + calls):
@@ -357,8 +393,9 @@ def dropin_suggest_p50(space, vals, losses, n_cand, calls=20, warmup=3):
     t = np.array(times[warmup:]) * 1e3
     return {"p50_ms": float(np.median(t)), "p90_ms": float(np.percentile(t, 90)),
             "calls": int(t.size),
-            "config": "C3 through tpe.suggest: %d-document Trials, n_EI_candidates=2^%d"
-                      % (losses.size, int(round(math.log2(n_cand))))}
+            "config": "C3 through tpe.suggest: %d-document %s, n_EI_candidates=2^%d"
+                      % (losses.size, "reference-shaped Trials (no columnar())" if foreign
+                         else "Trials", int(round(math.log2(n_cand))))}
 
 
 def valu_issue(prof, n_launch_cand):
@@ -716,6 +753,8 @@ def main():
                                     "(e^-40 margin), dense k_score64 for smaller ones"}
         line["append_step"] = append_steps(eng, space, mat, hist, losses, n_cand, units)
         line["dropin_suggest"] = dropin_suggest_p50(space, vals, losses, n_cand)
+        line["dropin_suggest_foreign"] = dropin_suggest_p50(space, vals, losses, n_cand,
+                                                            foreign=True)
         line["readme_suggest"] = readme_suggest_p50()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(space, vals, losses)

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -74,6 +74,7 @@ OP_CODES["tpe_fit_sorted"] = OP_STREAM_SYNC + 5
 OP_CODES["tpe_history_order"] = OP_STREAM_SYNC + 6
 OP_CODES["tpe_categorical_suggest"] = OP_STREAM_SYNC + 7
 OP_CODES["tpe_cat_posterior_hist"] = OP_STREAM_SYNC + 8
+OP_MAXLOC_ALLREDUCE = OP_CODES["tpe_maxloc_allreduce"]
 PRIOR_UNIFORM, PRIOR_LOGUNIFORM, PRIOR_NORMAL, PRIOR_LOGNORMAL, PRIOR_RANDINT, \
     PRIOR_CATEGORICAL = range(6)
 
@@ -136,6 +137,9 @@ _SIGNATURES = {
     "tpe_best_scatter": (_I, [_P, _P, _I, _P, _I, _P]),
     "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
     "tpe_run_ops": (_I, [_P, _I, ctypes.POINTER(_I)]),
+    "tpe_ops_capture": (_I, [_P, _I, _P, _P, ctypes.POINTER(_P), ctypes.POINTER(_I)]),
+    "tpe_graph_launch": (_I, [_P, _P]),
+    "tpe_graph_destroy": (_I, [_P]),
     "tpe_check_transcendentals": (_I, [_P, _P]),
     "tpe_mixture_scratch_bytes": (_I64, [_I, _I]),
     "tpe_mixture_prepare": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -17,6 +17,7 @@ import datetime
 import logging
 import numbers
 import sys
+import weakref
 
 import numpy as np
 
@@ -215,9 +216,22 @@ class Columnar(object):
         self.docs.extend(new)
         self.rows = need
 
+    VALID_SAMPLES = 16  # strided identity probes of valid_for, besides the first and last row
+
     def valid_for(self, docs):
+        """Whether rows [0, rows) are still ``docs``' first documents: the
+        first and the last cached row and a few strided rows between must be
+        the same objects.  A removal anywhere shifts the last cached row (or
+        shortens the list), so deletions and filtering are caught; a document
+        replaced in place by another object between probes is not."""
         n = min(self.rows, len(docs))
-        return n == 0 or (docs[n - 1] is self.docs[n - 1] and docs[0] is self.docs[0])
+        if n == 0:
+            return True
+        mine = self.docs
+        if docs[n - 1] is not mine[n - 1] or docs[0] is not mine[0]:
+            return False
+        step = max(1, n // self.VALID_SAMPLES)
+        return all(docs[i] is mine[i] for i in range(step, n - 1, step))
 
     def losses(self):
         """Loss of every row (tpe.py:880-882: None -> +inf), as a new array.
@@ -250,6 +264,60 @@ class Columnar(object):
         if dh.rows < self.rows:
             dh.append(self.vals[dh.rows:self.rows], self.active[dh.rows:self.rows])
         return dh
+
+
+_FOREIGN = weakref.WeakKeyDictionary()  # foreign trials object -> {labels: Columnar}
+
+
+def foreign_columnar(trials, docs, labels):
+    """The columnar cache of a ``Trials`` object that has no ``columnar()``
+    (the reference's own ``hyperopt.Trials``, or a subclass from another
+    backend), kept beside it and extended incrementally like
+    ``Trials.columnar``: rows are ``docs`` (``trials.trials``, the refreshed
+    document list) and a call walks only the documents appended since the last
+    one.  The whole cache is rebuilt when ``docs`` no longer starts with the
+    cached documents (``Columnar.valid_for``: deletion, ``delete_all``, a
+    refresh that filtered a document out).  Returns None when the object can
+    be neither weak-referenced nor given an attribute (the caller then walks
+    the documents, as the reference does: tpe.py:876-896, base.py:200-214).
+
+    Like ``Trials.columnar`` the losses of finished documents are read once
+    (``Columnar.losses``); ``invalidate_loss_cache(trials)`` forgets them."""
+    try:
+        cache = _FOREIGN.get(trials)
+        if cache is None:
+            cache = _FOREIGN[trials] = {}
+    except TypeError:  # not weak-referenceable / unhashable: an attribute instead
+        cache = getattr(trials, "_hyperopt_amd_columnar", None)
+        if cache is None:
+            try:
+                cache = {}
+                setattr(trials, "_hyperopt_amd_columnar", cache)
+            except (AttributeError, TypeError):
+                return None
+    if not isinstance(docs, list):
+        docs = list(docs)
+    key = tuple(labels)
+    col = cache.get(key)
+    if col is None or col.rows > len(docs) or not col.valid_for(docs):
+        col = cache[key] = Columnar(key)
+    col.extend(docs)
+    return col
+
+
+def invalidate_loss_cache(trials):
+    """Forget the cached losses of finished documents of any trials object
+    (ours: Trials.invalidate_loss_cache; a foreign one: its foreign_columnar
+    caches) -- call after editing the ``result`` of a DONE document."""
+    if hasattr(trials, "invalidate_loss_cache"):
+        trials.invalidate_loss_cache()
+        return
+    try:
+        caches = _FOREIGN.get(trials) or {}
+    except TypeError:
+        caches = getattr(trials, "_hyperopt_amd_columnar", None) or {}
+    for col in caches.values():
+        col.n_final = 0
 
 
 class Trials(object):

@@ -158,3 +158,92 @@ extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
   }
   return TPE_OK;
 }
+
+// ---- the level as a hipGraph ------------------------
+// A level re-issued with exactly the same records (bench.py's steps, any
+// suggest whose sizes repeat) is captured once -- its records issued into a
+// stream capture of `stream`, the level's main stream; side-stream forks
+// join back through the records' own events; work the records put on
+// `from_stream` goes to `capture_stream`, since the caller's stream may be the
+// null stream -- and replayed with one hipGraphLaunch on the caller's stream: the host no longer pays ~4 us per kernel launch, and the
+// GPU no longer waits between kernels for the host to issue the next one.
+namespace tpe {
+namespace {
+// the argument word of `op` that names its stream (every entry point's last
+// parameter; the runtime records' stream operand), or -1
+int stream_word(const tpe_op& op) {
+  switch (op.code) {
+    case TPE_OP_EVENT_RECORD: return 1;
+    case TPE_OP_STREAM_WAIT: return 0;
+    case TPE_OP_MEMCPY: return 4;
+    case TPE_OP_STREAM_SYNC: return 0;
+    default: return op.n_args > 0 ? op.n_args - 1 : -1;
+  }
+}
+}  // namespace
+}  // namespace tpe
+
+extern "C" int tpe_ops_capture(const tpe_op* ops, int n_ops, void* from_stream,
+                               void* capture_stream, void** graph_exec, int* failed_op) {
+  if (failed_op) *failed_op = -1;
+  if (!graph_exec || n_ops <= 0 || !ops || !capture_stream) {
+    tpe::set_error("tpe_ops_capture: n_ops=%d, null argument", n_ops);
+    return TPE_E_ARG;
+  }
+  *graph_exec = nullptr;
+  hipStream_t st = (hipStream_t)capture_stream;
+  hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed);
+  if (e != hipSuccess) return tpe::runtime(e, "hipStreamBeginCapture");
+  int rc = TPE_OK;
+  {
+    struct Defer {
+      Defer() { tpe::defer_launch_checks(true); }
+      ~Defer() { tpe::defer_launch_checks(false); }
+    } defer;
+    for (int i = 0; i < n_ops && rc == TPE_OK; ++i) {
+      const int32_t c = ops[i].code;
+      if (c == TPE_OP_STREAM_SYNC || c == TPE_OP_MAXLOC_ALLREDUCE) {
+        tpe::set_error("tpe_ops_capture: record %d (code %d) cannot be captured", i, c);
+        rc = TPE_E_ARG;
+      } else {
+        // the records' main stream (possibly the null stream, which cannot
+        // be captured) is issued into the capture stream instead
+        tpe_op op = ops[i];
+        const int w = tpe::stream_word(op);
+        if (w >= 0 && op.a[w] == (int64_t)(intptr_t)from_stream)
+          op.a[w] = (int64_t)(intptr_t)capture_stream;
+        rc = tpe::run_one(op);
+      }
+      if (rc != TPE_OK && failed_op) *failed_op = i;
+    }
+  }
+  hipGraph_t g = nullptr;
+  e = hipStreamEndCapture(st, &g);  // always: the stream leaves capture mode
+  (void)hipGetLastError();
+  if (rc == TPE_OK && e != hipSuccess) rc = tpe::runtime(e, "hipStreamEndCapture");
+  if (rc == TPE_OK) {
+    hipGraphExec_t x = nullptr;
+    e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+      rc = tpe::runtime(e, "hipGraphInstantiate");
+    } else {
+      *graph_exec = (void*)x;
+    }
+  }
+  if (g) (void)hipGraphDestroy(g);
+  return rc;
+}
+
+extern "C" int tpe_graph_launch(void* graph_exec, void* stream) {
+  if (!graph_exec) {
+    tpe::set_error("tpe_graph_launch: null graph");
+    return TPE_E_ARG;
+  }
+  return tpe::runtime(hipGraphLaunch((hipGraphExec_t)graph_exec, (hipStream_t)stream),
+                      "hipGraphLaunch");
+}
+
+extern "C" int tpe_graph_destroy(void* graph_exec) {
+  if (!graph_exec) return TPE_OK;
+  return tpe::runtime(hipGraphExecDestroy((hipGraphExec_t)graph_exec), "hipGraphExecDestroy");
+}

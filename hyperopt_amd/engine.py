@@ -54,6 +54,9 @@ _ALIGN = 256
 CONTINUOUS = ("uniform", "quniform", "loguniform", "qloguniform",
               "normal", "qnormal", "lognormal", "qlognormal")
 CATEGORICAL = ("randint", "categorical")
+# unquantized continuous kinds: scored by an fp32 argmax when the candidates
+# are injected or per-candidate outputs are asked for (Engine.run re-decides them)
+EXACT32_KINDS = ("uniform", "loguniform", "normal", "lognormal")
 
 
 @dataclass(slots=True)
@@ -324,10 +327,15 @@ class DeviceHistory:
         # (merging right after each append instead, on the GPU while the host
         # plans the level: same-box A/B 1.050 vs 1.036 ms per drop-in suggest)
         last = self.__dict__.get("_ordered")
-        if last is not None and last[1:] == sig and all(
-                self.order_rows.get(c) == last[0] for c in self.__dict__["_order_cols"]):
+        # (sig, specs, columns) of the last slow pass.  When the last pass had
+        # this signature no other column set has been ordered since, so the
+        # columns still carry these specs (each pass sets _ordered to its key)
+        cached = self.__dict__.get("_order_specs_for")
+        orows = self.order_rows
+        if last is not None and last[1:] == sig and cached is not None and cached[0] == sig \
+                and all(orows.get(c) == last[0] for c in cached[2]):
             # (the same columns and specs as last time, every one at its rows)
-            todo = {last[0]: self._order_specs}
+            todo = {last[0]: cached[1]}
         else:
             todo = {}
             specs_all = []
@@ -340,9 +348,11 @@ class DeviceHistory:
                     self.order_rows[c] = 0
                 if self.order_rows[c] < self.rows:
                     todo.setdefault(self.order_rows[c], []).append((c,) + spec)
-            self._order_specs = specs_all
-            self._order_cols = [x[0] for x in specs_all]
+            # the spec list is kept with the signature it belongs to, so a
+            # later fast pass never merges another column set's specs
+            self._order_specs_for = (sig, specs_all, [x[0] for x in specs_all])
         if not todo:
+            self._ordered = key
             return
         lib = eng.lib
         sp = ctypes.c_void_p(stream.cuda_stream)
@@ -511,6 +521,10 @@ class Engine:
         # launch, stream fork/join, readback and the final synchronise -- and
         # re-issued with one C call per level (hyperopt_amd/csrc/tpe_ops.hip)
         self.native = _knob("TPE_NATIVE_LAUNCH", "1") != "0"
+        # recorded levels re-issued with the same words replay a hipGraph of
+        # their records (_OpList.issue; TPE_GRAPHS=0: always tpe_run_ops)
+        self.graphs = _knob("TPE_GRAPHS", "1") == "1"
+        self._cap_stream = None
         self._oplists = {}      # launch key -> _OpList
         self._oplist_once = None
         self._replays = {}      # signature -> _Replay of a recorded WorkBatch level
@@ -571,6 +585,13 @@ class Engine:
         if n_rows:
             self._buf("fit_sorted_scratch", lib.tpe_fit_sorted_scratch_bytes(n_seg, n_rows))
         self._presized = (self._gen, sizes)
+
+    def _capture_stream(self):
+        """A stream of this engine's own to capture levels on (the caller's
+        stream may be the null stream, which cannot be captured)."""
+        if self._cap_stream is None:
+            self._cap_stream = self.torch.cuda.Stream(self.device)
+        return self._cap_stream.cuda_stream
 
     def _drop_oplists(self):
         self._replays.clear()
@@ -740,6 +761,55 @@ class Engine:
         fb_jobs["out_off"] = fb_jobs["cand_off"]
         return (jobs, np.zeros(1), fb_jobs, P["fb_slice"]) + tuple(P["counts"])
 
+    def _choose_plan(self, works, batch, prior_weight, lf, precision, scorer, outputs,
+                     sample_only, hist_mode, multi, _hmark):
+        """A level's plan: replayed from the plan recorded for its structure
+        (_plan_fast + _jobs_fast: only the per-call columns -- counts, keys,
+        candidate bases -- are filled in) or built from its works (_plan_new,
+        which records it when it can be replayed).  A WorkBatch's works are
+        materialised only when its structure is new.  Returns (works, plan
+        key, recorded plan or None, the plan tuple of _plan_new; a replayed
+        plan gives the gather table where _plan_new gives the gather list)."""
+        if batch is not None:
+            pkey = ("batch", batch.key, float(prior_weight), int(lf), int(precision), scorer,
+                    multi, self._big64(precision, batch.n_above))
+            cached = self._plans.get(pkey)
+            if cached is None:
+                works = batch.materialize()
+                if len(works) != len(batch):
+                    raise ValueError("WorkBatch.materialize() gave %d works for %d rows"
+                                     % (len(works), len(batch)))
+            elif len(self._plans) > 64:
+                self._plans.clear()
+        else:
+            pkey = self._plan_key(works, prior_weight, lf, precision, scorer, outputs,
+                                  sample_only, hist_mode, multi)
+            if pkey is not None:
+                pkey += (self._big64(precision, np.fromiter(
+                    (w.n_above if w.obs_above is None else np.size(w.obs_above) for w in works),
+                    np.int64, len(works))),)
+            cached = self._plans.get(pkey) if pkey is not None else None
+        if cached is None:
+            return works, pkey, None, self._plan_new(
+                works, pkey, prior_weight, lf, precision, scorer, outputs, sample_only, hist_mode,
+                _hmark)
+        cols = (batch.n_below, batch.n_above, batch.keys, batch.cand_base) \
+            if batch is not None else self._columns(works)
+        (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp, max_obs,
+         csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes, groups,
+         order, g_arr) = self._plan_fast(cached, cols[0], cols[1])
+        if batch is not None:
+            inj = lambda i: False  # noqa: E731
+        else:
+            inj = lambda i: works[i].cand is not None  # noqa: E731
+        (jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off, sort_off, cnt_off,
+         tbl_off) = self._jobs_fast(cached, cols[2], cols[3])
+        return works, pkey, cached, (
+            cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp, max_obs,
+            csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes, groups,
+            order, g_arr, inj, jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off,
+            sort_off, cnt_off, tbl_off)
+
     # -- main entry ----------------------------------------------------------
     def _plan_new(self, works, pkey, prior_weight, lf, precision, scorer, outputs, sample_only,
                   hist_mode, _hmark):
@@ -836,6 +906,28 @@ class Engine:
         p_pool = np.concatenate(p_init) if p_init else np.zeros(1)
 
         _hmark('cats')
+        (inj, lat_ranges, fallback, modes, groups, order, jobs, cand_pool, fb_jobs, fb_slice,
+         out_off, lat_off, qfb_off, sort_off, cnt_off, tbl_off) = self._plan_jobs(
+            works, cont, quant, cat, fit_ids, params, cat_meta, precision, scorer, outputs,
+            sample_only)
+        if pkey is not None and not any(k == "sorted" and ids for k, ids in groups):
+            self._plans[pkey] = self._plan_record(
+                works, cont, quant, cat, fit_ids, params, segs, csegs, p_pool, cat_meta,
+                lat_ranges, fallback, modes, groups, order, gathers, jobs, fb_slice, out_off,
+                lat_off, qfb_off, sort_off, cnt_off, tbl_off)
+
+        return (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp,
+                max_obs, csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes,
+                groups, order, gathers, inj, jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off,
+                qfb_off, sort_off, cnt_off, tbl_off)
+
+    def _plan_jobs(self, works, cont, quant, cat, fit_ids, params, cat_meta, precision, scorer,
+                   outputs, sample_only):
+        """The job table of a new plan (_plan_new): each label's scorer
+        (continuous: table / pruned64 / dense / sorted by precision, size and
+        hooks; quantized: lattice or dense fallback; categorical), the kernel
+        groups, and one tpe_job per label ordered so every kernel call takes a
+        contiguous slice, with its candidate, output, lattice and table offsets."""
         # ---- jobs, ordered so every kernel call takes a contiguous slice -----------
         inj = lambda i: works[i].cand is not None  # noqa: E731
         lat_ranges = {}
@@ -962,22 +1054,70 @@ class Engine:
         fb_slice = _slice_of(groups, [k for k, _ in groups].index("qfb"))
         fb_jobs = jobs[fb_slice[0]:fb_slice[1]].copy()
         fb_jobs["out_off"] = fb_jobs["cand_off"]
-        if pkey is not None and not any(k == "sorted" and ids for k, ids in groups):
-            self._plans[pkey] = self._plan_record(
-                works, cont, quant, cat, fit_ids, params, segs, csegs, p_pool, cat_meta,
-                lat_ranges, fallback, modes, groups, order, gathers, jobs, fb_slice, out_off,
-                lat_off, qfb_off, sort_off, cnt_off, tbl_off)
-
-        return (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp,
-                max_obs, csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes,
-                groups, order, gathers, inj, jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off,
-                qfb_off, sort_off, cnt_off, tbl_off)
+        return (inj, lat_ranges, fallback, modes, groups, order, jobs, cand_pool, fb_jobs,
+                fb_slice, out_off, lat_off, qfb_off, sort_off, cnt_off, tbl_off)
 
     def run(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
             outputs=False, stream=None, timers=None, sample_only=False,
             pruned=True, scorer=None, posteriors=False, history=None, rows=None,
             is_below=None, histories=None, timer_groups=None,
             table_scores=False, defer=False, exchange=None) -> List[LabelResult]:
+        """Run one level (``_run_level``); at precision 32 the labels scored by
+        an fp32 argmax -- injected candidates, or per-candidate ``outputs`` --
+        get the exact decision afterwards (``_exact_decision``), so every
+        default precision-32 winner is np.argmax of the exact scores, as the
+        suggest path's are.  Arguments: see ``_run_level``."""
+        res = self._run_level(works, prior_weight, lf, precision, outputs, stream, timers,
+                              sample_only, pruned, scorer, posteriors, history, rows, is_below,
+                              histories, timer_groups, table_scores, defer, exchange)
+        if precision == 32 and isinstance(works, list) and res and not (
+                sample_only or posteriors or table_scores or exchange is not None) and \
+                (scorer in (None, "auto") and pruned):
+            redo = [i for i, w in enumerate(works) if w.kind in EXACT32_KINDS and
+                    (w.cand is not None or outputs)]
+            if redo:
+                self._exact_decision(works, res, redo, prior_weight, lf, stream, history, rows,
+                                     is_below, histories)
+        return res
+
+    def _exact_decision(self, works, res, redo, prior_weight, lf, stream, history, rows,
+                        is_below, histories):
+        """The exact argmax of fp32-decided labels: their candidate values
+        (the injected ones, or the drawn ones read back with the outputs)
+        scored again in fp64 (tpe_score_pruned64 / the dense fp64 kernel,
+        index-exact against the oracle), first maximum, NaN winning
+        (np.argmax, tpe.py:649-658).  Patches index / value / score in place;
+        the fp32 per-candidate log-densities stay."""
+        import dataclasses
+        again = []
+        for i in redo:
+            w, r = works[i], res[i]
+            cand = w.cand if w.cand is not None else r.cand
+            if cand is None or np.size(cand) == 0:
+                continue
+            again.append((i, dataclasses.replace(w, cand=np.asarray(cand, np.float64),
+                                                 n_cand=int(np.size(cand)), cand_base=0)))
+        if not again:
+            return
+        kw = dict(history=history, rows=rows, is_below=is_below, histories=histories)
+        keep = tuple(getattr(self, k, None) for k in ("last_pairs", "last_table_stats",
+                                                      "last_plan"))  # the fp32 level's
+        exact = self._run_level([w for _, w in again], prior_weight, lf, 64, False, stream, None,
+                                False, True, None, False, **kw, timer_groups=None,
+                                table_scores=False, defer=False, exchange=None)
+        self.last_pairs, self.last_table_stats, self.last_plan = keep
+        for (i, w), e in zip(again, exact):
+            r = res[i]
+            local = int(e.index)
+            r.index = local if works[i].cand is not None else \
+                (int(works[i].cand_base) + local if local >= 0 else local)
+            r.value, r.score = e.value, e.score
+
+    def _run_level(self, works: List[LabelWork], prior_weight=1.0, lf=DEFAULT_LF, precision=32,
+                   outputs=False, stream=None, timers=None, sample_only=False,
+                   pruned=True, scorer=None, posteriors=False, history=None, rows=None,
+                   is_below=None, histories=None, timer_groups=None,
+                   table_scores=False, defer=False, exchange=None) -> List[LabelResult]:
         """Run one level.  ``timers`` (optional dict) collects HIP event pairs
         per kernel group ("fit", "cat_fit", "cont", "lat", ...) on ``stream``;
         ``timer_groups`` (optional set) limits them to those groups (each event
@@ -1061,48 +1201,19 @@ class Engine:
         if table_scores:  # the fast table path's per-candidate scores (test hook)
             outputs = False
         batch = works if isinstance(works, WorkBatch) else None
-        if batch is not None:
-            if not hist_mode or outputs or sample_only or posteriors or table_scores:
-                raise ValueError("a WorkBatch runs with history= / histories= and no output hooks")
-            pkey = ("batch", batch.key, float(prior_weight), int(lf), int(precision), scorer,
-                    histories is not None, self._big64(precision, batch.n_above))
-            cached = self._plans.get(pkey)
-            if cached is None:
-                works = batch.materialize()
-                if len(works) != len(batch):
-                    raise ValueError("WorkBatch.materialize() gave %d works for %d rows"
-                                     % (len(works), len(batch)))
-            elif len(self._plans) > 64:
-                self._plans.clear()
-        else:
-            pkey = self._plan_key(works, prior_weight, lf, precision, scorer, outputs,
-                                  sample_only, hist_mode, histories is not None)
-            if pkey is not None:
-                pkey += (self._big64(precision, np.fromiter(
-                    (w.n_above if w.obs_above is None else np.size(w.obs_above) for w in works),
-                    np.int64, len(works))),)
-            cached = self._plans.get(pkey) if pkey is not None else None
+        if batch is not None and (not hist_mode or outputs or sample_only or posteriors or
+                                  table_scores):
+            raise ValueError("a WorkBatch runs with history= / histories= and no output hooks")
+        works, pkey, cached, plan = self._choose_plan(
+            works, batch, prior_weight, lf, precision, scorer, outputs, sample_only, hist_mode,
+            histories is not None, _hmark)
+        (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp, max_obs,
+         csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes, groups,
+         order, gathers, inj, jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off,
+         sort_off, cnt_off, tbl_off) = plan
+        if cached is not None:
+            g_arr = gathers  # (a cached plan gives the gather table itself)
         pack = _Pack()
-        if cached is not None:
-            cols = (batch.n_below, batch.n_above, batch.keys, batch.cand_base) \
-                if batch is not None else self._columns(works)
-            (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp, max_obs,
-             csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes, groups,
-             order, g_arr) = self._plan_fast(cached, cols[0], cols[1])
-            if batch is not None:
-                inj = lambda i: False  # noqa: E731
-            else:
-                inj = lambda i: works[i].cand is not None  # noqa: E731
-        if cached is not None:
-            (jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off, sort_off, cnt_off,
-             tbl_off) = self._jobs_fast(cached, cols[2], cols[3])
-        else:
-            (cont, quant, cat, fit_ids, params, nf, segs, obs_pool, n_obs_total, n_comp, max_obs,
-             csegs, cobs_pool, p_pool, cat_meta, cobs_off, lat_ranges, fallback, modes, groups,
-             order, gathers, inj, jobs, cand_pool, fb_jobs, fb_slice, out_off, lat_off, qfb_off,
-             sort_off, cnt_off, tbl_off) = self._plan_new(
-                works, pkey, prior_weight, lf, precision, scorer, outputs, sample_only, hist_mode,
-                _hmark)
         _hmark('plan')
         # ---- upload (descriptors, jobs, injected candidates: one copy) -----------
         o_segs = pack.add(segs) if segs.size else None
@@ -1322,7 +1433,7 @@ class Engine:
                 else:
                     rec.add(L.OP_STREAM_SYNC, sp)
                 rec.finish((lv.jobs, lv.fb_jobs, lv.g_arr if lv.hist_mode else None,
-                            lv.h_arr if lv.histories is not None else None))
+                            lv.h_arr if lv.histories is not None else None), sp.value or 0)
                 if self._gen == gen0:  # every recorded pointer is still the live one
                     if len(self._oplists) >= 16 or any(
                             k[1] != gen0 for k in self._oplists):
@@ -1348,11 +1459,7 @@ class Engine:
         keep[1][...] = lv.fb_jobs
         if keep[2] is not None:
             keep[2][...] = lv.g_arr
-        failed = ctypes.c_int(-1)
-        rc = self.lib.tpe_run_ops(ops.ptr, ops.n, ctypes.byref(failed))
-        if rc != 0:
-            raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
-                rc, failed.value, self.lib.tpe_last_error().decode(errors="replace")))
+        ops.issue(self)
         self.graph_stats["native"] = self.graph_stats.get("native", 0) + 1
         return ops, ops.table_calls, ops.band_jobs, False
 
@@ -2140,14 +2247,13 @@ class _Replay(object):
     def _issue(self, eng, timers, defer, jobs, hm):
         if hm is not None:
             hm.append(("plan", time.perf_counter()))
-        failed = ctypes.c_int(-1)
-        rc = eng.lib.tpe_run_ops(self.ops.ptr, self.ops.n, ctypes.byref(failed))
+        try:
+            self.ops.issue(eng)
+        except L.TpeHipError:
+            eng._replays.clear()
+            raise
         if hm is not None:
             hm.append(("score launches", time.perf_counter()))
-        if rc != 0:
-            eng._replays.clear()
-            raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
-                rc, failed.value, eng.lib.tpe_last_error().decode(errors="replace")))
         eng.graph_stats["native"] = eng.graph_stats.get("native", 0) + 1
         eng.graph_stats["replay"] = eng.graph_stats.get("replay", 0) + 1
         after = None
@@ -2224,6 +2330,13 @@ class _OpList(_Timing):
         self.table_calls = []
         self.keep = self.arr = None
         self.ptr = self.n = 0
+        # the records as a hipGraph (Engine.graphs): the graph of records
+        # [0, cut) and the words it was captured from; the rest (the host's
+        # event or stream sync, an RCCL exchange) is issued after it
+        self.graph = self.graph_words = self.last_words = None
+        self.cut = 0
+        self.stream = None
+        self.no_graph = False
 
     def __getattr__(self, name):
         code = L.OP_CODES.get(name)
@@ -2247,8 +2360,14 @@ class _OpList(_Timing):
         self.add(L.OP_EVENT_RECORD, h, stream.cuda_stream)
         return h
 
-    def finish(self, keep):
+    def finish(self, keep, stream=None):
         arr = np.zeros(len(self.rows), L.OP_DTYPE)
+        self.stream = stream
+        codes = [code for code, _ in self.rows]
+        # captured: every record before the last (the result event or stream
+        # sync the host waits on) and before an RCCL exchange
+        self.cut = min([len(codes) - 1] + [i for i, c in enumerate(codes)
+                                           if c in (L.OP_MAXLOC_ALLREDUCE, L.OP_STREAM_SYNC)])
         self.sizes = []  # (record, argument, size name): the words _Replay rewrites
         for i, (code, args) in enumerate(self.rows):
             if len(args) > L.OP_ARGS:
@@ -2265,10 +2384,52 @@ class _OpList(_Timing):
         for i, j, name in self.sizes:
             a[i, j] = values[name]
 
+    def issue(self, eng):
+        """Issue the records (one tpe_run_ops call), or replay them as a
+        hipGraph: captured on the second issue in a row with the same words
+        (pointers, sizes, grids -- the per-call inputs are in the uploaded
+        pack), replayed while the words stay the same.  A level with timing
+        events is never captured.  Raises TpeHipError on failure."""
+        lib = self.lib
+        failed = ctypes.c_int(-1)
+        start = 0
+        if eng.graphs and self.cut > 0 and not self.timed and not self.no_graph:
+            words = self.arr.tobytes()
+            if self.graph is not None and words != self.graph_words:
+                lib.tpe_graph_destroy(self.graph)
+                self.graph = self.graph_words = None
+            if self.graph is None and words == self.last_words:
+                g = ctypes.c_void_p()
+                rc = lib.tpe_ops_capture(self.ptr, self.cut, self.stream, eng._capture_stream(),
+                                         ctypes.byref(g), ctypes.byref(failed))
+                if rc == 0:
+                    self.graph, self.graph_words = g, words
+                    eng.graph_stats["captured"] = eng.graph_stats.get("captured", 0) + 1
+                else:  # this level stays on tpe_run_ops (the reason kept for diagnosis)
+                    self.no_graph = True
+                    eng.graph_stats["capture_failed"] = lib.tpe_last_error().decode(
+                        errors="replace")
+            self.last_words = words
+            if self.graph is not None:
+                rc = lib.tpe_graph_launch(self.graph, self.stream)
+                if rc != 0:
+                    raise L.TpeHipError("tpe_graph_launch failed (%d): %s" % (
+                        rc, lib.tpe_last_error().decode(errors="replace")))
+                eng.graph_stats["graph"] = eng.graph_stats.get("graph", 0) + 1
+                start = self.cut
+        rc = lib.tpe_run_ops(self.ptr + start * L.OP_DTYPE.itemsize, self.n - start,
+                             ctypes.byref(failed))
+        if rc != 0:
+            raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
+                rc, start + failed.value, lib.tpe_last_error().decode(errors="replace")))
+
     def destroy(self, hip):
         for h in self.events:
             hip.hipEventDestroy(h)
         self.events = []
+        if self.graph is not None:
+            self.lib.tpe_graph_destroy(self.graph)
+            self.graph = self.graph_words = None
 
 
 def _lat_prefix(text):

@@ -38,7 +38,7 @@ import numpy as np
 from . import _lib as _L
 from . import dist as hdist
 from . import rand
-from .base import as_domain, doc_loss
+from .base import as_domain, doc_loss, foreign_columnar
 from .engine import (DEFAULT_LF, Engine, LabelResult, LabelWork, WorkBatch, _lattice_range,
                      _params)
 
@@ -178,7 +178,12 @@ def collect_history(trials, labels):
     has a NaN loss never gets a document and drops out of the history.
     """
     docs = trials.trials
-    col = trials.columnar(labels) if hasattr(trials, "columnar") else None
+    if hasattr(trials, "columnar"):
+        col = trials.columnar(labels)
+    else:  # the reference's Trials (fmin(algo=hyperopt_amd.tpe.suggest)): a cache beside it
+        if not isinstance(docs, list):
+            docs = list(docs)
+        col = foreign_columnar(trials, docs, labels)
     n = len(docs)
     if col is not None and n == col.rows and col.keys_increasing:
         # trials.trials is every cached row (a filtered subsequence of
@@ -190,6 +195,15 @@ def collect_history(trials, labels):
             return History(col.key_tid[:n], losses, col.obs_tid[:n], col=col)
         rows = np.flatnonzero(keep)
         return History(col.key_tid[rows], losses[rows], col.obs_tid[rows], col=col, rows=rows)
+    tids, losses, obs_tids, bdocs = _best_docs(docs)
+    if col is not None and all(id(d) in col.row_of for d in bdocs):
+        rows = np.fromiter((col.row_of[id(d)] for d in bdocs), dtype=np.int64, count=len(bdocs))
+        return History(tids, losses, obs_tids, col=col, rows=rows)
+    return walk_history(docs, labels, (tids, losses, obs_tids, bdocs))
+
+
+def _best_docs(docs):
+    """Per-tid best document, sorted by tid (tpe.py:874-896)."""
     best_loss, best_doc = {}, {}
     for doc in docs:
         tid = doc["misc"].get("from_tid", doc["tid"])
@@ -201,10 +215,14 @@ def collect_history(trials, labels):
     bdocs = [best_doc[t] for t in tids]
     losses = np.array([best_loss[t] for t in tids], dtype=np.float64)
     obs_tids = np.array([d["misc"]["tid"] for d in bdocs], dtype=np.int64)
-    tids = np.asarray(tids, dtype=np.int64)
-    if col is not None and all(id(d) in col.row_of for d in bdocs):
-        rows = np.fromiter((col.row_of[id(d)] for d in bdocs), dtype=np.int64, count=len(bdocs))
-        return History(tids, losses, obs_tids, col=col, rows=rows)
+    return np.asarray(tids, dtype=np.int64), losses, obs_tids, bdocs
+
+
+def walk_history(docs, labels, best=None):
+    """The history by the reference's walk over every document and label
+    (tpe.py:874-896 + miscs_to_idxs_vals, base.py:200-214), no cache: the
+    fallback of collect_history, and what its cached forms must equal."""
+    tids, losses, obs_tids, bdocs = _best_docs(docs) if best is None else best
     L = len(labels)
     index = {lab: j for j, lab in enumerate(labels)}
     vals = np.full((len(bdocs), L), np.nan)
@@ -419,7 +437,7 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
                 res = []   # the rank still joins the winners' all-gather below
             elif obs.device and _space_sig(domain) is not None:
                 res = _level_batch(eng, domain, obs, level, units, seed, n_ei, col,
-                                   prior_weight, linear_forgetting, prec)
+                                   prior_weight, linear_forgetting, prec, ws == 1)
             else:
                 keys = label_keys(seed, level)
                 works = [obs.work(level[i], domain.specs[level[i]], col[level[i]], n_cand=count,
@@ -430,8 +448,10 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
             if ws > 1:
                 best = hdist.gather_best(len(level), [(u[0], r) for u, r in zip(units, res)])
                 values = [b[2] for b in best]
-            else:
+            elif isinstance(res, list) and res and isinstance(res[0], LabelResult):
                 values = [r.value for r in res]
+            else:  # (_level_batch on one rank: the winners' values in level order)
+                values = res
             for lab, v in zip(level, values):
                 walk[lab], stored[lab] = _decode(domain.specs[lab], v)
             if hm is not None:
@@ -501,11 +521,13 @@ def _level_info(domain, level):
     return lv
 
 
-def _level_batch(eng, domain, obs, level, units, seed, n_ei, col, pw, lf, prec):
+def _level_batch(eng, domain, obs, level, units, seed, n_ei, col, pw, lf, prec, values=False):
     """One study's level (this rank's units of it) as a WorkBatch on the
     device history: counts from the split, keys from the cached label hashes,
     a structure key of a few small ints -- LabelWork objects only the first
-    time the structure is seen.  Returns one LabelResult per unit."""
+    time the structure is seen.  Returns one LabelResult per unit, or with
+    ``values`` (one rank: every unit a whole label, in level order) just the
+    winners' values."""
     lv = _level_info(domain, level)
     idx = np.fromiter((u[0] for u in units), np.int64, len(units))
     js = lv.js[idx]
@@ -525,6 +547,8 @@ def _level_batch(eng, domain, obs, level, units, seed, n_ei, col, pw, lf, prec):
     batch = WorkBatch(("suggest", lv.id, tuple(units), n_ei, lat), obs.nb[js], obs.n_above[js],
                       keys, [u[1] for u in units], materialize)
     r = eng.run(batch, prior_weight=pw, lf=lf, precision=prec, **obs.run_kwargs)
+    if values:
+        return r.value.tolist()
     return [LabelResult(level[u[0]], ix, v, sc, ns) for u, ix, v, sc, ns in
             zip(units, r.index.tolist(), r.value.tolist(), r.score.tolist(),
                 r.n_scored.tolist())]

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 19
+#define TPE_ABI_VERSION 20
 
 enum {
   TPE_OK = 0,
@@ -609,9 +609,8 @@ int tpe_maxloc_allreduce(const tpe_best* local, tpe_best* gathered, tpe_best* ou
  * first failing record (its index in *failed_op, -1 when all succeeded).  A
  * binding that replays the same level (same kernels, grids, workspace) keeps
  * its record array and re-issues it with one call: the per-call inputs live
- * in the device buffers the records point to (the level's upload).  This is
- * the host-side counterpart of a hipGraph; on ROCm 7 re-issuing the launches
- * is faster than replaying a captured graph. ---------- */
+ * in the device buffers the records point to (the level's upload), or captures
+ * them once into a hipGraph and replays that (tpe_ops_capture below). ------ */
 enum {
   TPE_OP_GATHER_OBS = 1,       /* tpe_gather_obs                             */
   TPE_OP_GATHER_OBS_MULTI,     /* tpe_gather_obs_multi                       */
@@ -651,6 +650,23 @@ typedef struct tpe_op {
   int64_t a[TPE_OP_ARGS];
 } tpe_op;                       /* 192 bytes */
 int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op);
+/* The same records as a hipGraph: tpe_ops_capture issues ops[0..n_ops) into a
+ * stream capture of `capture_stream` (a stream of the caller's, not the null
+ * stream), with every record's stream operand that names `from_stream` (the
+ * records' main stream, possibly the null stream) pointed at
+ * `capture_stream` instead; every stream the records fork to must be joined
+ * back by an event wait among the records.  The graph is instantiated in
+ * *graph_exec -- nothing runs.  Records that cannot be captured
+ * (TPE_OP_STREAM_SYNC, TPE_OP_MAXLOC_ALLREDUCE) fail it with TPE_E_ARG at
+ * *failed_op; a capture the runtime refuses fails it with TPE_E_LAUNCH.  The
+ * graph holds every record's words as captured (pointers, sizes, grids): a
+ * binding replays it with tpe_graph_launch only while re-issuing exactly those
+ * records, the per-call inputs again in the device buffers they point to.
+ * tpe_graph_destroy frees it. */
+int tpe_ops_capture(const tpe_op* ops, int n_ops, void* from_stream, void* capture_stream,
+                    void** graph_exec, int* failed_op);
+int tpe_graph_launch(void* graph_exec, void* stream);
+int tpe_graph_destroy(void* graph_exec);
 
 /* host: rows of the k smallest losses in np.argsort(losses, kind="stable")
  * order (NaN after +inf, ties to the earlier row) -- the below split of

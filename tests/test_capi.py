@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 19
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 20
     sizes = (ctypes.c_int32 * 11)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 11) == 11
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -79,6 +79,22 @@ def test_run_ops_records():
     ops = _ops((L.OP_MEMCPY, [0, 0, 0, 77, 0]))
     rc = lib.tpe_run_ops(ops.ctypes.data_as(ctypes.c_void_p), 1, ctypes.byref(failed))
     assert rc == -1 and b"memcpy kind" in lib.tpe_last_error()
+
+
+def test_graph_entry_points_check_arguments():
+    """tpe_ops_capture / tpe_graph_launch / tpe_graph_destroy: argument errors
+    are reported before any runtime call (no GPU needed here)."""
+    lib = L.load()
+    failed = ctypes.c_int(3)
+    g = ctypes.c_void_p()
+    ops = _ops((L.OP_STREAM_SYNC, [0]))
+    p = ops.ctypes.data_as(ctypes.c_void_p)
+    assert lib.tpe_ops_capture(p, 0, None, 1, ctypes.byref(g), ctypes.byref(failed)) == -1
+    assert failed.value == -1 and b"tpe_ops_capture" in lib.tpe_last_error()
+    assert lib.tpe_ops_capture(p, 1, None, None, ctypes.byref(g), ctypes.byref(failed)) == -1
+    assert lib.tpe_ops_capture(p, 1, None, 1, None, ctypes.byref(failed)) == -1
+    assert lib.tpe_graph_launch(None, None) == -1 and b"null graph" in lib.tpe_last_error()
+    assert lib.tpe_graph_destroy(None) == 0
 
 
 def test_argument_errors_are_reported():

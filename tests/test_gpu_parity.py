@@ -60,12 +60,10 @@ def test_golden_fp32(engine, case):
                                    err_msg="%s/%s below" % (case, w.label))
         np.testing.assert_allclose(r.above_llik, al, rtol=1e-4, atol=1e-4, equal_nan=True,
                                    err_msg="%s/%s above" % (case, w.label))
-        score = bl - al
-        if w.kind in ("randint", "categorical") or w.kind.startswith("q"):
-            assert r.index == best  # fp64 paths: exact
-        else:
-            # fp32 may pick a different candidate only within fp32 error of the max
-            assert score[r.index] >= np.nanmax(score) - 1e-4 * max(1.0, abs(np.nanmax(score)))
+        # every kind index-exact: the fp32 log-densities are within 1e-4, the
+        # argmax is decided on exact scores (Engine._exact_decision)
+        assert r.index == best, (case, w.label, r.index, best)
+        assert r.value == float(w.cand[best])
 
 
 def _mixture_case(rng, kind, args, n_obs_b, n_obs_a, n_cand):
@@ -109,6 +107,28 @@ def test_oracle_random_mixtures(engine, kind, args, n_above):
                                equal_nan=True)
     np.testing.assert_allclose(r32.above_llik, ref["above_llik"], rtol=1e-4, atol=1e-4,
                                equal_nan=True)
+    assert r32.index == ref["best"]  # injected at fp32: the exact argmax too
+    # injected without outputs (the fp32 scorers' own path) -- the same winner
+    r32n, = engine.run([w], precision=32)
+    assert (r32n.index, r32n.value) == (ref["best"], float(w.cand[ref["best"]]))
+
+
+@pytest.mark.parametrize("kind,args", KINDS[:4])
+@pytest.mark.parametrize("n_cand", [500, 1 << 17])
+def test_fp32_outputs_winner_is_exact(engine, kind, args, n_cand):
+    """Sampled candidates with per-candidate outputs at fp32 (the dense fp32
+    kernel below TABLE_MIN_CAND, the two-polynomial table scorer above): the
+    winner is np.argmax of the oracle's fp64 scores of the very candidates
+    returned, index and value."""
+    from hyperopt_amd.engine import LabelWork
+    rng = np.random.RandomState(n_cand)
+    w0 = _mixture_case(rng, kind, args, 25, 4000, 1)
+    w = LabelWork(kind, kind, args, w0.obs_below, w0.obs_above, n_cand=n_cand, key=4242,
+                  cand_base=77)
+    r, = engine.run([w], precision=32, outputs=True)
+    with np.errstate(all="ignore"):
+        ref = O.continuous_label_scores(kind, args, w.obs_below, w.obs_above, r.cand)
+    assert r.index == 77 + ref["best"] and r.value == r.cand[ref["best"]]
 
 
 def test_argmax_ties_and_far_tails(engine):
@@ -129,6 +149,7 @@ def test_argmax_ties_and_far_tails(engine):
     r32, = engine.run([w], precision=32, outputs=True)
     np.testing.assert_allclose(r32.above_llik, ref["above_llik"], rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(r32.below_llik, ref["below_llik"], rtol=1e-4, atol=1e-4)
+    assert r32.index == ref["best"]  # ties: the first index, at fp32 too
 
 
 SORT_KINDS = [("uniform", (-5.0, 5.0), lambda r, n: r.uniform(-5, 5, n)),

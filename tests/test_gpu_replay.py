@@ -254,3 +254,48 @@ def test_issue_orders_give_the_same_level(variant):
         a = base.run(works, history=hb, is_below=isb)
         b = other.run(works, history=ho, is_below=isb)
         assert _rows(a) == _rows(b), (variant, step)
+
+
+@pytest.mark.parametrize("side", ["1", "0"])
+def test_graph_replay_equals_eager(side):
+    """A recorded level re-issued with the same words is captured into a
+    hipGraph (tpe_ops_capture, on the engine's own stream: the caller's may be
+    the null stream) and replayed (tpe_graph_launch): the keys and split flags
+    still change per call through the uploaded pack, and the winners equal the
+    eager engine's and the records-only engine's (TPE_GRAPHS=0), with and
+    without the side stream; a timed level is not captured."""
+    from hyperopt_amd.engine import LabelWork, WorkBatch
+    eager, native, DeviceHistory = _pair("native")
+    _, plain, _ = _pair("native")
+    plain.graphs = False
+    for e in (eager, native, plain):
+        e.side_stream = side
+    T = 3000
+    mat, active, losses = _history(T, 21)
+    active[:] = True
+    hs = [DeviceHistory(e, len(SPACE), cap=4096) for e in (eager, native, plain)]
+    for h in hs:
+        h.append(mat, active)
+    rng = np.random.RandomState(7)
+    space = [(j, e) for j, e in enumerate(SPACE) if e[1] != "qnormal"]
+    n_below = 14
+    for step in range(7):
+        isb = np.zeros(T, np.uint8)
+        isb[rng.choice(T, n_below, replace=False)] = 1
+        works = [LabelWork(lab, kind, a, mat[isb == 1, j], None, n_cand=1 << 16,
+                           key=977 * step + j, cand_base=0, col=j, n_above=T - n_below)
+                 for j, (lab, kind, a) in space]
+        out = []
+        for eng, h in zip((eager, native, plain), hs):
+            b = WorkBatch(("graph-test", side), [n_below] * len(works),
+                          [T - n_below] * len(works), [w.key for w in works],
+                          [0] * len(works), lambda works=works: works)
+            timers = {} if step == 5 else None  # a timed level: records only
+            r = eng.run(b, history=h, is_below=isb, timers=timers)
+            out.append((r.index.tolist(), r.value.tolist(), r.score.tolist(),
+                        r.n_scored.tolist()))
+        assert out[0] == out[1] == out[2], step
+    st = native.graph_stats
+    assert "capture_failed" not in st, st
+    assert st.get("captured", 0) >= 1 and st.get("graph", 0) >= 3, st
+    assert plain.graph_stats.get("graph", 0) == 0

@@ -171,6 +171,33 @@ def test_column_under_another_transform_is_rebuilt():
                          ref.run([w], posteriors=True, history=hr, is_below=isb))
 
 
+def test_alternating_column_sets_then_append():
+    """Levels over different column sets at one row count (X, Y, X -- a
+    nested space's branches, or suggest_many requests on one Trials), then an
+    append, then Y: the merge must bring Y's own columns up to the new rows
+    (the cached spec list once belonged to X)."""
+    from hyperopt_amd.engine import DeviceHistory
+    rng = np.random.RandomState(12)
+    total = 900 + 300
+    mat = _cols(total, rng)
+    active = rng.uniform(size=mat.shape) >= 0.1
+    losses = rng.normal(size=total)
+    srt, ref = _engines()
+    hs, hr = DeviceHistory(srt, len(SPACE), cap=16), DeviceHistory(ref, len(SPACE), cap=16)
+    X, Y = [0, 1, 2], [3, 4, 5, 6]
+    T = 0
+    for k, seq in ((900, (X, Y, X, Y, X)), (300, (Y, X, Y))):
+        for h in (hs, hr):
+            h.append(mat[T:T + k], active[T:T + k])
+        T += k
+        works, isb = _level(hs, mat, active, losses, T)
+        for cols in seq:
+            sub = [works[j] for j in cols]
+            _same_posteriors(srt.run(sub, posteriors=True, history=hs, is_below=isb),
+                             ref.run(sub, posteriors=True, history=hr, is_below=isb))
+    assert all(hs.order_rows[c] == T for c in X + Y)
+
+
 def test_sorted_fit_count_mismatch_raises():
     from hyperopt_amd import _lib as L
     from hyperopt_amd.engine import DeviceHistory

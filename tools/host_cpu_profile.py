@@ -79,7 +79,8 @@ class _Lib(object):
         self._lib = lib
 
     def __getattr__(self, name):
-        if name in L.OP_CODES or name in ("tpe_run_ops", "tpe_history_append"):
+        if name in L.OP_CODES or name in ("tpe_run_ops", "tpe_history_append", "tpe_ops_capture",
+                                          "tpe_graph_launch", "tpe_graph_destroy"):
             return lambda *a: 0
         return getattr(self._lib, name)
 
@@ -108,6 +109,8 @@ def make_engine():
     eng._last_gkey, eng._gen = None, 0
     eng.graph_stats = {"eager": 0}
     eng.native = os.environ.get("TPE_NATIVE_LAUNCH", "1") != "0"
+    eng.graphs = os.environ.get("TPE_GRAPHS", "1") == "1"
+    eng._cap_stream = _Stream()
     eng._oplists, eng._oplist_once, eng._replays, eng._staged_sig = {}, None, {}, None
     E.torch_shim = shim
     L.hip = lambda: eng._hip  # (DeviceHistory.append's event calls)
