@@ -592,6 +592,9 @@ def main():
     if every > 1:  # the timed variant of the level recorded before timing starts
         for k in range(2):
             step(args.warmup + k, {}, {group})
+    if eng.graphs:  # (TPE_DIAG=1 TPE_GRAPHS=1) the level's hipGraph captured before timing
+        for k in range(2):
+            step(args.warmup + 2 + k)
 
     def barrier():
         if world > 1:
@@ -736,6 +739,7 @@ def main():
                    "rank0_units": len(units)},
         "roofline": roofline,
         "group_ms": group_ms,
+        "launch": dict(eng.graph_stats),
     }
     if rank == 0 and world == 1 and not args.no_extras:
         if args.precision == 32:  # the fp64 parity mode's throughput on the same workload

@@ -779,14 +779,16 @@ __device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
                                            const double* __restrict__ mu,
                                            const double* __restrict__ sigma,
                                            tpe_best* __restrict__ partial, int job, int64_t s,
-                                           int64_t nper, double* sh, const double* __restrict__ P,
+                                           int64_t nper, const double* __restrict__ P,
                                            const double* __restrict__ Sm);
+constexpr int kSlotsPerBlock = kBS / kWave;  // score_slot: one wave per lattice slot
 
 // Candidates [start, min(n_cand, limit)) of every job (start a multiple of the
 // kBS * kLatR tile); need (nullable): only the jobs whose flag is set.
 // slot_n > 0 (tpe_lattice_suggest's first launch): the grid's first
-// slot_n * n_jobs blocks score the lattice slots instead (score_slot; the
-// slot scores do not depend on the draws, so they share the launch)
+// ceil(slot_n / kSlotsPerBlock) * n_jobs blocks score the lattice slots
+// instead, one wave per slot (score_slot; the slot scores do not depend on
+// the draws, so they share the launch)
 template <bool POW2>
 #ifndef TPE_LAT_WPE  // diagnostic builds: waves-per-EU target of the lattice sampler
 #define TPE_LAT_WPE 4     // (power-of-two candidate counts: 128 VGPRs, no spill)
@@ -801,13 +803,16 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_
     const double* __restrict__ qS) {
   extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
-  __shared__ alignas(16) float s_stage[kLatR * kBS];  // (also the slot blocks' fp64 scratch)
+  __shared__ alignas(16) float s_stage[kLatR * kBS];
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
-  const int64_t slot_blocks = (int64_t)slot_n * n_jobs;
+  const int64_t spj = ((int64_t)slot_n + kSlotsPerBlock - 1) / kSlotsPerBlock;  // per job
+  const int64_t slot_blocks = spj * n_jobs;
   if ((int64_t)blockIdx.x < slot_blocks) {  // block-uniform
-    const int job = (int)(blockIdx.x / slot_n);
-    score_slot(jobs, segs, w, mu, sigma, slot_part, job, (int64_t)blockIdx.x - (int64_t)job * slot_n,
-               slot_n, reinterpret_cast<double*>(s_stage), qP, qS);
+    const int job = (int)(blockIdx.x / spj);
+    const int64_t sb = (int64_t)blockIdx.x - (int64_t)job * spj;
+    const int64_t slot = sb * kSlotsPerBlock + threadIdx.x / kWave;
+    if (slot < slot_n)  // wave-uniform
+      score_slot(jobs, segs, w, mu, sigma, slot_part, job, slot, slot_n, qP, qS);
     return;
   }
   const unsigned bid = (unsigned)((int64_t)blockIdx.x - slot_blocks);
@@ -1079,16 +1084,18 @@ __global__ __launch_bounds__(kQB) void k_qreach(const tpe_job* __restrict__ jobs
 }
 
 // how many leading k in [0, n) satisfy pred (pred holds on a prefix): a
-// block-wide search, kBS probes per round (three rounds for n <= 2^24)
+// wave-wide search, kWave probes per round (three rounds for n <= 2^18); call
+// by the whole wave (n wave-uniform)
 template <typename F>
-__device__ __forceinline__ int prefix_count(int n, F pred) {
+__device__ __forceinline__ int wave_prefix_count(int n, F pred) {
   int lo = 0, len = n;
-  while (len > 0) {  // block-uniform
-    const int stride = (len + kBS - 1) / kBS;
+  const int t = lane_id();
+  while (len > 0) {  // wave-uniform
+    const int stride = (len + kWave - 1) / kWave;
     const int nprobe = (len + stride - 1) / stride;
-    const int t = threadIdx.x;
     const int p = lo + min((t + 1) * stride, len) - 1;
-    const int c = __syncthreads_count(t < nprobe && pred(p));
+    // pred holds on a prefix, so the lanes whose probe holds are a prefix too
+    const int c = __popcll(__ballot(t < nprobe && pred(p)));
     if (c == nprobe) return lo + len;
     lo += c * stride;
     len = min(stride, len - c * stride) - 1;  // (probe c failed: the boundary is before it)
@@ -1096,15 +1103,22 @@ __device__ __forceinline__ int prefix_count(int n, F pred) {
   return lo;
 }
 
-// quantized mixture log-mass of one value, one block, threads stride components.
-// tpe.py:159-174 (GMM1) and :288-305 (LGMM1): sum_k w_k*cdf(ub) - w_k*cdf(lb),
-// then log(prob) - log(p_accept).  P / Sm (nullable): k_qreach's arrays --
-// the loop then covers the value's component window only (same sums).
+// quantized mixture log-mass of one value, one WAVE, lanes stride components
+// (lane l takes components k = l mod 64, in order).  tpe.py:159-174 (GMM1) and
+// :288-305 (LGMM1): sum_k w_k*cdf(ub) - w_k*cdf(lb), then log(prob) -
+// log(p_accept).  P / Sm (nullable): k_qreach's arrays -- the loop then
+// covers the value's component window only, entered at the full loop's pass
+// that holds the window's first component, so every lane visits the same
+// components in the same order and skips the same ones: the same sums, bit
+// for bit.  The lanes' partial sums meet in one fixed butterfly.  Round 6: a
+// wave per value instead of a 256-thread block (C4's ~370-component windows
+// left a block's threads one or two components each, behind eight block-wide
+// barriers per value).  Every lane returns the value.
 __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
                                         const double* __restrict__ w,
                                         const double* __restrict__ mu,
                                         const double* __restrict__ sigma, double x,
-                                        int32_t* err, double* sh,
+                                        int32_t* err,
                                         const double* __restrict__ P = nullptr,
                                         const double* __restrict__ Sm = nullptr) {
   const bool lg = J.family == TPE_LGMM1;
@@ -1113,32 +1127,31 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
   if (J.flags & TPE_F_HIGH) ub = fmin(ub, lg ? exp(J.high) : J.high);
   if (J.flags & TPE_F_LOW) lb = fmax(lb, lg ? exp(J.low) : J.low);
   double lub = 0.0, llb = 0.0;
+  const int lane = lane_id();
   if (lg) {
     lb = fmax(0.0, lb);
-    if (ub < 0.0 && threadIdx.x == 0 && err) atomicOr(err, 1);  // tpe.py:196-197
+    if (ub < 0.0 && lane == 0 && err) atomicOr(err, 1);  // tpe.py:196-197
     lub = log(ub < kEps ? kEps : ub);
     llb = log(lb < kEps ? kEps : lb);
   }
   const int nc = S.n_obs + 1;
   double acc = 0.0;
   const double xu = lg ? lub : ub, xl = lg ? llb : lb;
-  // kQU components per thread per pass, their loads issued together (the
-  // skip test is cheap; a serial load -> test chain per component is what
-  // bounded this loop)
+  // kQU components per lane per pass, their loads issued together
   constexpr int kQU = 4;
+  constexpr int kPassQ = kQU * kWave;
   int kbeg = 0, kend = nc;
   const double dl = 1e-9 * (1.0 + fabs(xl) + fabs(xu));  // (covers the fp64 rounding of mu +- b)
   const double wa = xl - dl, wb = xu + dl;
-  if (P && wa == wa && wb == wb) {  // block-uniform
-    kbeg = prefix_count(nc, [&](int k) { return P[S.comp_off + k] <= wa; });
-    kend = max(kbeg, prefix_count(nc, [&](int k) { return Sm[S.comp_off + k] < wb; }));
+  if (P && wa == wa && wb == wb) {  // wave-uniform
+    kbeg = wave_prefix_count(nc, [&](int k) { return P[S.comp_off + k] <= wa; });
+    kend = max(kbeg, wave_prefix_count(nc, [&](int k) { return Sm[S.comp_off + k] < wb; }));
   }
-  // the full loop's thread-to-component map, entered at the window's first pass
-  for (int k0 = kbeg / (kQU * kBS) * (kQU * kBS) + threadIdx.x; k0 < kend; k0 += kQU * kBS) {
+  for (int k0 = kbeg / kPassQ * kPassQ + lane; k0 < kend; k0 += kPassQ) {
     double mq[kQU], sq[kQU];
 #pragma unroll
     for (int u = 0; u < kQU; ++u) {
-      const int k = k0 + u * kBS;
+      const int k = k0 + u * kWave;
       const bool in = k >= kbeg && k < kend;
       mq[u] = in ? mu[S.comp_off + k] : INFINITY;
       sq[u] = in ? sigma[S.comp_off + k] : 1.0;
@@ -1151,7 +1164,7 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
       // (padding: m = +inf is skipped)
       const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
       if (xl - m >= b65 || xu - m <= -b65 || m == INFINITY) continue;
-      const double wk = w[S.comp_off + k0 + u * kBS];
+      const double wk = w[S.comp_off + k0 + u * kWave];
       double cu, cl;
       if (lg) {
         cu = lognormal_cdf_logx(lub, m, s);
@@ -1163,35 +1176,40 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
       acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
     }
   }
-  acc = block_sum<kBS, double>(acc, sh);
+#pragma unroll
+  for (int o = kWave / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, kWave);
   return log(acc) - log(S.p_accept);
 }
 
-// one block per value: 256 threads share its ~10^4 component CDF pairs, so a
-// level's ~10^3 present values keep every SIMD busy
-constexpr int kQW = 1;
+// one wave per value (kQW values per 256-thread block): the wave shares the
+// value's component CDF pairs
+constexpr int kQW = kBS / kWave;
 
+// grid (ceil(nper / kQW), n_jobs): value pos = kQW blockIdx.x + wave of job
+// blockIdx.y; nper = the partial entries per job (>= every job's count)
 __global__ __launch_bounds__(kBS) void k_score_q(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ w, const double* __restrict__ mu,
     const double* __restrict__ sigma, const double* __restrict__ vals,
     const int64_t* __restrict__ firsts, const unsigned long long* __restrict__ counts,
     double* __restrict__ out_bl, double* __restrict__ out_al, tpe_best* __restrict__ partial,
-    int32_t* __restrict__ err, const double* __restrict__ qP, const double* __restrict__ qS) {
-  __shared__ double sh[kBS / kWave];
+    int32_t* __restrict__ err, const double* __restrict__ qP, const double* __restrict__ qS,
+    int64_t nper) {
   const tpe_job J = jobs[blockIdx.y];
   const int64_t cnt = counts ? (int64_t)counts[blockIdx.y] : J.n_cand;
-  const int64_t pos = blockIdx.x;
-  tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-  if (pos >= cnt) {  // block-uniform
-    if (threadIdx.x == 0) *P = empty_best();
+  const int64_t pos = (int64_t)blockIdx.x * kQW + threadIdx.x / kWave;
+  if (pos >= nper) return;  // wave-uniform
+  tpe_best* P = partial + (int64_t)blockIdx.y * nper + pos;
+  const bool lead = lane_id() == 0;
+  if (pos >= cnt) {  // wave-uniform
+    if (lead) *P = empty_best();
     return;
   }
   const int64_t voff = counts ? J.lat_off : J.cand_off;
   const double v = vals[voff + pos];
-  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err, sh, qP, qS);
-  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err, sh, qP, qS);
-  if (threadIdx.x == 0) {
+  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err, qP, qS);
+  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err, qP, qS);
+  if (lead) {
     const int64_t idx = firsts ? firsts[J.lat_off + pos] : J.cand_base + pos;
     if (out_bl) out_bl[J.out_off + pos] = bl;
     if (out_al) out_al[J.out_off + pos] = al;
@@ -1217,18 +1235,18 @@ __device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
                                            const double* __restrict__ mu,
                                            const double* __restrict__ sigma,
                                            tpe_best* __restrict__ partial, int job, int64_t s,
-                                           int64_t nper, double* sh, const double* __restrict__ P,
+                                           int64_t nper, const double* __restrict__ P,
                                            const double* __restrict__ Sm) {
   const tpe_job J = jobs[job];
-  if (s >= J.lat_n) return;  // block-uniform
+  if (s >= J.lat_n) return;  // wave-uniform
   const double v = (double)(J.lat_kmin + s) * J.q;  // np.round(x/q) * q, as k_lattice_compact
   // every slot is scored, drawn or not: a slot below 0 (the bracket under a
   // qloguniform / qlognormal lattice, never drawn) must not raise the
   // reference's negative-argument error (tpe.py:196-197) -- a drawn value
   // x = round(exp(y)/q)*q >= 0 never has ub = x + q/2 < 0, so no err here
-  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, nullptr, sh, P, Sm);
-  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, nullptr, sh, P, Sm);
-  if (threadIdx.x == 0) partial[(int64_t)job * nper + s] = tpe_best{bl - al, -1, v, 0};
+  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, nullptr, P, Sm);
+  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, nullptr, P, Sm);
+  if (lane_id() == 0) partial[(int64_t)job * nper + s] = tpe_best{bl - al, -1, v, 0};
 }
 
 // Can the sampler put a draw on slot s at all?  Only unseen slots that could
@@ -1727,7 +1745,8 @@ static bool launch_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
     gx = std::max(gx, (n + (int64_t)kBS * kLatR - 1) / ((int64_t)kBS * kLatR));
   }
   const int64_t per = (gx * n_jobs + 7) / 8;
-  const int64_t sblocks = need ? 0 : slot_n * n_jobs;  // slot scoring rides on the prefix launch
+  // slot scoring rides on the prefix launch (one wave per slot)
+  const int64_t sblocks = need ? 0 : (slot_n + kSlotsPerBlock - 1) / kSlotsPerBlock * n_jobs;
   if (gx > INT32_MAX || 8 * per + sblocks > INT32_MAX || slot_n > INT32_MAX) {
     set_error("%s: %lld work items", who, (long long)(gx * n_jobs));
     return false;
@@ -1873,7 +1892,7 @@ extern "C" int tpe_lattice_compact(const tpe_job* jobs, const tpe_job* host_jobs
 
 extern "C" int64_t tpe_quantized_partials(const tpe_job* host_jobs, int n_jobs, int64_t max_vals) {
   (void)host_jobs;
-  return (int64_t)n_jobs * std::max((int64_t)1, (max_vals + kQW - 1) / kQW);
+  return (int64_t)n_jobs * std::max((int64_t)1, max_vals);  // one entry per value
 }
 
 extern "C" int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs, int n_jobs,
@@ -1896,7 +1915,7 @@ extern "C" int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs
       set_error("tpe_score_quantized: job %d is not quantized", i);
       return TPE_E_ARG;
     }
-  const int64_t gx = std::max((int64_t)1, (max_vals + kQW - 1) / kQW);
+  const int64_t gx = std::max((int64_t)1, max_vals);  // partial entries per job
   if (gx * n_jobs > n_partial) {
     set_error("tpe_score_quantized: partial workspace too small");
     return TPE_E_ARG;
@@ -1906,9 +1925,10 @@ extern "C" int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs
   if (win)
     hipLaunchKernelGGL(k_qreach, dim3(4 * n_jobs), dim3(kQB), 0, st, jobs, segs, mu, sigma,
                        reach_hi, reach_lo);
-  hipLaunchKernelGGL(k_score_q, dim3((unsigned)gx, (unsigned)n_jobs), dim3(kBS), 0, st, jobs,
-                     segs, w, mu, sigma, vals, firsts, (const unsigned long long*)counts, out_bl,
-                     out_al, partial, err, win ? reach_hi : nullptr, win ? reach_lo : nullptr);
+  hipLaunchKernelGGL(k_score_q, dim3((unsigned)((gx + kQW - 1) / kQW), (unsigned)n_jobs),
+                     dim3(kBS), 0, st, jobs, segs, w, mu, sigma, vals, firsts,
+                     (const unsigned long long*)counts, out_bl, out_al, partial, err,
+                     win ? reach_hi : nullptr, win ? reach_lo : nullptr, gx);
   hipLaunchKernelGGL(k_reduce, dim3(n_jobs), dim3(kBS), 0, st, jobs, partial, gx, best);
   return check_launch("tpe_score_quantized");
 }

@@ -2673,7 +2673,8 @@ __device__ __forceinline__ double lse64_pruned(const tpe_seg& S, const double* _
                                                const double* __restrict__ rh,
                                                const double* __restrict__ rl,
                                                const int32_t* __restrict__ wide, int n_wide,
-                                               double m, bool act, bool inr, double y) {
+                                               double m, bool act, bool inr, double y,
+                                               double4* stage) {
   const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
   int k_lo = nc, k_hi = -1;
@@ -2683,12 +2684,34 @@ __device__ __forceinline__ double lse64_pruned(const tpe_seg& S, const double* _
   }
   const int ulo = wave_min_i(k_lo), uhi = wave_max_i(k_hi);
   double s = 0.0;
-  for (int k = ulo; k <= uhi; ++k) {
-    const double4 c = ld4(coef64, off + k);
-    if (is_wide(S, k, c.y)) continue;
-    const double t = (y - c.x) * c.y;
-    const double e = exp(fma(-0.5 * t, t, c.z - m));
-    s += (k >= k_lo && k <= k_hi) ? e : 0.0;
+  // the union window in chunks of 64 components: one coalesced load per lane
+  // into the wave's LDS slice (the wide flag folded in as w = 0), then every
+  // lane reads the chunk's components in order by LDS broadcast -- the same
+  // terms added in the same order as a loop over the window with a scalar
+  // load per component (round 6: that loop waited on two dependent scalar
+  // loads per component), so the sums are the same bits
+  const int lane = lane_id();
+  for (int kb = ulo; kb <= uhi; kb += kWave) {  // wave-uniform
+    const int kk = kb + lane;
+    double4 c = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (kk <= uhi) {
+      c = ld4(coef64, off + kk);
+      c.w = is_wide(S, kk, c.y) ? 0.0 : 1.0;
+    }
+    stage[lane] = c;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int n = min(kWave, uhi - kb + 1);
+#pragma unroll 2
+    for (int j = 0; j < n; ++j) {
+      const double4 cj = stage[j];
+      const int k = kb + j;
+      const double t = (y - cj.x) * cj.y;
+      const double e = exp(fma(-0.5 * t, t, cj.z - m));
+      s += (cj.w != 0.0 && k >= k_lo && k <= k_hi) ? e : 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();  // (the chunk read before the next one is staged)
   }
   if (__any(act && inr)) {
     for (int i = 0; i < n_wide; ++i) {
@@ -2754,6 +2777,7 @@ __global__ __launch_bounds__(kBS) void k_score_pruned64(
   __shared__ double dred[kBS / kWave];
   __shared__ double s_key[kP64N], s_x[kP64N];
   __shared__ uint16_t s_idx[kP64N];
+  __shared__ double4 s_win[kBS / kWave][kWave];  // each wave's chunk of its union window
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kP64N;
@@ -2804,9 +2828,9 @@ __global__ __launch_bounds__(kBS) void k_score_pruned64(
     const double y = s_key[p], x = s_x[i];
     const bool inr = y >= Tb.lo && y <= Tb.hi;
     double bl = lse64_pruned(SB, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below, mb, act,
-                             inr, y);
+                             inr, y, s_win[wid]);
     double al = lse64_pruned(SA, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above, ma, act,
-                             inr, y);
+                             inr, y, s_win[wid]);
     if (!act) continue;
     if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
       bl -= y;

@@ -199,12 +199,22 @@ class _Pack:
         return off
 
 
+_KNOBS_WARNED = set()
+
+
 def _knob(name, default):
     """A level-launcher switch kept for A/B runs: the product
     path takes ``default``; an environment override is read only when
-    TPE_DIAG=1 (diagnostic runs)."""
+    TPE_DIAG=1 (diagnostic runs).  An override set without TPE_DIAG=1 is
+    ignored with a one-time warning, so it is never dropped silently."""
     if os.environ.get("TPE_DIAG") == "1":
         return os.environ.get(name, default)
+    if name in os.environ and name not in _KNOBS_WARNED:
+        _KNOBS_WARNED.add(name)
+        import warnings
+        warnings.warn("hyperopt_amd: %s=%s is ignored (engine switches are read only with "
+                      "TPE_DIAG=1; the product default %r is used)"
+                      % (name, os.environ[name], default), RuntimeWarning, stacklevel=3)
     return default
 
 
@@ -521,9 +531,11 @@ class Engine:
         # launch, stream fork/join, readback and the final synchronise -- and
         # re-issued with one C call per level (hyperopt_amd/csrc/tpe_ops.hip)
         self.native = _knob("TPE_NATIVE_LAUNCH", "1") != "0"
-        # recorded levels re-issued with the same words replay a hipGraph of
-        # their records (_OpList.issue; TPE_GRAPHS=0: always tpe_run_ops)
-        self.graphs = _knob("TPE_GRAPHS", "1") == "1"
+        # TPE_GRAPHS=1 (diagnostic): recorded levels re-issued with the same
+        # words replay a hipGraph of their records (_OpList.issue).  Off in the
+        # product: on ROCm 7 a replayed C3 level is no faster on the host and
+        # slower on the GPU than the records
+        self.graphs = _knob("TPE_GRAPHS", "0") == "1"
         self._cap_stream = None
         self._oplists = {}      # launch key -> _OpList
         self._oplist_once = None
@@ -2334,7 +2346,7 @@ class _OpList(_Timing):
         # [0, cut) and the words it was captured from; the rest (the host's
         # event or stream sync, an RCCL exchange) is issued after it
         self.graph = self.graph_words = self.last_words = None
-        self.cut = 0
+        self.cut = self.g0 = 0
         self.stream = None
         self.no_graph = False
 
@@ -2364,10 +2376,17 @@ class _OpList(_Timing):
         arr = np.zeros(len(self.rows), L.OP_DTYPE)
         self.stream = stream
         codes = [code for code, _ in self.rows]
-        # captured: every record before the last (the result event or stream
-        # sync the host waits on) and before an RCCL exchange
-        self.cut = min([len(codes) - 1] + [i for i, c in enumerate(codes)
-                                           if c in (L.OP_MAXLOC_ALLREDUCE, L.OP_STREAM_SYNC)])
+        # captured: the records between the pack's upload (a plain async copy
+        # from pinned memory, issued before the graph) and the first of the
+        # readback copy, an RCCL exchange, or the result event / stream sync
+        # the host waits on (issued after it): kernels and stream fork / join
+        self.g0 = 0
+        while self.g0 < len(codes) and codes[self.g0] == L.OP_MEMCPY:
+            self.g0 += 1
+        tail = [i for i, (c, a) in enumerate(self.rows)
+                if i >= self.g0 and (c in (L.OP_MAXLOC_ALLREDUCE, L.OP_STREAM_SYNC) or
+                                     (c == L.OP_MEMCPY and len(a) > 3 and a[3] == L.D2H))]
+        self.cut = min([len(codes) - 1] + tail)
         self.sizes = []  # (record, argument, size name): the words _Replay rewrites
         for i, (code, args) in enumerate(self.rows):
             if len(args) > L.OP_ARGS:
@@ -2393,32 +2412,41 @@ class _OpList(_Timing):
         lib = self.lib
         failed = ctypes.c_int(-1)
         start = 0
-        if eng.graphs and self.cut > 0 and not self.timed and not self.no_graph:
+        OPB = L.OP_DTYPE.itemsize
+        if eng.graphs and self.cut > self.g0 and not self.timed and not self.no_graph:
             words = self.arr.tobytes()
             if self.graph is not None and words != self.graph_words:
                 lib.tpe_graph_destroy(self.graph)
                 self.graph = self.graph_words = None
             if self.graph is None and words == self.last_words:
                 g = ctypes.c_void_p()
-                rc = lib.tpe_ops_capture(self.ptr, self.cut, self.stream, eng._capture_stream(),
-                                         ctypes.byref(g), ctypes.byref(failed))
+                t0 = time.perf_counter()
+                rc = lib.tpe_ops_capture(self.ptr + self.g0 * OPB, self.cut - self.g0,
+                                         self.stream, eng._capture_stream(), ctypes.byref(g),
+                                         ctypes.byref(failed))
                 if rc == 0:
                     self.graph, self.graph_words = g, words
                     eng.graph_stats["captured"] = eng.graph_stats.get("captured", 0) + 1
+                    eng.graph_stats["capture_ms"] = eng.graph_stats.get("capture_ms", 0.0) + \
+                        (time.perf_counter() - t0) * 1e3
                 else:  # this level stays on tpe_run_ops (the reason kept for diagnosis)
                     self.no_graph = True
                     eng.graph_stats["capture_failed"] = lib.tpe_last_error().decode(
                         errors="replace")
             self.last_words = words
             if self.graph is not None:
+                if self.g0:  # the upload
+                    rc = lib.tpe_run_ops(self.ptr, self.g0, ctypes.byref(failed))
+                    if rc != 0:
+                        raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
+                            rc, failed.value, lib.tpe_last_error().decode(errors="replace")))
                 rc = lib.tpe_graph_launch(self.graph, self.stream)
                 if rc != 0:
                     raise L.TpeHipError("tpe_graph_launch failed (%d): %s" % (
                         rc, lib.tpe_last_error().decode(errors="replace")))
                 eng.graph_stats["graph"] = eng.graph_stats.get("graph", 0) + 1
                 start = self.cut
-        rc = lib.tpe_run_ops(self.ptr + start * L.OP_DTYPE.itemsize, self.n - start,
-                             ctypes.byref(failed))
+        rc = lib.tpe_run_ops(self.ptr + start * OPB, self.n - start, ctypes.byref(failed))
         if rc != 0:
             raise L.TpeHipError("tpe_run_ops failed (%d) at record %d: %s" % (
                 rc, start + failed.value, lib.tpe_last_error().decode(errors="replace")))

@@ -267,7 +267,7 @@ def test_graph_replay_equals_eager(side):
     from hyperopt_amd.engine import LabelWork, WorkBatch
     eager, native, DeviceHistory = _pair("native")
     _, plain, _ = _pair("native")
-    plain.graphs = False
+    native.graphs, plain.graphs = True, False  # (graphs: a diagnostic switch, off by default)
     for e in (eager, native, plain):
         e.side_stream = side
     T = 3000

@@ -390,3 +390,79 @@ def test_split_inputs_fast_path_matches_split_masks():
             np.testing.assert_array_equal(np.sort(rows[:got]), np.flatnonzero(isb))
             np.testing.assert_array_equal(nb, nb_ref)
             np.testing.assert_array_equal(na, na_ref)
+
+
+def test_level_inputs_fast_equals_general_path():
+    """LevelInputs.fast itself (not only tpe_split_inputs) against
+    split_masks + LevelInputs on a real Columnar: flags, below values and
+    activity, below / above counts, run_kwargs; and its None fallbacks -- a
+    history over a row subset, from_tid aliasing, fewer history rows than
+    cached rows, no engine.  split_masks' n_alias == 0 shortcut equals its
+    np.isin path.  The HBM mirror is stubbed (device_history: no GPU here)."""
+    from hyperopt_amd import tpe as T_
+    from hyperopt_amd.base import Columnar
+    from hyperopt_amd.tpe import History, LevelInputs, split_masks
+
+    labels = ("a", "b", "c")
+    rng = np.random.RandomState(4)
+    sentinel = object()
+
+    def docs(n, alias=False):
+        out = []
+        for t in range(n):
+            vals = {lab: ([float(rng.normal())] if rng.uniform() < 0.8 else []) for lab in labels}
+            misc = {"tid": t, "vals": vals, "idxs": {}}
+            if alias and t > 3 and rng.uniform() < 0.3:
+                misc["from_tid"] = int(rng.randint(t))
+            out.append({"tid": t, "misc": misc, "state": 2,
+                        "result": {"loss": float(np.round(rng.normal() * 2) / 2)}})
+        return out
+
+    for T in (1, 30, 500):
+        col = Columnar(labels)
+        col.extend(docs(T))
+        col.device_history = lambda eng: sentinel
+        losses = col.losses()
+        hist = History(col.key_tid[:T], losses, col.obs_tid[:T], col=col)
+        for gamma in (0.25, 1.0):
+            fast = LevelInputs.fast(hist, gamma, eng=object())
+            isb, isa = split_masks(hist, gamma)
+            ref = LevelInputs(hist, isb, isa, eng=object())
+            assert fast is not None and fast.device and ref.device
+            np.testing.assert_array_equal(fast.isb, isb)
+            np.testing.assert_array_equal(fast.vb[fast.ab], ref.vb[ref.ab])
+            np.testing.assert_array_equal(fast.ab, ref.ab)
+            np.testing.assert_array_equal(fast.nb, ref.nb)
+            np.testing.assert_array_equal(fast.n_above, ref.n_above)
+            assert fast.run_kwargs["history"] is sentinel and fast.run_kwargs["rows"] is None
+            np.testing.assert_array_equal(fast.run_kwargs["is_below"], ref.run_kwargs["is_below"])
+            # the shortcut of split_masks (no aliasing) equals the np.isin path
+            below = np.zeros(T, bool)
+            below[T_._smallest_rows(hist.losses, isb.sum())] = True
+            np.testing.assert_array_equal(np.isin(hist.obs_tids, hist.tids[below]), isb)
+            np.testing.assert_array_equal(np.isin(hist.obs_tids, hist.tids[~below]), isa)
+        # the fallbacks
+        sub = History(col.key_tid[:T], losses, col.obs_tid[:T], col=col, rows=np.arange(T))
+        assert LevelInputs.fast(sub, 0.25, eng=object()) is None
+        assert LevelInputs.fast(hist, 0.25, eng=None) is None
+        if T > 1:
+            short = History(col.key_tid[:T - 1], losses[:T - 1], col.obs_tid[:T - 1], col=col)
+            assert LevelInputs.fast(short, 0.25, eng=object()) is None
+    col = Columnar(labels)
+    col.extend(docs(60, alias=True))
+    assert col.n_alias > 0
+    h = History(col.key_tid[:60], col.losses(), col.obs_tid[:60], col=col)
+    assert LevelInputs.fast(h, 0.25, eng=object()) is None
+
+
+def test_engine_switch_without_diag_warns(monkeypatch):
+    """an engine switch set without TPE_DIAG=1 is ignored with a
+    one-time warning; with TPE_DIAG=1 it is honoured."""
+    from hyperopt_amd import engine as E
+    monkeypatch.delenv("TPE_DIAG", raising=False)
+    monkeypatch.setenv("TPE_SIDE_STREAM", "0")
+    E._KNOBS_WARNED.discard("TPE_SIDE_STREAM")
+    with pytest.warns(RuntimeWarning, match="TPE_SIDE_STREAM"):
+        assert E._knob("TPE_SIDE_STREAM", "1") == "1"
+    monkeypatch.setenv("TPE_DIAG", "1")
+    assert E._knob("TPE_SIDE_STREAM", "1") == "0"

@@ -109,7 +109,7 @@ def make_engine():
     eng._last_gkey, eng._gen = None, 0
     eng.graph_stats = {"eager": 0}
     eng.native = os.environ.get("TPE_NATIVE_LAUNCH", "1") != "0"
-    eng.graphs = os.environ.get("TPE_GRAPHS", "1") == "1"
+    eng.graphs = os.environ.get("TPE_GRAPHS", "0") == "1"
     eng._cap_stream = _Stream()
     eng._oplists, eng._oplist_once, eng._replays, eng._staged_sig = {}, None, {}, None
     E.torch_shim = shim
