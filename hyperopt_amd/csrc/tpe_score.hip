@@ -773,22 +773,22 @@ __host__ __device__ __forceinline__ bool lattice_pow2(const tpe_job& j) {
          j.lat_n <= kLatLds;
 }
 
-__device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
-                                           const tpe_seg* __restrict__ segs,
-                                           const double* __restrict__ w,
-                                           const double* __restrict__ mu,
-                                           const double* __restrict__ sigma,
-                                           tpe_best* __restrict__ partial, int job, int64_t s,
-                                           int64_t nper, const double* __restrict__ P,
-                                           const double* __restrict__ Sm);
-constexpr int kSlotsPerBlock = kBS / kWave;  // score_slot: one wave per lattice slot
+__device__ __forceinline__ void score_slots(const tpe_job* __restrict__ jobs,
+                                            const tpe_seg* __restrict__ segs,
+                                            const double* __restrict__ w,
+                                            const double* __restrict__ mu,
+                                            const double* __restrict__ sigma,
+                                            tpe_best* __restrict__ partial, int job, int64_t sb,
+                                            int64_t nper, double* sh,
+                                            const double* __restrict__ P,
+                                            const double* __restrict__ Sm);
+constexpr int kSlotsPerBlock = kBS / kWave;  // score_slots: lattice slots per block
 
 // Candidates [start, min(n_cand, limit)) of every job (start a multiple of the
 // kBS * kLatR tile); need (nullable): only the jobs whose flag is set.
 // slot_n > 0 (tpe_lattice_suggest's first launch): the grid's first
-// ceil(slot_n / kSlotsPerBlock) * n_jobs blocks score the lattice slots
-// instead, one wave per slot (score_slot; the slot scores do not depend on
-// the draws, so they share the launch)
+// slot_n * n_jobs blocks score the lattice slots instead (score_slots; the
+// slot scores do not depend on the draws, so they share the launch)
 template <bool POW2>
 #ifndef TPE_LAT_WPE  // diagnostic builds: waves-per-EU target of the lattice sampler
 #define TPE_LAT_WPE 4     // (power-of-two candidate counts: 128 VGPRs, no spill)
@@ -803,16 +803,15 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_
     const double* __restrict__ qS) {
   extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
-  __shared__ alignas(16) float s_stage[kLatR * kBS];
+  __shared__ alignas(16) float s_stage[kLatR * kBS];  // (also the slot blocks' fp64 scratch)
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
-  const int64_t spj = ((int64_t)slot_n + kSlotsPerBlock - 1) / kSlotsPerBlock;  // per job
+  const int64_t spj = slot_n;  // slot blocks per job (score_slots)
   const int64_t slot_blocks = spj * n_jobs;
   if ((int64_t)blockIdx.x < slot_blocks) {  // block-uniform
     const int job = (int)(blockIdx.x / spj);
     const int64_t sb = (int64_t)blockIdx.x - (int64_t)job * spj;
-    const int64_t slot = sb * kSlotsPerBlock + threadIdx.x / kWave;
-    if (slot < slot_n)  // wave-uniform
-      score_slot(jobs, segs, w, mu, sigma, slot_part, job, slot, slot_n, qP, qS);
+    score_slots(jobs, segs, w, mu, sigma, slot_part, job, sb, slot_n,
+                reinterpret_cast<double*>(s_stage), qP, qS);
     return;
   }
   const unsigned bid = (unsigned)((int64_t)blockIdx.x - slot_blocks);
@@ -1181,12 +1180,110 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
   return log(acc) - log(S.p_accept);
 }
 
+// how many leading k in [0, n) satisfy pred (pred holds on a prefix): a
+// block-wide search, kBS probes per round (three rounds for n <= 2^24)
+template <typename F>
+__device__ __forceinline__ int prefix_count(int n, F pred) {
+  int lo = 0, len = n;
+  while (len > 0) {  // block-uniform
+    const int stride = (len + kBS - 1) / kBS;
+    const int nprobe = (len + stride - 1) / stride;
+    const int t = threadIdx.x;
+    const int p = lo + min((t + 1) * stride, len) - 1;
+    const int c = __syncthreads_count(t < nprobe && pred(p));
+    if (c == nprobe) return lo + len;
+    lo += c * stride;
+    len = min(stride, len - c * stride) - 1;  // (probe c failed: the boundary is before it)
+  }
+  return lo;
+}
+
+// The same log-mass with the whole BLOCK on one value (threads stride the
+// components, k = t mod 256; block-wide window search and sum): for mixtures
+// of more than kQBig components (C3's 10^4, C5's 10^5), whose windows give a wave
+// thousands of CDF pairs.  Its own bits (another lane map), chosen per
+// mixture size alone (qlpdf_big), so every kernel scoring a value picks the
+// same variant.
+__device__ __forceinline__ double qlpdf_block(const tpe_job& J, const tpe_seg& S,
+                                        const double* __restrict__ w,
+                                        const double* __restrict__ mu,
+                                        const double* __restrict__ sigma, double x,
+                                        int32_t* err, double* sh,
+                                        const double* __restrict__ P = nullptr,
+                                        const double* __restrict__ Sm = nullptr) {
+  const bool lg = J.family == TPE_LGMM1;
+  const double hq = J.q / 2.0;
+  double ub = x + hq, lb = x - hq;
+  if (J.flags & TPE_F_HIGH) ub = fmin(ub, lg ? exp(J.high) : J.high);
+  if (J.flags & TPE_F_LOW) lb = fmax(lb, lg ? exp(J.low) : J.low);
+  double lub = 0.0, llb = 0.0;
+  if (lg) {
+    lb = fmax(0.0, lb);
+    if (ub < 0.0 && threadIdx.x == 0 && err) atomicOr(err, 1);  // tpe.py:196-197
+    lub = log(ub < kEps ? kEps : ub);
+    llb = log(lb < kEps ? kEps : lb);
+  }
+  const int nc = S.n_obs + 1;
+  double acc = 0.0;
+  const double xu = lg ? lub : ub, xl = lg ? llb : lb;
+  // kQU components per thread per pass, their loads issued together (the
+  // skip test is cheap; a serial load -> test chain per component is what
+  // bounded this loop)
+  constexpr int kQU = 4;
+  int kbeg = 0, kend = nc;
+  const double dl = 1e-9 * (1.0 + fabs(xl) + fabs(xu));  // (covers the fp64 rounding of mu +- b)
+  const double wa = xl - dl, wb = xu + dl;
+  if (P && wa == wa && wb == wb) {  // block-uniform
+    kbeg = prefix_count(nc, [&](int k) { return P[S.comp_off + k] <= wa; });
+    kend = max(kbeg, prefix_count(nc, [&](int k) { return Sm[S.comp_off + k] < wb; }));
+  }
+  // the full loop's thread-to-component map, entered at the window's first pass
+  for (int k0 = kbeg / (kQU * kBS) * (kQU * kBS) + threadIdx.x; k0 < kend; k0 += kQU * kBS) {
+    double mq[kQU], sq[kQU];
+#pragma unroll
+    for (int u = 0; u < kQU; ++u) {
+      const int k = k0 + u * kBS;
+      const bool in = k >= kbeg && k < kend;
+      mq[u] = in ? mu[S.comp_off + k] : INFINITY;
+      sq[u] = in ? sigma[S.comp_off + k] : 1.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kQU; ++u) {
+      const double m = mq[u], s = sq[u];
+      // both erf arguments beyond +-6.5 (erf exactly +-1 in fp64): the two cdf
+      // values are equal and the term w*cu - w*cl is exactly 0 -- skip it
+      // (padding: m = +inf is skipped)
+      const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
+      if (xl - m >= b65 || xu - m <= -b65 || m == INFINITY) continue;
+      const double wk = w[S.comp_off + k0 + u * kBS];
+      double cu, cl;
+      if (lg) {
+        cu = lognormal_cdf_logx(lub, m, s);
+        cl = lognormal_cdf_logx(llb, m, s);
+      } else {
+        cu = normal_cdf(ub, m, s);
+        cl = normal_cdf(lb, m, s);
+      }
+      acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
+    }
+  }
+  acc = block_sum<kBS, double>(acc, sh);
+  return log(acc) - log(S.p_accept);
+}
+
+// mixtures above this many components take the block-wide log-mass
+constexpr int kQBig = 4096;
+__device__ __forceinline__ bool qlpdf_big(const tpe_seg& SB, const tpe_seg& SA) {
+  return max(SB.n_obs, SA.n_obs) + 1 > kQBig;
+}
+
 // one wave per value (kQW values per 256-thread block): the wave shares the
 // value's component CDF pairs
 constexpr int kQW = kBS / kWave;
 
-// grid (ceil(nper / kQW), n_jobs): value pos = kQW blockIdx.x + wave of job
-// blockIdx.y; nper = the partial entries per job (>= every job's count)
+// grid (nper, n_jobs), nper = the partial entries per job (>= every job's
+// count): a job of small mixtures scores value pos = kQW blockIdx.x + wave,
+// one of large ones (qlpdf_big) value blockIdx.x with the whole block
 __global__ __launch_bounds__(kBS) void k_score_q(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ w, const double* __restrict__ mu,
@@ -1195,26 +1292,43 @@ __global__ __launch_bounds__(kBS) void k_score_q(
     double* __restrict__ out_bl, double* __restrict__ out_al, tpe_best* __restrict__ partial,
     int32_t* __restrict__ err, const double* __restrict__ qP, const double* __restrict__ qS,
     int64_t nper) {
+  __shared__ double sh[kBS / kWave];
   const tpe_job J = jobs[blockIdx.y];
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
   const int64_t cnt = counts ? (int64_t)counts[blockIdx.y] : J.n_cand;
-  const int64_t pos = (int64_t)blockIdx.x * kQW + threadIdx.x / kWave;
-  if (pos >= nper) return;  // wave-uniform
-  tpe_best* P = partial + (int64_t)blockIdx.y * nper + pos;
-  const bool lead = lane_id() == 0;
-  if (pos >= cnt) {  // wave-uniform
-    if (lead) *P = empty_best();
-    return;
-  }
   const int64_t voff = counts ? J.lat_off : J.cand_off;
-  const double v = vals[voff + pos];
-  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, err, qP, qS);
-  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, err, qP, qS);
-  if (lead) {
+  auto put = [&](int64_t pos, double bl, double al, double v) __attribute__((always_inline)) {
     const int64_t idx = firsts ? firsts[J.lat_off + pos] : J.cand_base + pos;
     if (out_bl) out_bl[J.out_off + pos] = bl;
     if (out_al) out_al[J.out_off + pos] = al;
-    *P = tpe_best{bl - al, idx, v, 0};
+    partial[(int64_t)blockIdx.y * nper + pos] = tpe_best{bl - al, idx, v, 0};
+  };
+  if (qlpdf_big(SB, SA)) {  // block-uniform: block b scores value b with every thread
+    const int64_t pos = blockIdx.x;
+    if (pos >= nper) return;
+    if (pos >= cnt) {
+      if (threadIdx.x == 0) partial[(int64_t)blockIdx.y * nper + pos] = empty_best();
+      return;
+    }
+    const double v = vals[voff + pos];
+    const double bl = qlpdf_block(J, SB, w, mu, sigma, v, err, sh, qP, qS);
+    const double al = qlpdf_block(J, SA, w, mu, sigma, v, err, sh, qP, qS);
+    if (threadIdx.x == 0) put(pos, bl, al, v);
+    return;
   }
+  // otherwise block b < nper / kQW scores values kQW b .. one per wave (the
+  // grid has a block per value for the large-mixture jobs; the rest exit)
+  const int64_t pos = (int64_t)blockIdx.x * kQW + threadIdx.x / kWave;
+  if (pos >= nper) return;  // wave-uniform
+  const bool lead = lane_id() == 0;
+  if (pos >= cnt) {  // wave-uniform
+    if (lead) partial[(int64_t)blockIdx.y * nper + pos] = empty_best();
+    return;
+  }
+  const double v = vals[voff + pos];
+  const double bl = qlpdf(J, SB, w, mu, sigma, v, err, qP, qS);
+  const double al = qlpdf(J, SA, w, mu, sigma, v, err, qP, qS);
+  if (lead) put(pos, bl, al, v);
 }
 
 // Prefix-first lattice argmax (tpe_lattice_suggest).  A lattice value's score
@@ -1223,29 +1337,45 @@ __global__ __launch_bounds__(kBS) void k_score_q(
 // (np.argmax: first index of the maximum).  So after the first `prefix`
 // candidates the winner is settled unless some value not yet seen scores
 // strictly higher (or is NaN while the best seen is not): a value first seen
-// later has a larger index and loses every tie.  score_slot scores every
+// later has a larger index and loses every tie.  score_slots scores every
 // slot of the lattice (seen or not), k_lattice_decide takes the argmax over
 // the seen ones and flags the jobs where an unseen slot could still win; only
 // those draw the rest of their stream (the sampler with `need`) and decide
 // again over everything seen.  (The slots are scored by extra blocks of the
 // prefix's sampling launch, k_lattice_sample.)
-__device__ __forceinline__ void score_slot(const tpe_job* __restrict__ jobs,
-                                           const tpe_seg* __restrict__ segs,
-                                           const double* __restrict__ w,
-                                           const double* __restrict__ mu,
-                                           const double* __restrict__ sigma,
-                                           tpe_best* __restrict__ partial, int job, int64_t s,
-                                           int64_t nper, const double* __restrict__ P,
-                                           const double* __restrict__ Sm) {
+// Slot block sb of job `job` (slot_n blocks per job): slots
+// kSlotsPerBlock sb .. one per wave, or (mixtures past kQBig, qlpdf_big)
+// slot sb with the whole block; the blocks past a job's slots exit.  sh:
+// kBS / kWave doubles of LDS.  Call by the whole block.
+__device__ __forceinline__ void score_slots(const tpe_job* __restrict__ jobs,
+                                            const tpe_seg* __restrict__ segs,
+                                            const double* __restrict__ w,
+                                            const double* __restrict__ mu,
+                                            const double* __restrict__ sigma,
+                                            tpe_best* __restrict__ partial, int job, int64_t sb,
+                                            int64_t nper, double* sh, const double* __restrict__ P,
+                                            const double* __restrict__ Sm) {
   const tpe_job J = jobs[job];
-  if (s >= J.lat_n) return;  // wave-uniform
-  const double v = (double)(J.lat_kmin + s) * J.q;  // np.round(x/q) * q, as k_lattice_compact
+  const tpe_seg SB = segs[J.below], SA = segs[J.above];
   // every slot is scored, drawn or not: a slot below 0 (the bracket under a
   // qloguniform / qlognormal lattice, never drawn) must not raise the
   // reference's negative-argument error (tpe.py:196-197) -- a drawn value
   // x = round(exp(y)/q)*q >= 0 never has ub = x + q/2 < 0, so no err here
-  const double bl = qlpdf(J, segs[J.below], w, mu, sigma, v, nullptr, P, Sm);
-  const double al = qlpdf(J, segs[J.above], w, mu, sigma, v, nullptr, P, Sm);
+  auto value = [&](int64_t s) { return (double)(J.lat_kmin + s) * J.q; };  // as k_lattice_compact
+  if (qlpdf_big(SB, SA)) {  // block-uniform: slot sb with every thread
+    const int64_t s = sb;
+    if (s >= J.lat_n || s >= nper) return;
+    const double v = value(s);
+    const double bl = qlpdf_block(J, SB, w, mu, sigma, v, nullptr, sh, P, Sm);
+    const double al = qlpdf_block(J, SA, w, mu, sigma, v, nullptr, sh, P, Sm);
+    if (threadIdx.x == 0) partial[(int64_t)job * nper + s] = tpe_best{bl - al, -1, v, 0};
+    return;
+  }
+  const int64_t s = sb * kSlotsPerBlock + threadIdx.x / kWave;
+  if (s >= J.lat_n || s >= nper) return;  // wave-uniform
+  const double v = value(s);
+  const double bl = qlpdf(J, SB, w, mu, sigma, v, nullptr, P, Sm);
+  const double al = qlpdf(J, SA, w, mu, sigma, v, nullptr, P, Sm);
   if (lane_id() == 0) partial[(int64_t)job * nper + s] = tpe_best{bl - al, -1, v, 0};
 }
 
@@ -1745,8 +1875,7 @@ static bool launch_lattice_sample(const tpe_job* jobs, const tpe_job* host_jobs,
     gx = std::max(gx, (n + (int64_t)kBS * kLatR - 1) / ((int64_t)kBS * kLatR));
   }
   const int64_t per = (gx * n_jobs + 7) / 8;
-  // slot scoring rides on the prefix launch (one wave per slot)
-  const int64_t sblocks = need ? 0 : (slot_n + kSlotsPerBlock - 1) / kSlotsPerBlock * n_jobs;
+  const int64_t sblocks = need ? 0 : slot_n * n_jobs;  // slot scoring rides on the prefix launch
   if (gx > INT32_MAX || 8 * per + sblocks > INT32_MAX || slot_n > INT32_MAX) {
     set_error("%s: %lld work items", who, (long long)(gx * n_jobs));
     return false;
@@ -1925,7 +2054,7 @@ extern "C" int tpe_score_quantized(const tpe_job* jobs, const tpe_job* host_jobs
   if (win)
     hipLaunchKernelGGL(k_qreach, dim3(4 * n_jobs), dim3(kQB), 0, st, jobs, segs, mu, sigma,
                        reach_hi, reach_lo);
-  hipLaunchKernelGGL(k_score_q, dim3((unsigned)((gx + kQW - 1) / kQW), (unsigned)n_jobs),
+  hipLaunchKernelGGL(k_score_q, dim3((unsigned)gx, (unsigned)n_jobs),
                      dim3(kBS), 0, st, jobs, segs, w, mu, sigma, vals, firsts,
                      (const unsigned long long*)counts, out_bl, out_al, partial, err,
                      win ? reach_hi : nullptr, win ? reach_lo : nullptr, gx);

@@ -2645,8 +2645,42 @@ __global__ __launch_bounds__(kWave) void k_band_pick(const tpe_job* __restrict__
 // neighbours.  The offset is the mixture's largest log-coefficient (every
 // term <= 1, one exp per pair); a sum below 2^-900 (or a candidate off the
 // range, or NaN) is redone with the online log-sum-exp over all components.
-constexpr int kR64P = 4;                 // candidates per thread
+#ifndef TPE_R64P  // diagnostic builds: candidates per thread of k_score_pruned64
+#define TPE_R64P 8   // (2 048 sorted together: a wave's 64 span half the range of 4: fp64 C3 -10 %)
+#endif
+constexpr int kR64P = TPE_R64P;          // candidates per thread
 constexpr int kP64N = kBS * kR64P;       // candidates per block (sorted together)
+
+// exp(v) for the pruned sum's terms (v <= 0 or NaN; 0 below -745.2): n =
+// rint(32 v / ln2), r = v - n ln2/32 (Cody-Waite, the high part's 32 bits
+// keep n ln2_hi exact), exp(r) by its degree-6 Taylor polynomial (|r| <=
+// ln2/64: truncation < 2^-57), times 2^((n mod 32)/32) from a 32-entry table
+// (correctly rounded) and 2^(n div 32) -- ~1 ulp, the library exp's accuracy,
+// with 13 instead of 17 dependent fp64 steps and no overflow branch (round 6,
+// with 2 048 candidates per block: fp64 C3 level 256 -> 217 ms, same-box A/B)
+__constant__ double kExp2Tab[32] = {
+    0x1.0000000000000p+0, 0x1.059b0d3158574p+0, 0x1.0b5586cf9890fp+0, 0x1.11301d0125b51p+0,
+    0x1.172b83c7d517bp+0, 0x1.1d4873168b9aap+0, 0x1.2387a6e756238p+0, 0x1.29e9df51fdee1p+0,
+    0x1.306fe0a31b715p+0, 0x1.371a7373aa9cbp+0, 0x1.3dea64c123422p+0, 0x1.44e086061892dp+0,
+    0x1.4bfdad5362a27p+0, 0x1.5342b569d4f82p+0, 0x1.5ab07dd485429p+0, 0x1.6247eb03a5585p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.71f75e8ec5f74p+0, 0x1.7a11473eb0187p+0, 0x1.82589994cce13p+0,
+    0x1.8ace5422aa0dbp+0, 0x1.93737b0cdc5e5p+0, 0x1.9c49182a3f090p+0, 0x1.a5503b23e255dp+0,
+    0x1.ae89f995ad3adp+0, 0x1.b7f76f2fb5e47p+0, 0x1.c199bdd85529cp+0, 0x1.cb720dcef9069p+0,
+    0x1.d5818dcfba487p+0, 0x1.dfc97337b9b5fp+0, 0x1.ea4afa2a490dap+0, 0x1.f50765b6e4540p+0};
+__device__ __forceinline__ double exp_neg64(double v, const double* __restrict__ tab) {
+  const double n = rint(v * 0x1.71547652b82fep+5);
+  double r = fma(-n, 0x1.62e42fee00000p-6, v);
+  r = fma(-n, 0x1.a39ef35793c76p-38, r);
+  double p = fma(r, 1.0 / 720.0, 1.0 / 120.0);
+  p = fma(r, p, 1.0 / 24.0);
+  p = fma(r, p, 1.0 / 6.0);
+  p = fma(r, p, 0.5);
+  p = fma(r, p, 1.0);
+  p = fma(r, p, 1.0);
+  const int ni = (int)fmax(n, -40000.0);  // (NaN: the polynomial is NaN already)
+  const double e = ldexp(tab[ni & 31] * p, ni >> 5);
+  return v < -745.2 ? 0.0 : e;
+}
 
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
@@ -2674,7 +2708,7 @@ __device__ __forceinline__ double lse64_pruned(const tpe_seg& S, const double* _
                                                const double* __restrict__ rl,
                                                const int32_t* __restrict__ wide, int n_wide,
                                                double m, bool act, bool inr, double y,
-                                               double4* stage) {
+                                               double4* stage, const double* etab) {
   const int nc = S.n_obs + 1;
   const int64_t off = S.comp_off;
   int k_lo = nc, k_hi = -1;
@@ -2708,7 +2742,7 @@ __device__ __forceinline__ double lse64_pruned(const tpe_seg& S, const double* _
       const double4 cj = stage[j];
       const int k = kb + j;
       const double t = (y - cj.x) * cj.y;
-      const double e = exp(fma(-0.5 * t, t, cj.z - m));
+      const double e = exp_neg64(fma(-0.5 * t, t, cj.z - m), etab);
       s += (cj.w != 0.0 && k >= k_lo && k <= k_hi) ? e : 0.0;
     }
     __builtin_amdgcn_wave_barrier();  // (the chunk read before the next one is staged)
@@ -2778,6 +2812,8 @@ __global__ __launch_bounds__(kBS) void k_score_pruned64(
   __shared__ double s_key[kP64N], s_x[kP64N];
   __shared__ uint16_t s_idx[kP64N];
   __shared__ double4 s_win[kBS / kWave][kWave];  // each wave's chunk of its union window
+  __shared__ double s_etab[32];
+  if (threadIdx.x < 32) s_etab[threadIdx.x] = kExp2Tab[threadIdx.x];  // (before the sort's barriers)
   const tpe_job J = jobs[blockIdx.y];
   tpe_best* P = partial + (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kP64N;
@@ -2828,9 +2864,9 @@ __global__ __launch_bounds__(kBS) void k_score_pruned64(
     const double y = s_key[p], x = s_x[i];
     const bool inr = y >= Tb.lo && y <= Tb.hi;
     double bl = lse64_pruned(SB, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_below, mb, act,
-                             inr, y, s_win[wid]);
+                             inr, y, s_win[wid], s_etab);
     double al = lse64_pruned(SA, coef64, reach_hi, reach_lo, wide_idx, Tb.n_wide_above, ma, act,
-                             inr, y, s_win[wid]);
+                             inr, y, s_win[wid], s_etab);
     if (!act) continue;
     if (lgmm) {  // lognormal_lpdf's -log(x) (tpe.py:214-216)
       bl -= y;

@@ -18,6 +18,9 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 T = 2000
 doms = [Domain(lambda p: 0.0, S.c4_space(s)) for s in range(n)]
 trs = [S.flat_trials(d, T, s) for s, d in enumerate(doms)]
+import gc  # noqa: E402
+gc.collect()
+gc.freeze()  # (the documents are long-lived: tools/scale_configs.py c4)
 
 
 def call(k):
