@@ -1082,6 +1082,17 @@ __global__ __launch_bounds__(kQB) void k_qreach(const tpe_job* __restrict__ jobs
   }
 }
 
+// normal_cdf(x, m, s) (GMM1) or lognormal_cdf_logx(x = log of the bound, m,
+// s) (LGMM1) with one erf: the two share z = (x - m) / max(sqrt2 s, EPS) and
+// differ only in how erf(z) is combined (numpy's order for each: 0.5 * (1 +
+// e), tpe.py:109-114; 0.5 + 0.5 * e, tpe.py:186-205) -- one inlined erf per
+// bound instead of one per family and bound (register pressure)
+__device__ __forceinline__ double qcdf(bool lg, double x, double m, double s) {
+  const double bottom = fmax(__dmul_rn(kSqrt2, s), kEps);
+  const double e = erf((x - m) / bottom);
+  return lg ? __dadd_rn(0.5, __dmul_rn(0.5, e)) : __dmul_rn(0.5, __dadd_rn(1.0, e));
+}
+
 // how many leading k in [0, n) satisfy pred (pred holds on a prefix): a
 // wave-wide search, kWave probes per round (three rounds for n <= 2^18); call
 // by the whole wave (n wave-uniform)
@@ -1164,14 +1175,7 @@ __device__ __forceinline__ double qlpdf(const tpe_job& J, const tpe_seg& S,
       const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
       if (xl - m >= b65 || xu - m <= -b65 || m == INFINITY) continue;
       const double wk = w[S.comp_off + k0 + u * kWave];
-      double cu, cl;
-      if (lg) {
-        cu = lognormal_cdf_logx(lub, m, s);
-        cl = lognormal_cdf_logx(llb, m, s);
-      } else {
-        cu = normal_cdf(ub, m, s);
-        cl = normal_cdf(lb, m, s);
-      }
+      const double cu = qcdf(lg, xu, m, s), cl = qcdf(lg, xl, m, s);
       acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
     }
   }
@@ -1256,14 +1260,7 @@ __device__ __forceinline__ double qlpdf_block(const tpe_job& J, const tpe_seg& S
       const double b65 = 6.5 * fmax(__dmul_rn(kSqrt2, s), kEps);
       if (xl - m >= b65 || xu - m <= -b65 || m == INFINITY) continue;
       const double wk = w[S.comp_off + k0 + u * kBS];
-      double cu, cl;
-      if (lg) {
-        cu = lognormal_cdf_logx(lub, m, s);
-        cl = lognormal_cdf_logx(llb, m, s);
-      } else {
-        cu = normal_cdf(ub, m, s);
-        cl = normal_cdf(lb, m, s);
-      }
+      const double cu = qcdf(lg, xu, m, s), cl = qcdf(lg, xl, m, s);
       acc += __dsub_rn(__dmul_rn(wk, cu), __dmul_rn(wk, cl));  // two-stage, as tpe.py:171-173
     }
   }

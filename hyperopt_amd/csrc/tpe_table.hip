@@ -2724,13 +2724,19 @@ __device__ __forceinline__ double lse64_pruned(const tpe_seg& S, const double* _
   // terms added in the same order as a loop over the window with a scalar
   // load per component (round 6: that loop waited on two dependent scalar
   // loads per component), so the sums are the same bits
+  // (staged: x = mu, y = 1/sigma, z = log-coefficient - m, or -inf for a
+  // component of the wide list -- its term is then exactly 0, and the wide
+  // loop below adds it; the lane's own window as one unsigned compare)
   const int lane = lane_id();
+  // (k_hi < k_lo, no window: a base no k reaches; uint32 arithmetic wraps)
+  const uint32_t wlo = k_hi < k_lo ? 0x80000000u : (uint32_t)k_lo;
+  const uint32_t wspan = k_hi < k_lo ? 0u : (uint32_t)(k_hi - k_lo);
   for (int kb = ulo; kb <= uhi; kb += kWave) {  // wave-uniform
     const int kk = kb + lane;
-    double4 c = make_double4(0.0, 0.0, 0.0, 0.0);
+    double4 c = make_double4(0.0, 0.0, -INFINITY, 0.0);
     if (kk <= uhi) {
       c = ld4(coef64, off + kk);
-      c.w = is_wide(S, kk, c.y) ? 0.0 : 1.0;
+      c.z = is_wide(S, kk, c.y) ? -INFINITY : c.z - m;
     }
     stage[lane] = c;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2740,10 +2746,9 @@ __device__ __forceinline__ double lse64_pruned(const tpe_seg& S, const double* _
 #pragma unroll 2
     for (int j = 0; j < n; ++j) {
       const double4 cj = stage[j];
-      const int k = kb + j;
       const double t = (y - cj.x) * cj.y;
-      const double e = exp_neg64(fma(-0.5 * t, t, cj.z - m), etab);
-      s += (cj.w != 0.0 && k >= k_lo && k <= k_hi) ? e : 0.0;
+      const double e = exp_neg64(fma(-0.5 * t, t, cj.z), etab);
+      s += ((uint32_t)(kb + j) - wlo <= wspan) ? e : 0.0;
     }
     __builtin_amdgcn_wave_barrier();  // (the chunk read before the next one is staged)
   }

