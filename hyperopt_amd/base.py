@@ -216,21 +216,25 @@ class Columnar(object):
         self.docs.extend(new)
         self.rows = need
 
-    VALID_SAMPLES = 16  # strided identity probes of valid_for, besides the first and last row
+    VALID_SAMPLES = 16  # strided identity probes of valid_for (foreign lists), besides the ends
 
-    def valid_for(self, docs):
+    def valid_for(self, docs, probes=0):
         """Whether rows [0, rows) are still ``docs``' first documents: the
-        first and the last cached row and a few strided rows between must be
-        the same objects.  A removal anywhere shifts the last cached row (or
+        first and the last cached row -- and ``probes`` strided rows between,
+        for lists this package does not own (foreign_columnar) -- must be the
+        same objects.  A removal anywhere shifts the last cached row (or
         shortens the list), so deletions and filtering are caught; a document
-        replaced in place by another object between probes is not."""
+        replaced in place by another object between probes is not.
+        (``Trials._dynamic_trials`` only grows, or is replaced whole.)"""
         n = min(self.rows, len(docs))
         if n == 0:
             return True
         mine = self.docs
         if docs[n - 1] is not mine[n - 1] or docs[0] is not mine[0]:
             return False
-        step = max(1, n // self.VALID_SAMPLES)
+        if not probes:
+            return True
+        step = max(1, n // probes)
         return all(docs[i] is mine[i] for i in range(step, n - 1, step))
 
     def losses(self):
@@ -256,7 +260,7 @@ class Columnar(object):
         (engine.DeviceHistory, device row r == row r here), brought up to date
         by appending the rows added since the last call."""
         from .engine import DeviceHistory
-        key = str(engine.device)
+        key = engine.device  # (a torch.device: hashed by type and index)
         dh = self._device.get(key)
         if dh is None or dh.rows > self.rows:
             dh = self._device[key] = DeviceHistory(engine, len(self.labels),
@@ -299,7 +303,7 @@ def foreign_columnar(trials, docs, labels):
         docs = list(docs)
     key = tuple(labels)
     col = cache.get(key)
-    if col is None or col.rows > len(docs) or not col.valid_for(docs):
+    if col is None or col.rows > len(docs) or not col.valid_for(docs, Columnar.VALID_SAMPLES):
         col = cache[key] = Columnar(key)
     col.extend(docs)
     return col

@@ -303,6 +303,11 @@ def _decode(spec, value):
     return float(value), float(value)
 
 
+def _addr(a):
+    """Data address of a numpy array (for ctypes void* arguments)."""
+    return a.__array_interface__["data"][0]
+
+
 class LevelInputs(object):
     """The observation inputs of every label for Engine.run.
 
@@ -363,9 +368,11 @@ class LevelInputs(object):
         rows_b = np.empty(max(n_below, 1), np.int64)
         nb = np.empty(L, np.int64)
         na = np.empty(L, np.int64)
-        got = _L.load().tpe_split_inputs(losses.ctypes.data, T, n_below, act.ctypes.data, L,
-                                         c.n_active.ctypes.data, isb.ctypes.data,
-                                         rows_b.ctypes.data, nb.ctypes.data, na.ctypes.data)
+        # (raw addresses: numpy's .ctypes builds a helper object per access,
+        # ~1 us each -- seven per study add up in suggest_many)
+        got = _L.load().tpe_split_inputs(_addr(losses), T, n_below, _addr(act), L,
+                                         _addr(c.n_active), _addr(isb), _addr(rows_b), _addr(nb),
+                                         _addr(na))
         if got != min(n_below, T):
             raise _L.TpeHipError("tpe_split_inputs returned %d" % got)
         self = cls.__new__(cls)
@@ -509,6 +516,13 @@ class _Level(object):
             spec = domain.specs[lab]
             if spec.kind in ("qnormal", "qlognormal"):
                 self.lat.append((i, lab, spec))
+        # _decode as a plan: (label, 0 continuous / 1 integer, offset)
+        self.decode = []
+        for lab in level:
+            spec = domain.specs[lab]
+            off = int(spec.args[0]) if (spec.kind == "randint" and spec.args[1] is not None) \
+                else 0
+            self.decode.append((lab, 1 if spec.kind in ("randint", "categorical") else 0, off))
 
 
 def _level_info(domain, level):
@@ -701,9 +715,17 @@ def _suggest_many(requests, shard_studies=False):
                 values.append(r[a:a + len(level)])
                 a += len(level)
         for (st, level), vals in zip(items, values):
-            specs, walk, stored = st["rq"].domain.specs, st["walk"], st["stored"]
-            for lab, v in zip(level, vals):
-                walk[lab], stored[lab] = _decode(specs[lab], v)
+            walk, stored, dom = st["walk"], st["stored"], st["rq"].domain
+            if _space_sig(dom) is None:  # (no cached level plan for this space)
+                for lab, v in zip(level, vals):
+                    walk[lab], stored[lab] = _decode(dom.specs[lab], v)
+                continue
+            for (lab, mode, off), v in zip(_level_info(dom, level).decode, vals):
+                if mode == 0:  # a continuous label: the value itself
+                    walk[lab] = stored[lab] = float(v)
+                else:  # randint (offset re-applied, tpe.py:945-948) / categorical
+                    k = int(round(v))
+                    walk[lab], stored[lab] = k, k + off
 
     # Level by level; within a level the studies go in chunks, each chunk's
     # batches launched without waiting (Engine.run defer=True, two engines

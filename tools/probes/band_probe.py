@@ -1,14 +1,14 @@
 """Band sizes of the C3 table labels (diagnostic): per job the survivors and
 listed cells the select kernel leaves (library built with
-TPE_DIAG_BAND_KEEP, tools/diag_variants.sh), and the scorer's raw entries.
+TPE_DIAG_BAND_KEEP, tools/probes/diag_variants.sh), and the scorer's raw entries.
 
-    TPE_DIAG=1 TPE_NATIVE_LAUNCH=0 HYPEROPT_AMD_LIB=tools/_variants/lib_BAND_KEEP.so python tools/band_probe.py
+    TPE_DIAG=1 TPE_NATIVE_LAUNCH=0 HYPEROPT_AMD_LIB=tools/_variants/lib_BAND_KEEP.so python tools/probes/band_probe.py
 """
 import ctypes
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

@@ -1,12 +1,12 @@
 """Cell-table mismatch finder (diagnostic): runs one golden case through the
 table scorer and prints the worst candidates with their cells.
 
-    python tools/debug_table.py [case] [label]
+    python tools/probes/debug_table.py [case] [label]
 """
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np  # noqa: E402
 
 from hyperopt_amd.engine import Engine  # noqa: E402

@@ -2,9 +2,9 @@
 # Diagnostic builds of libtpe_hip.so with parts of a kernel switched off or
 # swapped (tools/_variants/lib<name>.so; load with HYPEROPT_AMD_LIB=...).
 # Never used by the product path or the tests.
-#   tools/diag_variants.sh MACRO[,MACRO...] ...   (each argument = one library)
+#   tools/probes/diag_variants.sh MACRO[,MACRO...] ...   (each argument = one library)
 set -e
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p tools/_variants
 C=hyperopt_amd/csrc
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off"

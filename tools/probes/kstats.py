@@ -1,4 +1,4 @@
-"""Compare rocprofv3 kernel_stats CSVs: python tools/kstats.py a.csv [b.csv ...]"""
+"""Compare rocprofv3 kernel_stats CSVs: python tools/probes/kstats.py a.csv [b.csv ...]"""
 import csv
 import sys
 

@@ -1,8 +1,8 @@
 """GPU idle time around stream-ordering operations (diagnostic for the gaps
 the level timeline shows after event records / waits).
 
-    rocprofv3 --kernel-trace -d gpurun_out/evgap -o run -- python tools/probe_event_gap.py
-    python tools/probe_event_gap.py --report gpurun_out/evgap
+    rocprofv3 --kernel-trace -d gpurun_out/evgap -o run -- python tools/probes/probe_event_gap.py
+    python tools/probes/probe_event_gap.py --report gpurun_out/evgap
 
 Each variant runs 20 times between host syncs and 2 ms sleeps; the report
 prints, per variant, the median idle gap on the main stream between the

@@ -1,11 +1,11 @@
 """Per-kind timing of the C3 labels through one scorer (diagnostic).
 
-    python tools/probe_table.py [n_cand] [kinds,comma,separated] [scorer]
+    python tools/probes/probe_table.py [n_cand] [kinds,comma,separated] [scorer]
 """
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

@@ -2,13 +2,13 @@
 C3's histories: cells per label, components per cell, and the work of a
 graded grid (diagnostic for DESIGN.md 3.1's build cost).
 
-    python tools/table_plan_probe.py
+    python tools/probes/table_plan_probe.py
 """
 import math
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np  # noqa: E402
 
 import bench  # noqa: E402
