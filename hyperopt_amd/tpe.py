@@ -439,7 +439,11 @@ def suggest(new_ids, domain, trials, seed, prior_weight=_default_prior_weight,
             # under torch.distributed this rank scores its units of the level
             # (whole labels, or candidate ranges when labels < ranks) and the
             # winners are combined across ranks (hyperopt_amd/dist.py)
-            units = hdist.plan_units([domain.specs[lab].kind for lab in level], n_ei, ws)[rank]
+            if ws == 1:  # every label whole (dist.plan_units' one-rank plan), cached
+                units = _whole_units(len(level), n_ei)
+            else:
+                units = hdist.plan_units([domain.specs[lab].kind for lab in level], n_ei,
+                                         ws)[rank]
             if not units:  # more ranks than shards of this level: nothing here, but
                 res = []   # the rank still joins the winners' all-gather below
             elif obs.device and _space_sig(domain) is not None:
@@ -535,6 +539,19 @@ def _level_info(domain, level):
     return lv
 
 
+@functools.lru_cache(maxsize=256)
+def _whole_units(n, n_ei):
+    """dist.plan_units(kinds, n_ei, 1)[0] as a tuple: every label whole."""
+    return tuple((i, 0, n_ei) for i in range(n))
+
+
+@functools.lru_cache(maxsize=256)
+def _zero_bases(n):
+    z = np.zeros(n, np.int64)
+    z.flags.writeable = False
+    return z
+
+
 def _level_batch(eng, domain, obs, level, units, seed, n_ei, col, pw, lf, prec, values=False):
     """One study's level (this rank's units of it) as a WorkBatch on the
     device history: counts from the split, keys from the cached label hashes,
@@ -543,23 +560,32 @@ def _level_batch(eng, domain, obs, level, units, seed, n_ei, col, pw, lf, prec, 
     ``values`` (one rank: every unit a whole label, in level order) just the
     winners' values."""
     lv = _level_info(domain, level)
-    idx = np.fromiter((u[0] for u in units), np.int64, len(units))
-    js = lv.js[idx]
+    whole = isinstance(units, tuple) and units is _whole_units(len(level), n_ei)
+    if whole:  # (one rank: every label, in level order)
+        idx = None
+        js = lv.js
+    else:
+        idx = np.fromiter((u[0] for u in units), np.int64, len(units))
+        js = lv.js[idx]
     lat = ()
     if lv.lat:
         lat = tuple(_lattice_range(obs.work(lab, spec, int(lv.js[i])),
                                    _params(spec.kind, spec.args)) for i, lab, spec in lv.lat)
     s = np.uint64(_mix64((int(seed) * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF))
     with np.errstate(over="ignore"):
-        keys = _mix64_np(lv.h[idx] ^ s)
+        keys = _mix64_np((lv.h if whole else lv.h[idx]) ^ s)
 
     def materialize():
         specs = domain.specs
         return [obs.work(level[i], specs[level[i]], col[level[i]], n_cand=count,
                          key=int(k), cand_base=start, n_total=n_ei)
                 for (i, start, count), k in zip(units, keys.tolist())]
-    batch = WorkBatch(("suggest", lv.id, tuple(units), n_ei, lat), obs.nb[js], obs.n_above[js],
-                      keys, [u[1] for u in units], materialize)
+    # (the key names the units: a token for the one-rank plan -- tuples do
+    # not cache their hash, and this key is hashed a few times per call)
+    batch = WorkBatch(("suggest", lv.id, ("whole", len(units)) if whole else tuple(units), n_ei,
+                       lat), obs.nb[js],
+                      obs.n_above[js], keys,
+                      _zero_bases(len(units)) if whole else [u[1] for u in units], materialize)
     r = eng.run(batch, prior_weight=pw, lf=lf, precision=prec, **obs.run_kwargs)
     if values:
         return r.value.tolist()
