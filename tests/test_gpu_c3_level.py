@@ -8,7 +8,8 @@ and its replay) is run once more and EVERY label's winner is re-derived
 exactly from the label's own materialised candidate stream:
   * continuous labels (table path): np.argmax over the fp64 scores of the
     2^22 drawn values (the pruned exact fp64 scorer on the injected stream),
-    and the winner and runner-up re-scored by the ORACLE;
+    and the stream's 256 best plus 256 random candidates re-scored by the
+    ORACLE (values, and the order of the best);
   * quantized labels (prefix-first lattice path): the ORACLE's fp64 score of
     each distinct drawn value, np.argmax over the stream (first index);
   * categorical labels (prefix-first categorical path): the ORACLE's
@@ -82,21 +83,30 @@ def test_every_label_is_the_exact_argmax_of_its_stream(level, kind):
             assert index[j] == x.index, (lab, index[j], x.index)
             assert value[j] == cand[x.index]
             np.testing.assert_allclose(score[j], x.score, rtol=1e-12, atol=1e-12)
-            # pinned to the oracle directly: the winner and the runner-up of
-            # the stream re-scored by the numpy restatement (tpe.py:117-180,
-            # 265-307), same values, same order
+            # pinned to the oracle directly: the stream's 256 best candidates
+            # (the whole band the fp32 table could have confused, winner and
+            # runner-up first) and 256 drawn at random, re-scored by the numpy
+            # restatement (tpe.py:117-180, 265-307): same values, same order
             s64 = x.below_llik - x.above_llik
             best = int(index[j])
             assert best == int(np.argmax(s64))
-            second = int(np.argmax(np.where(np.arange(n) == best, -np.inf, s64)))
-            pick = np.array([best, second])
+            top = np.argsort(-s64, kind="stable")[:256]
+            assert top[0] == best
+            rnd = np.random.RandomState(j).randint(0, n, 256)
+            pick = np.concatenate([top, rnd])
             with np.errstate(all="ignore"):
                 ref = O.continuous_label_scores(k, a, w.obs_below, w.obs_above, cand[pick])
             rs = ref["below_llik"] - ref["above_llik"]
             np.testing.assert_allclose(rs, s64[pick], rtol=1e-9, atol=1e-9)
-            gap = s64[best] - s64[second]
-            if gap > 1e-13 * max(1.0, abs(s64[best])):  # beyond fp64 rounding noise
-                assert rs[0] > rs[1], (lab, rs, gap)
+            # the oracle's order of the top candidates is the device's wherever
+            # two scores differ by more than the two scorers' largest observed
+            # disagreement (fp64 summation-order noise)
+            err = float(np.max(np.abs(rs - s64[pick])))
+            tol = 2 * err + 1e-13 * max(1.0, abs(s64[best]))
+            d_dev, d_ref = np.diff(s64[top]), np.diff(rs[:256])
+            loud = np.abs(d_dev) > tol
+            assert np.all(d_ref[loud] < 0), (lab, np.flatnonzero(loud & (d_ref >= 0))[:5])
+            assert rs[0] >= rs.max() - tol, (lab, rs[0], rs.max())
         elif kind == "quniform":
             cand = _stream(eng, w).cand
             u, inv = np.unique(cand, return_inverse=True)

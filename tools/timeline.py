@@ -3,7 +3,9 @@ for the last level(s) of a run, every dispatch's start offset from the
 level's first kernel, duration, queue and the idle gap before it on the GPU
 (diagnostic for the multi-GPU critical path).
 
-    python tools/timeline.py gpurun_out/tl8 [levels=2] [first-kernel=k_gather_obs]
+    python tools/timeline.py gpurun_out/tl8 [levels=2] [first-kernel]
+
+(no first kernel: levels are split at GPU idle gaps of more than 40 us)
 
 The last level of a bench.py trace is its untimed all-groups timer pass
 (HIP events around every kernel group, ~10 us each on the stream): look at
@@ -21,7 +23,7 @@ def short(name):
     return m.group(1) if m else name[:40]
 
 
-def main(src, levels=2, first="k_gather_obs"):
+def main(src, levels=2, first=None):
     db = sorted(glob.glob(os.path.join(src, "**", "*.db"), recursive=True))[0]
     c = sqlite3.connect(db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
@@ -29,9 +31,16 @@ def main(src, levels=2, first="k_gather_obs"):
     rows = list(c.execute("select name, start, end%s from kernels order by start"
                           % ((", " + qcol) if qcol else "")))
     starts = []
-    for i, r in enumerate(rows):  # a level's first `first` kernel (a second one
-        if short(r[0]) == first and (not starts or r[1] - rows[starts[-1]][1] > 100e3):
-            starts.append(i)      # within 100 us is the same level's, on the side stream)
+    if first:
+        for i, r in enumerate(rows):  # a level's first `first` kernel (a second one
+            if short(r[0]) == first and (not starts or r[1] - rows[starts[-1]][1] > 100e3):
+                starts.append(i)      # within 100 us is the same level's, on the side stream)
+    else:  # a level starts after the GPU was idle for more than 40 us
+        busy = None
+        for i, r in enumerate(rows):
+            if busy is None or r[1] - busy > 40e3:
+                starts.append(i)
+            busy = r[2] if busy is None else max(busy, r[2])
     for li in starts[-levels:]:
         nxt = [s for s in starts if s > li]
         seg = rows[li:nxt[0] if nxt else len(rows)]
