@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -137,6 +137,7 @@ _SIGNATURES = {
     "tpe_best_scatter": (_I, [_P, _P, _I, _P, _I, _P]),
     "tpe_prior_sample": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P]),
     "tpe_run_ops": (_I, [_P, _I, ctypes.POINTER(_I)]),
+    "tpe_set_issue_threads": (_I, [_I]),
     "tpe_ops_capture": (_I, [_P, _I, _P, _P, ctypes.POINTER(_P), ctypes.POINTER(_I)]),
     "tpe_graph_launch": (_I, [_P, _P]),
     "tpe_graph_destroy": (_I, [_P]),

@@ -11,11 +11,16 @@
 // point's parameter types by the call adapter below (the prototypes in
 // tpe_hip.h drive the conversion, so a record can only call a function with
 // exactly its declared arity).
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
 #include <type_traits>
 #include <utility>
 
@@ -122,6 +127,171 @@ int run_one(const tpe_op& op) {
 }  // namespace
 }  // namespace tpe
 
+namespace tpe {
+namespace {
+
+// ---- two issuing threads ---------------------------------------------------
+// A level's records go to two streams: the main chain (fit, table, scorer,
+// band) and the side stream (categorical and lattice groups), joined by event
+// records.  Each launch costs the issuing thread ~4 us inside the runtime, and
+// at a small label share the host's ~25 launches, not the GPU, set the
+// level's length: the GPU's main stream idles while the
+// host issues the side group.  With two issuing threads the caller issues the
+// main stream's records and a resident worker the other streams' records,
+// each in list order; event records (hipEventRecord / hipStreamWaitEvent) are
+// issued in their global list order -- a thread about to issue the k-th event
+// record waits until the first k-1 are issued -- so every wait sees the same
+// record as in one-thread issue, and the GPU's work and dependencies are the
+// ones the single thread would have queued.
+bool is_event_op(int32_t c) { return c == TPE_OP_EVENT_RECORD || c == TPE_OP_STREAM_WAIT; }
+
+// the argument word of `op` that names its stream (every entry point's last
+// parameter; the runtime records' stream operand), or -1
+int stream_word(const tpe_op& op) {
+  switch (op.code) {
+    case TPE_OP_EVENT_RECORD: return 1;
+    case TPE_OP_STREAM_WAIT: return 0;
+    case TPE_OP_MEMCPY: return 4;
+    case TPE_OP_STREAM_SYNC: return 0;
+    default: return op.n_args > 0 ? op.n_args - 1 : -1;
+  }
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+struct Batch {
+  const tpe_op* ops = nullptr;
+  int n = 0;
+  int64_t main = 0;                 // the caller thread's stream word
+  std::atomic<int> ev_done{0};      // event records issued so far (list order)
+  std::atomic<int> abort{0};        // a thread failed: the other stops at its next event record
+};
+
+// the caller's part (main = true: records on the main stream, and records
+// without a stream) or the worker's (every other record), in list order
+int issue_part(Batch& b, bool main, int* failed) {
+  int ev = 0;
+  for (int i = 0; i < b.n; ++i) {
+    const tpe_op& op = b.ops[i];
+    const int w = stream_word(op);
+    const bool mine = (w < 0 || op.a[w] == b.main) == main;
+    const bool evop = is_event_op(op.code);
+    if (!mine) {
+      ev += evop;
+      continue;
+    }
+    if (evop)
+      while (b.ev_done.load(std::memory_order_acquire) != ev) {
+        if (b.abort.load(std::memory_order_acquire)) return TPE_OK;  // the other's failure is reported
+        cpu_relax();
+      }
+    const int rc = run_one(op);
+    if (evop) b.ev_done.store(++ev, std::memory_order_release);
+    if (rc != TPE_OK) {
+      *failed = i;
+      b.abort.store(1, std::memory_order_release);
+      return rc;
+    }
+  }
+  const hipError_t e = hipGetLastError();  // this thread's launches
+  if (e != hipSuccess) {
+    set_error("tpe_run_ops: a launch of the batch failed: %s", hipGetErrorString(e));
+    *failed = b.n;
+    b.abort.store(1, std::memory_order_release);
+    return TPE_E_LAUNCH;
+  }
+  return TPE_OK;
+}
+
+// the resident worker: spins for kSpinUs after each batch (levels follow each
+// other closely), then sleeps on a condition variable; never destroyed (a
+// detached thread, so process exit does not wait for it)
+class Worker {
+ public:
+  static Worker* get() {
+    static Worker* w = new Worker();
+    return w;
+  }
+  std::mutex use;  // one batch at a time (a second caller issues alone)
+
+  void post(Batch* b, int device) {
+    device_ = device;
+    rc_ = TPE_OK;
+    failed_ = -1;
+    err_[0] = 0;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_.store(b, std::memory_order_release);
+    }
+    if (sleeping_.load(std::memory_order_acquire)) cv_.notify_one();
+  }
+  // waits for the posted batch; its status, failing record and message
+  int wait(int* failed, char* err, size_t n) {
+    while (job_.load(std::memory_order_acquire) != nullptr) cpu_relax();
+    *failed = failed_;
+    strncpy(err, err_, n - 1);
+    err[n - 1] = 0;
+    return rc_;
+  }
+
+ private:
+  static constexpr double kSpinUs = 2000.0;
+  Worker() { std::thread([this] { loop(); }).detach(); }
+  void loop() {
+    int dev = -1;
+    for (;;) {
+      Batch* b = job_.load(std::memory_order_acquire);
+      if (!b) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!(b = job_.load(std::memory_order_acquire)) &&
+               std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
+                       .count() < kSpinUs)
+          for (int k = 0; k < 64; ++k) cpu_relax();
+        if (!b) {
+          std::unique_lock<std::mutex> g(m_);
+          sleeping_.store(true, std::memory_order_release);
+          cv_.wait(g, [&] { return (b = job_.load(std::memory_order_acquire)) != nullptr; });
+          sleeping_.store(false, std::memory_order_release);
+        }
+      }
+      if (device_ != dev) {
+        (void)hipSetDevice(device_);
+        dev = device_;
+      }
+      defer_launch_checks(true);
+      int failed = -1;
+      const int rc = issue_part(*b, false, &failed);
+      defer_launch_checks(false);
+      if (rc != TPE_OK) {
+        strncpy(err_, tpe_last_error(), sizeof(err_) - 1);
+        err_[sizeof(err_) - 1] = 0;
+      }
+      rc_ = rc;
+      failed_ = failed;
+      job_.store(nullptr, std::memory_order_release);
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::atomic<Batch*> job_{nullptr};
+  std::atomic<bool> sleeping_{false};
+  int device_ = 0, rc_ = TPE_OK, failed_ = -1;
+  char err_[512] = "";
+};
+
+std::atomic<int> g_issue_threads{1};
+
+}  // namespace
+}  // namespace tpe
+
+extern "C" int tpe_set_issue_threads(int n) {
+  if (n != 1 && n != 2) {
+    tpe::set_error("tpe_set_issue_threads: n=%d (1 or 2)", n);
+    return TPE_E_ARG;
+  }
+  return tpe::g_issue_threads.exchange(n);
+}
+
 extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
   if (failed_op) *failed_op = -1;
   if (n_ops < 0 || (n_ops > 0 && !ops)) {
@@ -130,12 +300,52 @@ extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
   }
   // TPE_OPS_TRACE=1 (diagnostic): host time of every record on stderr
   static const bool trace = getenv("TPE_OPS_TRACE") && getenv("TPE_OPS_TRACE")[0] == '1';
-  auto t_prev = std::chrono::steady_clock::now();
   // launch status read once for the whole batch (check_launch), not per record
   struct Defer {
     Defer() { tpe::defer_launch_checks(true); }
     ~Defer() { tpe::defer_launch_checks(false); }
   } defer;
+  // two issuing threads when the records use more than one stream
+  int64_t main = 0;
+  bool have_main = false, multi = false;
+  if (!trace && tpe::g_issue_threads.load(std::memory_order_relaxed) == 2) {
+    for (int i = 0; i < n_ops && !multi; ++i) {
+      const int w = tpe::stream_word(ops[i]);
+      if (w < 0) continue;
+      if (!have_main) {
+        main = ops[i].a[w];
+        have_main = true;
+      } else if (ops[i].a[w] != main) {
+        multi = true;
+      }
+    }
+  }
+  if (multi) {
+    tpe::Worker* wk = tpe::Worker::get();
+    std::unique_lock<std::mutex> g(wk->use, std::try_to_lock);
+    int dev = 0;
+    if (g.owns_lock() && hipGetDevice(&dev) == hipSuccess) {
+      tpe::Batch b;
+      b.ops = ops;
+      b.n = n_ops;
+      b.main = main;
+      wk->post(&b, dev);
+      int f_main = -1, f_side = -1;
+      const int rc_main = tpe::issue_part(b, true, &f_main);
+      char err[512];
+      const int rc_side = wk->wait(&f_side, err, sizeof(err));
+      // the first failing record in list order is reported
+      const bool side_first = rc_side != TPE_OK && (rc_main == TPE_OK || f_side < f_main);
+      if (side_first) {
+        tpe::set_error("%s", err);
+        if (failed_op) *failed_op = f_side < n_ops ? f_side : -1;
+        return rc_side;
+      }
+      if (rc_main != TPE_OK && failed_op) *failed_op = f_main < n_ops ? f_main : -1;
+      return rc_main;
+    }
+  }
+  auto t_prev = std::chrono::steady_clock::now();
   for (int i = 0; i < n_ops; ++i) {
     const int rc = tpe::run_one(ops[i]);
     if (trace) {
@@ -167,22 +377,6 @@ extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
 // `from_stream` goes to `capture_stream`, since the caller's stream may be the
 // null stream -- and replayed with one hipGraphLaunch on the caller's stream: the host no longer pays ~4 us per kernel launch, and the
 // GPU no longer waits between kernels for the host to issue the next one.
-namespace tpe {
-namespace {
-// the argument word of `op` that names its stream (every entry point's last
-// parameter; the runtime records' stream operand), or -1
-int stream_word(const tpe_op& op) {
-  switch (op.code) {
-    case TPE_OP_EVENT_RECORD: return 1;
-    case TPE_OP_STREAM_WAIT: return 0;
-    case TPE_OP_MEMCPY: return 4;
-    case TPE_OP_STREAM_SYNC: return 0;
-    default: return op.n_args > 0 ? op.n_args - 1 : -1;
-  }
-}
-}  // namespace
-}  // namespace tpe
-
 extern "C" int tpe_ops_capture(const tpe_op* ops, int n_ops, void* from_stream,
                                void* capture_stream, void** graph_exec, int* failed_op) {
   if (failed_op) *failed_op = -1;

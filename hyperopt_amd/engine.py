@@ -536,6 +536,13 @@ class Engine:
         # product: on ROCm 7 a replayed C3 level is no faster on the host and
         # slower on the GPU than the records
         self.graphs = _knob("TPE_GRAPHS", "0") == "1"
+        # recorded levels are issued by two host threads (the caller: the main
+        # stream's records; a worker of the library: the side stream's), so the
+        # main chain no longer waits while the host issues the side group
+        # (tpe_set_issue_threads); TPE_ISSUE_THREADS=1: one thread
+        self.issue_threads = int(_knob("TPE_ISSUE_THREADS", "2"))
+        rc = self.lib.tpe_set_issue_threads(self.issue_threads)
+        L.check(min(rc, 0), "tpe_set_issue_threads")
         self._cap_stream = None
         self._oplists = {}      # launch key -> _OpList
         self._oplist_once = None

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 20
+#define TPE_ABI_VERSION 21
 
 enum {
   TPE_OK = 0,
@@ -650,6 +650,17 @@ typedef struct tpe_op {
   int64_t a[TPE_OP_ARGS];
 } tpe_op;                       /* 192 bytes */
 int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op);
+/* Issuing threads of tpe_run_ops (1, the default, or 2); returns the previous
+ * setting, TPE_E_ARG for another n.  With 2, a batch whose records use more
+ * than one stream is issued by the caller (the records on the stream of the
+ * first record that names one, and records without a stream) and a resident
+ * worker thread of the library (every other stream's records), each in list
+ * order; event records (TPE_OP_EVENT_RECORD / TPE_OP_STREAM_WAIT) are issued
+ * in their global list order, so the streams' work and dependencies are those
+ * of one-thread issue.  *failed_op names the first failing record in list
+ * order.  A batch issued while another thread's batch holds the worker, and
+ * every batch under TPE_OPS_TRACE=1, is issued by the caller alone. */
+int tpe_set_issue_threads(int n);
 /* The same records as a hipGraph: tpe_ops_capture issues ops[0..n_ops) into a
  * stream capture of `capture_stream` (a stream of the caller's, not the null
  * stream), with every record's stream operand that names `from_stream` (the

@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 20
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 21
     sizes = (ctypes.c_int32 * 11)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 11) == 11
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,
@@ -258,3 +258,26 @@ def test_categorical_suggest_argument_errors():
     jobs["flags"] = L.F_INJECTED
     assert call(1 << 16, 1 << 10) == -1
     assert b"not a sampled categorical job" in lib.tpe_last_error()
+
+
+def test_issue_threads_setting():
+    """tpe_set_issue_threads: 1 or 2 (the previous setting is returned), any
+    other count is an argument error; records still stop at the first failing
+    one whatever the setting (no GPU here: the caller issues them alone)."""
+    lib = L.load()
+    prev = lib.tpe_set_issue_threads(2)
+    try:
+        assert prev in (1, 2)
+        assert lib.tpe_set_issue_threads(2) == 2
+        for bad in (0, 3, -1):
+            assert lib.tpe_set_issue_threads(bad) == -1
+            assert b"tpe_set_issue_threads" in lib.tpe_last_error()
+        fit = L.OP_CODES["tpe_parzen_fit"]
+        nfit = len(L._SIGNATURES["tpe_parzen_fit"][1])
+        rec = lambda n_seg, stream: (fit, [0, 0, 0, n_seg] + [0] * (nfit - 5) + [stream])
+        ops = _ops(rec(0, 0), rec(0, 1234), rec(-1, 1234), rec(-1, 0))
+        failed = ctypes.c_int(7)
+        rc = lib.tpe_run_ops(ops.ctypes.data_as(ctypes.c_void_p), len(ops), ctypes.byref(failed))
+        assert rc == -1 and failed.value == 2 and b"tpe_parzen_fit" in lib.tpe_last_error()
+    finally:
+        lib.tpe_set_issue_threads(prev)
