@@ -162,6 +162,8 @@ inline void cpu_relax() { __builtin_ia32_pause(); }
 struct Batch {
   const tpe_op* ops = nullptr;
   int n = 0;
+  double* t_us = nullptr;           // TPE_OPS_TRACE: each record's issue end (us from t0)
+  std::chrono::steady_clock::time_point t0;
   int64_t main = 0;                 // the caller thread's stream word
   std::atomic<int> ev_done{0};      // event records issued so far (list order)
   std::atomic<int> abort{0};        // a thread failed: the other stops at its next event record
@@ -187,6 +189,9 @@ int issue_part(Batch& b, bool main, int* failed) {
       }
     const int rc = run_one(op);
     if (evop) b.ev_done.store(++ev, std::memory_order_release);
+    if (b.t_us)
+      b.t_us[i] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - b.t0)
+                      .count();
     if (rc != TPE_OK) {
       *failed = i;
       b.abort.store(1, std::memory_order_release);
@@ -308,7 +313,7 @@ extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
   // two issuing threads when the records use more than one stream
   int64_t main = 0;
   bool have_main = false, multi = false;
-  if (!trace && tpe::g_issue_threads.load(std::memory_order_relaxed) == 2) {
+  if (tpe::g_issue_threads.load(std::memory_order_relaxed) == 2) {
     for (int i = 0; i < n_ops && !multi; ++i) {
       const int w = tpe::stream_word(ops[i]);
       if (w < 0) continue;
@@ -329,11 +334,26 @@ extern "C" int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op) {
       b.ops = ops;
       b.n = n_ops;
       b.main = main;
+      double* t_us = nullptr;
+      if (trace) {
+        t_us = new double[n_ops];
+        for (int i = 0; i < n_ops; ++i) t_us[i] = -1.0;
+        b.t_us = t_us;
+      }
+      b.t0 = std::chrono::steady_clock::now();
       wk->post(&b, dev);
       int f_main = -1, f_side = -1;
       const int rc_main = tpe::issue_part(b, true, &f_main);
       char err[512];
       const int rc_side = wk->wait(&f_side, err, sizeof(err));
+      if (t_us) {
+        for (int i = 0; i < n_ops; ++i) {
+          const int w = tpe::stream_word(ops[i]);
+          fprintf(stderr, "op %2d code %2d %s issued at %7.2f us\n", i, ops[i].code,
+                  (w < 0 || ops[i].a[w] == main) ? "caller" : "worker", t_us[i]);
+        }
+        delete[] t_us;
+      }
       // the first failing record in list order is reported
       const bool side_first = rc_side != TPE_OK && (rc_main == TPE_OK || f_side < f_main);
       if (side_first) {

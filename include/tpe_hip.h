@@ -658,8 +658,8 @@ int tpe_run_ops(const tpe_op* ops, int n_ops, int* failed_op);
  * order; event records (TPE_OP_EVENT_RECORD / TPE_OP_STREAM_WAIT) are issued
  * in their global list order, so the streams' work and dependencies are those
  * of one-thread issue.  *failed_op names the first failing record in list
- * order.  A batch issued while another thread's batch holds the worker, and
- * every batch under TPE_OPS_TRACE=1, is issued by the caller alone. */
+ * order.  A batch issued while another thread's batch holds the worker is
+ * issued by the caller alone. */
 int tpe_set_issue_threads(int n);
 /* The same records as a hipGraph: tpe_ops_capture issues ops[0..n_ops) into a
  * stream capture of `capture_stream` (a stream of the caller's, not the null
