@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("HYPEROPT_AMD_LIB", os.path.join(HERE, "libtpe_hip.so"
 GMM1, LGMM1, CAT = 0, 1, 2
 OBS_IDENTITY, OBS_LOG = 0, 1
 F_LOW, F_HIGH, F_QUANT, F_INJECTED, F_DRAW32, F_LATTICE_READY = 1, 2, 4, 8, 16, 32
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 SEG_DTYPE = np.dtype([
     ("obs_off", "<i8"), ("comp_off", "<i8"), ("n_obs", "<i4"), ("lf", "<i4"),
@@ -98,7 +98,8 @@ _SIGNATURES = {
     "tpe_cat_posterior": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "tpe_history_append": (_I, [_P, _I, _I64, _P, _P, _I64, _I64, _P]),
     "tpe_cat_posterior_hist": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _I, _P, _P, _P, _P,
-                                    _P]),
+                                    _I64, _P, _P]),
+    "tpe_cat_hist_scratch_bytes": (_I64, [_I, _I, _I64]),
     "tpe_gather_obs": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I, _P, _P, _P, _P]),
     "tpe_gather_obs_multi": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P]),
     "tpe_table_partials": (_I64, [_P, _I]),

@@ -498,6 +498,395 @@ __global__ __launch_bounds__(kCHB) void k_cat_counts_hist(
   }
 }
 
+// Long histories (n_rows >= kCathMinRows, at most kCathMaxCat categories):
+// the single block per (segment, category) above walks every row itself --
+// 13 windows of 7 680 rows at 100k rows, ~115 us of scanning alone (C5's
+// categorical levels).  Chunked instead, the same bits:
+//   k_cath_count  one block per (4096-row chunk, segment): the chunk's members
+//                 and matches per category (ballots);
+//   k_cath_emit   one block per (chunk, segment): every member's position in
+//                 the segment (chunk base + wave base + rank in the tile) gives
+//                 its LF weight, every match its place in its category's list,
+//                 in row order -- the lists the single-block kernel folds;
+//   k_cath_fold   one wave per (segment, category): the list folded in order
+//                 (fold_list: the serial chain's bits), staged through LDS.
+constexpr int kCathMinRows = 32768;
+constexpr int kCathMaxCat = 32;
+constexpr int kCC = 4096;                 // rows per chunk
+constexpr int kCathBS = 256;              // k_cath_count / k_cath_emit block
+constexpr int kCathW = kCathBS / kWave;   // waves per chunk block
+constexpr int kCathRPW = kCC / kCathW;    // rows per wave (1024)
+constexpr int kCathT = kCathRPW / kWave;  // tiles of 64 rows per wave (16)
+constexpr int kCathStride = 1 + kCathMaxCat;  // counts per (segment, chunk): members, matches
+
+__host__ __device__ inline int64_t cath_chunks(int64_t n_rows) { return (n_rows + kCC - 1) / kCC; }
+__host__ __device__ inline int64_t cath_count_bytes(int n_seg, int64_t n_rows) {
+  return ((int64_t)4 * n_seg * cath_chunks(n_rows) * kCathStride + 255) & ~(int64_t)255;
+}
+
+// row i of the walk: a member of the segment (active label, the segment's
+// side of the split) and its category (-1: none of 0..n_cat-1)
+__device__ __forceinline__ void cath_row(const double* __restrict__ V,
+                                         const uint8_t* __restrict__ Ac,
+                                         const int32_t* __restrict__ rows,
+                                         const uint8_t* __restrict__ is_below, int64_t i,
+                                         int64_t n_rows, uint8_t side, int64_t offset, int n_cat,
+                                         bool& mem, int& cat) {
+  mem = false;
+  cat = -1;
+  if (i < n_rows) {
+    const int64_t r = rows ? (int64_t)rows[i] : i;
+    const bool a = Ac[r] != 0;
+    const double v = V[r];
+    mem = a && is_below[i] == side;
+    const int64_t cv = (int64_t)v - offset;  // (k_cat_counts_hist's test)
+    if (mem && cv >= 0 && cv < (int64_t)n_cat) cat = (int)cv;
+  }
+}
+
+__global__ __launch_bounds__(kCathBS) void k_cath_count(
+    const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
+    const int32_t* __restrict__ rows, int64_t n_rows, const uint8_t* __restrict__ is_below,
+    const tpe_gather* __restrict__ gathers, const tpe_cat_seg* __restrict__ segs,
+    uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_c[kCathW][kCathStride];
+  const int seg = blockIdx.y, c = blockIdx.x;
+  const tpe_cat_seg S = segs[seg];
+  const tpe_gather G = gathers[seg];
+  const double* __restrict__ V = vals + (int64_t)G.col * ld;
+  const uint8_t* __restrict__ Ac = active + (int64_t)G.col * ld;
+  const uint8_t side = G.below ? 1 : 0;
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const int K = S.n_cat;
+  bool mem[kCathT];
+  int cat[kCathT];
+  const int64_t r0 = (int64_t)c * kCC + (int64_t)w * kCathRPW;
+#pragma unroll
+  for (int t = 0; t < kCathT; ++t)
+    cath_row(V, Ac, rows, is_below, r0 + t * kWave + lane, n_rows, side, G.offset, K, mem[t],
+             cat[t]);
+  uint32_t nm = 0;
+#pragma unroll
+  for (int t = 0; t < kCathT; ++t) nm += (uint32_t)__popcll(__ballot(mem[t]));
+  if (lane == 0) s_c[w][0] = nm;
+  for (int k = 0; k < K; ++k) {  // (block-uniform)
+    uint32_t nk = 0;
+#pragma unroll
+    for (int t = 0; t < kCathT; ++t) nk += (uint32_t)__popcll(__ballot(cat[t] == k));
+    if (lane == 0) s_c[w][1 + k] = nk;
+  }
+  __syncthreads();
+  uint32_t* out = cnt + ((int64_t)seg * gridDim.x + c) * kCathStride;
+  for (int j = threadIdx.x; j < 1 + K; j += kCathBS) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < kCathW; ++q) v += s_c[q][j];
+    out[j] = v;
+  }
+}
+
+__global__ __launch_bounds__(kCathBS) void k_cath_emit(
+    const double* __restrict__ vals, const uint8_t* __restrict__ active, int64_t ld,
+    const int32_t* __restrict__ rows, int64_t n_rows, const uint8_t* __restrict__ is_below,
+    const tpe_gather* __restrict__ gathers, const tpe_cat_seg* __restrict__ segs,
+    const uint32_t* __restrict__ cnt, double* __restrict__ lists) {
+  __shared__ uint32_t s_w[kCathW][kCathStride];   // per wave: members, matches
+  __shared__ int64_t s_pre[kCathStride];          // chunks before this one
+  __shared__ int64_t s_tot[kCathStride];          // the whole segment
+  __shared__ int64_t s_cur[kCathW][kCathStride];  // per wave: next member position, list slots
+  const int seg = blockIdx.y, c = blockIdx.x, nch = gridDim.x;
+  const tpe_cat_seg S = segs[seg];
+  const tpe_gather G = gathers[seg];
+  const double* __restrict__ V = vals + (int64_t)G.col * ld;
+  const uint8_t* __restrict__ Ac = active + (int64_t)G.col * ld;
+  const uint8_t side = G.below ? 1 : 0;
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int K = S.n_cat;
+  bool mem[kCathT];
+  int cat[kCathT];
+  const int64_t r0 = (int64_t)c * kCC + (int64_t)w * kCathRPW;
+#pragma unroll
+  for (int t = 0; t < kCathT; ++t)
+    cath_row(V, Ac, rows, is_below, r0 + t * kWave + lane, n_rows, side, G.offset, K, mem[t],
+             cat[t]);
+  // this wave's members and matches
+  uint32_t nm = 0;
+#pragma unroll
+  for (int t = 0; t < kCathT; ++t) nm += (uint32_t)__popcll(__ballot(mem[t]));
+  if (lane == 0) s_w[w][0] = nm;
+  for (int k = 0; k < K; ++k) {
+    uint32_t nk = 0;
+#pragma unroll
+    for (int t = 0; t < kCathT; ++t) nk += (uint32_t)__popcll(__ballot(cat[t] == k));
+    if (lane == 0) s_w[w][1 + k] = nk;
+  }
+  // the chunks before this one, and the segment's totals per category
+  const uint32_t* C = cnt + (int64_t)seg * nch * kCathStride;
+  for (int j = threadIdx.x; j < 1 + K; j += kCathBS) {
+    int64_t pre = 0, tot = 0;
+    for (int q = 0; q < nch; ++q) {
+      const int64_t v = C[(int64_t)q * kCathStride + j];
+      pre += q < c ? v : 0;
+      tot += v;
+    }
+    s_pre[j] = pre;
+    s_tot[j] = tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // per wave: its first member position and list slots
+    int64_t m = s_pre[0];
+    int64_t koff[kCathMaxCat];
+    int64_t acc = (int64_t)seg * n_rows;  // (segment seg's lists start at seg * n_rows)
+    for (int k = 0; k < K; ++k) {
+      koff[k] = acc + s_pre[1 + k];
+      acc += s_tot[1 + k];
+    }
+    for (int q = 0; q < kCathW; ++q) {
+      s_cur[q][0] = m;
+      m += s_w[q][0];
+      for (int k = 0; k < K; ++k) {
+        s_cur[q][1 + k] = koff[k];
+        koff[k] += s_w[q][1 + k];
+      }
+    }
+  }
+  __syncthreads();
+  // the wave's tiles in row order: member positions -> LF weights -> list slots
+  const int n = S.n_obs;
+  const bool ramp = S.lf > 0 && S.lf < n;
+  const int64_t num = n - S.lf;
+  const double start = 1.0 / (double)n;
+  const double step = (ramp && num > 1) ? (1.0 - start) / (double)(num - 1) : 0.0;
+  int64_t mpos = s_cur[w][0];
+#pragma unroll
+  for (int t = 0; t < kCathT; ++t) {
+    const uint64_t mb = __ballot(mem[t]);
+    const int64_t pos = mpos + __popcll(mb & lt);
+    mpos += __popcll(mb);
+    int64_t slot = -1;
+    for (int k = 0; k < K; ++k) {  // (block-uniform)
+      const uint64_t kb = __ballot(cat[t] == k);
+      if (kb == 0) continue;  // (wave-uniform)
+      const int64_t base = s_cur[w][1 + k];
+      if (cat[t] == k) slot = base + __popcll(kb & lt);
+      if (lane == 0) s_cur[w][1 + k] = base + __popcll(kb);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (slot >= 0) {
+      double wt = 1.0;
+      if (ramp && pos < num) {
+        if (num == 1) wt = start;
+        else if (pos == num - 1) wt = 1.0;
+        else wt = __dadd_rn(__dmul_rn((double)pos, step), start);
+      }
+      lists[slot] = wt;
+    }
+  }
+}
+
+// seq_fold across a whole block (kFW waves): the same binade-grid steps, the
+// parity maps and the integer increments scanned over the block (wave scans,
+// then the waves' totals through LDS), so one pass covers kSE * 64 * kFW
+// entries -- a long chain's ~50k weights take ~15 passes instead of ~100
+// (a pass is a latency-bound chain of dependent steps, not throughput).
+// Every thread returns the same S (block-uniform control).
+constexpr int kFW = 16;               // waves of k_cath_fold
+constexpr int kFB = kFW * kWave;      // its block
+constexpr int kFoldN = kCHSE * kFB;   // entries per pass / per staged chunk (8 192)
+struct FoldX {
+  uint32_t wmap[kFW];        // each wave's composed parity map (inclusive)
+  uint64_t wsum[kFW];        // each wave's increment total
+  int64_t wcross[kFW];       // each wave's first leaving entry (-1: none) ...
+  uint64_t wcum[kFW];        // ... and the increments before it
+  double S;                  // (the serial prefix's result, broadcast)
+};
+__device__ double block_seq_fold(double S, const double* list, int n, FoldX& X) {
+  constexpr int kSE = kCHSE;
+  const int lane = lane_id(), wid = threadIdx.x / kWave;
+  double v[kSE];
+#pragma unroll
+  for (int j = 0; j < kSE; ++j) {
+    const int i = threadIdx.x * kSE + j;
+    v[j] = i < n ? list[i] : 0.0;
+  }
+  constexpr uint64_t kFrac = (1ull << 52) - 1, kTop = 1ull << 53;
+  int r0 = 0;
+  while (r0 < n) {  // (block-uniform)
+    const uint64_t sb = (uint64_t)__double_as_longlong(S);
+    const int es = (int)((sb >> 52) & 0x7ff);
+    if (S == 0.0 || es == 0) {
+      S = __dadd_rn(S, list[r0]);
+      ++r0;
+      continue;
+    }
+    const uint64_t A = (sb & kFrac) | (1ull << 52);
+    uint64_t d[kSE];
+    uint32_t tie = 0, huge = 0;
+#pragma unroll
+    for (int j = 0; j < kSE; ++j) {
+      const int i = threadIdx.x * kSE + j;
+      d[j] = fold_step(v[j], es, i >= r0 && i < n, tie, huge, j);
+    }
+    uint32_t a = 1, c = 0;
+#pragma unroll
+    for (int j = 0; j < kSE; ++j) {
+      if ((tie >> j) & 1u) {
+        a = 0;
+        c = 0;
+      } else {
+        c ^= (uint32_t)(d[j] & 1ull);
+      }
+    }
+    uint32_t x = a | (c << 1);
+    scan_step_map<0x111, 0xF>(x);
+    scan_step_map<0x112, 0xF>(x);
+    scan_step_map<0x114, 0xF>(x);
+    scan_step_map<0x118, 0xF>(x);
+    scan_step_map<0x142, 0xA>(x);
+    scan_step_map<0x143, 0xC>(x);
+    const uint32_t ex = dpp_u32<0x138, 0xF>(1u, x);  // the wave's lanes before this one
+    if (lane == kWave - 1) X.wmap[wid] = x;
+    __syncthreads();
+    uint32_t pre = 1u;  // the waves before this one (identity map first)
+    for (int q = 0; q < wid; ++q) pre = map_then(pre, X.wmap[q]);
+    const uint32_t in = map_then(pre, ex);
+    uint32_t P = ((in & 1u) & (uint32_t)(A & 1ull)) ^ (in >> 1);
+    uint64_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < kSE; ++j) {
+      if ((tie >> j) & 1u) {
+        d[j] += (P + d[j]) & 1ull;  // ties to the even A_{k+1}
+        P = 0;
+      } else {
+        P ^= (uint32_t)(d[j] & 1ull);
+      }
+      tot += d[j];
+    }
+    const uint64_t incl = wave_incl_sum_u64(tot);
+    if (lane == kWave - 1) X.wsum[wid] = incl;
+    __syncthreads();
+    uint64_t base = 0;
+    for (int q = 0; q < wid; ++q) base += X.wsum[q];
+    uint64_t cum = base + incl - tot;
+    int jc = -1;
+#pragma unroll
+    for (int j = 0; j < kSE; ++j) {
+      if (jc < 0) {
+        if (((huge >> j) & 1u) || A + cum + d[j] >= kTop) jc = j;
+        else cum += d[j];
+      }
+    }
+    const uint64_t bal = __ballot(jc >= 0);
+    if (lane == 0) {
+      if (bal == 0) {
+        X.wcross[wid] = -1;
+      } else {
+        const int L = __ffsll((unsigned long long)bal) - 1;
+        X.wcross[wid] = (int64_t)(wid * kWave + L) * kSE + __builtin_amdgcn_readlane(jc, L);
+        X.wcum[wid] =
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cum >> 32), L) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cum, L);
+      }
+    }
+    __syncthreads();
+    int qc = -1;
+    uint64_t all = 0;
+    for (int q = 0; q < kFW; ++q) {
+      if (qc < 0 && X.wcross[q] >= 0) qc = q;
+      all += X.wsum[q];
+    }
+    if (qc < 0) {
+      S = ldexp((double)(A + all), es - 1075);
+      r0 = n;
+    } else {
+      const int g = (int)X.wcross[qc];
+      S = __dadd_rn(ldexp((double)(A + X.wcum[qc]), es - 1075), list[g]);
+      r0 = g + 1;
+    }
+    __syncthreads();  // (X is rewritten by the next pass)
+  }
+  return S;
+}
+
+__global__ __launch_bounds__(kFB) void k_cath_fold(const tpe_cat_seg* __restrict__ segs,
+                                                   const uint32_t* __restrict__ cnt, int nch,
+                                                   int64_t n_rows,
+                                                   const double* __restrict__ lists,
+                                                   double* __restrict__ p,
+                                                   int32_t* __restrict__ err) {
+  __shared__ double s_l[kFoldN];
+  __shared__ FoldX X;
+  __shared__ int64_t s_meta[3];
+  const int seg = blockIdx.y, k = blockIdx.x;
+  const tpe_cat_seg S = segs[seg];
+  if (k >= S.n_cat) return;  // (block-uniform)
+  const int lane = lane_id();
+  const uint32_t* C = cnt + (int64_t)seg * nch * kCathStride;
+  if (threadIdx.x < kWave) {  // this category's list: after the lists of categories < k
+    int64_t before = 0, n_k = 0, members = 0;
+    for (int q = lane; q < nch; q += kWave) {
+      const uint32_t* Cq = C + (int64_t)q * kCathStride;
+      for (int j = 0; j < k; ++j) before += Cq[1 + j];
+      n_k += Cq[1 + k];
+      members += Cq[0];
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      before += __shfl_xor(before, o, kWave);
+      n_k += __shfl_xor(n_k, o, kWave);
+      members += __shfl_xor(members, o, kWave);
+    }
+    if (lane == 0) {
+      s_meta[0] = before;
+      s_meta[1] = n_k;
+      if (k == 0 && members != (int64_t)S.n_obs && err) atomicOr(err, 4);
+    }
+  }
+  __syncthreads();
+  const int64_t n_k = s_meta[1];
+  const double* L = lists + (int64_t)seg * n_rows + s_meta[0];
+  double cntv = 0.0;
+  int64_t done = 0;
+  for (int64_t f0 = 0; f0 < n_k; f0 += kFoldN) {
+    const int m = (int)min((int64_t)kFoldN, n_k - f0);
+    double t[kCHSE];
+#pragma unroll
+    for (int u = 0; u < kCHSE; ++u) {  // (all loads in flight, then the stores)
+      const int i = u * kFB + (int)threadIdx.x;
+      t[u] = i < m ? L[f0 + i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kCHSE; ++u) {
+      const int i = u * kFB + (int)threadIdx.x;
+      if (i < m) s_l[i] = t[u];
+    }
+    __syncthreads();
+    int f = 0;
+    if (done < kSerialHits) {  // the chain's first entries: one thread, one add each
+      f = (int)min((int64_t)m, kSerialHits - done);
+      if (threadIdx.x < kWave) {
+        const double sv = serial_fold(cntv, s_l, f, lane);
+        if (threadIdx.x == 0) X.S = sv;
+      }
+      __syncthreads();
+      cntv = X.S;
+    }
+    if (f < m) cntv = block_seq_fold(cntv, s_l + f, m - f, X);
+    done += m;
+    __syncthreads();  // (s_l is restaged next)
+  }
+  if (threadIdx.x == 0) {
+    double pseudo;
+    if (S.mode == 0) {
+      pseudo = cntv + S.prior_weight;  // tpe.py:589
+    } else {
+      const double pk = p[S.prior_p_off + k];
+      pseudo = cntv + (double)S.n_cat * (S.prior_weight * pk);  // tpe.py:603
+    }
+    p[S.p_off + k] = pseudo;
+  }
+}
+
 // normalise (numpy pairwise sum), log p (categorical_lpdf, tpe.py:60-73) and
 // the cumulative p of the inverse-CDF sampler; one block per segment
 __global__ __launch_bounds__(kCatBS) void k_cat_finalize(const tpe_cat_seg* __restrict__ segs,
@@ -564,12 +953,19 @@ extern "C" int tpe_cat_posterior(const int64_t* obs, const tpe_cat_seg* segs, in
   return check_launch("tpe_cat_posterior");
 }
 
+extern "C" int64_t tpe_cat_hist_scratch_bytes(int n_seg, int max_cat, int64_t n_rows) {
+  if (n_seg < 0 || max_cat < 0 || n_rows < 0) return -1;
+  if (n_seg == 0 || n_rows < kCathMinRows || max_cat > kCathMaxCat) return 0;
+  return cath_count_bytes(n_seg, n_rows) + (int64_t)8 * n_seg * n_rows;
+}
+
 extern "C" int tpe_cat_posterior_hist(const double* vals, const uint8_t* active, int64_t ld,
                                       const int32_t* rows, int64_t n_rows,
                                       const uint8_t* is_below, const tpe_gather* gathers,
                                       const tpe_cat_seg* segs, int n_seg, int max_cat,
                                       double* p_pool, double* logp_pool, double* cdf_pool,
-                                      int32_t* err, void* stream) {
+                                      void* work, int64_t work_bytes, int32_t* err,
+                                      void* stream) {
   if (n_seg < 0 || n_rows < 0 ||
       (n_seg > 0 && (!vals || !active || !is_below || !gathers || !segs || !p_pool ||
                      !logp_pool || !cdf_pool))) {
@@ -581,9 +977,33 @@ extern "C" int tpe_cat_posterior_hist(const double* vals, const uint8_t* active,
     set_error("tpe_cat_posterior_hist: n_seg=%d max_cat=%d", n_seg, max_cat);
     return TPE_E_ARG;
   }
+  if (work_bytes < 0) {
+    set_error("tpe_cat_posterior_hist: work_bytes=%lld", (long long)work_bytes);
+    return TPE_E_ARG;
+  }
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_cat_counts_hist, dim3(std::max(max_cat, 1), n_seg), dim3(kCHB), 0, st,
-                     vals, active, ld, rows, n_rows, is_below, gathers, segs, p_pool, err);
+  const int64_t need = tpe_cat_hist_scratch_bytes(n_seg, max_cat, n_rows);
+  if (need > 0 && work && work_bytes >= need && max_cat >= 1) {
+    // a long history: chunked (k_cath_*); the same bits as k_cat_counts_hist
+    const int64_t nch = cath_chunks(n_rows);
+    if (nch > INT32_MAX) {
+      set_error("tpe_cat_posterior_hist: n_rows=%lld", (long long)n_rows);
+      return TPE_E_UNSUPPORTED;
+    }
+    uint32_t* cnt = static_cast<uint32_t*>(work);
+    double* lists = reinterpret_cast<double*>(static_cast<char*>(work) +
+                                              cath_count_bytes(n_seg, n_rows));
+    const dim3 g((unsigned)nch, n_seg);
+    hipLaunchKernelGGL(k_cath_count, g, dim3(kCathBS), 0, st, vals, active, ld, rows, n_rows,
+                       is_below, gathers, segs, cnt);
+    hipLaunchKernelGGL(k_cath_emit, g, dim3(kCathBS), 0, st, vals, active, ld, rows, n_rows,
+                       is_below, gathers, segs, cnt, lists);
+    hipLaunchKernelGGL(k_cath_fold, dim3(max_cat, n_seg), dim3(kFB), 0, st, segs, cnt,
+                       (int)nch, n_rows, lists, p_pool, err);
+  } else {
+    hipLaunchKernelGGL(k_cat_counts_hist, dim3(std::max(max_cat, 1), n_seg), dim3(kCHB), 0, st,
+                       vals, active, ld, rows, n_rows, is_below, gathers, segs, p_pool, err);
+  }
   hipLaunchKernelGGL(k_cat_finalize, dim3(n_seg), dim3(kCatBS), 0, st, segs, p_pool, logp_pool,
                      cdf_pool);
   return check_launch("tpe_cat_posterior_hist");

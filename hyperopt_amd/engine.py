@@ -505,6 +505,9 @@ class Engine:
         # from the HBM history (tpe_cat_posterior_hist) instead of a gather
         # of their lists plus tpe_cat_posterior (TPE_CAT_HIST=0)
         self.cat_hist = _knob("TPE_CAT_HIST", "1") == "1"
+        # ... over a long history in row chunks by many blocks (the same bits;
+        # TPE_CAT_CHUNKED=0: one block per segment and category)
+        self.cat_chunked = _knob("TPE_CAT_CHUNKED", "1") == "1"
         # where the host issues that categorical work: "pre" (before the fit's
         # launches), "post" (after them), "late" (after the table build)
         self.cat_issue = _knob("TPE_CAT_ISSUE", "post")
@@ -1684,11 +1687,17 @@ class Engine:
         d_p = lv.base + lv.o_p  # the posterior is formed in place in the staged pool
         if st.cat_hist:  # (the categorical gather descriptors follow the fit's nfs)
             history = lv.history
+            max_cat = int(csegs["n_cat"].max())
+            # a long history is counted in row chunks (work sized for the
+            # history's capacity: it holds while the history does)
+            ws = max(0, int(lib.tpe_cat_hist_scratch_bytes(len(csegs), max_cat, history.ld))) \
+                if self.cat_chunked else 0
+            d_ws = self._buf("cat_hist_ws", ws) if ws else None
             L.check(lib.tpe_cat_posterior_hist(
                 history.vals.data_ptr(), history.active.data_ptr(), history.ld,
                 lv.base + lv.o_rows if lv.o_rows is not None else None, _V("n_rows", lv.n_rows),
                 lv.base + lv.o_isb, lv.base + lv.o_g + lv.nfs * L.GATHER_DTYPE.itemsize,
-                lv.d_csegs, len(csegs), int(csegs["n_cat"].max()), d_p, lv.d_logp, lv.d_ccdf,
+                lv.d_csegs, len(csegs), max_cat, d_p, lv.d_logp, lv.d_ccdf, d_ws, ws,
                 lv.d_err, side_p), "tpe_cat_posterior_hist")
         else:
             L.check(lib.tpe_cat_posterior(st.d_cobs, lv.d_csegs, len(csegs),

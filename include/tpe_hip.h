@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 21
+#define TPE_ABI_VERSION 22
 
 enum {
   TPE_OK = 0,
@@ -279,12 +279,18 @@ int tpe_cat_posterior(const int64_t* obs, const tpe_cat_seg* segs, int n_seg, in
  * counted without writing them.  gathers: device array aligned with segs
  * (obs_off unused).  An observation count other than segs[i].n_obs sets bit
  * 4 of *err.  Replaces tpe_gather_obs + tpe_cat_posterior for the
- * categorical labels of a level (tpe.py:578-615, pyll/base.py:1053-1060). */
+ * categorical labels of a level (tpe.py:578-615, pyll/base.py:1053-1060).
+ * work (device, nullable) of work_bytes >= tpe_cat_hist_scratch_bytes(n_seg,
+ * max_cat, n_rows) > 0: a long history is counted in row chunks by many
+ * blocks (the same bits); otherwise one block per (segment, category). */
 int tpe_cat_posterior_hist(const double* vals, const uint8_t* active, int64_t ld,
                            const int32_t* rows, int64_t n_rows, const uint8_t* is_below,
                            const struct tpe_gather* gathers, const tpe_cat_seg* segs, int n_seg,
                            int max_cat, double* p_pool, double* logp_pool, double* cdf_pool,
-                           int32_t* err, void* stream);
+                           void* work, int64_t work_bytes, int32_t* err, void* stream);
+/* Work bytes of tpe_cat_posterior_hist's chunked path for these sizes (0:
+ * the sizes take the single-block path; -1: bad arguments). */
+int64_t tpe_cat_hist_scratch_bytes(int n_seg, int max_cat, int64_t n_rows);
 
 /* ---- continuous candidates: sample (or read) + score + argmax ------------
  * Replaces GMM1/LGMM1 sampling (tpe.py:79-106, 229-257), GMM1_lpdf /

@@ -30,7 +30,7 @@ def test_header_symbols_exported():
 
 def test_struct_sizes_and_abi():
     lib = L.load()
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 21
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 22
     sizes = (ctypes.c_int32 * 11)()
     assert lib.tpe_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 11) == 11
     assert tuple(sizes) == (L.SEG_DTYPE.itemsize, L.CAT_SEG_DTYPE.itemsize,

@@ -216,3 +216,54 @@ def test_suggest_many_multi_history_matches_host_lists(monkeypatch):
                 for s, t in enumerate(studies) for n in (24, 1 << 14)]
         out[dev] = [d[0]["misc"]["vals"] for d in tpe.suggest_many(reqs)]
     assert out[True] == out[False]
+
+
+@pytest.mark.parametrize("T,K,rows", [(32769, 2, False), (40000, 32, False), (70001, 5, True),
+                                      (131072, 3, False)])
+def test_categorical_counts_chunked_equal_single_block(T, K, rows):
+    """The chunked count of a long history (k_cath_count / k_cath_emit /
+    k_cath_fold: many blocks, each list folded in order) gives the posterior
+    bits of the single block per (segment, category) and of np.bincount:
+    chunk and wave boundaries inside the LF ramp, 32 categories, a row list
+    (a subset of the history's rows)."""
+    from hyperopt_amd.engine import DeviceHistory, Engine, LabelWork
+    rng = np.random.RandomState(T + 7 * K)
+    p = rng.dirichlet(np.full(K, 0.7))
+    col = rng.choice(K, size=T, p=p).astype(float)
+    mat = np.stack([col, rng.choice(K, size=T).astype(float) + 1], axis=1)
+    active = rng.uniform(size=mat.shape) >= 0.15
+    losses = rng.normal(size=T)
+    sel = np.sort(rng.choice(T, size=T - T // 7, replace=False)) if rows else np.arange(T)
+    out = []
+    for chunked in (True, False):
+        eng = Engine()
+        eng.cat_chunked = chunked
+        hist = DeviceHistory(eng, 2)
+        hist.append(mat, active)
+        n = sel.size
+        n_below = min(int(np.ceil(0.25 * np.sqrt(n))), 25)
+        isb = np.zeros(n, np.uint8)
+        isb[np.argsort(losses[sel], kind="stable")[:n_below]] = 1
+        specs = [("c", "categorical", (tuple(p.tolist()),)), ("r", "randint", (1, 1 + K))]
+        works = []
+        for j, (lab, kind, a) in enumerate(specs):
+            act = active[sel, j]
+            v = mat[sel, j][act]
+            b = isb[act] == 1
+            works.append(LabelWork(lab, kind, a, v[b], None, col=j, n_above=int((~b).sum())))
+        res = eng.run(works, posteriors=True, history=hist, is_below=isb,
+                      rows=None if not rows else sel.astype(np.int32))
+        out.append([(r.extra["p_below"].copy(), r.extra["p_above"].copy()) for r in res])
+        if not chunked:
+            for j, (lab, kind, a) in enumerate(specs):
+                act = active[sel, j]
+                v = mat[sel, j][act].astype(np.int64)
+                b = isb[act] == 1
+                if kind == "categorical":
+                    want = O.categorical_posterior(v[~b], 1.0, p)
+                else:
+                    want = O.randint_posterior(v[~b], 1.0, 1, 1 + K)
+                np.testing.assert_array_equal(res[j].extra["p_above"], want, err_msg=lab)
+    for (ab, aa), (bb, ba) in zip(out[0], out[1]):
+        np.testing.assert_array_equal(ab, bb)
+        np.testing.assert_array_equal(aa, ba)
