@@ -694,6 +694,15 @@ __global__ __launch_bounds__(kCathBS) void k_cath_emit(
 constexpr int kFW = 16;               // waves of k_cath_fold
 constexpr int kFB = kFW * kWave;      // its block
 constexpr int kFoldN = kCHSE * kFB;   // entries per pass / per staged chunk (8 192)
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int o) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, kWave);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, kWave);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
 struct FoldX {
   uint32_t wmap[kFW];        // each wave's composed parity map (inclusive)
   uint64_t wsum[kFW];        // each wave's increment total
@@ -748,8 +757,15 @@ __device__ double block_seq_fold(double S, const double* list, int n, FoldX& X) 
     const uint32_t ex = dpp_u32<0x138, 0xF>(1u, x);  // the wave's lanes before this one
     if (lane == kWave - 1) X.wmap[wid] = x;
     __syncthreads();
-    uint32_t pre = 1u;  // the waves before this one (identity map first)
-    for (int q = 0; q < wid; ++q) pre = map_then(pre, X.wmap[q]);
+    // the waves before this one, composed in order: lane q < wid holds wave
+    // q's map (the others the identity), an ordered scan over 16 lanes
+    uint32_t pre = (lane < kFW && lane < wid) ? X.wmap[lane] : 1u;
+#pragma unroll
+    for (int o = 1; o < kFW; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)pre, o, kWave);
+      pre = lane >= o ? map_then(y, pre) : pre;
+    }
+    pre = (uint32_t)__builtin_amdgcn_readlane((int)pre, kFW - 1);
     const uint32_t in = map_then(pre, ex);
     uint32_t P = ((in & 1u) & (uint32_t)(A & 1ull)) ^ (in >> 1);
     uint64_t tot = 0;
@@ -766,8 +782,16 @@ __device__ double block_seq_fold(double S, const double* list, int n, FoldX& X) 
     const uint64_t incl = wave_incl_sum_u64(tot);
     if (lane == kWave - 1) X.wsum[wid] = incl;
     __syncthreads();
-    uint64_t base = 0;
-    for (int q = 0; q < wid; ++q) base += X.wsum[q];
+    // the waves' increment totals: before this wave, and all of them
+    const uint64_t wsl = lane < kFW ? X.wsum[lane] : 0ull;
+    uint64_t base = lane < wid ? wsl : 0ull, all = wsl;
+#pragma unroll
+    for (int o = 1; o < kFW; o <<= 1) {  // (lanes 0..15 reduce; lane 0's sums broadcast)
+      base += shfl_xor_u64(base, o);
+      all += shfl_xor_u64(all, o);
+    }
+    base = readlane_u64(base, 0);
+    all = readlane_u64(all, 0);
     uint64_t cum = base + incl - tot;
     int jc = -1;
 #pragma unroll
@@ -790,12 +814,8 @@ __device__ double block_seq_fold(double S, const double* list, int n, FoldX& X) 
       }
     }
     __syncthreads();
-    int qc = -1;
-    uint64_t all = 0;
-    for (int q = 0; q < kFW; ++q) {
-      if (qc < 0 && X.wcross[q] >= 0) qc = q;
-      all += X.wsum[q];
-    }
+    const uint64_t cb = __ballot(lane < kFW && X.wcross[lane < kFW ? lane : 0] >= 0);
+    const int qc = cb ? __ffsll((unsigned long long)cb) - 1 : -1;  // the first wave leaving
     if (qc < 0) {
       S = ldexp((double)(A + all), es - 1075);
       r0 = n;
