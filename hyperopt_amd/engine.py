@@ -44,7 +44,7 @@ TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
 BAND_TILE_CAP = 256  # per scorer tile: band entries kept (tpe_score_table_fast's tile_cap, <= 256)
 LAT_PREFIX = 1 << 16  # lattice argmax: candidates drawn before the early decision
-LAT_SUGGEST_MAX_SLOTS = 1 << 10  # ... for lattices of at most this many slots (all scored)
+LAT_SUGGEST_MAX_SLOTS = 1 << 14  # ... for lattices of at most this many slots (all scored)
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
 SCORERS = ("auto", "dense", "sorted", "table")
 SIDE_KINDS = ("lat", "qfb", "qinj", "cat")  # groups scored on the side stream
@@ -508,6 +508,12 @@ class Engine:
         # ... over a long history in row chunks by many blocks (the same bits;
         # TPE_CAT_CHUNKED=0: one block per segment and category)
         self.cat_chunked = _knob("TPE_CAT_CHUNKED", "1") == "1"
+        # quantized labels on the main stream when it has no scorer of its own
+        # (Engine._launch_level); TPE_LAT_MAIN=0: always on the side stream
+        self.lat_main = _knob("TPE_LAT_MAIN", "1") == "1"
+        # lattices of at most this many slots take the prefix-first argmax
+        # (every slot scored); larger ones draw and score their whole stream
+        self.lat_max_slots = int(_knob("TPE_LAT_MAX_SLOTS", str(LAT_SUGGEST_MAX_SLOTS)))
         # where the host issues that categorical work: "pre" (before the fit's
         # launches), "post" (after them), "late" (after the table build)
         self.cat_issue = _knob("TPE_CAT_ISSUE", "post")
@@ -1357,7 +1363,8 @@ class Engine:
                     None if exchange is None else
                     (int(x_comm), int(x_labels), int(x_world), x_slots.tobytes()),
                     self.side_stream, self.table_scorer, self.exact64, self.lat_prefix,
-                    self.cat_early, self.cat_issue, self.cat_hist,
+                    self.cat_early, self.cat_issue, self.cat_hist, self.lat_main,
+                    self.lat_max_slots,
                     "off" if timers is None else
                     ("all" if timer_groups is None else frozenset(timer_groups)))
         band_jobs = []  # (first, end) job positions scored by tpe_score_table_fast
@@ -1497,9 +1504,16 @@ class Engine:
         if lib is None:
             lib = self.lib
         sp, cat, groups, hist_mode = lv.sp, lv.cat, lv.groups, lv.hist_mode
+        # quantized labels on the main stream when it has no scorer of its own
+        # (a level of quantized and categorical labels only -- C5's middle
+        # level): the lattice work then runs beside the categorical chain on
+        # the side stream instead of after it
+        has_q = any(ids for k, ids in groups if k in SIDE_KINDS and k != "cat")
+        lat_main = self.lat_main and has_q and not any(
+            ids for k, ids in groups if k not in SIDE_KINDS)
         side = None
         if self.side_stream != "0" and not lv.sample_only and not lv.posteriors and any(
-                ids for k, ids in groups if k in SIDE_KINDS):
+                ids for k, ids in groups if k in SIDE_KINDS and not (lat_main and k != "cat")):
             if self._side is None:
                 self._side = lv.torch.cuda.Stream(self.device)
             side = self._side
@@ -1526,7 +1540,7 @@ class Engine:
             cat_early=side is not None and bool(cat) and self.cat_early,
             joined=side is None, side_started=side is None, cat_started=False,
             table_calls=[], jobs_ptr=lv.jobs.__array_interface__["data"][0],
-            d_obs=None, d_cobs=None)
+            d_obs=None, d_cobs=None, lat_main=lat_main)
         self._launch_gather(lv, st)
         lv._hmark('upload+gather')
         # side stream (TPE_SIDE_STREAM != "0"): quantized and categorical work
@@ -1569,7 +1583,7 @@ class Engine:
         # ---- scoring, one call per group ----------------------------------------
         # quantized and categorical groups go to the side stream (after the job
         # table has landed); continuous groups stay on `stream`
-        if side is not None:  # quantized groups need the continuous fit
+        if side is not None and not lat_main:  # quantized groups need the continuous fit
             ctx.stream_rec("fitted", sp)
         for g, stage in self._group_order(lv, st):
             self._launch_group(lv, st, g, stage)
@@ -1718,7 +1732,8 @@ class Engine:
             if not st.gather_side:  # (else the gather ran on the side stream)
                 ctx.stream_wait("gathered", st.side_p)
             self._cat_fit(lv, st)
-        if not st.side_started and kind in SIDE_KINDS and not (st.cat_early and kind == "cat"):
+        side_kind = kind in SIDE_KINDS and not (st.lat_main and kind != "cat")
+        if not st.side_started and side_kind and not (st.cat_early and kind == "cat"):
             st.side_started = True  # the side stream's groups that need the fit
             ctx.stream_wait("fitted", st.side_p)
             if lv.cat and not st.cat_early:
@@ -1731,7 +1746,7 @@ class Engine:
                                           lv.d_segs, lv.d_mu, lv.d_sig, lv.d_cdf, lv.precision,
                                           st.d_x, lv.sp), "tpe_sample")
             return
-        on_side = st.side is not None and kind in SIDE_KINDS
+        on_side = st.side is not None and side_kind
         kst = st.side if on_side else None
         sl = _LaunchState(
             kind=kind, ids=ids, a=a, b=b, nj=b - a, hj=lv.jobs[a:b],
@@ -1865,7 +1880,7 @@ class Engine:
             d_slot = self._buf("lat_slot", 8 * lv.lat_off)
             d_cnt = self._buf("lat_cnt", 8 * nj)
         max_vals = int(hj["lat_n"].max())
-        if self.lat_prefix and max_vals <= LAT_SUGGEST_MAX_SLOTS and \
+        if self.lat_prefix and max_vals <= self.lat_max_slots and \
                 int(hj["n_cand"].max()) > self.lat_prefix:
             # prefix first: the rest of a stream only where an unseen value
             # could still win (tpe_lattice_suggest)
@@ -2199,7 +2214,8 @@ class _Replay(object):
         return (stream, works.key, float(prior_weight), int(lf), int(precision), scorer, pruned,
                 history.vals.data_ptr(), history.active.data_ptr(), history.ld,
                 exchange, eng.side_stream, eng.table_scorer, eng.exact64, eng.lat_prefix,
-                eng.cat_early, eng.cat_issue, eng.cat_hist, eng.device_events,
+                eng.cat_early, eng.cat_issue, eng.cat_hist, eng.lat_main, eng.lat_max_slots,
+                eng.device_events,
                 eng.sorted_fit, "off" if timers is None else
                 ("all" if timer_groups is None else frozenset(timer_groups)))
 

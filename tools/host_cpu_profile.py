@@ -104,6 +104,8 @@ def make_engine():
     eng.cat_issue = os.environ.get("TPE_CAT_ISSUE", "post")
     eng.cat_hist = os.environ.get("TPE_CAT_HIST", "1") == "1"
     eng.cat_chunked = True
+    eng.lat_main = os.environ.get("TPE_LAT_MAIN", "1") == "1"
+    eng.lat_max_slots = E.LAT_SUGGEST_MAX_SLOTS
     eng.lat_prefix = int(os.environ.get("TPE_LAT_PREFIX", str(E.LAT_PREFIX)))
     eng.device_events = True
     eng.sorted_fit = os.environ.get("TPE_SORTED_FIT", "1") == "1"
