@@ -691,9 +691,16 @@ __global__ __launch_bounds__(kCathBS) void k_cath_emit(
 // entries -- a long chain's ~50k weights take ~15 passes instead of ~100
 // (a pass is a latency-bound chain of dependent steps, not throughput).
 // Every thread returns the same S (block-uniform control).
-constexpr int kFW = 16;               // waves of k_cath_fold
+#ifndef TPE_FOLD_WAVES  // diagnostic builds: k_cath_fold's waves and entries per lane
+#define TPE_FOLD_WAVES 8
+#endif
+#ifndef TPE_FOLD_SE
+#define TPE_FOLD_SE 8
+#endif
+constexpr int kFW = TPE_FOLD_WAVES;   // waves of k_cath_fold
 constexpr int kFB = kFW * kWave;      // its block
-constexpr int kFoldN = kCHSE * kFB;   // entries per pass / per staged chunk (8 192)
+constexpr int kFSE = TPE_FOLD_SE;     // entries per lane per pass
+constexpr int kFoldN = kFSE * kFB;    // entries per pass / per staged chunk (4 096)
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int o) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, kWave);
   const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, kWave);
@@ -711,7 +718,7 @@ struct FoldX {
   double S;                  // (the serial prefix's result, broadcast)
 };
 __device__ double block_seq_fold(double S, const double* list, int n, FoldX& X) {
-  constexpr int kSE = kCHSE;
+  constexpr int kSE = kFSE;
   const int lane = lane_id(), wid = threadIdx.x / kWave;
   double v[kSE];
 #pragma unroll
@@ -869,14 +876,14 @@ __global__ __launch_bounds__(kFB) void k_cath_fold(const tpe_cat_seg* __restrict
   int64_t done = 0;
   for (int64_t f0 = 0; f0 < n_k; f0 += kFoldN) {
     const int m = (int)min((int64_t)kFoldN, n_k - f0);
-    double t[kCHSE];
+    double t[kFSE];
 #pragma unroll
-    for (int u = 0; u < kCHSE; ++u) {  // (all loads in flight, then the stores)
+    for (int u = 0; u < kFSE; ++u) {  // (all loads in flight, then the stores)
       const int i = u * kFB + (int)threadIdx.x;
       t[u] = i < m ? L[f0 + i] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < kCHSE; ++u) {
+    for (int u = 0; u < kFSE; ++u) {
       const int i = u * kFB + (int)threadIdx.x;
       if (i < m) s_l[i] = t[u];
     }

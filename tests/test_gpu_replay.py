@@ -299,3 +299,28 @@ def test_graph_replay_equals_eager(side):
     assert "capture_failed" not in st, st
     assert st.get("captured", 0) >= 1 and st.get("graph", 0) >= 3, st
     assert plain.graph_stats.get("graph", 0) == 0
+
+
+def test_quantized_on_idle_main_stream_gives_the_same_level():
+    """A level of quantized and categorical labels only (no continuous
+    scorer on the main stream): with lat_main the lattice work runs on the
+    main stream beside the side stream's categorical chain; the winners equal
+    the all-on-the-side-stream engine's, eager and re-issued."""
+    base, other, DeviceHistory = _pair("native")
+    base.native = True
+    base.lat_main, other.lat_main = False, True
+    T = 3000
+    mat, active, losses = _history(T, 41)
+    keep = [j for j, (_, kind, _) in enumerate(SPACE)
+            if kind in ("quniform", "qnormal", "randint", "categorical")]
+    hb = DeviceHistory(base, len(SPACE), cap=4096)
+    ho = DeviceHistory(other, len(SPACE), cap=4096)
+    for h in (hb, ho):
+        h.append(mat, active)
+    for step in range(5):
+        works, isb = _works(mat, active, losses, T, step % 2, 1 << 18)
+        works = [works[j] for j in keep]
+        a = base.run(works, history=hb, is_below=isb)
+        b = other.run(works, history=ho, is_below=isb)
+        assert _rows(a) == _rows(b), step
+    assert other.graph_stats.get("native", 0) >= 2, other.graph_stats
