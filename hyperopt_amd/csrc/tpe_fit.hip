@@ -625,7 +625,8 @@ __global__ __launch_bounds__(kCathBS) void k_cath_emit(
   const uint32_t* C = cnt + (int64_t)seg * nch * kCathStride;
   for (int j = threadIdx.x; j < 1 + K; j += kCathBS) {
     int64_t pre = 0, tot = 0;
-    for (int q = 0; q < nch; ++q) {
+#pragma unroll 8
+    for (int q = 0; q < nch; ++q) {  // (eight loads in flight)
       const int64_t v = C[(int64_t)q * kCathStride + j];
       pre += q < c ? v : 0;
       tot += v;
