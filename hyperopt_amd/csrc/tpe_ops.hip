@@ -24,6 +24,8 @@
 #include <type_traits>
 #include <utility>
 
+#include <unistd.h>
+
 #include "tpe_common.hpp"
 
 namespace tpe {
@@ -214,8 +216,21 @@ int issue_part(Batch& b, bool main, int* failed) {
 class Worker {
  public:
   static Worker* get() {
-    static Worker* w = new Worker();
-    return w;
+    // (a forked child has no worker thread: it starts its own)
+    static std::atomic<Worker*> w{nullptr};
+    static std::atomic<pid_t> owner{0};
+    static std::mutex make;
+    const pid_t me = getpid();
+    Worker* cur = w.load(std::memory_order_acquire);
+    if (cur && owner.load(std::memory_order_acquire) == me) return cur;
+    std::lock_guard<std::mutex> g(make);
+    cur = w.load(std::memory_order_acquire);
+    if (!cur || owner.load(std::memory_order_acquire) != me) {
+      cur = new Worker();
+      w.store(cur, std::memory_order_release);
+      owner.store(me, std::memory_order_release);
+    }
+    return cur;
   }
   std::mutex use;  // one batch at a time (a second caller issues alone)
 
