@@ -762,16 +762,15 @@ __global__ __launch_bounds__(kBS) void k_score_sorted(
 // ---------------------------------------------------------------------------
 // quantized labels
 // ---------------------------------------------------------------------------
-// POW2: every job draws in fp32 (TPE_F_DRAW32) with q a power of two (C3's
-// quniform labels, C5's qlognormal) -- slots come from rintf in fp32 (x * 1/q
-// is exact, so rintf is np.round(x / q)) and the kernel carries no fp64 slot
-// code (fewer registers); the general instantiation handles the rest.  lfirst
-// is dynamic LDS sized by the host to the largest lattice of the launch, up to
-// kLatLds slots; the slots past it (a wide lattice's tail) are marked in
-// global memory directly.
+// POW2: every job draws in fp32 (TPE_F_DRAW32) with q a power of two and at
+// most kLatLds lattice slots (C3's quniform labels) -- slots come from rintf
+// in fp32 and the kernel carries no fp64 slot code (fewer registers); the
+// general instantiation handles the rest.  lfirst is dynamic LDS sized by the
+// host to the largest lattice of the launch (up to kLatLds slots).
 __host__ __device__ __forceinline__ bool lattice_pow2(const tpe_job& j) {
   int qe;
-  return (j.flags & TPE_F_DRAW32) && frexp(j.q, &qe) == 0.5 && qe > -100 && qe < 100;
+  return (j.flags & TPE_F_DRAW32) && frexp(j.q, &qe) == 0.5 && qe > -100 && qe < 100 &&
+         j.lat_n <= kLatLds;
 }
 
 __device__ __forceinline__ void score_slots(const tpe_job* __restrict__ jobs,
@@ -794,10 +793,7 @@ template <bool POW2>
 #ifndef TPE_LAT_WPE  // diagnostic builds: waves-per-EU target of the lattice sampler
 #define TPE_LAT_WPE 4     // (power-of-two candidate counts: 128 VGPRs, no spill)
 #endif
-#ifndef TPE_LAT_WPE_G  // ... and of the generic (wide-lattice) sampler
-#define TPE_LAT_WPE_G 3
-#endif
-__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_LAT_WPE : TPE_LAT_WPE_G))) void k_lattice_sample(
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_LAT_WPE : 1))) void k_lattice_sample(
     const tpe_job* __restrict__ jobs, const tpe_seg* __restrict__ segs,
     const double* __restrict__ mu, const double* __restrict__ sigma,
     const double* __restrict__ wcdf, unsigned long long* __restrict__ slot_first,
@@ -807,7 +803,6 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_
     const double* __restrict__ qS) {
   extern __shared__ uint32_t lfirst[];
   __shared__ MixLds s_mix;
-  __shared__ LeanMix s_lean;
   __shared__ alignas(16) float s_stage[kLatR * kBS];  // (also the slot blocks' fp64 scratch)
   __shared__ uint16_t s_list[(kBS / kWave) * kRetryList];
   const int64_t spj = slot_n;  // slot blocks per job (score_slots)
@@ -833,13 +828,7 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_
     // beyond go to the global marks directly, each read before its atomic
     const int n_loc = (int)min((int64_t)kLatLds, J.lat_n);
     for (int s = threadIdx.x; s < n_loc; s += kBS) lfirst[s] = 0xFFFFFFFFu;
-    const int nmix = SB.n_obs + 1;
-    // fp32 draws of a wide lattice from a staged below mixture: the lean
-    // sampler (block-uniform)
-    const bool lean = !POW2 && (J.flags & TPE_F_DRAW32) && nmix <= kStage;
-    const Mix M = lean ? Mix{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nmix}
-                       : stage_mix(SB, wcdf, mu, sigma, s_mix);
-    if (lean) stage_lean(SB, wcdf, mu, sigma, s_lean);
+    const Mix M = stage_mix(SB, wcdf, mu, sigma, s_mix);
     __syncthreads();
     if constexpr (POW2) {
       // kLatR consecutive candidates per thread (draw32_pairs); q a power of two:
@@ -852,21 +841,14 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_
                           (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList,
                           x);
       const float inv_q32 = (float)(1.0 / J.q);
-      const int64_t kmin = J.lat_kmin, nl = J.lat_n;
+      const int kmin = (int)J.lat_kmin, nl = (int)J.lat_n;
 #pragma unroll
       for (int r = 0; r < kLatR; ++r) {
         if (r >= nv) continue;
         const float t = rintf(x[r] * inv_q32);
-        const int64_t slot = (fabsf(t) < 9.0e18f) ? (int64_t)t - kmin : -1;
+        const int slot = (fabsf(t) < 2147483648.0f) ? (int)t - kmin : -1;
         if (slot < 0 || slot >= nl) {
           atomicOr(err, 2);
-          continue;
-        }
-        if (slot >= n_loc) {  // a wide lattice's tail: the global mark directly
-          unsigned long long* dst = &slot_first[J.lat_off + slot];
-          const unsigned long long g = (unsigned long long)(J.cand_base + t0 + r);
-          if (g < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            atomicMin(dst, g);
           continue;
         }
         // most draws land on slots already holding a smaller index: a plain read
@@ -904,32 +886,13 @@ __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(POW2 ? TPE_
       if (J.flags & TPE_F_DRAW32) {
         const int64_t t0 = base + (int64_t)threadIdx.x * kLatR;
         const int nv = (int)max((int64_t)0, min((int64_t)kLatR, n_lim - t0));
-        float* wst = s_stage + (threadIdx.x / kWave) * (kLatR * kWave);
-        uint16_t* wl = s_list + (threadIdx.x / kWave) * kRetryList;
-        if (lean) {
-          // the lean sampler (draw32_pairs' stream, bit for bit) into the
-          // wave's stage, read back one draw at a time: the draws never sit in
-          // VGPRs (a wide lattice's sampler had run at 188 VGPRs)
-          if (lo_on || hi_on)
-            lean_draw<kLatR, true>(s_lean, nmix, J.key, J.cand_base + t0, nv, lo_on, hi_on,
-                                   (float)J.low, (float)J.high, wst, wl);
-          else
-            lean_draw<kLatR, false>(s_lean, nmix, J.key, J.cand_base + t0, nv, false, false,
-                                    (float)J.low, (float)J.high, wst, wl);
-          const int lane = lane_id();
-          for (int r = 0; r < nv; ++r) {
-            float y = wst[r * kWave + lane];
-            if (lgmm) y = __expf(y);  // (draw32_pairs' to_x)
-            mark((double)y, t0 + r);
-          }
-        } else {
-          float x[kLatR];
-          draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
-                              (float)J.high, lgmm, wst, wl, x);
+        float x[kLatR];
+        draw32_pairs<kLatR>(M, J.key, J.cand_base + t0, nv, lo_on, hi_on, (float)J.low,
+                            (float)J.high, lgmm, s_stage + (threadIdx.x / kWave) * (kLatR * kWave), s_list + (threadIdx.x / kWave) * kRetryList,
+                            x);
 #pragma unroll
-          for (int r = 0; r < kLatR; ++r)
-            if (r < nv) mark((double)x[r], t0 + r);
-        }
+        for (int r = 0; r < kLatR; ++r)
+          if (r < nv) mark((double)x[r], t0 + r);
       } else {
         for (int r = 0; r < kLatR; ++r) {
           const int64_t li = base + r * kBS + threadIdx.x;
