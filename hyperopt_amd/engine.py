@@ -44,7 +44,7 @@ TABLE_CAP = 1 << 15  # cells per label in the cell-table path (128 B each)
 TABLE_MIN_CAND = 1 << 16  # auto scorer: table path from this many candidates per label
 BAND_TILE_CAP = 256  # per scorer tile: band entries kept (tpe_score_table_fast's tile_cap, <= 256)
 LAT_PREFIX = 1 << 16  # lattice argmax: candidates drawn before the early decision
-LAT_SUGGEST_MAX_SLOTS = 1 << 14  # ... for lattices of at most this many slots (all scored)
+LAT_SUGGEST_MAX_SLOTS = 1 << 10  # ... for lattices of at most this many slots (all scored)
 PRUNED64_MIN_COMP = 256  # fp64: pruned exact scorer from this many above components
 SCORERS = ("auto", "dense", "sorted", "table")
 SIDE_KINDS = ("lat", "qfb", "qinj", "cat")  # groups scored on the side stream
